@@ -1,0 +1,207 @@
+"""Benchmark of the MI355X content-defined chunker (BASELINE.json metric).
+
+One "step" = one pass of the chunker over the whole device-resident synthetic stream
+(phase A scan + exact blocks + sort + min/max resolve + cut list to the host).
+Default workload = BASELINE config 3: 64 GiB VM-image-like stream, 4 MiB average.
+Multi-GPU (config 4): one independent stream per rank (seed + rank), no data-path
+collective; an all-reduce (RCCL) of the per-rank elapsed time (MAX) and byte count.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size-gib 64] [--avg 4194304]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "proxmox-backup_amd"))
+
+METRIC = "GiB/s chunked (device-resident), 4 MiB mean, 64 GiB stream; boundaries bit-exact"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+GEN = {"counter": 0, "random": 1, "vmimage": 2}
+SEEDS = {"counter": 0, "random": 0x5EED0002, "vmimage": 0x5EED0003}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size-gib", type=float, default=64.0)
+    ap.add_argument("--avg", type=int, default=4 * 1024 * 1024)
+    ap.add_argument("--workload", choices=list(GEN), default="vmimage")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample-mib", type=int, default=512)
+    ap.add_argument("--host-inclusive-gib", type=float, default=4.0,
+                    help="also time the host-buffer path (H2D + kernels + D2H) on this many GiB; 0 = skip")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per scan launch (written by profiles/collect_traffic.py)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, workload, seed, avg):
+    """The oracle (faithful C restatement of chunker.rs) on the host cores, on a bounded
+    sample of the same stream: `threads` threads each chunk their own sample slice."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle
+
+    n = args.cpu_sample_mib * 1024 * 1024
+    gen = {"counter": lambda o: oracle.gen_counter(n, o),
+           "random": lambda o: oracle.gen_random(n, seed, o),
+           "vmimage": lambda o: oracle.gen_vmimage(n, seed, o)}[workload]
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    bufs = [None] * threads
+
+    def mk(t):
+        bufs[t] = gen(t * n)
+
+    ths = [threading.Thread(target=mk, args=(t,)) for t in range(threads)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    # single thread, one slice
+    t0 = time.perf_counter()
+    oracle.chunk_feed(avg, bufs[0])
+    single = n / (1 << 30) / (time.perf_counter() - t0)
+    # all threads, independent slices (ctypes releases the GIL)
+    ths = [threading.Thread(target=oracle.chunk_feed, args=(avg, bufs[t])) for t in range(threads)]
+    t0 = time.perf_counter()
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    agg = threads * n / (1 << 30) / (time.perf_counter() - t0)
+    cpu = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": ") \
+        if os.path.exists("/proc/cpuinfo") else "unknown"
+    del bufs
+    return {"value": round(agg, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} x {args.cpu_sample_mib} MiB slices of the same {workload} stream, "
+                      f"whole-buffer scan loop (oracle/chunker_oracle.c, gcc -O2); "
+                      f"1 thread: {single:.3f} GiB/s; host CPU: {cpu}"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import pbschunk
+
+    size = int(args.size_gib * (1 << 30)) // 8 * 8
+    seed = SEEDS[args.workload] + rank  # config 4: independent stream per GPU
+    buf = torch.empty(size, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    pbschunk.generate_device(buf.data_ptr(), size, GEN[args.workload], seed, 0, stream.cuda_stream)
+    torch.cuda.synchronize()
+
+    ch = pbschunk.Chunker(args.avg)
+    ch.set_stream(stream.cuda_stream)
+    ptr = buf.data_ptr()
+
+    def step():
+        return ch.find_cuts_device(ptr, size, is_final=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    scan_ms, ncuts, cand = [], 0, 0
+    for _ in range(args.steps):
+        cuts = step()
+        t = ch.last_timing()
+        scan_ms.append(t["scan_ms"])
+        ncuts, cand = int(cuts.size), int(t["candidates"])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        e = torch.tensor([elapsed, float(size)], dtype=torch.float64, device=dev)
+        mx = e.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0].item())
+        total_bytes = float(e[1].item())
+    else:
+        total_bytes = float(size)
+
+    step_s = elapsed / max(1, args.steps)
+    value = total_bytes * args.steps / (1 << 30) / elapsed
+    avg_scan_s = float(np.mean(scan_ms)) / 1e3 if scan_ms else float("nan")
+    achieved = size / avg_scan_s / 1e9  # algorithmic bytes (input read once) per launch
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("size") == size and tj.get("avg") == args.avg and tj.get("workload") == args.workload:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    host_incl = None
+    if rank == 0 and world == 1 and args.host_inclusive_gib > 0:
+        hn = int(args.host_inclusive_gib * (1 << 30)) // 8 * 8
+        hbuf = buf[:hn].cpu().numpy()  # pageable host copy of the stream prefix
+        ch2 = pbschunk.Chunker(args.avg)
+        ch2.find_cuts(hbuf[: 64 << 20], is_final=True)  # warm allocation
+        t1 = time.perf_counter()
+        ch2.find_cuts(hbuf, is_final=True)
+        host_incl = hn / (1 << 30) / (time.perf_counter() - t1)
+        ch2.close()
+        del hbuf
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": f"synthetic ({args.workload} generator, seed {hex(SEEDS[args.workload])}+rank, "
+                f"generated in HBM before timing)",
+        "config": {"workload": f"{args.workload}-{args.size_gib:g}GiB-avg{args.avg}",
+                   "stream_bytes_per_gpu": size, "avg_chunk": args.avg,
+                   "parallelism": f"independent stream per GPU x{world}",
+                   "chunks_per_stream": ncuts, "candidates_per_stream": cand},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "scan_main_kernel", "avg_launch_ms": round(avg_scan_s * 1e3, 4)},
+    }
+    if host_incl is not None:
+        out["host_inclusive_gib_s"] = round(host_incl, 3)
+    if args.cpu_baseline and world == 1:
+        del buf
+        out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

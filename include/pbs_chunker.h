@@ -1,0 +1,129 @@
+/*
+ * pbs_chunker.h -- C ABI of the MI355X (gfx950) content-defined chunker.
+ *
+ * Drop-in boundary for proxmox-backup's `pbs_datastore::Chunker`
+ * (pbs-datastore/src/chunker.rs, re-exported at pbs-datastore/src/lib.rs:177,199).
+ * Every entry point names the reference interface it replaces.  The Rust binding a
+ * maintainer would add (extern "C" block + a `Chunker` newtype keeping the
+ * reference's `new`/`scan` signatures) is in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Offsets are absolute stream offsets (u64).
+ *  - A handle is single-owner, not thread-safe (the reference's `&mut self`,
+ *    chunker.rs:112); distinct handles may be used concurrently, one HIP stream each.
+ *  - The hash scan runs on the GPU; a handle cannot be created without a HIP device
+ *    (pbs_chunker_new fails with PBS_ERR_NO_DEVICE).  There is no CPU fallback.
+ *  - Cut offsets are chunk END offsets (exclusive), i.e. the cut byte + 1, the same
+ *    quantity as `chunk_offset` after `DynamicChunkWriter::write`
+ *    (pbs-datastore/src/dynamic_index.rs:497-500).
+ */
+#ifndef PBS_CHUNKER_H
+#define PBS_CHUNKER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes (negative) */
+#define PBS_OK 0
+#define PBS_ERR_NOT_POW2 (-1)   /* chunker.rs:87-89 panics: "not a power of two" */
+#define PBS_ERR_NO_DEVICE (-2)  /* no HIP device visible */
+#define PBS_ERR_HIP (-3)        /* a HIP runtime call or kernel launch failed */
+#define PBS_ERR_NOMEM (-4)      /* host or device allocation failed */
+#define PBS_ERR_CAPACITY (-5)   /* output array too small; nothing was consumed */
+#define PBS_ERR_INVALID (-6)    /* bad argument (NULL handle, NULL data with len > 0) */
+
+typedef struct pbs_chunker pbs_chunker;
+
+/* Replaces `Chunker::new(chunk_size_avg: usize) -> Chunker` (chunker.rs:75-106).
+ * Thresholds: min = avg >> 2, max = avg << 2, mask = (2*avg - 1) as u32,
+ * minimum = mask - 2 (chunker.rs:91-105).  Returns NULL and *err = PBS_ERR_NOT_POW2
+ * where the reference panics (avg not a power of two), PBS_ERR_NO_DEVICE without a
+ * GPU.  `err` may be NULL. */
+pbs_chunker *pbs_chunker_new(size_t chunk_size_avg, int *err);
+
+/* Drop for `Chunker` (no explicit destructor in the reference). */
+void pbs_chunker_free(pbs_chunker *c);
+
+/* Replaces `Chunker::scan(&mut self, data: &[u8]) -> usize` (chunker.rs:112-168).
+ * Same contract: returns 0 if `data` holds no chunk boundary (the whole slice is
+ * consumed into the state), else the position just after the cut byte, relative to
+ * `data`.  The caller re-submits the unconsumed remainder starting at that position
+ * (pbs-client/src/chunk_stream.rs:44-54); bytes already scanned are not rescanned
+ * (their candidates are cached by absolute offset).  The reference's `scan` is
+ * infallible; on a device error this returns SIZE_MAX and pbs_chunker_last_error()
+ * tells why (the Rust shim turns that into a panic). */
+size_t pbs_chunker_scan(pbs_chunker *c, const uint8_t *data, size_t len);
+
+/* Batch form of repeated `scan` calls over a host buffer (the loop of
+ * examples/test_chunk_speed.rs:25-36 and of ChunkStream::poll_next).  `data` starts at
+ * the first unconsumed stream byte.  Writes the END offsets of every cut decided
+ * inside `data` to `out` (ascending) and their number to *n_out.  With is_final != 0
+ * the tail chunk's end (the stream length) is appended if the tail is non-empty, as
+ * ChunkStream does at EOF (chunk_stream.rs:64-68), and the handle starts a new
+ * stream.  `cap` must be >= pbs_chunker_max_cuts(len) (else PBS_ERR_CAPACITY and no
+ * state change).  Returns PBS_OK or an error code. */
+int pbs_chunker_find_cuts(pbs_chunker *c, const uint8_t *data, size_t len, int is_final,
+                          uint64_t *out, size_t cap, size_t *n_out);
+
+/* Same as pbs_chunker_find_cuts with `dev_data` a device pointer (HBM-resident
+ * input, e.g. a torch tensor's data_ptr()); `out` is a host array. */
+int pbs_chunker_find_cuts_device(pbs_chunker *c, const uint8_t *dev_data, size_t len,
+                                 int is_final, uint64_t *out, size_t cap, size_t *n_out);
+
+/* Upper bound of the cuts one find_cuts call over `len` bytes can return. */
+size_t pbs_chunker_max_cuts(size_t len);
+
+/* Absolute offset of the next unconsumed byte and of the open chunk's start. */
+uint64_t pbs_chunker_stream_offset(const pbs_chunker *c);
+uint64_t pbs_chunker_chunk_start(const pbs_chunker *c);
+
+/* Start a new stream with the same average (what `Chunker::new` would give). */
+int pbs_chunker_reset(pbs_chunker *c);
+
+/* Run the handle's kernels on this hipStream_t (NULL = the handle's own stream). */
+int pbs_chunker_set_stream(pbs_chunker *c, void *hip_stream);
+
+/* Error of the last failed call on this handle, and a message for any code. */
+int pbs_chunker_last_error(const pbs_chunker *c);
+const char *pbs_strerror(int code);
+
+/* Timing of the last find_cuts / scan device pass (HIP events on the handle's stream). */
+typedef struct {
+    float scan_ms;      /* main candidate kernel (scan_main_kernel) */
+    float exact_ms;     /* exact block re-evaluation + candidate sort */
+    float resolve_ms;   /* min/max resolve over the candidate list */
+    float total_ms;     /* first kernel start .. cut list on the host */
+    uint64_t bytes;     /* bytes scanned by the pass */
+    uint64_t suspects;  /* 128-byte blocks flagged by the main kernel */
+    uint64_t candidates;
+    uint64_t cuts;
+} pbs_timing;
+int pbs_chunker_last_timing(const pbs_chunker *c, pbs_timing *t);
+
+/* ---- helpers for tests and the benchmark harness ------------------------------ */
+
+/* Phase-A hook: every position p (>= 63) of a host buffer whose window hash passes
+ * the cut test for `avg` (chunker.rs:185), computed on the GPU; ascending. */
+int pbs_candidates_host(const uint8_t *data, size_t len, size_t avg, uint64_t *out, size_t cap,
+                        size_t *n_out);
+
+/* Fill a device buffer with a synthetic stream (kind 0 = LE-u32 counter
+ * (examples/test_chunk_speed.rs:8-14), 1 = splitmix64 random, 2 = VM-image-like).
+ * `len` and `offset` must be multiples of 8. */
+int pbs_generate_device(uint8_t *dev, size_t len, int kind, uint64_t seed, uint64_t offset,
+                        void *hip_stream);
+
+/* Number of visible HIP devices (0 without a GPU). */
+int pbs_device_count(void);
+
+/* Copy of the library's Buzhash table (256 entries), for the digest check. */
+int pbs_table_copy(uint32_t *out256);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBS_CHUNKER_H */

@@ -1,0 +1,137 @@
+"""ctypes wrapper of the CPU oracle (oracle/chunker_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` as the checker.  The product (the HIP path in
+``proxmox-backup_amd/``) never imports this module.
+
+Reference: pbs-datastore/src/chunker.rs:75-186 (see chunker_oracle.c header).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+WINDOW = 64
+TABLE_SHA256 = "5b52080d38287da9d2e278466e3e0db7ec98e5e8b226f50612a56fa012b1f660"
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u64, p = ctypes.c_uint64, ctypes.c_void_p
+        L.ora_sizeof_chunker.restype = u64
+        L.ora_new.argtypes = [p, u64]
+        L.ora_new.restype = ctypes.c_int
+        L.ora_scan.argtypes = [p, p, u64]
+        L.ora_scan.restype = u64
+        L.ora_chunk_feed.argtypes = [u64, p, u64, u64, p, u64]
+        L.ora_chunk_feed.restype = ctypes.c_int64
+        L.ora_window_hash.argtypes = [p, u64]
+        L.ora_window_hash.restype = ctypes.c_uint32
+        L.ora_candidates.argtypes = [u64, p, u64, p, u64]
+        L.ora_candidates.restype = ctypes.c_int64
+        L.ora_resolve.argtypes = [u64, p, u64, u64, p, u64]
+        L.ora_resolve.restype = ctypes.c_int64
+        L.ora_splitmix64.argtypes = [u64]
+        L.ora_splitmix64.restype = u64
+        for name in ("ora_gen_random", "ora_gen_vmimage"):
+            getattr(L, name).argtypes = [p, u64, u64, u64]
+            getattr(L, name).restype = None
+        L.ora_gen_counter.argtypes = [p, u64, u64]
+        L.ora_gen_counter.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+class Chunker:
+    """Streaming oracle with the reference's surface: Chunker::new(avg) / scan(data)."""
+
+    def __init__(self, chunk_size_avg: int):
+        L = lib()
+        self._buf = ctypes.create_string_buffer(int(L.ora_sizeof_chunker()))
+        if L.ora_new(self._buf, int(chunk_size_avg)) != 0:
+            raise ValueError("got unexpected chunk size - not a power of two.")
+
+    def scan(self, data) -> int:
+        a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        return int(lib().ora_scan(self._buf, _ptr(a), a.size))
+
+
+def chunk_feed(avg: int, data: np.ndarray, feed: int = 0) -> np.ndarray:
+    """Chunk END offsets (exclusive) of every cut when the stream arrives in pieces of
+    ``feed`` bytes (0 = whole buffer).  The tail is not included."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    cap = data.size // 65 + 2
+    out = np.empty(cap, dtype=np.uint64)
+    n = lib().ora_chunk_feed(int(avg), _ptr(data), data.size, int(feed), _ptr(out), cap)
+    if n < 0:
+        raise ValueError(f"oracle chunk_feed failed ({n})")
+    return out[:n].copy()
+
+
+def window_hash(data: np.ndarray, p: int) -> int:
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    assert p >= WINDOW - 1
+    return int(lib().ora_window_hash(_ptr(data), int(p)))
+
+
+def candidates(avg: int, data: np.ndarray) -> np.ndarray:
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    cap = max(16, data.size)
+    out = np.empty(cap, dtype=np.uint64)
+    n = lib().ora_candidates(int(avg), _ptr(data), data.size, _ptr(out), cap)
+    if n < 0:
+        raise ValueError(f"oracle candidates failed ({n})")
+    return out[:n].copy()
+
+
+def resolve(avg: int, cand: np.ndarray, length: int) -> np.ndarray:
+    cand = np.ascontiguousarray(cand, dtype=np.uint64)
+    cap = length // 65 + 2
+    out = np.empty(cap, dtype=np.uint64)
+    n = lib().ora_resolve(int(avg), _ptr(cand), cand.size, int(length), _ptr(out), cap)
+    if n < 0:
+        raise ValueError(f"oracle resolve failed ({n})")
+    return out[:n].copy()
+
+
+def gen_counter(length: int, offset: int = 0) -> np.ndarray:
+    a = np.empty(length, dtype=np.uint8)
+    lib().ora_gen_counter(_ptr(a), length, offset)
+    return a
+
+
+def gen_random(length: int, seed: int, offset: int = 0) -> np.ndarray:
+    a = np.empty(length, dtype=np.uint8)
+    lib().ora_gen_random(_ptr(a), length, seed, offset)
+    return a
+
+
+def gen_vmimage(length: int, seed: int, offset: int = 0) -> np.ndarray:
+    a = np.empty(length, dtype=np.uint8)
+    lib().ora_gen_vmimage(_ptr(a), length, seed, offset)
+    return a
+
+
+def splitmix64(x: int) -> int:
+    return int(lib().ora_splitmix64(x & 0xFFFFFFFFFFFFFFFF))

@@ -1,0 +1,620 @@
+// C ABI (include/pbs_chunker.h) and host pipeline of the MI355X chunker.
+//
+// Reference interface replaced: pbs_datastore::Chunker (pbs-datastore/src/chunker.rs:18-186)
+// and the caller loops around it (pbs-client/src/chunk_stream.rs:40-77,
+// pbs-datastore/src/dynamic_index.rs:493-515, examples/test_chunk_speed.rs:25-36).
+//
+// Pipeline for a range of new stream bytes (DESIGN.md "Pipeline"):
+//   1. scan_main_kernel   flags 128-byte blocks holding a hash candidate (HBM-bound scan)
+//   2. scan_exact_kernel  exact candidate positions in flagged blocks, the stream head
+//                         block and the tail that does not fill a wave tile
+//   3. radix sort of the candidate positions (hipcub)
+//   4. resolve kernels    min/max chunk-size rule -> cut list (pointer doubling)
+// Steps 1-4 run on the handle's HIP stream; only the counts (8 bytes), the cut list
+// and the few candidates of the still-open chunk come back to the host.
+//
+// `Chunker::scan` semantics (stateful, 0 or the boundary relative to the slice) are
+// kept by tracking absolute offsets: consumed (caller position), chunk_start (open
+// chunk), scanned_end (bytes whose candidates are known).  Re-submitted bytes are
+// never rescanned.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "buzhash_table.h"
+#include "pbs_chunker.h"
+#include "pbs_chunker_internal.h"
+
+using namespace pbs;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+struct Params {
+    uint64_t avg = 0, min = 0, max = 0, min_eff = 0, max_eff = 0;
+    uint32_t mask = 0, minimum = 0, rot = 0, thr = 0;
+    bool hash_cuts = false;  // false when no hash test can pass (avg == 1)
+};
+
+// chunker.rs:75-106 (+ the rotated-threshold form used by scan_main_kernel)
+int make_params(uint64_t avg, Params* p) {
+    if (__builtin_popcountll(avg) != 1) return PBS_ERR_NOT_POW2;
+    p->avg = avg;
+    p->mask = (uint32_t)(avg * 2 - 1);
+    p->minimum = p->mask - 2u;
+    p->min = avg >> 2;
+    p->max = avg << 2;
+    p->min_eff = std::max<uint64_t>(p->min, 65);  // first test at chunk_size 65 (fill phase)
+    p->max_eff = std::max<uint64_t>(p->max, 65);
+    p->hash_cuts = p->minimum <= p->mask;
+    const int n = __builtin_popcount(p->mask);  // mask = 2^n - 1
+    p->rot = (uint32_t)(32 - n) & 31u;
+    p->thr = p->hash_cuts ? (p->minimum << p->rot) : 0xFFFFFFFFu;
+    return PBS_OK;
+}
+
+inline uint32_t rotl32(uint32_t x, uint32_t r) {
+    r &= 31u;
+    return r ? (x << r) | (x >> (32u - r)) : x;
+}
+
+}  // namespace
+
+struct pbs_chunker {
+    Params prm;
+    // stream state (absolute offsets)
+    uint64_t consumed = 0;
+    uint64_t chunk_start = 0;
+    uint64_t scanned_end = 0;
+    uint8_t carry[64];
+    uint32_t carry_len = 0;
+    std::vector<uint64_t> pending;  // sorted candidates >= chunk_start, < scanned_end
+    size_t pend_head = 0;
+    // device
+    int device = 0;
+    int cu = 256;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    DevBuf d_table, d_pre, d_counters, d_susp, d_cand, d_C, d_sort_tmp, d_nxt, d_jtmp, d_nf, d_on,
+        d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in;
+    uint32_t susp_cap = 0, cand_cap = 0;
+    uint64_t* h_small = nullptr;  // pinned: counters / resolve results
+    hipEvent_t ev[5] = {};
+    pbs_timing timing{};
+    int last_error = 0;
+};
+
+namespace {
+
+int fail(pbs_chunker* c, int code) {
+    if (c) c->last_error = code;
+    return code;
+}
+
+#define HIP_TRY(c, x)                                   \
+    do {                                                \
+        if ((x) != hipSuccess) return fail(c, PBS_ERR_HIP); \
+    } while (0)
+
+uint64_t batch_max(const Params& p) {
+    // keep 32-bit candidate counters safe for tiny averages
+    if (p.avg >= 4096) return 1ull << 40;
+    return 1ull << 30;
+}
+
+// Phase A over d_data[0..len) (stream offset `base`): scan_main_kernel flags blocks,
+// scan_exact_kernel writes exact candidate positions (unsorted) to c->d_cand.  The
+// handle's carry (the <= 63 stream bytes before `base`) is the warm-up history.
+int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t base,
+                    uint32_t* ncand_out) {
+    const Params& p = c->prm;
+    *ncand_out = 0;
+    if (!p.hash_cuts || len == 0) return PBS_OK;
+    HIP_TRY(c, c->d_pre.ensure(64));
+    if (c->carry_len)
+        HIP_TRY(c, hipMemcpyAsync(c->d_pre.p, c->carry, c->carry_len, hipMemcpyHostToDevice,
+                                  c->stream));
+    const uint64_t ntiles = len / kWaveTileBytes;
+    const uint64_t covered = ntiles * kWaveTileBytes;
+    const int head = ntiles > 0 ? 1 : 0;
+    const uint64_t ext_first = covered / kBlockBytes;
+    const uint64_t ext_count = (len - covered + kBlockBytes - 1) / kBlockBytes;
+    const uint64_t blocks = (len + kBlockBytes - 1) / kBlockBytes;
+    const uint64_t expected = len / p.avg * 3 / 2 + 1;
+    const uint32_t want_s =
+        (uint32_t)std::min<uint64_t>(std::min<uint64_t>(blocks + 2, expected * 2 + 4096), 0xFFFFFFF0u);
+    const uint32_t want_c =
+        (uint32_t)std::min<uint64_t>(std::min<uint64_t>(len + 1, expected * 2 + 8192), 0xFFFFFFF0u);
+    c->susp_cap = std::max(c->susp_cap, want_s);
+    c->cand_cap = std::max(c->cand_cap, want_c);
+    uint32_t nsusp = 0, ncand = 0;
+    for (int attempt = 0;; ++attempt) {
+        HIP_TRY(c, c->d_susp.ensure((size_t)c->susp_cap * 8));
+        HIP_TRY(c, c->d_cand.ensure((size_t)c->cand_cap * 8));
+        HIP_TRY(c, c->d_counters.ensure(16));
+        HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 16, c->stream));
+        uint32_t* d_nsusp = c->d_counters.as<uint32_t>();
+        uint32_t* d_ncand = d_nsusp + 1;
+        HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+        HIP_TRY(c, launch_scan_main(d_data, ntiles, c->d_table.as<uint32_t>(), p.thr,
+                                    c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu,
+                                    c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
+        const uint64_t max_items = (uint64_t)c->susp_cap + 1 + ext_count;
+        HIP_TRY(c, launch_scan_exact(d_data, len, c->d_pre.as<uint8_t>(), c->carry_len,
+                                     c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, ext_first,
+                                     ext_count, head, p.mask, p.minimum, base,
+                                     c->d_cand.as<uint64_t>(), d_ncand, c->cand_cap, max_items,
+                                     c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_counters.p, 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        const uint32_t* cnt = reinterpret_cast<const uint32_t*>(c->h_small);
+        nsusp = cnt[0];
+        ncand = cnt[1];
+        bool again = false;
+        if (nsusp > c->susp_cap) {
+            c->susp_cap = (uint32_t)std::min<uint64_t>((uint64_t)nsusp * 2 + 1024, blocks + 2);
+            again = true;
+        }
+        if (ncand > c->cand_cap) {
+            c->cand_cap = (uint32_t)std::min<uint64_t>((uint64_t)ncand * 2 + 1024, 0xFFFFFFF0u);
+            again = true;
+        }
+        if (!again) break;
+        if (attempt > 4) return fail(c, PBS_ERR_NOMEM);
+    }
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->timing.scan_ms += ms;
+    c->timing.bytes += len;
+    c->timing.suspects += nsusp;
+    c->timing.candidates += ncand;
+    *ncand_out = ncand;
+    return PBS_OK;
+}
+
+// Radix-sort c->d_cand[0..n) into dst (device).
+int sort_candidates(pbs_chunker* c, uint32_t n, uint64_t* dst) {
+    if (n == 0) return PBS_OK;
+    size_t tb = 0;
+    HIP_TRY(c, sort_u64(nullptr, &tb, c->d_cand.as<uint64_t>(), dst, n, c->stream));
+    HIP_TRY(c, c->d_sort_tmp.ensure(tb));
+    tb = c->d_sort_tmp.cap;
+    HIP_TRY(c, sort_u64(c->d_sort_tmp.p, &tb, c->d_cand.as<uint64_t>(), dst, n, c->stream));
+    return PBS_OK;
+}
+
+// Keep the last <= 63 stream bytes before scanned_end as warm-up history.
+void update_carry(pbs_chunker* c, const uint8_t* tail, uint64_t tail_len) {
+    const uint32_t W = kWindow - 1;
+    if (tail_len >= W) {
+        std::memcpy(c->carry, tail + tail_len - W, W);
+        c->carry_len = W;
+        return;
+    }
+    uint8_t tmp[128];
+    std::memcpy(tmp, c->carry, c->carry_len);
+    std::memcpy(tmp + c->carry_len, tail, tail_len);
+    const uint32_t tot = c->carry_len + (uint32_t)tail_len;
+    const uint32_t keep = tot < W ? tot : W;
+    std::memcpy(c->carry, tmp + tot - keep, keep);
+    c->carry_len = keep;
+}
+
+// Carry update from device-resident bytes.
+int update_carry_device(pbs_chunker* c, const uint8_t* d_src, uint64_t len) {
+    uint8_t tail[64];
+    const uint64_t t = std::min<uint64_t>(len, kWindow - 1);
+    if (t) {
+        HIP_TRY(c, hipMemcpyAsync(tail, d_src + len - t, t, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    update_carry(c, tail, t);
+    return PBS_OK;
+}
+
+// Resolve the min/max rule over c->d_C[0..m) (sorted, absolute) from chunk_start with
+// bytes known up to `end`.  Appends cut END offsets to host `out` at *n, moves
+// chunk_start to the open chunk and keeps the open chunk's candidates pending.
+int run_resolve(pbs_chunker* c, uint32_t m, uint64_t end, uint64_t* out, size_t cap, size_t* n) {
+    const Params& p = c->prm;
+    const uint32_t nodes = m + 2;
+    HIP_TRY(c, c->d_C.ensure((size_t)nodes * 8));  // no-op: d_C already holds m entries
+    HIP_TRY(c, c->d_nxt.ensure((size_t)nodes * 4));
+    HIP_TRY(c, c->d_jtmp.ensure((size_t)nodes * 8));
+    HIP_TRY(c, c->d_nf.ensure((size_t)nodes * 8));
+    HIP_TRY(c, c->d_on.ensure((size_t)nodes * 4));
+    HIP_TRY(c, c->d_cnt.ensure((size_t)nodes * 8));
+    HIP_TRY(c, c->d_off.ensure((size_t)nodes * 8));
+    HIP_TRY(c, c->d_res.ensure(32));
+    size_t tb = 0;
+    HIP_TRY(c, exclusive_sum_u64(nullptr, &tb, c->d_cnt.as<uint64_t>(), c->d_off.as<uint64_t>(),
+                                 m + 1, c->stream));
+    HIP_TRY(c, c->d_scan_tmp.ensure(tb));
+    const uint64_t span = end > c->chunk_start ? end - c->chunk_start : 0;
+    const uint64_t out_cap = span / 65 + 2;
+    HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
+    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    ResolveParams rp{p.min_eff, p.max_eff, end, c->chunk_start};
+    HIP_TRY(c, launch_resolve(c->d_C.as<uint64_t>(), m, rp, c->d_nxt.as<uint32_t>(),
+                              c->d_jtmp.as<uint32_t>(), c->d_nf.as<uint64_t>(),
+                              c->d_on.as<uint32_t>(), c->d_cnt.as<uint64_t>(),
+                              c->d_off.as<uint64_t>(), c->d_scan_tmp.p, c->d_scan_tmp.cap,
+                              c->d_cuts.as<uint64_t>(), out_cap, c->d_res.as<uint64_t>(),
+                              c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_res.p, 24, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const uint64_t ncut = c->h_small[0], s_open = c->h_small[1], idx = c->h_small[2];
+    if (*n + ncut > cap || ncut > out_cap) return fail(c, PBS_ERR_CAPACITY);
+    if (ncut)
+        HIP_TRY(c, hipMemcpyAsync(out + *n, c->d_cuts.p, ncut * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+    std::vector<uint64_t> keep(m > idx ? m - idx : 0);
+    if (!keep.empty())
+        HIP_TRY(c, hipMemcpyAsync(keep.data(), c->d_C.as<uint64_t>() + idx, keep.size() * 8,
+                                  hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    *n += ncut;
+    c->chunk_start = s_open;
+    // pending = open-chunk candidates ++ older pending entries at/after `end` (not uploaded)
+    for (size_t i = c->pend_head; i < c->pending.size(); ++i)
+        if (c->pending[i] >= end) keep.push_back(c->pending[i]);
+    c->pending.swap(keep);
+    c->pend_head = 0;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->timing.resolve_ms += ms;
+    c->timing.cuts += ncut;
+    return PBS_OK;
+}
+
+void reset_stream(pbs_chunker* c) {
+    c->consumed = c->chunk_start = c->scanned_end = 0;
+    c->carry_len = 0;
+    c->pending.clear();
+    c->pend_head = 0;
+}
+
+// Scan new bytes [pos, pos + bl) (device source `dsrc`, host mirror `hsrc` or NULL)
+// and append their sorted candidates either to d_C after `np` pending entries
+// (to_device) or to the host pending list.  Returns the number of new candidates.
+int scan_new_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos,
+                   uint64_t bl, size_t np, bool to_device, uint32_t* nnew) {
+    uint32_t ncand = 0;
+    int rc = scan_candidates(c, dsrc, bl, pos, &ncand);
+    if (rc) return rc;
+    if (to_device) {
+        // d_C = [pending (np) | new sorted (ncand)]; pending is uploaded by the caller
+        // after this (d_C may be reallocated here).
+        HIP_TRY(c, c->d_C.ensure(((size_t)np + ncand + 2) * 8));
+        rc = sort_candidates(c, ncand, c->d_C.as<uint64_t>() + np);
+        if (rc) return rc;
+    } else if (ncand) {
+        HIP_TRY(c, c->d_C.ensure(((size_t)ncand + 2) * 8));
+        rc = sort_candidates(c, ncand, c->d_C.as<uint64_t>());
+        if (rc) return rc;
+        const size_t old = c->pending.size();
+        c->pending.resize(old + ncand);
+        HIP_TRY(c, hipMemcpyAsync(c->pending.data() + old, c->d_C.p, (size_t)ncand * 8,
+                                  hipMemcpyDeviceToHost, c->stream));
+    }
+    float ms = 0;
+    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) == hipSuccess) c->timing.exact_ms += ms;
+    if (hsrc)
+        update_carry(c, hsrc, bl);
+    else {
+        rc = update_carry_device(c, dsrc, bl);
+        if (rc) return rc;
+    }
+    c->scanned_end = pos + bl;
+    *nnew = ncand;
+    return PBS_OK;
+}
+
+int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final, uint64_t* out,
+                   size_t cap, size_t* n_out, bool device) {
+    if (!c) return PBS_ERR_INVALID;
+    if (!n_out || (len && !data) || (!out && cap)) return fail(c, PBS_ERR_INVALID);
+    *n_out = 0;
+    if (cap < pbs_chunker_max_cuts(len)) return fail(c, PBS_ERR_CAPACITY);
+    HIP_TRY(c, hipSetDevice(c->device));
+    c->timing = pbs_timing{};
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+    const uint64_t end = c->consumed + len;
+    uint64_t pos = std::max(c->consumed, c->scanned_end);
+    size_t n = 0;
+    bool first = true;
+    while (pos < end || first) {
+        first = false;
+        const uint64_t bl = std::min<uint64_t>(end > pos ? end - pos : 0, batch_max(c->prm));
+        const uint64_t rend = bl ? pos + bl : end;  // resolve horizon of this batch
+        size_t np = 0;
+        while (c->pend_head + np < c->pending.size() && c->pending[c->pend_head + np] < rend) ++np;
+        uint32_t nnew = 0;
+        if (bl) {
+            const uint8_t* dsrc;
+            const uint8_t* hsrc = nullptr;
+            if (device) {
+                dsrc = data + (pos - c->consumed);
+            } else {
+                hsrc = data + (pos - c->consumed);
+                HIP_TRY(c, c->d_in.ensure(bl));
+                HIP_TRY(c, hipMemcpyAsync(c->d_in.p, hsrc, bl, hipMemcpyHostToDevice, c->stream));
+                dsrc = c->d_in.as<uint8_t>();
+            }
+            int rc = scan_new_bytes(c, dsrc, hsrc, pos, bl, np, true, &nnew);
+            if (rc) return rc;
+        } else {
+            HIP_TRY(c, c->d_C.ensure(((size_t)np + 2) * 8));
+        }
+        if (np)
+            HIP_TRY(c, hipMemcpyAsync(c->d_C.p, c->pending.data() + c->pend_head, np * 8,
+                                      hipMemcpyHostToDevice, c->stream));
+        const uint64_t m = (uint64_t)np + nnew;
+        if (m > 0xFFFFFFF0ull) return fail(c, PBS_ERR_NOMEM);
+        int rc = run_resolve(c, (uint32_t)m, rend, out, cap, &n);
+        if (rc) return rc;
+        pos += bl;
+    }
+    c->consumed = end;
+    if (is_final) {
+        if (c->chunk_start < end) {
+            if (n >= cap) return fail(c, PBS_ERR_CAPACITY);
+            out[n++] = end;
+        }
+        reset_stream(c);
+    }
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(c, hipEventSynchronize(c->ev[3]));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev[4], c->ev[3]) == hipSuccess) c->timing.total_ms = ms;
+    *n_out = n;
+    return PBS_OK;
+}
+
+void destroy(pbs_chunker* c) {
+    DevBuf* bufs[] = {&c->d_table, &c->d_pre, &c->d_counters, &c->d_susp, &c->d_cand, &c->d_C,
+                      &c->d_sort_tmp, &c->d_nxt, &c->d_jtmp, &c->d_nf, &c->d_on, &c->d_cnt,
+                      &c->d_off, &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->h_small) (void)hipHostFree(c->h_small);
+    delete c;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------
+extern "C" {
+
+const char* pbs_strerror(int code) {
+    switch (code) {
+        case PBS_OK: return "ok";
+        case PBS_ERR_NOT_POW2: return "got unexpected chunk size - not a power of two.";
+        case PBS_ERR_NO_DEVICE: return "no HIP device available (the chunker has no CPU path)";
+        case PBS_ERR_HIP: return "HIP runtime error";
+        case PBS_ERR_NOMEM: return "out of memory";
+        case PBS_ERR_CAPACITY: return "output array too small";
+        case PBS_ERR_INVALID: return "invalid argument";
+        default: return "unknown error";
+    }
+}
+
+int pbs_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+size_t pbs_chunker_max_cuts(size_t len) { return len / 65 + 2; }
+
+pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
+    int dummy;
+    if (!err) err = &dummy;
+    Params prm;
+    if (make_params(chunk_size_avg, &prm) != PBS_OK) {
+        *err = PBS_ERR_NOT_POW2;
+        return nullptr;
+    }
+    if (pbs_device_count() <= 0) {
+        *err = PBS_ERR_NO_DEVICE;
+        return nullptr;
+    }
+    pbs_chunker* c = new (std::nothrow) pbs_chunker();
+    if (!c) {
+        *err = PBS_ERR_NOMEM;
+        return nullptr;
+    }
+    c->prm = prm;
+    bool ok = hipGetDevice(&c->device) == hipSuccess;
+    hipDeviceProp_t prop;
+    if (ok && hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->cu = prop.multiProcessorCount;
+    ok = ok && hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess;
+    c->stream = c->own_stream;
+    for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+    ok = ok && hipHostMalloc((void**)&c->h_small, 64, hipHostMallocDefault) == hipSuccess;
+    ok = ok && c->d_table.ensure(256 * 4) == hipSuccess;
+    if (ok) {
+        uint32_t t[256];
+        for (int i = 0; i < 256; ++i) t[i] = rotl32(kBuzhashTable[i], prm.rot);
+        ok = hipMemcpy(c->d_table.p, t, sizeof(t), hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (!ok) {
+        destroy(c);
+        *err = PBS_ERR_HIP;
+        return nullptr;
+    }
+    *err = PBS_OK;
+    return c;
+}
+
+void pbs_chunker_free(pbs_chunker* c) {
+    if (c) destroy(c);
+}
+
+int pbs_chunker_reset(pbs_chunker* c) {
+    if (!c) return PBS_ERR_INVALID;
+    reset_stream(c);
+    return PBS_OK;
+}
+
+int pbs_chunker_set_stream(pbs_chunker* c, void* hip_stream) {
+    if (!c) return PBS_ERR_INVALID;
+    c->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->own_stream;
+    return PBS_OK;
+}
+
+int pbs_chunker_last_error(const pbs_chunker* c) { return c ? c->last_error : PBS_ERR_INVALID; }
+
+uint64_t pbs_chunker_stream_offset(const pbs_chunker* c) { return c ? c->consumed : 0; }
+uint64_t pbs_chunker_chunk_start(const pbs_chunker* c) { return c ? c->chunk_start : 0; }
+
+int pbs_chunker_last_timing(const pbs_chunker* c, pbs_timing* t) {
+    if (!c || !t) return PBS_ERR_INVALID;
+    *t = c->timing;
+    return PBS_OK;
+}
+
+size_t pbs_chunker_scan(pbs_chunker* c, const uint8_t* data, size_t len) {
+    if (!c) return SIZE_MAX;
+    if (len && !data) {
+        fail(c, PBS_ERR_INVALID);
+        return SIZE_MAX;
+    }
+    if (hipSetDevice(c->device) != hipSuccess) {
+        fail(c, PBS_ERR_HIP);
+        return SIZE_MAX;
+    }
+    const uint64_t end = c->consumed + len;
+    if (end > c->scanned_end) {
+        c->timing = pbs_timing{};
+        uint64_t pos = c->scanned_end;
+        while (pos < end) {
+            const uint64_t bl = std::min<uint64_t>(end - pos, batch_max(c->prm));
+            const uint8_t* hsrc = data + (pos - c->consumed);
+            if (c->d_in.ensure(bl) != hipSuccess ||
+                hipMemcpyAsync(c->d_in.p, hsrc, bl, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+                fail(c, PBS_ERR_HIP);
+                return SIZE_MAX;
+            }
+            uint32_t nnew = 0;
+            if (scan_new_bytes(c, c->d_in.as<uint8_t>(), hsrc, pos, bl, 0, false, &nnew) != PBS_OK)
+                return SIZE_MAX;
+            pos += bl;
+        }
+    }
+    // shall_break (chunker.rs:172-186) over the cached candidates
+    const Params& p = c->prm;
+    const uint64_t lo = c->chunk_start + p.min_eff - 1;
+    const uint64_t hi = c->chunk_start + p.max_eff - 1;
+    while (c->pend_head < c->pending.size() && c->pending[c->pend_head] < lo) ++c->pend_head;
+    if (c->pend_head > 4096) {
+        c->pending.erase(c->pending.begin(), c->pending.begin() + (ptrdiff_t)c->pend_head);
+        c->pend_head = 0;
+    }
+    uint64_t cut = UINT64_MAX;
+    if (c->pend_head < c->pending.size() && c->pending[c->pend_head] <= hi &&
+        c->pending[c->pend_head] < end)
+        cut = c->pending[c->pend_head];
+    else if (hi < end)
+        cut = hi;
+    if (cut == UINT64_MAX) {
+        c->consumed = end;
+        return 0;
+    }
+    const size_t ret = (size_t)(cut + 1 - c->consumed);
+    c->consumed = c->chunk_start = cut + 1;
+    return ret;
+}
+
+int pbs_chunker_find_cuts(pbs_chunker* c, const uint8_t* data, size_t len, int is_final,
+                          uint64_t* out, size_t cap, size_t* n_out) {
+    return find_cuts_impl(c, data, len, is_final, out, cap, n_out, false);
+}
+
+int pbs_chunker_find_cuts_device(pbs_chunker* c, const uint8_t* dev_data, size_t len,
+                                 int is_final, uint64_t* out, size_t cap, size_t* n_out) {
+    return find_cuts_impl(c, dev_data, len, is_final, out, cap, n_out, true);
+}
+
+int pbs_candidates_host(const uint8_t* data, size_t len, size_t avg, uint64_t* out, size_t cap,
+                        size_t* n_out) {
+    if (!n_out || (len && !data)) return PBS_ERR_INVALID;
+    int err = 0;
+    pbs_chunker* c = pbs_chunker_new(avg, &err);
+    if (!c) return err;
+    int rc = PBS_OK;
+    uint32_t n = 0;
+    if (len) {
+        if (c->d_in.ensure(len) != hipSuccess ||
+            hipMemcpyAsync(c->d_in.p, data, len, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            rc = PBS_ERR_HIP;
+        if (!rc) rc = scan_candidates(c, c->d_in.as<uint8_t>(), len, 0, &n);
+        if (!rc && n > cap) rc = PBS_ERR_CAPACITY;
+        if (!rc && n) {
+            if (c->d_C.ensure((size_t)n * 8) != hipSuccess) rc = PBS_ERR_HIP;
+            if (!rc) rc = sort_candidates(c, n, c->d_C.as<uint64_t>());
+            if (!rc && (hipMemcpyAsync(out, c->d_C.p, (size_t)n * 8, hipMemcpyDeviceToHost,
+                                       c->stream) != hipSuccess ||
+                        hipStreamSynchronize(c->stream) != hipSuccess))
+                rc = PBS_ERR_HIP;
+        }
+    }
+    *n_out = n;
+    pbs_chunker_free(c);
+    return rc;
+}
+
+int pbs_generate_device(uint8_t* dev, size_t len, int kind, uint64_t seed, uint64_t offset,
+                        void* hip_stream) {
+    if ((len & 7) || (offset & 7) || (len && !dev)) return PBS_ERR_INVALID;
+    if (kind < kGenCounter || kind > kGenVmImage) return PBS_ERR_INVALID;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (launch_gen(reinterpret_cast<uint64_t*>(dev), len / 8, seed, offset / 8, kind, s) !=
+        hipSuccess)
+        return PBS_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return PBS_ERR_HIP;
+    return PBS_OK;
+}
+
+int pbs_table_copy(uint32_t* out256) {
+    if (!out256) return PBS_ERR_INVALID;
+    std::memcpy(out256, kBuzhashTable, sizeof(kBuzhashTable));
+    return PBS_OK;
+}
+
+}  // extern "C"

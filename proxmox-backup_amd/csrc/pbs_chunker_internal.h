@@ -1,0 +1,50 @@
+// Internal declarations shared by the kernels TU and the C-ABI/host pipeline TU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbs {
+
+// Bytes of one lane's segment in scan_main_kernel (a wave tile = 64 segments).
+// 16 KiB keeps the 128-byte warm-up per segment at 0.8 % of the work and of the
+// HBM traffic; a wave tile is 1 MiB.
+constexpr int kSegBytes = 16384;
+constexpr uint64_t kWaveTileBytes = 64ull * kSegBytes;
+constexpr uint64_t kBlockBytes = 128;  // exact-evaluation granule (one lane iteration)
+
+// generator kinds (see oracle/chunker_oracle.c; bytes must match)
+constexpr int kGenCounter = 0;
+constexpr int kGenRandom = 1;
+constexpr int kGenVmImage = 2;
+constexpr uint64_t kVmSeedPage = 0x7A65726F50414745ull;
+constexpr uint64_t kVmSeedWord = 0x52414E44574F5244ull;
+constexpr uint64_t kVmSeedExt = 0x4558544E54000000ull;
+
+struct ResolveParams {
+    uint64_t min_eff;  // max(avg/4, 65): first length at which a hash cut may happen
+    uint64_t max_eff;  // max(avg*4, 65): forced cut length
+    uint64_t end;      // absolute end of the bytes known so far (exclusive)
+    uint64_t s0;       // absolute start of the open chunk
+};
+
+hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, const uint32_t* table_rot,
+                            uint32_t thr, uint64_t* susp, uint32_t* nsusp, uint32_t cap,
+                            int grid, hipStream_t stream);
+hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
+                             uint32_t pre_len, const uint64_t* susp, const uint32_t* nsusp,
+                             uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head,
+                             uint32_t mask, uint32_t minimum, uint64_t base, uint64_t* cand,
+                             uint32_t* ncand, uint32_t cand_cap, uint64_t max_items,
+                             hipStream_t stream);
+hipError_t sort_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
+                    hipStream_t stream);
+hipError_t exclusive_sum_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
+                             uint32_t n, hipStream_t stream);
+hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p, uint32_t* nxt,
+                          uint32_t* jtmp, uint64_t* nforced, uint32_t* on, uint64_t* cnt,
+                          uint64_t* off, void* scan_tmp, size_t scan_tmp_bytes, uint64_t* out,
+                          uint64_t out_cap, uint64_t* res, hipStream_t stream);
+hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,
+                      int kind, hipStream_t stream);
+
+}  // namespace pbs

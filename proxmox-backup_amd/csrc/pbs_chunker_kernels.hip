@@ -1,0 +1,480 @@
+// HIP kernels of the MI355X (gfx950) content-defined chunker.
+//
+// Reference semantics: pbs-datastore/src/chunker.rs:112-186 (Chunker::scan / shall_break).
+// The reference rolls one 32-bit Buzhash over the stream byte by byte.  This file
+// computes the same cut boundaries in two phases (DESIGN.md "Algorithm"):
+//
+//   Phase A  (scan_main_kernel + scan_exact_kernel): the hash test
+//            (h & mask) >= mask-2 (chunker.rs:185) at EVERY stream position p >= 63.
+//            Once the 64-byte window is full, h at p is a pure function of the 64
+//            bytes ending at p (rotl by 64 = identity, chunker.rs:146), so positions
+//            are independent and are evaluated in parallel: each lane rolls the
+//            hash over its own contiguous segment after a 128-byte warm-up.
+//   Phase B  (resolve_* kernels): the min/max chunk-size rule (chunker.rs:172-183)
+//            applied to the sorted candidate list.  The chain of cuts is a pointer
+//            chain over candidates (next[j] = the cut taken after a cut at candidate
+//            j); the nodes on the chain from the stream start are marked by pointer
+//            doubling, then emitted with an exclusive scan.
+//
+// No MFMA: this is a byte scan bound by HBM bandwidth.  The per-byte work is one
+// v_perm_b32 (LDS address), one ds_read_b32 (replicated table), one v_alignbit_b32
+// (rotl 1), one v_bitop3_b32 (3-input XOR; gfx950 has no v_xor3_b32) and half a
+// v_max3_u32.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "buzhash_table.h"
+#include "pbs_chunker_internal.h"
+
+namespace pbs {
+
+// ---------------------------------------------------------------------------------
+// Phase A, main kernel
+// ---------------------------------------------------------------------------------
+// Geometry.  One workgroup of 8 waves per CU (persistent).  A wave owns a "wave tile"
+// of 64 contiguous segments of SEG bytes; lane l rolls the hash over segment l.  Each
+// iteration every lane consumes 128 bytes of its segment; the wave stages the
+// 64 x 128-byte block (8 KiB) through LDS with 8 LDS-DMA instructions
+// (global_load_lds_dwordx4), each covering 8 full 128-byte lines.
+//
+// LDS (128 KiB per workgroup):
+//   table  [0, 64 KiB):  T'[b] replicated 64x, byte address b*256 + lane*4, so a
+//                        wave64 ds_read_b32 of random bytes is bank-conflict-free
+//                        (bank = lane mod 32) and the address is ONE v_perm_b32.
+//   stage  [64, 128 KiB): 8 KiB per wave.  Chunk k (16 B) of lane l's 128-byte block
+//                        sits at l*128 + ((k ^ ((l>>1)&7)) * 16): the XOR swizzle
+//                        makes the per-lane ds_read_b128 conflict-free.
+//
+// Hash representation.  h' = rotl(h, rot) with rot = 32 - popcount(mask), so the
+// mask bits sit at the top of the word and the test (h & mask) >= mask-2 becomes
+// the unsigned compare h' >= thr, thr = (mask-2) << rot.  Rotation commutes with
+// the recurrence, so the table is pre-rotated: T'[b] = rotl(T[b], rot).  The max
+// over a 128-byte block (v_max3_u32) flags the rare blocks that hold a candidate;
+// those blocks are re-evaluated exactly by scan_exact_kernel.
+
+constexpr int kWavesPerWG = 8;
+constexpr int kThreadsMain = kWavesPerWG * 64;
+constexpr int kIter = 128;                       // bytes per lane per iteration
+constexpr int kStagePerWave = 64 * kIter;        // 8 KiB
+constexpr int kTableDwords = 256 * 64;           // 64 KiB
+
+__device__ __forceinline__ uint32_t rotl1(uint32_t h) {
+    return __builtin_amdgcn_alignbit(h, h, 31);
+}
+__device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t m = a > b ? a : b;
+    return m > c ? m : c;
+}
+
+// One 128-byte step of the rolling hash for this lane.  `ring` holds T' of the last
+// 64 bytes (the "leave" values); the unrolled body indexes it statically, so it lives
+// in 64 VGPRs.  Returns the max of h' over the 128 positions.
+__device__ __forceinline__ uint32_t roll128(const uint4 (&d)[8], uint32_t (&ring)[64],
+                                            uint32_t& h, const uint32_t* s_tab,
+                                            uint32_t lanebase) {
+    uint32_t acc = 0, hp = 0;
+#pragma unroll
+    for (int i = 0; i < 128; ++i) {
+        const uint4 q = d[i >> 4];
+        const int wi = (i >> 2) & 3;
+        const uint32_t w = wi == 0 ? q.x : (wi == 1 ? q.y : (wi == 2 ? q.z : q.w));
+        // bytes of {w, lanebase}: result = [0, 0, byte (i&3) of w, lane*4]
+        const uint32_t sel = 0x0c0c0000u | ((4u + (uint32_t)(i & 3)) << 8);
+        const uint32_t a = __builtin_amdgcn_perm(w, lanebase, sel);
+        const uint32_t t = *(const uint32_t*)((const char*)s_tab + a);
+        h = __builtin_amdgcn_bitop3_b32(rotl1(h), ring[i & 63], t, 0x96);  // v_bitop3 xor3
+        ring[i & 63] = t;
+        if (i & 1)
+            acc = umax3(acc, hp, h);
+        else
+            hp = h;
+    }
+    return acc;
+}
+
+template <int SEG>
+__global__ __launch_bounds__(kThreadsMain, 2) void scan_main_kernel(
+    const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
+    uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {
+    static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
+    __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + kWavesPerWG * kStagePerWave / 4];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    uint32_t* s_tab = s_lds;
+    for (int i = tid; i < kTableDwords; i += kThreadsMain) s_tab[i] = table_rot[i >> 6];
+    __syncthreads();
+
+    uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
+    const uint32_t lanebase = (uint32_t)lane * 4u;
+
+    // LDS-DMA instruction j, lane i stages chunk k of segment l = 8j + (i>>3) with
+    // k = (i & 7) ^ ((l >> 1) & 7), so the linear LDS destination j*1024 + i*16 equals
+    // the swizzled slot l*128 + ((k ^ ((l>>1)&7)) * 16).
+    uint32_t dma_off[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t l = 8u * j + ((uint32_t)lane >> 3);
+        const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
+        dma_off[j] = l * (uint32_t)SEG + k * 16u;
+    }
+    const uint32_t rd_base = (uint32_t)lane * 128u;
+    const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
+
+    constexpr int NIT = SEG / kIter + 1;  // iteration 0 is the warm-up block [-128, 0)
+    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
+    uint64_t tile = (uint64_t)blockIdx.x * kWavesPerWG + wave;
+    if (tile >= ntiles) return;
+
+    auto issue = [&](uint64_t t, int it) {
+        const uint8_t* tb = data + t * (64ull * SEG);
+        const int32_t boff = (it - 1) * kIter;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            int32_t off = (int32_t)dma_off[j] + boff;
+            // Only segment 0 of the stream has no bytes before it: read any valid
+            // bytes there, its warm-up state is discarded below.
+            if (t == 0 && off < 0) off = 0;
+            __builtin_amdgcn_global_load_lds(
+                (const void __attribute__((address_space(1)))*)(tb + off),
+                (void __attribute__((address_space(3)))*)(stage + j * 1024), 16, 0, 0);
+        }
+    };
+
+    uint32_t ring[64];
+    uint32_t h = 0;
+    issue(tile, 0);
+    for (;;) {
+        for (int it = 0; it < NIT; ++it) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint4 d[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                d[k] = *(const uint4*)(stage + rd_base + (((uint32_t)k ^ rsw) << 4));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // prefetch the next block of this wave (next iteration or next tile)
+            {
+                uint64_t nt = tile;
+                int nit = it + 1;
+                if (nit == NIT) {
+                    nt = tile + nw;
+                    nit = 0;
+                }
+                if (nt < ntiles) issue(nt, nit);
+            }
+            if (it == 0) {
+                h = 0;
+#pragma unroll
+                for (int r = 0; r < 64; ++r) ring[r] = 0;
+            }
+            const uint32_t acc = roll128(d, ring, h, s_tab, lanebase);
+            if (it == 0) {
+                if (tile == 0 && lane == 0) {  // stream segment 0: no warm-up bytes
+                    h = 0;
+#pragma unroll
+                    for (int r = 0; r < 64; ++r) ring[r] = 0;
+                }
+            } else if (acc >= thr) {
+                const uint64_t pos =
+                    (tile * 64ull + (uint64_t)lane) * (uint64_t)SEG + (uint64_t)(it - 1) * kIter;
+                // block 0 is always re-evaluated by scan_exact_kernel (the `pre` bytes)
+                if (pos != 0) {
+                    const uint32_t idx = atomicAdd(nsusp, 1u);
+                    if (idx < cap) susp[idx] = pos;
+                }
+            }
+        }
+        tile += nw;
+        if (tile >= ntiles) break;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Phase A, exact evaluation of 128-byte blocks (suspect blocks, stream head, tail)
+// ---------------------------------------------------------------------------------
+// Bytes before data[0] come from `pre` (the last pre_len <= 63 bytes of the stream
+// before this buffer); bytes before that do not exist and contribute nothing, as in
+// the reference's fill phase.  Position p is a candidate iff the window is full
+// (p + pre_len >= 63) and (H(p) & mask) >= minimum; it is written as base + p.
+__global__ __launch_bounds__(256) void scan_exact_kernel(
+    const uint8_t* __restrict__ data, uint64_t len, const uint8_t* __restrict__ pre,
+    uint32_t pre_len, const uint64_t* __restrict__ susp, const uint32_t* __restrict__ nsusp,
+    uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head, uint32_t mask,
+    uint32_t minimum, uint64_t base, uint64_t* __restrict__ cand, uint32_t* __restrict__ ncand,
+    uint32_t cand_cap) {
+    __shared__ uint32_t tab[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = kBuzhashTable[i];
+    __syncthreads();
+    const uint32_t ns0 = nsusp ? *nsusp : 0u;
+    const uint64_t ns = ns0 < susp_cap ? ns0 : susp_cap;
+    const uint64_t total = ns + (uint64_t)(head ? 1 : 0) + ext_count;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += stride) {
+        uint64_t B;
+        if (w < ns)
+            B = susp[w];
+        else if (head && w == ns)
+            B = 0;
+        else
+            B = (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
+        const uint64_t end = B + kIter < len ? B + kIter : len;
+        uint32_t h = 0;
+        const int64_t q0 = (int64_t)B - 64;
+        for (int64_t q = q0; q < (int64_t)end; ++q) {
+            uint32_t tin = 0, tout = 0;
+            if (q >= 0)
+                tin = tab[data[q]];
+            else if (q >= -(int64_t)pre_len)
+                tin = tab[pre[pre_len + q]];
+            const int64_t r = q - 64;
+            if (r >= q0) {
+                if (r >= 0)
+                    tout = tab[data[r]];
+                else if (r >= -(int64_t)pre_len)
+                    tout = tab[pre[pre_len + r]];
+            }
+            h = ((h << 1) | (h >> 31)) ^ tin ^ tout;
+            if (q >= (int64_t)B && q + (int64_t)pre_len >= 63 && (h & mask) >= minimum) {
+                const uint32_t idx = atomicAdd(ncand, 1u);
+                if (idx < cand_cap) cand[idx] = base + (uint64_t)q;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Phase B: resolve the min/max rule over the sorted candidate list
+// ---------------------------------------------------------------------------------
+// Node j < m: "a cut was taken at candidate C[j]" (next chunk starts at C[j]+1).
+// Node m: the stream/buffer state (chunk starts at s0).  Node m+1: sink ("undecided":
+// the open chunk needs bytes beyond `end`).
+__device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t* __restrict__ C, uint32_t lo,
+                                                    uint32_t hi, uint64_t key) {
+    // galloping from lo, then binary search
+    uint32_t step = 1, prev = lo;
+    uint32_t cur = lo;
+    while (cur < hi && C[cur] < key) {
+        prev = cur + 1;
+        cur = lo + step;
+        step <<= 1;
+        if (cur > hi) cur = hi;
+    }
+    uint32_t a = prev, b = cur;
+    while (a < b) {
+        const uint32_t mid = a + ((b - a) >> 1);
+        if (C[mid] < key)
+            a = mid + 1;
+        else
+            b = mid;
+    }
+    return a;
+}
+
+__global__ __launch_bounds__(256) void resolve_next_kernel(const uint64_t* __restrict__ C,
+                                                           uint32_t m, ResolveParams p,
+                                                           uint32_t* __restrict__ nxt,
+                                                           uint64_t* __restrict__ nforced,
+                                                           uint32_t* __restrict__ on) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t none = m + 1;
+    if (j > m + 1) return;
+    if (j == m + 1) {
+        nxt[j] = none;
+        nforced[j] = 0;
+        on[j] = 0;
+        return;
+    }
+    uint64_t s = (j == m) ? p.s0 : C[j] + 1;
+    uint32_t i = (j == m) ? 0u : j + 1;
+    uint64_t nf = 0;
+    uint32_t res = none;
+    for (;;) {
+        const uint64_t lo = s + p.min_eff - 1, hi = s + p.max_eff - 1;
+        i = lower_bound_u64(C, i, m, lo);
+        if (i < m && C[i] <= hi) {
+            res = i;
+            break;
+        }
+        if (hi >= p.end) break;  // undecided: needs bytes beyond `end`
+        uint64_t k;
+        if (i < m) {
+            k = (C[i] - hi + p.max_eff - 1) / p.max_eff;  // forced cuts before C[i] fits
+        } else {
+            k = (p.end - s) / p.max_eff;  // forced cuts until the data ends
+            nf += k;
+            s += k * p.max_eff;
+            break;
+        }
+        nf += k;
+        s += k * p.max_eff;
+    }
+    nxt[j] = res;
+    nforced[j] = nf;
+    on[j] = (j == m) ? 1u : 0u;
+}
+
+// One pointer-doubling round: J_{t+1} = J_t o J_t, and every marked node marks its
+// 2^t-th successor.  Races on `on` are benign (marks only ever go 0 -> 1, and any
+// node marked is on the chain).
+__global__ __launch_bounds__(256) void resolve_double_kernel(uint32_t n, const uint32_t* __restrict__ jin,
+                                                             uint32_t* __restrict__ jout,
+                                                             uint32_t* on) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t J = jin[j];
+    if (on[j]) on[J] = 1u;
+    jout[j] = jin[J];
+}
+
+__global__ __launch_bounds__(256) void resolve_count_kernel(uint32_t m, const uint32_t* __restrict__ nxt,
+                                                            const uint64_t* __restrict__ nforced,
+                                                            const uint32_t* __restrict__ on,
+                                                            uint64_t* __restrict__ cnt) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > m) return;  // nodes 0..m
+    cnt[j] = on[j] ? nforced[j] + (nxt[j] != m + 1 ? 1u : 0u) : 0u;
+}
+
+// out[] = chunk END offsets (absolute, exclusive).  res[0] = number of cuts,
+// res[1] = start of the open (undecided) chunk, res[2] = index of the first
+// candidate >= res[1].
+__global__ __launch_bounds__(256) void resolve_emit_kernel(
+    const uint64_t* __restrict__ C, uint32_t m, ResolveParams p, const uint32_t* __restrict__ nxt,
+    const uint64_t* __restrict__ nforced, const uint32_t* __restrict__ on,
+    const uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off, uint64_t* __restrict__ out,
+    uint64_t out_cap, uint64_t* __restrict__ res) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > m || !on[j]) return;
+    const uint64_t s = (j == m) ? p.s0 : C[j] + 1;
+    const uint64_t o = off[j];
+    const uint64_t nf = nforced[j];
+    for (uint64_t t = 0; t < nf; ++t)
+        if (o + t < out_cap) out[o + t] = s + (t + 1) * p.max_eff;
+    if (nxt[j] != m + 1) {
+        if (o + nf < out_cap) out[o + nf] = C[nxt[j]] + 1;
+    } else {
+        const uint64_t s_open = s + nf * p.max_eff;
+        res[0] = o + cnt[j];
+        res[1] = s_open;
+        res[2] = lower_bound_u64(C, 0, m, s_open);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Synthetic stream generator (bench / tests; same bytes as oracle/chunker_oracle.c)
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void gen_kernel(uint64_t* __restrict__ out, uint64_t nwords,
+                                                  uint64_t seed, uint64_t word_offset, int kind) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += stride) {
+        const uint64_t gw = word_offset + w;  // global word index
+        uint64_t v;
+        if (kind == kGenCounter) {
+            const uint32_t i0 = (uint32_t)(2 * gw), i1 = (uint32_t)(2 * gw + 1);
+            v = (uint64_t)i0 | ((uint64_t)i1 << 32);
+        } else if (kind == kGenRandom) {
+            v = splitmix64(seed ^ gw);
+        } else {
+            const uint64_t x = gw << 3;
+            const uint64_t g = x >> 30;
+            const uint64_t ext = (splitmix64(seed ^ kVmSeedExt ^ g) & 15u) << 26;
+            const uint64_t in_g = x & ((1ull << 30) - 1);
+            if (in_g >= ext && in_g < ext + (1ull << 26))
+                v = 0;
+            else if (splitmix64(seed ^ kVmSeedPage ^ (x >> 12)) % 100u < 40u)
+                v = 0;
+            else
+                v = splitmix64(seed ^ kVmSeedWord ^ gw);
+        }
+        out[w] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Host-side launchers (called from pbs_chunker_capi.cpp)
+// ---------------------------------------------------------------------------------
+hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, const uint32_t* table_rot,
+                            uint32_t thr, uint64_t* susp, uint32_t* nsusp, uint32_t cap,
+                            int grid, hipStream_t stream) {
+    if (ntiles == 0) return hipSuccess;
+    const uint64_t need = (ntiles + kWavesPerWG - 1) / kWavesPerWG;
+    const int g = (uint64_t)grid < need ? grid : (int)need;
+    hipLaunchKernelGGL(scan_main_kernel<kSegBytes>, dim3(g), dim3(kThreadsMain), 0, stream, data,
+                       ntiles, table_rot, thr, susp, nsusp, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
+                             uint32_t pre_len, const uint64_t* susp, const uint32_t* nsusp,
+                             uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head,
+                             uint32_t mask, uint32_t minimum, uint64_t base, uint64_t* cand,
+                             uint32_t* ncand, uint32_t cand_cap, uint64_t max_items,
+                             hipStream_t stream) {
+    uint64_t blocks = (max_items + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(scan_exact_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, data, len,
+                       pre, pre_len, susp, nsusp, susp_cap, ext_first, ext_count, head, mask,
+                       minimum, base, cand, ncand, cand_cap);
+    return hipGetLastError();
+}
+
+hipError_t sort_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
+                    hipStream_t stream) {
+    return hipcub::DeviceRadixSort::SortKeys(tmp, *tmp_bytes, in, out, (int)n, 0, 64, stream);
+}
+
+hipError_t exclusive_sum_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
+                             uint32_t n, hipStream_t stream) {
+    return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, stream);
+}
+
+hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p, uint32_t* nxt,
+                          uint32_t* jtmp, uint64_t* nforced, uint32_t* on, uint64_t* cnt,
+                          uint64_t* off, void* scan_tmp, size_t scan_tmp_bytes, uint64_t* out,
+                          uint64_t out_cap, uint64_t* res, hipStream_t stream) {
+    const uint32_t n = m + 2;
+    const unsigned blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(resolve_next_kernel, dim3(blocks), dim3(256), 0, stream, C, m, p, nxt,
+                       nforced, on);
+    // pointer doubling over copies of nxt (nxt itself is kept for emission)
+    hipError_t e = hipMemcpyAsync(jtmp, nxt, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, stream);
+    if (e != hipSuccess) return e;
+    uint32_t* ja = jtmp;
+    uint32_t* jb = jtmp + n;
+    for (uint32_t span = 1; span < n; span <<= 1) {
+        hipLaunchKernelGGL(resolve_double_kernel, dim3(blocks), dim3(256), 0, stream, n, ja, jb, on);
+        uint32_t* t = ja;
+        ja = jb;
+        jb = t;
+    }
+    hipLaunchKernelGGL(resolve_count_kernel, dim3(blocks), dim3(256), 0, stream, m, nxt, nforced,
+                       on, cnt);
+    size_t tb = scan_tmp_bytes;
+    e = exclusive_sum_u64(scan_tmp, &tb, cnt, off, m + 1, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(resolve_emit_kernel, dim3(blocks), dim3(256), 0, stream, C, m, p, nxt,
+                       nforced, on, cnt, off, out, out_cap, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,
+                      int kind, hipStream_t stream) {
+    uint64_t blocks = (nwords + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(gen_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, out, nwords,
+                       seed, word_offset, kind);
+    return hipGetLastError();
+}
+
+}  // namespace pbs

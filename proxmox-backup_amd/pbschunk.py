@@ -1,0 +1,337 @@
+"""Python host mirror of proxmox-backup's chunker interface over the C ABI
+(include/pbs_chunker.h, built as proxmox-backup_amd/csrc/libpbschunk.so).
+
+Mirrors, with the same names, argument meaning and error behaviour:
+  * ``Chunker(chunk_size_avg)`` / ``Chunker.scan(data) -> int``
+      pbs-datastore/src/chunker.rs:75-106 and :112-168.  A non-power-of-two average
+      raises (the reference panics: "got unexpected chunk size - not a power of two.").
+  * ``ChunkStream(input, chunk_size=None)`` -- iterator of chunks (bytes)
+      pbs-client/src/chunk_stream.rs:12-78 (default average 4 MiB, tail emitted at EOF).
+  * ``DynamicChunkWriter(sink, chunk_size)`` -- ``write(data) -> consumed`` / ``close()``
+      pbs-datastore/src/dynamic_index.rs:397-523, with the digest/compress/index step
+      replaced by a callback ``sink(chunk_end_offset, chunk_bytes)``.
+
+The hash scan always runs on the GPU through the HIP library; there is no CPU path.
+Loading fails loudly (``ChunkerLibraryError``) when the library is missing and handle
+creation fails when no HIP device is visible.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Callable, Iterable, Iterator, Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "csrc", "libpbschunk.so")
+
+PBS_OK = 0
+PBS_ERR_NOT_POW2 = -1
+PBS_ERR_NO_DEVICE = -2
+PBS_ERR_HIP = -3
+PBS_ERR_NOMEM = -4
+PBS_ERR_CAPACITY = -5
+PBS_ERR_INVALID = -6
+
+GEN_COUNTER, GEN_RANDOM, GEN_VMIMAGE = 0, 1, 2
+
+EXPORTED_SYMBOLS = (
+    "pbs_chunker_new", "pbs_chunker_free", "pbs_chunker_scan", "pbs_chunker_find_cuts",
+    "pbs_chunker_find_cuts_device", "pbs_chunker_max_cuts", "pbs_chunker_stream_offset",
+    "pbs_chunker_chunk_start", "pbs_chunker_reset", "pbs_chunker_set_stream",
+    "pbs_chunker_last_error", "pbs_strerror", "pbs_chunker_last_timing",
+    "pbs_candidates_host", "pbs_generate_device", "pbs_device_count", "pbs_table_copy",
+)
+
+
+class ChunkerLibraryError(RuntimeError):
+    pass
+
+
+class ChunkerError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what}: {strerror(code)} ({code})" if what else f"{strerror(code)} ({code})")
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [
+        ("scan_ms", ctypes.c_float), ("exact_ms", ctypes.c_float),
+        ("resolve_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
+        ("bytes", ctypes.c_uint64), ("suspects", ctypes.c_uint64),
+        ("candidates", ctypes.c_uint64), ("cuts", ctypes.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """Load libpbschunk.so (no fallback: raises if it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # torch wheels bundle their own libamdhip64.so.7; load it first so this library
+    # binds to the same HIP runtime instead of a second copy from /opt/rocm.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ChunkerLibraryError(
+            f"{LIB_PATH} not built; run `make -C proxmox-backup_amd/csrc` or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    p, u64, sz, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int
+    sig = {
+        "pbs_chunker_new": ([sz, ctypes.POINTER(i)], p),
+        "pbs_chunker_free": ([p], None),
+        "pbs_chunker_scan": ([p, p, sz], sz),
+        "pbs_chunker_find_cuts": ([p, p, sz, i, p, sz, ctypes.POINTER(sz)], i),
+        "pbs_chunker_find_cuts_device": ([p, p, sz, i, p, sz, ctypes.POINTER(sz)], i),
+        "pbs_chunker_max_cuts": ([sz], sz),
+        "pbs_chunker_stream_offset": ([p], u64),
+        "pbs_chunker_chunk_start": ([p], u64),
+        "pbs_chunker_reset": ([p], i),
+        "pbs_chunker_set_stream": ([p, p], i),
+        "pbs_chunker_last_error": ([p], i),
+        "pbs_strerror": ([i], ctypes.c_char_p),
+        "pbs_chunker_last_timing": ([p, ctypes.POINTER(Timing)], i),
+        "pbs_candidates_host": ([p, sz, sz, p, sz, ctypes.POINTER(sz)], i),
+        "pbs_generate_device": ([p, sz, i, u64, u64, p], i),
+        "pbs_device_count": ([], i),
+        "pbs_table_copy": ([p], i),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def strerror(code: int) -> str:
+    return lib().pbs_strerror(code).decode()
+
+
+def device_count() -> int:
+    return int(lib().pbs_device_count())
+
+
+def table() -> np.ndarray:
+    t = np.empty(256, dtype=np.uint32)
+    lib().pbs_table_copy(t.ctypes.data)
+    return t
+
+
+def max_cuts(length: int) -> int:
+    return int(lib().pbs_chunker_max_cuts(length))
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+
+
+def _ptr(a: np.ndarray) -> Optional[int]:
+    return a.ctypes.data if a.size else None
+
+
+class Chunker:
+    """`pbs_datastore::Chunker` (chunker.rs:18) backed by the gfx950 kernels."""
+
+    def __init__(self, chunk_size_avg: int):
+        L = lib()
+        err = ctypes.c_int(0)
+        h = L.pbs_chunker_new(int(chunk_size_avg), ctypes.byref(err))
+        if not h:
+            if err.value == PBS_ERR_NOT_POW2:
+                # the reference panics here (chunker.rs:87-89)
+                raise ValueError("got unexpected chunk size - not a power of two.")
+            raise ChunkerError(err.value, "pbs_chunker_new")
+        self._h = ctypes.c_void_p(h)
+        self.chunk_size_avg = int(chunk_size_avg)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pbs_chunker_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != PBS_OK:
+            raise ChunkerError(rc, what)
+
+    def scan(self, data) -> int:
+        """chunker.rs:112 -- 0 (no boundary, slice consumed) or the position after the cut."""
+        a = _as_u8(data)
+        r = lib().pbs_chunker_scan(self._h, _ptr(a), a.size)
+        if r == ctypes.c_size_t(-1).value:
+            raise ChunkerError(lib().pbs_chunker_last_error(self._h), "pbs_chunker_scan")
+        return int(r)
+
+    def find_cuts(self, data, is_final: bool = False) -> np.ndarray:
+        """Chunk END offsets (absolute) of every cut decided inside ``data``."""
+        a = _as_u8(data)
+        cap = max_cuts(a.size)
+        out = np.empty(cap, dtype=np.uint64)
+        n = ctypes.c_size_t(0)
+        rc = lib().pbs_chunker_find_cuts(self._h, _ptr(a), a.size, int(bool(is_final)),
+                                        out.ctypes.data, cap, ctypes.byref(n))
+        self._check(rc, "pbs_chunker_find_cuts")
+        return out[: n.value].copy()
+
+    def find_cuts_device(self, dev_ptr: int, length: int, is_final: bool = False) -> np.ndarray:
+        """Same over a device (HBM) buffer, e.g. ``tensor.data_ptr()``."""
+        cap = max_cuts(length)
+        out = np.empty(cap, dtype=np.uint64)
+        n = ctypes.c_size_t(0)
+        rc = lib().pbs_chunker_find_cuts_device(self._h, ctypes.c_void_p(dev_ptr), length,
+                                               int(bool(is_final)), out.ctypes.data, cap,
+                                               ctypes.byref(n))
+        self._check(rc, "pbs_chunker_find_cuts_device")
+        return out[: n.value].copy()
+
+    def set_stream(self, hip_stream: int):
+        self._check(lib().pbs_chunker_set_stream(self._h, ctypes.c_void_p(hip_stream)),
+                    "pbs_chunker_set_stream")
+
+    def reset(self):
+        self._check(lib().pbs_chunker_reset(self._h), "pbs_chunker_reset")
+
+    @property
+    def stream_offset(self) -> int:
+        return int(lib().pbs_chunker_stream_offset(self._h))
+
+    @property
+    def chunk_start(self) -> int:
+        return int(lib().pbs_chunker_chunk_start(self._h))
+
+    def last_timing(self) -> dict:
+        t = Timing()
+        self._check(lib().pbs_chunker_last_timing(self._h, ctypes.byref(t)), "last_timing")
+        return t.as_dict()
+
+
+class ChunkStream:
+    """pbs-client/src/chunk_stream.rs:12-78: split an iterable of byte pieces into
+    dynamic-size chunks (yields ``bytes``); the remainder is emitted at EOF."""
+
+    def __init__(self, input: Iterable, chunk_size: Optional[int] = None):
+        self.input = iter(input)
+        self.chunker = Chunker(chunk_size if chunk_size is not None else 4 * 1024 * 1024)
+        self.buffer = bytearray()
+        self.scan_pos = 0
+
+    def __iter__(self) -> Iterator[bytes]:
+        return self
+
+    def __next__(self) -> bytes:
+        while True:
+            if self.scan_pos < len(self.buffer):
+                boundary = self.chunker.scan(memoryview(self.buffer)[self.scan_pos:])
+                chunk_size = self.scan_pos + boundary
+                if boundary == 0:
+                    self.scan_pos = len(self.buffer)
+                elif chunk_size <= len(self.buffer):
+                    result = bytes(self.buffer[:chunk_size])
+                    del self.buffer[:chunk_size]
+                    self.scan_pos = 0
+                    return result
+                else:
+                    raise RuntimeError("got unexpected chunk boundary from chunker")
+            try:
+                data = next(self.input)
+            except StopIteration:
+                self.scan_pos = 0
+                if self.buffer:
+                    result = bytes(self.buffer)
+                    self.buffer = bytearray()
+                    return result
+                raise
+            self.buffer += bytes(data)
+
+
+class DynamicChunkWriter:
+    """dynamic_index.rs:397-523 Write adapter: ``write`` returns the bytes consumed
+    (re-submit the rest, as ``write_all`` does); ``close`` flushes the tail.  Each
+    finished chunk goes to ``sink(chunk_end_offset, chunk_bytes)``."""
+
+    def __init__(self, sink: Callable[[int, bytes], None], chunk_size: int):
+        self.sink = sink
+        self.chunker = Chunker(chunk_size)
+        self.chunk_offset = 0
+        self.last_chunk = 0
+        self.chunk_buffer = bytearray()
+        self.closed = False
+        self.chunk_count = 0
+
+    def _write_chunk_buffer(self):
+        if not self.chunk_buffer:
+            return
+        expected = self.chunk_offset - self.last_chunk
+        if expected != len(self.chunk_buffer):
+            raise RuntimeError(f"wrong chunk size {expected} != {len(self.chunk_buffer)}")
+        self.chunk_count += 1
+        self.last_chunk = self.chunk_offset
+        self.sink(self.chunk_offset, bytes(self.chunk_buffer))
+        self.chunk_buffer = bytearray()
+
+    def write(self, data) -> int:
+        mv = memoryview(data).cast("B")
+        pos = self.chunker.scan(mv)
+        if pos > 0:
+            self.chunk_buffer += mv[:pos]
+            self.chunk_offset += pos
+            self._write_chunk_buffer()
+            return pos
+        self.chunk_offset += len(mv)
+        self.chunk_buffer += mv
+        return len(mv)
+
+    def write_all(self, data):
+        mv = memoryview(data).cast("B")
+        while len(mv):
+            k = self.write(mv)
+            mv = mv[k:]
+
+    def close(self):
+        if self.closed:
+            return
+        self.closed = True
+        self._write_chunk_buffer()
+
+
+def candidates_host(data, avg: int) -> np.ndarray:
+    """Phase-A hook: positions p >= 63 whose window hash passes the cut test (GPU)."""
+    a = _as_u8(data)
+    cap = max(16, a.size)
+    out = np.empty(cap, dtype=np.uint64)
+    n = ctypes.c_size_t(0)
+    rc = lib().pbs_candidates_host(_ptr(a), a.size, int(avg), out.ctypes.data, cap, ctypes.byref(n))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_candidates_host")
+    return out[: n.value].copy()
+
+
+def generate_device(dev_ptr: int, length: int, kind: int, seed: int, offset: int = 0,
+                    hip_stream: int = 0):
+    rc = lib().pbs_generate_device(ctypes.c_void_p(dev_ptr), length, kind, seed & (2**64 - 1),
+                                   offset, ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_generate_device")

@@ -1,0 +1,101 @@
+"""CPU-only checks of the C-ABI library (no compute calls): it loads, exports every
+symbol include/pbs_chunker.h declares, carries the right table, and fails loudly
+without a device.  Plus the Python host mirror's caller logic (ChunkStream,
+DynamicChunkWriter) driven by the oracle chunker as a stand-in."""
+import hashlib
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pbs_chunker.h")
+KiB, MiB = 1024, 1024 * 1024
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pbs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_api():
+    names = declared_functions()
+    for n in ("pbs_chunker_new", "pbs_chunker_scan", "pbs_chunker_free", "pbs_chunker_find_cuts",
+              "pbs_chunker_find_cuts_device", "pbs_chunker_last_error"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol(pbschunk):
+    lib = pbschunk.lib()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert set(declared_functions()) == set(pbschunk.EXPORTED_SYMBOLS)
+    nm = subprocess.run(["nm", "-D", "--defined-only", pbschunk.LIB_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (pbs_[a-z0-9_]+)\b", nm))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_has_gfx950_code_object(pbschunk):
+    # the fat binary embeds the offload bundle id "hipv4-amdgcn-amd-amdhsa--gfx950"
+    assert b"amdgcn-amd-amdhsa--gfx950" in open(pbschunk.LIB_PATH, "rb").read()
+
+
+def test_table_digest_of_library(pbschunk, oracle):
+    t = pbschunk.table()
+    assert hashlib.sha256(t.astype("<u4").tobytes()).hexdigest() == oracle.TABLE_SHA256
+
+
+def test_strerror_and_max_cuts(pbschunk):
+    assert "power of two" in pbschunk.strerror(pbschunk.PBS_ERR_NOT_POW2)
+    assert pbschunk.max_cuts(0) >= 1
+    assert pbschunk.max_cuts(65 * 1000) >= 1000
+
+
+def test_non_power_of_two_rejected_like_reference(pbschunk):
+    for avg in (0, 3, 3 * MiB):
+        with pytest.raises(ValueError, match="not a power of two"):
+            pbschunk.Chunker(avg)
+
+
+def test_no_device_fails_loudly(pbschunk):
+    if pbschunk.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(pbschunk.ChunkerError) as ei:
+        pbschunk.Chunker(4 * MiB)
+    assert ei.value.code == pbschunk.PBS_ERR_NO_DEVICE
+
+
+# ---- host caller logic, with the oracle Chunker standing in for the GPU one --------
+
+def _patch_chunker(monkeypatch, pbschunk, oracle):
+    monkeypatch.setattr(pbschunk, "Chunker", lambda avg: oracle.Chunker(avg))
+
+
+def test_chunk_stream_logic(monkeypatch, pbschunk, oracle):
+    _patch_chunker(monkeypatch, pbschunk, oracle)
+    data = oracle.gen_random(3 * MiB + 17, 21)
+    ref = oracle.chunk_feed(64 * KiB, data)
+    for piece in (1000, 64 * KiB, 256 * KiB):
+        pieces = [data[i:i + piece].tobytes() for i in range(0, data.size, piece)]
+        chunks = list(pbschunk.ChunkStream(pieces, 64 * KiB))
+        ends = np.cumsum([len(c) for c in chunks])
+        assert b"".join(chunks) == data.tobytes()
+        assert np.array_equal(ends[:-1], ref) or np.array_equal(ends, ref)
+
+
+def test_dynamic_chunk_writer_logic(monkeypatch, pbschunk, oracle):
+    _patch_chunker(monkeypatch, pbschunk, oracle)
+    data = oracle.gen_vmimage(2 * MiB, 5, 0)
+    got = []
+    w = pbschunk.DynamicChunkWriter(lambda end, b: got.append((end, len(b))), 16 * KiB)
+    for i in range(0, data.size, 65536):
+        w.write_all(data[i:i + 65536].tobytes())
+    w.close()
+    ref = oracle.chunk_feed(16 * KiB, data).tolist()
+    ends = [e for e, _ in got]
+    assert ends[:len(ref)] == ref and ends[-1] == data.size
+    assert sum(n for _, n in got) == data.size

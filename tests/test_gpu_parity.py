@@ -1,0 +1,269 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle and the
+golden fixtures.  Bit-exact comparison of candidate positions and cut lists.
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+"""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import gen_np
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+KiB, MiB, GiB = 1024, 1024 * 1024, 1024 * 1024 * 1024
+
+
+def _golden_cases():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)["cases"]
+
+
+def _golden_input(case):
+    gen = case["generator"]
+    if gen == "counter":
+        return gen_np.gen_counter(case["length"], case["offset"])
+    if gen == "random":
+        return gen_np.gen_random(case["length"], case["seed"], case["offset"])
+    if gen == "vmimage":
+        return gen_np.gen_vmimage(case["length"], case["seed"], case["offset"])
+    return np.zeros(case["length"], dtype=np.uint8)
+
+
+# ---------------------------------------------------------------- phase A (candidates)
+
+CAND_CASES = [
+    # (name, maker, avg) -- sizes cover exact-only (< 1 MiB wave tile), several wave tiles
+    # plus a ragged tail, and dense candidates (tiny averages) that overflow the first
+    # suspect/candidate capacity estimate.
+    ("random_3M+77_64K", lambda: gen_np.gen_random(3 * MiB + 77, 0x5EED0002), 64 * KiB),
+    ("random_3M+77_16", lambda: gen_np.gen_random(3 * MiB + 77, 0x5EED0002), 16),
+    ("random_2M+5_128", lambda: gen_np.gen_random(2 * MiB + 5, 3), 128),
+    ("random_700K_4096", lambda: gen_np.gen_random(700 * KiB + 1, 4), 4096),
+    ("random_40M+3_256K", lambda: gen_np.gen_random(40 * MiB + 3, 5), 256 * KiB),
+    ("counter_20M_64K", lambda: gen_np.gen_counter(20 * MiB), 64 * KiB),
+    ("vm_64M_4M", lambda: gen_np.gen_vmimage(64 * MiB, 0x5EED0003, 500 * MiB), 4 * MiB),
+    ("zeros_5M_64K", lambda: np.zeros(5 * MiB, np.uint8), 64 * KiB),
+    ("tiny_100_64", lambda: gen_np.gen_random(100, 1), 64),
+    ("empty_64", lambda: np.zeros(0, np.uint8), 64),
+    ("random_4M_avg2", lambda: gen_np.gen_random(4 * MiB, 9), 2),
+    ("random_1M_avg1", lambda: gen_np.gen_random(1 * MiB, 9), 1),
+]
+
+
+@pytest.mark.parametrize("name,mk,avg", CAND_CASES, ids=[c[0] for c in CAND_CASES])
+def test_candidates_match_oracle(gpu, oracle, name, mk, avg):
+    data = mk()
+    got = gpu.candidates_host(data, avg)
+    ref = oracle.candidates(avg, data)
+    assert np.array_equal(got, ref), (name, got.size, ref.size)
+
+
+def test_candidates_golden(gpu):
+    for case in _golden_cases():
+        if "ncand" not in case:
+            continue
+        data = _golden_input(case)
+        ref = np.load(os.path.join(GOLDEN, case["name"] + ".cand.npy"), allow_pickle=False)
+        assert np.array_equal(gpu.candidates_host(data, case["avg"]), ref), case["name"]
+
+
+# ---------------------------------------------------------------- cut lists
+
+@pytest.mark.parametrize("case", _golden_cases(), ids=lambda c: c["name"])
+def test_find_cuts_golden(gpu, case):
+    data = _golden_input(case)
+    ref = np.load(os.path.join(GOLDEN, case["name"] + ".cuts.npy"), allow_pickle=False)
+    with gpu.Chunker(case["avg"]) as c:
+        got = c.find_cuts(data, is_final=False)
+    assert np.array_equal(got, ref), (case["name"], got[:5], ref[:5])
+
+
+def test_find_cuts_final_tail(gpu, oracle):
+    data = gen_np.gen_random(5 * MiB + 11, 77)
+    ref = oracle.chunk_feed(256 * KiB, data)
+    with gpu.Chunker(256 * KiB) as c:
+        got = c.find_cuts(data, is_final=True)
+        assert np.array_equal(got[:-1], ref) and int(got[-1]) == data.size
+        assert c.stream_offset == 0  # handle restarted
+        again = c.find_cuts(data, is_final=True)  # a fresh stream gives the same cuts
+    assert np.array_equal(again, got)
+
+
+@pytest.mark.parametrize("avg", [64, 4096, 64 * KiB, 4 * MiB])
+def test_find_cuts_split_calls(gpu, oracle, avg):
+    """State carried across calls (carry bytes, open chunk, pending candidates)."""
+    n = 24 * MiB if avg >= 64 * KiB else 1 * MiB
+    data = gen_np.gen_vmimage(n, 0x5EED0003, 512 * MiB - n // 3)
+    ref = oracle.chunk_feed(avg, data)
+    rng = np.random.default_rng(avg)
+    cuts = np.concatenate([[0], np.sort(rng.choice(np.arange(1, n), 12, replace=False)), [n]])
+    got = []
+    with gpu.Chunker(avg) as c:
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            got.append(c.find_cuts(data[a:b]))
+            assert c.stream_offset == b
+    got = np.concatenate(got)
+    assert np.array_equal(got, ref)
+
+
+def test_find_cuts_device(gpu, oracle):
+    import torch
+    n = 48 * MiB + 8
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n, gpu.GEN_VMIMAGE, 0x5EED0003, 480 * MiB)
+    host = dev.cpu().numpy()
+    assert np.array_equal(host, oracle.gen_vmimage(n, 0x5EED0003, 480 * MiB))
+    ref = oracle.chunk_feed(1 * MiB, host)
+    with gpu.Chunker(1 * MiB) as c:
+        c.set_stream(torch.cuda.current_stream().cuda_stream)
+        half = 20 * MiB + 3
+        g1 = c.find_cuts_device(dev.data_ptr(), half)
+        g2 = c.find_cuts_device(dev.data_ptr() + half, n - half, is_final=True)
+        t = c.last_timing()
+    got = np.concatenate([g1, g2])
+    assert np.array_equal(got[:-1], ref) and int(got[-1]) == n
+    assert t["bytes"] == n - half and t["total_ms"] > 0
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_device_generator_matches_oracle(gpu, oracle, kind):
+    import torch
+    n, off = 3 * MiB + 8, 1 * GiB - 1 * MiB
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n, kind, 0x5EED0002, off)
+    host = dev.cpu().numpy()
+    ref = [oracle.gen_counter(n, off), oracle.gen_random(n, 0x5EED0002, off),
+           oracle.gen_vmimage(n, 0x5EED0002, off)][kind]
+    assert np.array_equal(host, ref)
+
+
+# ---------------------------------------------------------------- scan() drop-in surface
+
+@pytest.mark.parametrize("feed,avg,n", [(1, 1024, 24 * KiB), (7, 256, 64 * KiB),
+                                        (65, 4096, 256 * KiB), (4096, 64 * KiB, 3 * MiB),
+                                        (256 * KiB, 64 * KiB, 12 * MiB)])
+def test_scan_feed_granularity(gpu, oracle, feed, avg, n):
+    """test_chunker1 (chunker.rs:202-271) style: same cuts for any feed size."""
+    data = gen_np.gen_random(n, feed)
+    ref = oracle.chunk_feed(avg, data, feed)
+    assert np.array_equal(ref, oracle.chunk_feed(avg, data, 0))
+    got = []
+    with gpu.Chunker(avg) as c:
+        for piece in range(0, n, feed):
+            p = data[piece:piece + feed]
+            off = 0
+            while off < p.size:
+                k = c.scan(p[off:])
+                if k == 0:
+                    break
+                off += k
+                got.append(piece + off)
+    assert np.array_equal(np.array(got, dtype=np.uint64), ref)
+
+
+def test_chunker1_whole_buffer(gpu):
+    """test_chunker1's test2 loop on its own 1 MiB counter buffer (chunker.rs:246-257)."""
+    buf = gen_np.gen_counter(1 * MiB)
+    with gpu.Chunker(64 * KiB) as c:
+        chunks, pos = [], 0
+        while pos < buf.size:
+            k = c.scan(buf[pos:])
+            if k == 0:
+                break
+            chunks.append((pos, k))
+            pos += k
+    assert [p + k for p, k in chunks] == [143377, 405521, 667665, 929809]
+    assert buf.size - pos == 118767
+
+
+def test_test_chunk_speed_loop(gpu, oracle):
+    """examples/test_chunk_speed.rs: 5 passes over an 80 MiB counter at 64 KiB with the
+    chunker state carried across passes (the chunker is never reset)."""
+    buf = oracle.gen_counter(80 * MiB)
+    ref_c = oracle.Chunker(64 * KiB)
+    with gpu.Chunker(64 * KiB) as c:
+        for _ in range(2):
+            pos = 0
+            while pos < buf.size:
+                k = c.scan(buf[pos:])
+                r = ref_c.scan(buf[pos:])
+                assert k == r
+                if k == 0:
+                    break
+                pos += k
+
+
+def test_chunk_stream_and_writer(gpu, oracle):
+    data = gen_np.gen_vmimage(20 * MiB + 5, 0x5EED0003, 510 * MiB)
+    ref = oracle.chunk_feed(1 * MiB, data)
+    pieces = [data[i:i + 256 * KiB].tobytes() for i in range(0, data.size, 256 * KiB)]
+    chunks = list(gpu.ChunkStream(pieces, 1 * MiB))
+    ends = np.cumsum([len(ch) for ch in chunks])
+    assert b"".join(chunks) == data.tobytes()
+    assert np.array_equal(ends[:-1], ref) and ends[-1] == data.size
+    got = []
+    w = gpu.DynamicChunkWriter(lambda end, b: got.append(end), 1 * MiB)
+    for i in range(0, data.size, 64 * KiB):
+        w.write_all(data[i:i + 64 * KiB].tobytes())
+    w.close()
+    assert np.array_equal(np.array(got[:-1], dtype=np.uint64), ref) and got[-1] == data.size
+
+
+def test_invalid_arguments(gpu):
+    with pytest.raises(ValueError):
+        gpu.Chunker(12345)
+    with gpu.Chunker(4 * MiB) as c:
+        assert c.scan(b"") == 0
+        assert c.find_cuts(b"").size == 0
+
+
+# ---------------------------------------------------------------- full-size (config 2)
+
+def _oracle_two_phase_parallel(oracle, data: np.ndarray, avg: int, threads: int = 16):
+    """Multi-threaded oracle: phase-A candidates per segment (63-byte overlap; ctypes
+    releases the GIL), then the oracle's resolve.  Equivalent to the streaming oracle
+    (tests/test_oracle.py::test_two_phase_equivalence)."""
+    n = data.size
+    seg = (n + threads - 1) // threads
+    parts = [None] * threads
+
+    def work(t):
+        a, b = t * seg, min(n, (t + 1) * seg)
+        if a >= b:
+            parts[t] = np.zeros(0, np.uint64)
+            return
+        lo = max(0, a - 63)
+        c = oracle.candidates(avg, data[lo:b]).astype(np.uint64) + np.uint64(lo)
+        parts[t] = c[c >= a]
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    cand = np.concatenate(parts)
+    return cand, oracle.resolve(avg, cand, n)
+
+
+@pytest.mark.slow
+def test_config2_8GiB_random_in_hbm(gpu, oracle):
+    """BASELINE config 2: 8 GiB random already in HBM, 4 MiB average, full cut list
+    diffed against the oracle."""
+    import torch
+    n = 8 * GiB
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n, gpu.GEN_RANDOM, 0x5EED0002, 0)
+    with gpu.Chunker(4 * MiB) as c:
+        got = c.find_cuts_device(dev.data_ptr(), n, is_final=False)
+        t = c.last_timing()
+    host = dev.cpu().numpy()
+    del dev
+    cand, ref = _oracle_two_phase_parallel(oracle, host, 4 * MiB)
+    assert t["candidates"] == cand.size
+    assert np.array_equal(got, ref)
+    # spot-check against the streaming oracle on the first 1 GiB
+    head = oracle.chunk_feed(4 * MiB, host[:1 * GiB])
+    assert np.array_equal(got[:head.size], head)
