@@ -192,7 +192,8 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
         if (attempt > 4) return fail(c, PBS_ERR_NOMEM);
     }
     float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->timing.scan_ms += ms;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    c->timing.scan_ms += ms;
     c->timing.bytes += len;
     c->timing.suspects += nsusp;
     c->timing.candidates += ncand;
@@ -290,7 +291,8 @@ int run_resolve(pbs_chunker* c, uint32_t m, uint64_t end, uint64_t* out, size_t 
     c->pending.swap(keep);
     c->pend_head = 0;
     float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->timing.resolve_ms += ms;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+    c->timing.resolve_ms += ms;
     c->timing.cuts += ncut;
     return PBS_OK;
 }
@@ -325,10 +327,13 @@ int scan_new_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uin
         HIP_TRY(c, hipMemcpyAsync(c->pending.data() + old, c->d_C.p, (size_t)ncand * 8,
                                   hipMemcpyDeviceToHost, c->stream));
     }
-    float ms = 0;
     HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) == hipSuccess) c->timing.exact_ms += ms;
+    if (c->prm.hash_cuts && bl) {  // ev[1] was recorded by scan_candidates
+        float ms = 0;
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+        c->timing.exact_ms += ms;
+    }
     if (hsrc)
         update_carry(c, hsrc, bl);
     else {
@@ -396,7 +401,8 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
     HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
     HIP_TRY(c, hipEventSynchronize(c->ev[3]));
     float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev[4], c->ev[3]) == hipSuccess) c->timing.total_ms = ms;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[4], c->ev[3]));
+    c->timing.total_ms = ms;
     *n_out = n;
     return PBS_OK;
 }

@@ -328,13 +328,16 @@ __global__ __launch_bounds__(256) void resolve_double_kernel(uint32_t n, const u
     jout[j] = jin[J];
 }
 
+__device__ __forceinline__ uint32_t slot_of(uint32_t j, uint32_t m) { return j == m ? 0u : j + 1u; }
+
 __global__ __launch_bounds__(256) void resolve_count_kernel(uint32_t m, const uint32_t* __restrict__ nxt,
                                                             const uint64_t* __restrict__ nforced,
                                                             const uint32_t* __restrict__ on,
                                                             uint64_t* __restrict__ cnt) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > m) return;  // nodes 0..m
-    cnt[j] = on[j] ? nforced[j] + (nxt[j] != m + 1 ? 1u : 0u) : 0u;
+    // slot 0 = the start node m (its cuts come first), slot j+1 = candidate node j
+    cnt[slot_of(j, m)] = on[j] ? nforced[j] + (nxt[j] != m + 1 ? 1u : 0u) : 0u;
 }
 
 // out[] = chunk END offsets (absolute, exclusive).  res[0] = number of cuts,
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(256) void resolve_emit_kernel(
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > m || !on[j]) return;
     const uint64_t s = (j == m) ? p.s0 : C[j] + 1;
-    const uint64_t o = off[j];
+    const uint64_t o = off[slot_of(j, m)];
     const uint64_t nf = nforced[j];
     for (uint64_t t = 0; t < nf; ++t)
         if (o + t < out_cap) out[o + t] = s + (t + 1) * p.max_eff;
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(256) void resolve_emit_kernel(
         if (o + nf < out_cap) out[o + nf] = C[nxt[j]] + 1;
     } else {
         const uint64_t s_open = s + nf * p.max_eff;
-        res[0] = o + cnt[j];
+        res[0] = o + cnt[slot_of(j, m)];
         res[1] = s_open;
         res[2] = lower_bound_u64(C, 0, m, s_open);
     }
@@ -406,6 +409,7 @@ hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, const uint32_t
                             uint32_t thr, uint64_t* susp, uint32_t* nsusp, uint32_t cap,
                             int grid, hipStream_t stream) {
     if (ntiles == 0) return hipSuccess;
+    (void)hipGetLastError();  // launch errors below must not be confused with stale ones
     const uint64_t need = (ntiles + kWavesPerWG - 1) / kWavesPerWG;
     const int g = (uint64_t)grid < need ? grid : (int)need;
     hipLaunchKernelGGL(scan_main_kernel<kSegBytes>, dim3(g), dim3(kThreadsMain), 0, stream, data,
@@ -419,6 +423,7 @@ hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* p
                              uint32_t mask, uint32_t minimum, uint64_t base, uint64_t* cand,
                              uint32_t* ncand, uint32_t cand_cap, uint64_t max_items,
                              hipStream_t stream) {
+    (void)hipGetLastError();
     uint64_t blocks = (max_items + 255) / 256;
     if (blocks < 1) blocks = 1;
     if (blocks > 2048) blocks = 2048;
@@ -444,6 +449,7 @@ hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p,
                           uint64_t out_cap, uint64_t* res, hipStream_t stream) {
     const uint32_t n = m + 2;
     const unsigned blocks = (n + 255) / 256;
+    (void)hipGetLastError();
     hipLaunchKernelGGL(resolve_next_kernel, dim3(blocks), dim3(256), 0, stream, C, m, p, nxt,
                        nforced, on);
     // pointer doubling over copies of nxt (nxt itself is kept for emission)
@@ -469,6 +475,7 @@ hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p,
 
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,
                       int kind, hipStream_t stream) {
+    (void)hipGetLastError();
     uint64_t blocks = (nwords + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
