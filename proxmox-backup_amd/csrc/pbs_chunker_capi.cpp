@@ -141,8 +141,9 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
     if (c->carry_len)
         HIP_TRY(c, hipMemcpyAsync(c->d_pre.p, c->carry, c->carry_len, hipMemcpyHostToDevice,
                                   c->stream));
-    const uint64_t ntiles = len / kWaveTileBytes;
-    const uint64_t covered = ntiles * kWaveTileBytes;
+    uint64_t ntiles = 0;
+    const int seg = scan_main_plan(len, c->cu, &ntiles);
+    const uint64_t covered = ntiles * 64ull * (uint64_t)seg;
     const int head = ntiles > 0 ? 1 : 0;
     const uint64_t ext_first = covered / kBlockBytes;
     const uint64_t ext_count = (len - covered + kBlockBytes - 1) / kBlockBytes;
@@ -163,7 +164,7 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
         uint32_t* d_nsusp = c->d_counters.as<uint32_t>();
         uint32_t* d_ncand = d_nsusp + 1;
         HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
-        HIP_TRY(c, launch_scan_main(d_data, ntiles, c->d_table.as<uint32_t>(), p.thr,
+        HIP_TRY(c, launch_scan_main(d_data, ntiles, seg, c->d_table.as<uint32_t>(), p.thr,
                                     c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu,
                                     c->stream));
         HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));

@@ -5,11 +5,6 @@
 
 namespace pbs {
 
-// Bytes of one lane's segment in scan_main_kernel (a wave tile = 64 segments).
-// 16 KiB keeps the 128-byte warm-up per segment at 0.8 % of the work and of the
-// HBM traffic; a wave tile is 1 MiB.
-constexpr int kSegBytes = 16384;
-constexpr uint64_t kWaveTileBytes = 64ull * kSegBytes;
 constexpr uint64_t kBlockBytes = 128;  // exact-evaluation granule (one lane iteration)
 
 // generator kinds (see oracle/chunker_oracle.c; bytes must match)
@@ -27,9 +22,12 @@ struct ResolveParams {
     uint64_t s0;       // absolute start of the open chunk
 };
 
-hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, const uint32_t* table_rot,
-                            uint32_t thr, uint64_t* susp, uint32_t* nsusp, uint32_t cap,
-                            int grid, hipStream_t stream);
+// Segment bytes per lane for a scan of `len` bytes (a wave tile = 64 segments) and
+// the number of full wave tiles; bytes past ntiles*64*seg are the tail.
+int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles);
+hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
+                            const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
+                            uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
                              uint32_t pre_len, const uint64_t* susp, const uint32_t* nsusp,
                              uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head,

@@ -26,6 +26,7 @@
 
 #include "buzhash_table.h"
 #include "pbs_chunker_internal.h"
+#include "scan_main.h"  // scan_main_kernel (phase A main pass)
 
 namespace pbs {
 
@@ -52,144 +53,6 @@ namespace pbs {
 // the recurrence, so the table is pre-rotated: T'[b] = rotl(T[b], rot).  The max
 // over a 128-byte block (v_max3_u32) flags the rare blocks that hold a candidate;
 // those blocks are re-evaluated exactly by scan_exact_kernel.
-
-constexpr int kWavesPerWG = 8;
-constexpr int kThreadsMain = kWavesPerWG * 64;
-constexpr int kIter = 128;                       // bytes per lane per iteration
-constexpr int kStagePerWave = 64 * kIter;        // 8 KiB
-constexpr int kTableDwords = 256 * 64;           // 64 KiB
-
-__device__ __forceinline__ uint32_t rotl1(uint32_t h) {
-    return __builtin_amdgcn_alignbit(h, h, 31);
-}
-__device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t m = a > b ? a : b;
-    return m > c ? m : c;
-}
-
-// One 128-byte step of the rolling hash for this lane.  `ring` holds T' of the last
-// 64 bytes (the "leave" values); the unrolled body indexes it statically, so it lives
-// in 64 VGPRs.  Returns the max of h' over the 128 positions.
-__device__ __forceinline__ uint32_t roll128(const uint4 (&d)[8], uint32_t (&ring)[64],
-                                            uint32_t& h, const uint32_t* s_tab,
-                                            uint32_t lanebase) {
-    uint32_t acc = 0, hp = 0;
-#pragma unroll
-    for (int i = 0; i < 128; ++i) {
-        const uint4 q = d[i >> 4];
-        const int wi = (i >> 2) & 3;
-        const uint32_t w = wi == 0 ? q.x : (wi == 1 ? q.y : (wi == 2 ? q.z : q.w));
-        // bytes of {w, lanebase}: result = [0, 0, byte (i&3) of w, lane*4]
-        const uint32_t sel = 0x0c0c0000u | ((4u + (uint32_t)(i & 3)) << 8);
-        const uint32_t a = __builtin_amdgcn_perm(w, lanebase, sel);
-        const uint32_t t = *(const uint32_t*)((const char*)s_tab + a);
-        h = __builtin_amdgcn_bitop3_b32(rotl1(h), ring[i & 63], t, 0x96);  // v_bitop3 xor3
-        ring[i & 63] = t;
-        if (i & 1)
-            acc = umax3(acc, hp, h);
-        else
-            hp = h;
-    }
-    return acc;
-}
-
-template <int SEG>
-__global__ __launch_bounds__(kThreadsMain, 2) void scan_main_kernel(
-    const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
-    uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {
-    static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
-    __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + kWavesPerWG * kStagePerWave / 4];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    uint32_t* s_tab = s_lds;
-    for (int i = tid; i < kTableDwords; i += kThreadsMain) s_tab[i] = table_rot[i >> 6];
-    __syncthreads();
-
-    uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
-    const uint32_t lanebase = (uint32_t)lane * 4u;
-
-    // LDS-DMA instruction j, lane i stages chunk k of segment l = 8j + (i>>3) with
-    // k = (i & 7) ^ ((l >> 1) & 7), so the linear LDS destination j*1024 + i*16 equals
-    // the swizzled slot l*128 + ((k ^ ((l>>1)&7)) * 16).
-    uint32_t dma_off[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const uint32_t l = 8u * j + ((uint32_t)lane >> 3);
-        const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
-        dma_off[j] = l * (uint32_t)SEG + k * 16u;
-    }
-    const uint32_t rd_base = (uint32_t)lane * 128u;
-    const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
-
-    constexpr int NIT = SEG / kIter + 1;  // iteration 0 is the warm-up block [-128, 0)
-    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerWG;
-    uint64_t tile = (uint64_t)blockIdx.x * kWavesPerWG + wave;
-    if (tile >= ntiles) return;
-
-    auto issue = [&](uint64_t t, int it) {
-        const uint8_t* tb = data + t * (64ull * SEG);
-        const int32_t boff = (it - 1) * kIter;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            int32_t off = (int32_t)dma_off[j] + boff;
-            // Only segment 0 of the stream has no bytes before it: read any valid
-            // bytes there, its warm-up state is discarded below.
-            if (t == 0 && off < 0) off = 0;
-            __builtin_amdgcn_global_load_lds(
-                (const void __attribute__((address_space(1)))*)(tb + off),
-                (void __attribute__((address_space(3)))*)(stage + j * 1024), 16, 0, 0);
-        }
-    };
-
-    uint32_t ring[64];
-    uint32_t h = 0;
-    issue(tile, 0);
-    for (;;) {
-        for (int it = 0; it < NIT; ++it) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint4 d[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                d[k] = *(const uint4*)(stage + rd_base + (((uint32_t)k ^ rsw) << 4));
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            // prefetch the next block of this wave (next iteration or next tile)
-            {
-                uint64_t nt = tile;
-                int nit = it + 1;
-                if (nit == NIT) {
-                    nt = tile + nw;
-                    nit = 0;
-                }
-                if (nt < ntiles) issue(nt, nit);
-            }
-            if (it == 0) {
-                h = 0;
-#pragma unroll
-                for (int r = 0; r < 64; ++r) ring[r] = 0;
-            }
-            const uint32_t acc = roll128(d, ring, h, s_tab, lanebase);
-            if (it == 0) {
-                if (tile == 0 && lane == 0) {  // stream segment 0: no warm-up bytes
-                    h = 0;
-#pragma unroll
-                    for (int r = 0; r < 64; ++r) ring[r] = 0;
-                }
-            } else if (acc >= thr) {
-                const uint64_t pos =
-                    (tile * 64ull + (uint64_t)lane) * (uint64_t)SEG + (uint64_t)(it - 1) * kIter;
-                // block 0 is always re-evaluated by scan_exact_kernel (the `pre` bytes)
-                if (pos != 0) {
-                    const uint32_t idx = atomicAdd(nsusp, 1u);
-                    if (idx < cap) susp[idx] = pos;
-                }
-            }
-        }
-        tile += nw;
-        if (tile >= ntiles) break;
-    }
-}
 
 // ---------------------------------------------------------------------------------
 // Phase A, exact evaluation of 128-byte blocks (suspect blocks, stream head, tail)
@@ -405,15 +268,49 @@ __global__ __launch_bounds__(256) void gen_kernel(uint64_t* __restrict__ out, ui
 // ---------------------------------------------------------------------------------
 // Host-side launchers (called from pbs_chunker_capi.cpp)
 // ---------------------------------------------------------------------------------
-hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, const uint32_t* table_rot,
-                            uint32_t thr, uint64_t* susp, uint32_t* nsusp, uint32_t cap,
-                            int grid, hipStream_t stream) {
+int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles) {
+    // largest segment that still gives every wave >= 2 tiles (load balance); the
+    // 128-byte warm-up per segment costs 128/SEG of the work and traffic
+    const uint64_t waves = (uint64_t)cu * kWavesPerWG;
+    int seg = 4096;
+    for (int s : {32768, 16384, 8192}) {
+        if (len / (64ull * s) >= 2 * waves) {
+            seg = s;
+            break;
+        }
+    }
+    *ntiles = len / (64ull * seg);
+    return seg;
+}
+
+hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
+                            const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
+                            uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream) {
     if (ntiles == 0) return hipSuccess;
     (void)hipGetLastError();  // launch errors below must not be confused with stale ones
     const uint64_t need = (ntiles + kWavesPerWG - 1) / kWavesPerWG;
     const int g = (uint64_t)grid < need ? grid : (int)need;
-    hipLaunchKernelGGL(scan_main_kernel<kSegBytes>, dim3(g), dim3(kThreadsMain), 0, stream, data,
-                       ntiles, table_rot, thr, susp, nsusp, cap);
+    const dim3 gd(g), bd(kWavesPerWG * 64);
+    switch (seg) {
+        case 32768:
+            hipLaunchKernelGGL((scan_main_kernel<32768>), gd, bd, 0, stream, data, ntiles,
+                               table_rot, thr, susp, nsusp, cap);
+            break;
+        case 16384:
+            hipLaunchKernelGGL((scan_main_kernel<16384>), gd, bd, 0, stream, data, ntiles,
+                               table_rot, thr, susp, nsusp, cap);
+            break;
+        case 8192:
+            hipLaunchKernelGGL((scan_main_kernel<8192>), gd, bd, 0, stream, data, ntiles,
+                               table_rot, thr, susp, nsusp, cap);
+            break;
+        case 4096:
+            hipLaunchKernelGGL((scan_main_kernel<4096>), gd, bd, 0, stream, data, ntiles,
+                               table_rot, thr, susp, nsusp, cap);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

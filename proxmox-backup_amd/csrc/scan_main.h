@@ -1,0 +1,165 @@
+// scan_main_kernel: phase A main pass of the gfx950 chunker (geometry and hash
+// representation: pbs_chunker_kernels.hip and DESIGN.md "Kernel: scan_main").  Kept in a
+// header so the product library and the microbenchmarks (scripts/microbench/) build the
+// same code; the rejected design variants live in scripts/microbench/scan_variants.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+namespace pbs {
+
+// MODE 0: product.  MODE 1: loads only (DMA + LDS reads, no hash) and MODE 2: hash
+// only (the staged block is re-used, no HBM traffic) -- microbenchmark ablations.
+constexpr int kModeFull = 0, kModeLoadOnly = 1, kModeComputeOnly = 2;
+
+#include "roll128_asm.h"  // roll128_asm(): hand-scheduled 128-byte body (gen_roll_asm.py)
+
+constexpr int kWavesPerWG = 8;  // product geometry
+constexpr int kIter = 128;                       // bytes per lane per iteration
+constexpr int kStagePerWave = 64 * kIter;        // 8 KiB
+constexpr int kTableDwords = 256 * 64;           // 64 KiB
+
+__device__ __forceinline__ uint32_t rotl1(uint32_t h) {
+    return __builtin_amdgcn_alignbit(h, h, 31);
+}
+__device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t m = a > b ? a : b;
+    return m > c ? m : c;
+}
+
+// ---------------------------------------------------------------------------------
+// 8 waves per CU (one 512-thread workgroup, persistent), 128-byte iterations, one
+// 8 KiB LDS stage per wave.  The block of iteration it+1 is staged by 8 LDS-DMA
+// instructions (buffer_load_dwordx4 ... lds, nt) issued from a per-tile buffer
+// descriptor (SGPR base + SGPR iteration offset + constant per-lane VGPR offset: no
+// VALU address math) as soon as iteration it's block is in VGPRs; the hash loop is the
+// hand-scheduled roll128_asm_g4 (G = bytes per lgkmcnt wait).  PF > 0 adds an L2
+// "touch" DMA PF iterations ahead (measured slower; kept for the microbenchmark).
+// Design record of the variants measured against it: DESIGN.md "Kernel: scan_main".
+template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0>
+__global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
+    const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
+    uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {
+    static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
+    constexpr int NW = kWavesPerWG;
+    // + 256 B per wave: landing area of the L2 "touch" DMAs (PF > 0)
+    __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4 + NW * 64];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < kTableDwords; i += NW * 64) s_lds[i] = table_rot[i >> 6];
+    __syncthreads();
+
+    uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
+    uint8_t* touch_area = (uint8_t*)(s_lds + kTableDwords + NW * kStagePerWave / 4) + wave * 256;
+    const uint32_t voff_touch = (uint32_t)lane * (uint32_t)SEG + 64u;
+    const uint32_t lanebase = (uint32_t)lane * 4u;
+    uint32_t voff[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t l = 8u * j + ((uint32_t)lane >> 3);
+        const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
+        voff[j] = l * (uint32_t)SEG + k * 16u;
+    }
+    const uint32_t rd_base = (uint32_t)lane * 128u;
+    const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
+
+    constexpr int NIT = SEG / kIter + 1;  // iteration 0 is the warm-up block [-128, 0)
+    const uint64_t nw = (uint64_t)gridDim.x * NW;
+    uint64_t tile = (uint64_t)blockIdx.x * NW + wave;
+    if (tile >= ntiles) return;
+
+    // Tile t > 0: base = tile start - 128, iteration offset it*128.  Tile 0: base = tile
+    // start, offset it*128 - 128 wraps for the warm-up, which the range check
+    // (num_records = tile bytes + 128) turns into zeros for segment 0 only.
+    auto issue = [&](uint64_t t, int it) {
+        const uint8_t* tb = data + t * (64ull * SEG);
+        const bool first = (t == 0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(first ? tb : tb - kIter), 0, (int)(64u * SEG + kIter), 0x00020000);
+        const uint32_t soff = (uint32_t)it * kIter - (first ? (uint32_t)kIter : 0u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, voff[j], soff,
+                0, AUX);
+        if constexpr (PF > 0) {
+            // pull the 64 lines of iteration it+PF into L2 (4 bytes per lane, dummy LDS)
+            if (it + PF < NIT)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)touch_area, 4, voff_touch,
+                    soff + (uint32_t)PF * kIter, 0, 0);
+        }
+    };
+
+    uint32_t ring[128];
+#pragma unroll
+    for (int r = 0; r < 128; ++r) ring[r] = 0;
+    uint32_t h = 0;
+    issue(tile, 0);
+    for (;;) {
+        for (int it = 0; it < NIT; ++it) {
+            if (PF > 0 && it + PF < NIT)
+                asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // the touch may stay in flight
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t d[32];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint4 v = *(const uint4*)(stage + rd_base + (((uint32_t)k ^ rsw) << 4));
+                d[4 * k] = v.x;
+                d[4 * k + 1] = v.y;
+                d[4 * k + 2] = v.z;
+                d[4 * k + 3] = v.w;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            {
+                uint64_t nt = tile;
+                int nit = it + 1;
+                if (nit == NIT) {
+                    nt = tile + nw;
+                    nit = 0;
+                }
+                if (MODE != kModeComputeOnly && nt < ntiles) issue(nt, nit);
+            }
+            if (it == 0) {
+                h = 0;
+#pragma unroll
+                for (int r = 64; r < 128; ++r) ring[r] = 0;
+            }
+            uint32_t acc;
+            if constexpr (MODE == kModeLoadOnly) {
+                acc = 0;
+#pragma unroll
+                for (int k = 0; k < 32; ++k) acc ^= d[k];
+                acc = (acc == 0x9E3779B9u && lane == 65) ? 0xFFFFFFFFu : 0u;
+            } else if constexpr (G == 4) {
+                acc = roll128_asm_g4(d, ring, h, lanebase);
+            } else {
+                acc = roll128_asm(d, ring, h, lanebase);
+            }
+            if (it == 0) {
+                if (tile == 0 && lane == 0) {
+                    h = 0;
+#pragma unroll
+                    for (int r = 64; r < 128; ++r) ring[r] = 0;
+                }
+            } else if (acc >= thr) {
+                const uint64_t pos =
+                    (tile * 64ull + (uint64_t)lane) * (uint64_t)SEG + (uint64_t)(it - 1) * kIter;
+                if (pos != 0) {
+                    const uint32_t idx = atomicAdd(nsusp, 1u);
+                    if (idx < cap) susp[idx] = pos;
+                }
+            }
+        }
+        tile += nw;
+        if (tile >= ntiles) break;
+    }
+}
+
+
+}  // namespace pbs

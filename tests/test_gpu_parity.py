@@ -249,21 +249,25 @@ def _oracle_two_phase_parallel(oracle, data: np.ndarray, avg: int, threads: int 
 
 
 @pytest.mark.slow
-def test_config2_8GiB_random_in_hbm(gpu, oracle):
-    """BASELINE config 2: 8 GiB random already in HBM, 4 MiB average, full cut list
-    diffed against the oracle."""
+@pytest.mark.parametrize("gib,kind,avg", [(8, 1, 4 * MiB), (6, 2, 256 * KiB), (3, 1, 64 * KiB)],
+                         ids=["config2-8GiB-random-4M", "6GiB-vm-256K", "3GiB-random-64K"])
+def test_full_size_in_hbm(gpu, oracle, gib, kind, avg):
+    """BASELINE config 2 (8 GiB random already in HBM, 4 MiB average) and two sizes that
+    select the other scan_main segment lengths (16 KiB, 8 KiB): the full cut list is
+    diffed against the (multi-threaded two-phase) oracle."""
     import torch
-    n = 8 * GiB
+    n = gib * GiB
+    seed = 0x5EED0002 if kind == 1 else 0x5EED0003
     dev = torch.empty(n, dtype=torch.uint8, device="cuda")
-    gpu.generate_device(dev.data_ptr(), n, gpu.GEN_RANDOM, 0x5EED0002, 0)
-    with gpu.Chunker(4 * MiB) as c:
+    gpu.generate_device(dev.data_ptr(), n, kind, seed, 0)
+    with gpu.Chunker(avg) as c:
         got = c.find_cuts_device(dev.data_ptr(), n, is_final=False)
         t = c.last_timing()
     host = dev.cpu().numpy()
     del dev
-    cand, ref = _oracle_two_phase_parallel(oracle, host, 4 * MiB)
+    cand, ref = _oracle_two_phase_parallel(oracle, host, avg)
     assert t["candidates"] == cand.size
     assert np.array_equal(got, ref)
-    # spot-check against the streaming oracle on the first 1 GiB
-    head = oracle.chunk_feed(4 * MiB, host[:1 * GiB])
+    # spot-check against the streaming oracle on the first 256 MiB
+    head = oracle.chunk_feed(avg, host[:256 * MiB])
     assert np.array_equal(got[:head.size], head)
