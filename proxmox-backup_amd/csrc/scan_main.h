@@ -72,20 +72,25 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     uint64_t tile = (uint64_t)blockIdx.x * NW + wave;
     if (tile >= ntiles) return;
 
-    // Tile t > 0: base = tile start - 128, iteration offset it*128.  Tile 0: base = tile
-    // start, offset it*128 - 128 wraps for the warm-up, which the range check
-    // (num_records = tile bytes + 128) turns into zeros for segment 0 only.
+    // Tile t > 0: base = tile start - 128, iteration offset it*128 (the warm-up block of
+    // segment 0 is the previous tile's last line).  Tile 0: base = tile start; its
+    // warm-up iteration (it == 0) uses explicit per-lane offsets voff - 128 (segment 0
+    // has no bytes before it: it reads offset 0 and its warm-up state is discarded).
+    // Offsets must not wrap: the buffer unit range-checks voffset + soffset unwrapped.
     auto issue = [&](uint64_t t, int it) {
         const uint8_t* tb = data + t * (64ull * SEG);
         const bool first = (t == 0);
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(first ? tb : tb - kIter), 0, (int)(64u * SEG + kIter), 0x00020000);
-        const uint32_t soff = (uint32_t)it * kIter - (first ? (uint32_t)kIter : 0u);
+        const bool warm0 = first && it == 0;
+        const uint32_t soff = warm0 ? 0u : (uint32_t)it * kIter - (first ? (uint32_t)kIter : 0u);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t vo = warm0 ? (voff[j] >= (uint32_t)kIter ? voff[j] - kIter : 0u) : voff[j];
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, voff[j], soff,
-                0, AUX);
+                rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, vo, soff, 0,
+                AUX);
+        }
         if constexpr (PF > 0) {
             // pull the 64 lines of iteration it+PF into L2 (4 bytes per lane, dummy LDS)
             if (it + PF < NIT)
