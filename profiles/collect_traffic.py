@@ -1,0 +1,44 @@
+"""Derive HBM read bytes per scan_main_kernel launch from a rocprofv3 --pmc FETCH_SIZE
+run of bench.py and write profiles/traffic_latest.json (read by bench.py).
+
+FETCH_SIZE is in KiB; on gfx950 it reports exactly half the bytes of a wide coalesced
+streaming read (MI355X_MICROARCH.md "HBM"), so bytes = FETCH_SIZE * 1024 * 2.
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
+        python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-inclusive-gib 0
+    python profiles/collect_traffic.py gpurun_out/pmc_fetch --size-gib 64 --avg 4194304 --workload vmimage
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+ap = argparse.ArgumentParser()
+ap.add_argument("pmc_dir")
+ap.add_argument("--size-gib", type=float, default=64.0)
+ap.add_argument("--avg", type=int, default=4 * 1024 * 1024)
+ap.add_argument("--workload", default="vmimage")
+ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "traffic_latest.json"))
+a = ap.parse_args()
+
+files = glob.glob(os.path.join(a.pmc_dir, "**", "*counter_collection.csv"), recursive=True)
+per_dispatch = {}
+for f in files:
+    for row in csv.DictReader(open(f)):
+        if "scan_main_kernel" not in row.get("Kernel_Name", "") or row.get("Counter_Name") != "FETCH_SIZE":
+            continue
+        key = (f, row.get("Dispatch_Id"))
+        per_dispatch[key] = per_dispatch.get(key, 0.0) + float(row["Counter_Value"])
+vals = sorted(per_dispatch.values())
+if not vals:
+    raise SystemExit("no scan_main_kernel FETCH_SIZE rows found")
+kib = statistics.median(vals)
+size = int(a.size_gib * (1 << 30)) // 8 * 8
+out = {"size": size, "avg": a.avg, "workload": a.workload, "dispatches": len(vals),
+       "fetch_size_kib_median": kib, "hbm_bytes_per_launch": int(kib * 1024 * 2),
+       "ratio_to_algorithmic": kib * 1024 * 2 / size,
+       "note": "FETCH_SIZE x 1024 x 2 (gfx950 half-count correction), median over dispatches"}
+json.dump(out, open(a.out, "w"), indent=1)
+print(json.dumps(out))
