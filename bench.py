@@ -43,6 +43,25 @@ def parse():
     return ap.parse_args()
 
 
+def stream_seed(workload: str, rank: int) -> int:
+    """Config 4: every GPU chunks its own independent stream (seed + rank)."""
+    return SEEDS[workload] + rank
+
+
+def aggregate(elapsed: float, nbytes: int, dist, device):
+    """Whole-job numbers for N ranks: the slowest rank's time (MAX) and all ranks'
+    bytes (SUM), one all-reduce each (RCCL on GPUs, gloo in the CPU tests)."""
+    import torch
+
+    if dist is None:
+        return elapsed, float(nbytes)
+    mx = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    tot = torch.tensor([float(nbytes)], dtype=torch.float64, device=device)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    return float(mx.item()), float(tot.item())
+
+
 def cpu_baseline(args, workload, seed, avg):
     """The oracle (faithful C restatement of chunker.rs) on the host cores, on a bounded
     sample of the same stream: `threads` threads each chunk their own sample slice."""
@@ -102,7 +121,7 @@ def main():
     import pbschunk
 
     size = int(args.size_gib * (1 << 30)) // 8 * 8
-    seed = SEEDS[args.workload] + rank  # config 4: independent stream per GPU
+    seed = stream_seed(args.workload, rank)
     buf = torch.empty(size, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     pbschunk.generate_device(buf.data_ptr(), size, GEN[args.workload], seed, 0, stream.cuda_stream)
@@ -132,15 +151,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist:
-        e = torch.tensor([elapsed, float(size)], dtype=torch.float64, device=dev)
-        mx = e.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(e, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0].item())
-        total_bytes = float(e[1].item())
-    else:
-        total_bytes = float(size)
+    elapsed, total_bytes = aggregate(elapsed, size, dist, dev)
 
     step_s = elapsed / max(1, args.steps)
     value = total_bytes * args.steps / (1 << 30) / elapsed
