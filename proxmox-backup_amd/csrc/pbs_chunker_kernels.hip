@@ -61,6 +61,39 @@ namespace pbs {
 // before this buffer); bytes before that do not exist and contribute nothing, as in
 // the reference's fill phase.  Position p is a candidate iff the window is full
 // (p + pre_len >= 63) and (H(p) & mask) >= minimum; it is written as base + p.
+// Exact hash at positions [B, B+128) of one block, window bytes [B-64, B+128).
+// Fast path (the whole window inside `data`, 16-byte aligned since B % 128 == 0): the
+// 192 bytes come in with 12 x 16-byte loads and the roll is fully unrolled from
+// registers.  Otherwise (stream head with `pre` bytes, ragged tail) a byte-wise loop.
+__device__ __forceinline__ void exact_block_fast(const uint8_t* __restrict__ data, uint64_t B,
+                                                 const uint32_t* tab, uint32_t mask,
+                                                 uint32_t minimum, uint64_t base,
+                                                 uint64_t* __restrict__ cand,
+                                                 uint32_t* __restrict__ ncand, uint32_t cand_cap) {
+    uint32_t w[48];
+    const uint4* src = reinterpret_cast<const uint4*>(data + B - 64);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const uint4 v = src[k];
+        w[4 * k] = v.x;
+        w[4 * k + 1] = v.y;
+        w[4 * k + 2] = v.z;
+        w[4 * k + 3] = v.w;
+    }
+    uint32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < 192; ++i) {
+        const uint32_t bin = (w[i >> 2] >> ((i & 3) * 8)) & 0xffu;
+        uint32_t x = tab[bin];
+        if (i >= 64) x ^= tab[(w[(i - 64) >> 2] >> (((i - 64) & 3) * 8)) & 0xffu];
+        h = ((h << 1) | (h >> 31)) ^ x;
+        if (i >= 64 && (h & mask) >= minimum) {
+            const uint32_t idx = atomicAdd(ncand, 1u);
+            if (idx < cand_cap) cand[idx] = base + B + (uint64_t)(i - 64);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void scan_exact_kernel(
     const uint8_t* __restrict__ data, uint64_t len, const uint8_t* __restrict__ pre,
     uint32_t pre_len, const uint64_t* __restrict__ susp, const uint32_t* __restrict__ nsusp,
@@ -82,6 +115,10 @@ __global__ __launch_bounds__(256) void scan_exact_kernel(
             B = 0;
         else
             B = (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
+        if (B >= 64 && B + kIter <= len && ((uintptr_t)(data + B - 64) & 15) == 0) {
+            exact_block_fast(data, B, tab, mask, minimum, base, cand, ncand, cand_cap);
+            continue;
+        }
         const uint64_t end = B + kIter < len ? B + kIter : len;
         uint32_t h = 0;
         const int64_t q0 = (int64_t)B - 64;

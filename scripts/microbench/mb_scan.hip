@@ -156,14 +156,30 @@ int main(int argc, char** argv) {
         char nm[96]; snprintf(nm, sizeof nm, "v5 SEG=%d mode=%d aux=%d susp=%u", SEG, MODE, AUX, h_cnt); \
         report(nm, best);                                                                   \
     }
+#define RUN6(SEG, MODE, AUX, G)                                                             \
+    if (only < 0 || only == vid++) {                                                        \
+        float best = 1e30f; uint32_t h_cnt = 0;                                             \
+        const uint64_t tiles = n / (64ull * SEG);                                           \
+        for (int r = 0; r < reps; ++r) {                                                    \
+            CK(hipMemset(cnt, 0, 16));                                                      \
+            CK(hipEventRecord(e0));                                                         \
+            hipLaunchKernelGGL((pbs::scan_main_v6<SEG, MODE, AUX, G>), dim3(cu), dim3(8 * 64), 0, 0, \
+                               d, tiles, tab, thr, susp, cnt, 1u << 21);                    \
+            CK(hipGetLastError());                                                          \
+            CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));                            \
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = ms < best ? ms : best;   \
+            CK(hipMemcpy(&h_cnt, cnt, 4, hipMemcpyDeviceToHost));                           \
+        }                                                                                   \
+        char nm[96]; snprintf(nm, sizeof nm, "v6 SEG=%d mode=%d aux=%d G=%d susp=%u", SEG, MODE, AUX, G, h_cnt); \
+        report(nm, best);                                                                   \
+    }
     RUN3(32768, 0, 2, 4, 0)
-    RUN5(32768, 0, 2)
-    RUN5(32768, 1, 2)
-    RUN5(32768, 0, 0)
-    RUN5(32768, 1, 0)
-    RUN5(32768, 0, 1)
-    RUN5(8192, 0, 2)
+    RUN6(32768, 0, 2, 4)
+    RUN6(32768, 1, 2, 4)
+    RUN6(32768, 2, 2, 4)
     RUN4(32768, 0, 2, 4)
+    RUN6(16384, 0, 2, 4)
     RUN3(32768, 0, 2, 4, 0)
+    RUN6(32768, 0, 2, 4)
     return 0;
 }

@@ -425,6 +425,146 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_v4(
 }
 
 // ---------------------------------------------------------------------------------
+// v6: v4 with the loads in inline asm and hand-counted vmcnt (the compiler drained
+// both batches at the loop head in v4).  v4: register-staged loads, two iterations in flight per wave.  Each iteration the
+// wave's 8 x 1 KiB pieces (8 segments x 128-byte lines each) arrive by
+// buffer_load_dwordx4 (nt) into one of two 32-VGPR batches, are written to the wave's
+// 8 KiB LDS stage (linear, conflict-free ds_write_b128) and read back transposed
+// (each lane its own 128 bytes, swizzled ds_read_b128).  Loads for step q+2 are
+// issued as soon as step q's batch is in LDS, so ~2 iterations hide HBM latency
+// without a second LDS stage.
+template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4>
+__global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_v6(
+    const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
+    uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {
+    static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
+    constexpr int NW = kWavesPerWG;
+    __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < kTableDwords; i += NW * 64) s_lds[i] = table_rot[i >> 6];
+    __syncthreads();
+
+    uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
+    const uint32_t lanebase = (uint32_t)lane * 4u;
+    uint32_t voff[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t l = 8u * j + ((uint32_t)lane >> 3);
+        const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
+        voff[j] = l * (uint32_t)SEG + k * 16u;
+    }
+    const uint32_t wr_base = (uint32_t)lane * 16u;  // piece j lands at j*1024 + lane*16
+    const uint32_t rd_base = (uint32_t)lane * 128u;
+    const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
+
+    constexpr int NIT = SEG / kIter + 1;
+    const uint64_t nw = (uint64_t)gridDim.x * NW;
+    uint64_t tile = (uint64_t)blockIdx.x * NW + wave;
+    if (tile >= ntiles) return;
+    int it = 0;
+    uint64_t t1 = tile, t2;
+    int it1 = 1, it2;
+    if (it1 == NIT) { it1 = 0; t1 += nw; }
+    t2 = t1; it2 = it1 + 1;
+    if (it2 == NIT) { it2 = 0; t2 += nw; }
+
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    auto load = [&](uint64_t t, int itx, v4i (&g)[8]) {
+        const uint8_t* tb = data + t * (64ull * SEG);
+        const bool first = (t == 0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(first ? tb : tb - kIter), 0, (int)(64u * SEG + kIter), 0x00020000);
+        const uint32_t soff = (uint32_t)itx * kIter - (first ? (uint32_t)kIter : 0u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen nt" : "=v"(g[j]) : "v"(voff[j]), "s"(rs), "s"(soff) : "memory");
+    };
+
+    uint32_t ring[128];
+#pragma unroll
+    for (int r = 0; r < 128; ++r) ring[r] = 0;
+    uint32_t h = 0;
+    v4i gA[8], gB[8];
+
+    auto step = [&](v4i (&g)[8]) -> bool {
+        // this step's batch landed; the next step's batch (8 loads) may stay in flight
+        if (t1 < ntiles && MODE != kModeComputeOnly)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // batch -> LDS stage (linear) -> own 128 bytes (swizzled)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *(v4i*)(stage + j * 1024 + wr_base) = g[j];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint32_t d[32];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint4 v = *(const uint4*)(stage + rd_base + (((uint32_t)k ^ rsw) << 4));
+            d[4 * k] = v.x;
+            d[4 * k + 1] = v.y;
+            d[4 * k + 2] = v.z;
+            d[4 * k + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (MODE != kModeComputeOnly && t2 < ntiles) load(t2, it2, g);  // step q+2
+        if (it == 0) {
+            h = 0;
+#pragma unroll
+            for (int r = 64; r < 128; ++r) ring[r] = 0;
+        }
+        uint32_t acc;
+        if constexpr (MODE == kModeLoadOnly) {
+            acc = 0;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) acc ^= d[k];
+            acc = (acc == 0x9E3779B9u && lane == 65) ? 0xFFFFFFFFu : 0u;
+        } else if constexpr (G == 4) {
+            acc = roll128_asm_g4(d, ring, h, lanebase);
+        } else {
+            acc = roll128_asm(d, ring, h, lanebase);
+        }
+        if (it == 0) {
+            if (tile == 0 && lane == 0) {
+                h = 0;
+#pragma unroll
+                for (int r = 64; r < 128; ++r) ring[r] = 0;
+            }
+        } else if (acc >= thr) {
+            const uint64_t pos =
+                (tile * 64ull + (uint64_t)lane) * (uint64_t)SEG + (uint64_t)(it - 1) * kIter;
+            if (pos != 0) {
+                const uint32_t idx = atomicAdd(nsusp, 1u);
+                if (idx < cap) susp[idx] = pos;
+            }
+        }
+        tile = t1;
+        it = it1;
+        t1 = t2;
+        it1 = it2;
+        if (++it2 == NIT) {
+            it2 = 0;
+            t2 += nw;
+        }
+        return tile < ntiles;
+    };
+
+    load(tile, 0, gA);
+    if (t1 < ntiles) load(t1, it1, gB);
+    else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gB[j] = v4i{0, 0, 0, 0};
+    }
+    for (;;) {
+        if (!step(gA)) break;
+        if (!step(gB)) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------
 // v5 (experiment): every lane loads its own segment's 128 bytes straight into VGPRs
 // (8 x buffer_load_dwordx4 at per-lane offset lane*SEG, 64 lines per instruction),
 // two iterations in flight, no LDS staging.
