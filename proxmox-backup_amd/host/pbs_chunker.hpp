@@ -1,0 +1,184 @@
+// C++ host mirror of proxmox-backup's chunker interface over the C ABI
+// (include/pbs_chunker.h).  Header-only; link with libpbschunk.so.
+//
+//   pbs::Chunker            pbs-datastore/src/chunker.rs:18-186   (new / scan)
+//   pbs::ChunkStream        pbs-client/src/chunk_stream.rs:12-78  (pull iterator of chunks)
+//   pbs::DynamicChunkWriter pbs-datastore/src/dynamic_index.rs:397-523 (write / close)
+//
+// Same names, argument meaning and error behaviour as the reference: a non-power-of-two
+// average throws std::invalid_argument with the reference's panic text; `scan` is
+// infallible in the reference, so a device error throws std::runtime_error (the Rust
+// shim in INTEGRATION.md panics at the same point).  The hash scan runs on the GPU.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "pbs_chunker.h"
+
+namespace pbs {
+
+class Chunker {
+  public:
+    explicit Chunker(size_t chunk_size_avg) {
+        int err = 0;
+        h_ = pbs_chunker_new(chunk_size_avg, &err);
+        if (!h_) {
+            if (err == PBS_ERR_NOT_POW2)
+                throw std::invalid_argument("got unexpected chunk size - not a power of two.");
+            throw std::runtime_error(std::string("pbs_chunker_new: ") + pbs_strerror(err));
+        }
+    }
+    Chunker(const Chunker&) = delete;
+    Chunker& operator=(const Chunker&) = delete;
+    Chunker(Chunker&& o) noexcept : h_(std::exchange(o.h_, nullptr)) {}
+    Chunker& operator=(Chunker&& o) noexcept {
+        if (this != &o) {
+            reset_handle();
+            h_ = std::exchange(o.h_, nullptr);
+        }
+        return *this;
+    }
+    ~Chunker() { reset_handle(); }
+
+    // chunker.rs:112 -- 0 if no boundary in `data` (all consumed), else the position
+    // just after the cut byte, relative to `data`.
+    size_t scan(const uint8_t* data, size_t len) {
+        const size_t r = pbs_chunker_scan(h_, data, len);
+        if (r == SIZE_MAX)
+            throw std::runtime_error(std::string("pbs_chunker_scan: ") +
+                                     pbs_strerror(pbs_chunker_last_error(h_)));
+        return r;
+    }
+    size_t scan(const std::vector<uint8_t>& v) { return scan(v.data(), v.size()); }
+
+    // All chunk END offsets (absolute) decided inside `data`; with is_final the tail too.
+    std::vector<uint64_t> find_cuts(const uint8_t* data, size_t len, bool is_final = false) {
+        std::vector<uint64_t> out(pbs_chunker_max_cuts(len));
+        size_t n = 0;
+        const int rc = pbs_chunker_find_cuts(h_, data, len, is_final ? 1 : 0, out.data(),
+                                             out.size(), &n);
+        if (rc != PBS_OK)
+            throw std::runtime_error(std::string("pbs_chunker_find_cuts: ") + pbs_strerror(rc));
+        out.resize(n);
+        return out;
+    }
+
+    pbs_chunker* handle() const { return h_; }
+
+  private:
+    void reset_handle() {
+        if (h_) pbs_chunker_free(h_);
+        h_ = nullptr;
+    }
+    pbs_chunker* h_ = nullptr;
+};
+
+// ChunkStream: `next()` pulls input pieces from `source` (returns false at EOF) and
+// yields chunks; the remainder is yielded at EOF (chunk_stream.rs:64-68).
+class ChunkStream {
+  public:
+    using Source = std::function<bool(std::vector<uint8_t>&)>;
+    explicit ChunkStream(Source source, std::optional<size_t> chunk_size = std::nullopt)
+        : source_(std::move(source)), chunker_(chunk_size.value_or(4 * 1024 * 1024)) {}
+
+    std::optional<std::vector<uint8_t>> next() {
+        for (;;) {
+            if (scan_pos_ < buffer_.size()) {
+                const size_t boundary =
+                    chunker_.scan(buffer_.data() + scan_pos_, buffer_.size() - scan_pos_);
+                const size_t chunk_size = scan_pos_ + boundary;
+                if (boundary == 0) {
+                    scan_pos_ = buffer_.size();
+                } else if (chunk_size <= buffer_.size()) {
+                    std::vector<uint8_t> out(buffer_.begin(), buffer_.begin() + chunk_size);
+                    buffer_.erase(buffer_.begin(), buffer_.begin() + chunk_size);
+                    scan_pos_ = 0;
+                    return out;
+                } else {
+                    throw std::logic_error("got unexpected chunk boundary from chunker");
+                }
+            }
+            std::vector<uint8_t> piece;
+            if (!source_(piece)) {
+                scan_pos_ = 0;
+                if (buffer_.empty()) return std::nullopt;
+                std::vector<uint8_t> out;
+                out.swap(buffer_);
+                return out;
+            }
+            buffer_.insert(buffer_.end(), piece.begin(), piece.end());
+        }
+    }
+
+  private:
+    Source source_;
+    Chunker chunker_;
+    std::vector<uint8_t> buffer_;
+    size_t scan_pos_ = 0;
+};
+
+// DynamicChunkWriter: `write` returns the bytes consumed (the caller re-submits the
+// rest, as write_all does); every finished chunk goes to sink(chunk_end_offset, bytes)
+// in place of the digest/compress/insert/add_chunk step (dynamic_index.rs:444-490).
+class DynamicChunkWriter {
+  public:
+    using Sink = std::function<void(uint64_t, const std::vector<uint8_t>&)>;
+    DynamicChunkWriter(Sink sink, size_t chunk_size) : sink_(std::move(sink)), chunker_(chunk_size) {
+        chunk_buffer_.reserve(chunk_size * 4);
+    }
+
+    size_t write(const uint8_t* data, size_t len) {
+        const size_t pos = chunker_.scan(data, len);
+        if (pos > 0) {
+            chunk_buffer_.insert(chunk_buffer_.end(), data, data + pos);
+            chunk_offset_ += pos;
+            write_chunk_buffer();
+            return pos;
+        }
+        chunk_offset_ += len;
+        chunk_buffer_.insert(chunk_buffer_.end(), data, data + len);
+        return len;
+    }
+
+    void write_all(const uint8_t* data, size_t len) {
+        while (len) {
+            const size_t k = write(data, len);
+            data += k;
+            len -= k;
+        }
+    }
+
+    void close() {
+        if (closed_) return;
+        closed_ = true;
+        write_chunk_buffer();
+    }
+
+    uint64_t chunk_count() const { return chunk_count_; }
+
+  private:
+    void write_chunk_buffer() {
+        if (chunk_buffer_.empty()) return;
+        if (chunk_offset_ - last_chunk_ != chunk_buffer_.size())
+            throw std::logic_error("wrong chunk size");
+        ++chunk_count_;
+        last_chunk_ = chunk_offset_;
+        sink_(chunk_offset_, chunk_buffer_);
+        chunk_buffer_.clear();
+    }
+
+    Sink sink_;
+    Chunker chunker_;
+    std::vector<uint8_t> chunk_buffer_;
+    uint64_t chunk_offset_ = 0, last_chunk_ = 0, chunk_count_ = 0;
+    bool closed_ = false;
+};
+
+}  // namespace pbs

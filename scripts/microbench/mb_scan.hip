@@ -174,12 +174,10 @@ int main(int argc, char** argv) {
         report(nm, best);                                                                   \
     }
     RUN3(32768, 0, 2, 4, 0)
+    RUN3(32768, 1, 2, 4, 0)
+    RUN3(32768, 2, 2, 4, 0)
     RUN6(32768, 0, 2, 4)
     RUN6(32768, 1, 2, 4)
     RUN6(32768, 2, 2, 4)
-    RUN4(32768, 0, 2, 4)
-    RUN6(16384, 0, 2, 4)
-    RUN3(32768, 0, 2, 4, 0)
-    RUN6(32768, 0, 2, 4)
     return 0;
 }

@@ -1,0 +1,90 @@
+// Drives the C++ host mirror (proxmox-backup_amd/host/pbs_chunker.hpp) the way the
+// reference's callers do, and prints the chunk END offsets per caller, one line each:
+//   scan <ends...>      Chunker::scan loop of test_chunker1's test2 (chunker.rs:246-257)
+//   stream <ends...>    ChunkStream over pieces of `piece` bytes (chunk_stream.rs:40-77)
+//   writer <ends...>    DynamicChunkWriter via write_all (dynamic_index.rs:493-515)
+//   batch <ends...>     find_cuts(is_final)
+// usage: host_mirror <avg> <len> <seed> <piece>   (input: splitmix64 random stream)
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "pbs_chunker.hpp"
+
+static uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static void print(const char* tag, const std::vector<uint64_t>& v) {
+    std::printf("%s", tag);
+    for (uint64_t e : v) std::printf(" %llu", (unsigned long long)e);
+    std::printf("\n");
+}
+
+int main(int argc, char** argv) {
+    if (argc != 5) {
+        std::fprintf(stderr, "usage: %s avg len seed piece\n", argv[0]);
+        return 2;
+    }
+    const size_t avg = std::strtoull(argv[1], nullptr, 0), len = std::strtoull(argv[2], nullptr, 0);
+    const uint64_t seed = std::strtoull(argv[3], nullptr, 0);
+    const size_t piece = std::strtoull(argv[4], nullptr, 0);
+    std::vector<uint8_t> data(len);
+    for (size_t x = 0; x < len; ++x) data[x] = (uint8_t)(splitmix64(seed ^ (x >> 3)) >> ((x & 7) * 8));
+    try {
+        {
+            pbs::Chunker c(avg);
+            std::vector<uint64_t> ends;
+            size_t pos = 0;
+            while (pos < len) {
+                const size_t k = c.scan(data.data() + pos, len - pos);
+                if (k == 0) break;
+                pos += k;
+                ends.push_back(pos);
+            }
+            print("scan", ends);
+        }
+        {
+            size_t off = 0;
+            pbs::ChunkStream s([&](std::vector<uint8_t>& out) {
+                if (off >= len) return false;
+                const size_t n = std::min(piece, len - off);
+                out.assign(data.begin() + off, data.begin() + off + n);
+                off += n;
+                return true;
+            }, avg);
+            std::vector<uint64_t> ends;
+            uint64_t total = 0;
+            while (auto ch = s.next()) {
+                total += ch->size();
+                ends.push_back(total);
+            }
+            print("stream", ends);
+        }
+        {
+            std::vector<uint64_t> ends;
+            pbs::DynamicChunkWriter w([&](uint64_t end, const std::vector<uint8_t>&) { ends.push_back(end); }, avg);
+            for (size_t off = 0; off < len; off += piece)
+                w.write_all(data.data() + off, std::min(piece, len - off));
+            w.close();
+            print("writer", ends);
+        }
+        {
+            pbs::Chunker c(avg);
+            print("batch", c.find_cuts(data.data(), len, true));
+        }
+        try {
+            pbs::Chunker bad(avg + 1 == 2 ? 3 : avg + 1);
+            std::printf("badavg accepted\n");
+        } catch (const std::invalid_argument& e) {
+            std::printf("badavg %s\n", e.what());
+        }
+    } catch (const std::exception& e) {
+        std::printf("error %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

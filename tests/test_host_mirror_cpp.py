@@ -1,0 +1,43 @@
+"""The C++ host mirror (proxmox-backup_amd/host/pbs_chunker.hpp): compiles against the
+C ABI on CPU; on the GPU its ChunkStream / DynamicChunkWriter / scan loop / find_cuts
+give the oracle's cut list."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "host_mirror_main.cpp")
+LIBDIR = os.path.join(ROOT, "proxmox-backup_amd", "csrc")
+
+
+def _build(tmp_path):
+    exe = str(tmp_path / "host_mirror")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(ROOT, "proxmox-backup_amd", "host"), SRC, "-L", LIBDIR,
+                    "-lpbschunk", f"-Wl,-rpath,{LIBDIR}", "-o", exe], check=True)
+    return exe
+
+
+def test_host_mirror_compiles_and_fails_loudly_without_device(tmp_path, pbschunk):
+    exe = _build(tmp_path)
+    if pbschunk.device_count() > 0:
+        pytest.skip("device visible: covered by the gpu test")
+    r = subprocess.run([exe, "65536", "100000", "1", "4096"], capture_output=True, text=True)
+    assert r.returncode == 1 and "no HIP device" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("avg,n,piece", [(4096, 3 << 20, 65536), (65536, 9 << 20, 262144), (64, 200000, 1000)])
+def test_host_mirror_matches_oracle(tmp_path, gpu, oracle, avg, n, piece):
+    exe = _build(tmp_path)
+    r = subprocess.run([exe, str(avg), str(n), "7", str(piece)], capture_output=True, text=True, check=True)
+    lines = {ln.split(" ", 1)[0]: ln.split()[1:] for ln in r.stdout.strip().splitlines()}
+    data = oracle.gen_random(n, 7)
+    ref = oracle.chunk_feed(avg, data).tolist()
+    assert [int(x) for x in lines["scan"]] == ref
+    for tag in ("stream", "writer", "batch"):
+        ends = [int(x) for x in lines[tag]]
+        assert ends[:-1] == ref and ends[-1] == n, tag
+    assert "not a power of two" in " ".join(lines["badavg"])
