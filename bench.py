@@ -5,6 +5,9 @@ One "step" = one pass of the chunker over the whole device-resident synthetic st
 Default workload = BASELINE config 3: 64 GiB VM-image-like stream, 4 MiB average.
 Multi-GPU (config 4): one independent stream per rank (seed + rank), no data-path
 collective; an all-reduce (RCCL) of the per-rank elapsed time (MAX) and byte count.
+--mode sharded: ONE stream of --size-gib split over the ranks (strong scaling; SURVEY
+8(e)): halo all-gather, per-rank phase A, candidate all-gather, resolve on every rank
+(proxmox-backup_amd/shard.py).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size-gib 64] [--avg 4194304]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -33,6 +36,9 @@ def parse():
     ap.add_argument("--size-gib", type=float, default=64.0)
     ap.add_argument("--avg", type=int, default=4 * 1024 * 1024)
     ap.add_argument("--workload", choices=list(GEN), default="vmimage")
+    ap.add_argument("--mode", choices=["streams", "sharded"], default="streams",
+                    help="streams: one independent stream per GPU (config 4); "
+                         "sharded: one stream split over the GPUs")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-sample-mib", type=int, default=512)
@@ -121,18 +127,33 @@ def main():
     import pbschunk
 
     size = int(args.size_gib * (1 << 30)) // 8 * 8
-    seed = stream_seed(args.workload, rank)
-    buf = torch.empty(size, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
-    pbschunk.generate_device(buf.data_ptr(), size, GEN[args.workload], seed, 0, stream.cuda_stream)
-    torch.cuda.synchronize()
-
     ch = pbschunk.Chunker(args.avg)
     ch.set_stream(stream.cuda_stream)
-    ptr = buf.data_ptr()
+    if args.mode == "sharded":
+        import shard
+        seed = SEEDS[args.workload]  # one stream; this rank generates its range of it
+        base, local = shard.shard_ranges(size, world)[rank]
+        buf = torch.empty(local, dtype=torch.uint8, device=dev)
+        pbschunk.generate_device(buf.data_ptr(), local, GEN[args.workload], seed, base,
+                                 stream.cuda_stream)
+        torch.cuda.synchronize()
+        ptr, tail = buf.data_ptr(), buf[max(0, local - shard.HALO):]
 
-    def step():
-        return ch.find_cuts_device(ptr, size, is_final=True)
+        def step():
+            return shard.chunk_sharded(ch, ptr, local, base, size, tail, dist, rank, world, dev)
+        work_bytes = local
+    else:
+        seed = stream_seed(args.workload, rank)
+        buf = torch.empty(size, dtype=torch.uint8, device=dev)
+        pbschunk.generate_device(buf.data_ptr(), size, GEN[args.workload], seed, 0,
+                                 stream.cuda_stream)
+        torch.cuda.synchronize()
+        ptr = buf.data_ptr()
+
+        def step():
+            return ch.find_cuts_device(ptr, size, is_final=True)
+        work_bytes = size
 
     for _ in range(args.warmup):
         step()
@@ -151,23 +172,24 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    elapsed, total_bytes = aggregate(elapsed, size, dist, dev)
+    elapsed, total_bytes = aggregate(elapsed, work_bytes, dist, dev)
 
     step_s = elapsed / max(1, args.steps)
     value = total_bytes * args.steps / (1 << 30) / elapsed
     avg_scan_s = float(np.mean(scan_ms)) / 1e3 if scan_ms else float("nan")
-    achieved = size / avg_scan_s / 1e9  # algorithmic bytes (input read once) per launch
+    achieved = work_bytes / avg_scan_s / 1e9  # algorithmic bytes (input read once) per launch
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("size") == size and tj.get("avg") == args.avg and tj.get("workload") == args.workload:
+        if (tj.get("size") == work_bytes and tj.get("avg") == args.avg
+                and tj.get("workload") == args.workload and args.mode == "streams"):
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
 
     host_incl = None
-    if rank == 0 and world == 1 and args.host_inclusive_gib > 0:
+    if rank == 0 and world == 1 and args.host_inclusive_gib > 0 and args.mode == "streams":
         hn = int(args.host_inclusive_gib * (1 << 30)) // 8 * 8
         hbuf = buf[:hn].cpu().numpy()  # pageable host copy of the stream prefix
         ch2 = pbschunk.Chunker(args.avg)
@@ -191,14 +213,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.mode == "streams" else "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic ({args.workload} generator, seed {hex(SEEDS[args.workload])}+rank, "
                 f"generated in HBM before timing)",
         "config": {"workload": f"{args.workload}-{args.size_gib:g}GiB-avg{args.avg}",
-                   "stream_bytes_per_gpu": size, "avg_chunk": args.avg,
-                   "parallelism": f"independent stream per GPU x{world}",
+                   "stream_bytes_per_gpu": work_bytes, "avg_chunk": args.avg,
+                   "parallelism": (f"independent stream per GPU x{world}" if args.mode == "streams"
+                                   else f"one stream sharded over {world} GPU(s)"),
                    "chunks_per_stream": ncuts, "candidates_per_stream": cand},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -64,8 +64,8 @@ size_t pbs_chunker_scan(pbs_chunker *c, const uint8_t *data, size_t len);
  * inside `data` to `out` (ascending) and their number to *n_out.  With is_final != 0
  * the tail chunk's end (the stream length) is appended if the tail is non-empty, as
  * ChunkStream does at EOF (chunk_stream.rs:64-68), and the handle starts a new
- * stream.  `cap` must be >= pbs_chunker_max_cuts(len) (else PBS_ERR_CAPACITY and no
- * state change).  Returns PBS_OK or an error code. */
+ * stream.  `cap` must be >= pbs_chunker_cuts_bound(c, len) (else PBS_ERR_CAPACITY and
+ * no state change).  Returns PBS_OK or an error code. */
 int pbs_chunker_find_cuts(pbs_chunker *c, const uint8_t *data, size_t len, int is_final,
                           uint64_t *out, size_t cap, size_t *n_out);
 
@@ -74,8 +74,13 @@ int pbs_chunker_find_cuts(pbs_chunker *c, const uint8_t *data, size_t len, int i
 int pbs_chunker_find_cuts_device(pbs_chunker *c, const uint8_t *dev_data, size_t len,
                                  int is_final, uint64_t *out, size_t cap, size_t *n_out);
 
-/* Upper bound of the cuts one find_cuts call over `len` bytes can return. */
+/* Upper bound of the cuts one find_cuts call over `len` bytes can return, for any
+ * average (every chunk but the tail is >= 65 bytes long). */
 size_t pbs_chunker_max_cuts(size_t len);
+
+/* The same bound for this handle's average: every chunk that starts and ends inside
+ * the call is >= max(avg/4, 65) bytes long (chunker.rs:172-183), so len/that + 3. */
+size_t pbs_chunker_cuts_bound(const pbs_chunker *c, size_t len);
 
 /* Absolute offset of the next unconsumed byte and of the open chunk's start. */
 uint64_t pbs_chunker_stream_offset(const pbs_chunker *c);
@@ -103,6 +108,31 @@ typedef struct {
     uint64_t cuts;
 } pbs_timing;
 int pbs_chunker_last_timing(const pbs_chunker *c, pbs_timing *t);
+
+/* ---- one stream sharded over several GPUs ------------
+ * The cut test is a pure function of the 64-byte window (chunker.rs:146: rotl by 64 is
+ * the identity), so contiguous ranges of one stream are scanned independently given
+ * the 63 bytes before each range (a halo exchanged between neighbours); the sorted
+ * per-range candidate lists concatenate into the stream's list (one all-gather), and
+ * the min/max rule (chunker.rs:172-183) is resolved once over it. */
+
+/* Phase A over the device range holding stream bytes [base, base + len): every
+ * position p in it with p >= 63 whose window hash passes the cut test, ascending and
+ * absolute, to `out_dev` (device memory, cap entries).  `pre` holds the
+ * pre_len = min(base, 63) stream bytes before `base` (host memory).  *n_out receives
+ * the number of candidates, also when it exceeds cap (then PBS_ERR_CAPACITY and
+ * nothing is written).  Complete on return; the handle's stream state is untouched. */
+int pbs_chunker_candidates_device(pbs_chunker *c, const uint8_t *dev, size_t len,
+                                  const uint8_t *pre, size_t pre_len, uint64_t base,
+                                  uint64_t *out_dev, size_t cap, size_t *n_out);
+
+/* Phase B: the cut list (chunk END offsets, host `out`, cap >= cuts_bound(c, end))
+ * of a stream of `end` bytes from its complete sorted candidate list (device, n
+ * entries, all < end), from the stream start; is_final appends the tail like
+ * find_cuts.  Restarts the handle's stream (before and after).  last_timing keeps
+ * the phase-A fields of the preceding candidates_device call. */
+int pbs_chunker_resolve_device(pbs_chunker *c, const uint64_t *cand_dev, size_t n, uint64_t end,
+                               int is_final, uint64_t *out, size_t cap, size_t *n_out);
 
 /* ---- helpers for tests and the benchmark harness ------------------------------ */
 

@@ -8,10 +8,13 @@
 //   1. scan_main_kernel   flags 128-byte blocks holding a hash candidate (HBM-bound scan)
 //   2. scan_exact_kernel  exact candidate positions in flagged blocks, the stream head
 //                         block and the tail that does not fill a wave tile
-//   3. radix sort of the candidate positions (hipcub)
-//   4. resolve kernels    min/max chunk-size rule -> cut list (pointer doubling)
-// Steps 1-4 run on the handle's HIP stream; only the counts (8 bytes), the cut list
-// and the few candidates of the still-open chunk come back to the host.
+//   3. resolve            min/max chunk-size rule -> cut list (pointer doubling):
+//                         up to kSmallResolveMax candidates one workgroup sorts and
+//                         resolves in LDS and writes the cuts into mapped pinned memory;
+//                         above that a hipcub radix sort + the multi-kernel resolve
+// Steps 1-3 run on the handle's HIP stream with two host syncs per batch (candidate
+// counts, then results); only the counts, the cut list, the open chunk's candidates
+// and the 63-byte warm-up tail come back to the host.
 //
 // `Chunker::scan` semantics (stateful, 0 or the boundary relative to the slice) are
 // kept by tracking absolute offsets: consumed (caller position), chunk_start (open
@@ -21,6 +24,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -105,10 +110,14 @@ struct pbs_chunker {
     DevBuf d_table, d_pre, d_counters, d_susp, d_cand, d_C, d_sort_tmp, d_nxt, d_jtmp, d_nf, d_on,
         d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in;
     uint32_t susp_cap = 0, cand_cap = 0;
-    uint64_t* h_small = nullptr;  // pinned: counters / resolve results
-    hipEvent_t ev[5] = {};
+    uint64_t* h_small = nullptr;  // pinned + mapped: [0] counters, [8..19] results, [24..31] tail
+    uint64_t* h_cuts = nullptr;   // pinned + mapped: cut list of the small resolve
+    uint64_t* h_keep = nullptr;   // pinned + mapped: open-chunk candidates of the small resolve
+    // events: 0/1 main scan, 2 exact end, 3/4 resolve, 5 call start
+    hipEvent_t ev[6] = {};
     pbs_timing timing{};
     int last_error = 0;
+    bool debug_phases = false;  // PBS_DEBUG_PHASES=1: small-resolve phase times to stderr
 };
 
 namespace {
@@ -122,6 +131,10 @@ int fail(pbs_chunker* c, int code) {
     do {                                                \
         if ((x) != hipSuccess) return fail(c, PBS_ERR_HIP); \
     } while (0)
+
+constexpr uint64_t kHostCuts = 1ull << 20;  // h_cuts entries (8 MiB)
+constexpr uint64_t kHostKeep = 1ull << 16;  // h_keep entries
+constexpr size_t kSmallBytes = 256;         // h_small bytes
 
 uint64_t batch_max(const Params& p) {
     // keep 32-bit candidate counters safe for tiny averages
@@ -174,6 +187,7 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
                                      ext_count, head, p.mask, p.minimum, base,
                                      c->d_cand.as<uint64_t>(), d_ncand, c->cand_cap, max_items,
                                      c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
         HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_counters.p, 8, hipMemcpyDeviceToHost,
                                   c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -195,6 +209,8 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
     float ms = 0;
     HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     c->timing.scan_ms += ms;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+    c->timing.exact_ms += ms;
     c->timing.bytes += len;
     c->timing.suspects += nsusp;
     c->timing.candidates += ncand;
@@ -230,15 +246,26 @@ void update_carry(pbs_chunker* c, const uint8_t* tail, uint64_t tail_len) {
     c->carry_len = keep;
 }
 
-// Carry update from device-resident bytes.
-int update_carry_device(pbs_chunker* c, const uint8_t* d_src, uint64_t len) {
-    uint8_t tail[64];
-    const uint64_t t = std::min<uint64_t>(len, kWindow - 1);
-    if (t) {
-        HIP_TRY(c, hipMemcpyAsync(tail, d_src + len - t, t, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-    }
-    update_carry(c, tail, t);
+// Upper bound on the cuts a resolve from chunk_start over m candidates up to `end` can
+// emit: at most one per candidate plus the forced cuts, and at most one per 65 bytes.
+uint64_t cut_bound(const pbs_chunker* c, uint64_t m, uint64_t end) {
+    const uint64_t span = end > c->chunk_start ? end - c->chunk_start : 0;
+    return std::min<uint64_t>(span / 65, m + span / c->prm.max_eff) + 2;
+}
+
+// After a resolve: move chunk_start to the open chunk; pending = the open chunk's
+// candidates ++ older pending entries at/after `end` (not uploaded).
+int finish_resolve(pbs_chunker* c, uint64_t s_open, uint64_t end, std::vector<uint64_t>& keep,
+                   uint64_t ncut) {
+    c->chunk_start = s_open;
+    for (size_t i = c->pend_head; i < c->pending.size(); ++i)
+        if (c->pending[i] >= end) keep.push_back(c->pending[i]);
+    c->pending.swap(keep);
+    c->pend_head = 0;
+    float ms = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[3], c->ev[4]));
+    c->timing.resolve_ms += ms;
+    c->timing.cuts += ncut;
     return PBS_OK;
 }
 
@@ -260,10 +287,9 @@ int run_resolve(pbs_chunker* c, uint32_t m, uint64_t end, uint64_t* out, size_t 
     HIP_TRY(c, exclusive_sum_u64(nullptr, &tb, c->d_cnt.as<uint64_t>(), c->d_off.as<uint64_t>(),
                                  m + 1, c->stream));
     HIP_TRY(c, c->d_scan_tmp.ensure(tb));
-    const uint64_t span = end > c->chunk_start ? end - c->chunk_start : 0;
-    const uint64_t out_cap = span / 65 + 2;
+    const uint64_t out_cap = cut_bound(c, m, end);
     HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
-    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
     ResolveParams rp{p.min_eff, p.max_eff, end, c->chunk_start};
     HIP_TRY(c, launch_resolve(c->d_C.as<uint64_t>(), m, rp, c->d_nxt.as<uint32_t>(),
                               c->d_jtmp.as<uint32_t>(), c->d_nf.as<uint64_t>(),
@@ -282,20 +308,66 @@ int run_resolve(pbs_chunker* c, uint32_t m, uint64_t end, uint64_t* out, size_t 
     if (!keep.empty())
         HIP_TRY(c, hipMemcpyAsync(keep.data(), c->d_C.as<uint64_t>() + idx, keep.size() * 8,
                                   hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     *n += ncut;
-    c->chunk_start = s_open;
-    // pending = open-chunk candidates ++ older pending entries at/after `end` (not uploaded)
-    for (size_t i = c->pend_head; i < c->pending.size(); ++i)
-        if (c->pending[i] >= end) keep.push_back(c->pending[i]);
-    c->pending.swap(keep);
-    c->pend_head = 0;
-    float ms = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
-    c->timing.resolve_ms += ms;
-    c->timing.cuts += ncut;
-    return PBS_OK;
+    return finish_resolve(c, s_open, end, keep, ncut);
+}
+
+// Single-workgroup resolve (np + nnew + 2 <= kSmallResolveMax): pending candidates are
+// in d_C[0..np), the new unsorted ones in d_cand[0..nnew).  One host sync.
+int run_resolve_small(pbs_chunker* c, const uint64_t* newc, uint32_t np, uint32_t nnew,
+                      uint64_t end, uint64_t* out, size_t cap, size_t* n) {
+    const Params& p = c->prm;
+    const uint32_t m = np + nnew;
+    HIP_TRY(c, c->d_nxt.ensure(((size_t)m + 2) * 4));
+    HIP_TRY(c, c->d_nf.ensure(((size_t)m + 2) * 8));
+    HIP_TRY(c, c->d_res.ensure(32));
+    const uint64_t out_cap = cut_bound(c, m, end);
+    HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
+    if (!c->h_cuts) HIP_TRY(c, hipHostMalloc((void**)&c->h_cuts, kHostCuts * 8, hipHostMallocMapped));
+    if (!c->h_keep) HIP_TRY(c, hipHostMalloc((void**)&c->h_keep, kHostKeep * 8, hipHostMallocMapped));
+    uint64_t *cuts_dev = nullptr, *keep_dev = nullptr, *small_dev = nullptr;
+    HIP_TRY(c, hipHostGetDevicePointer((void**)&cuts_dev, c->h_cuts, 0));
+    HIP_TRY(c, hipHostGetDevicePointer((void**)&keep_dev, c->h_keep, 0));
+    HIP_TRY(c, hipHostGetDevicePointer((void**)&small_dev, c->h_small, 0));
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    ResolveParams rp{p.min_eff, p.max_eff, end, c->chunk_start};
+    HIP_TRY(c, launch_resolve_small(newc, nnew, c->d_C.as<uint64_t>(), np, rp,
+                                    c->d_nxt.as<uint32_t>(), c->d_nf.as<uint64_t>(),
+                                    c->d_cuts.as<uint64_t>(), out_cap, cuts_dev, kHostCuts,
+                                    keep_dev, kHostKeep, c->d_res.as<uint64_t>(), small_dev + 8,
+                                    c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const uint64_t ncut = c->h_small[8], s_open = c->h_small[9], idx = c->h_small[10];
+    if (c->debug_phases)
+        std::fprintf(stderr,
+                     "resolve_small m=%u hist %.1f bscan %.1f scatter %.1f isort %.1f next %.1f "
+                     "double %.1f scan %.1f emit %.1f copy %.1f us\n",
+                     m, c->h_small[11] / 100.0, c->h_small[12] / 100.0, c->h_small[13] / 100.0,
+                     c->h_small[14] / 100.0, c->h_small[15] / 100.0, c->h_small[16] / 100.0,
+                     c->h_small[17] / 100.0, c->h_small[18] / 100.0, c->h_small[19] / 100.0);
+    if (*n + ncut > cap || ncut > out_cap) return fail(c, PBS_ERR_CAPACITY);
+    const uint64_t nkeep = m > idx ? m - idx : 0;
+    std::vector<uint64_t> keep(nkeep);
+    bool wait = false;
+    if (ncut <= kHostCuts) {
+        std::memcpy(out + *n, c->h_cuts, ncut * 8);
+    } else {
+        HIP_TRY(c, hipMemcpyAsync(out + *n, c->d_cuts.p, ncut * 8, hipMemcpyDeviceToHost, c->stream));
+        wait = true;
+    }
+    if (nkeep <= kHostKeep) {
+        if (nkeep) std::memcpy(keep.data(), c->h_keep, nkeep * 8);
+    } else {
+        HIP_TRY(c, hipMemcpyAsync(keep.data(), c->d_C.as<uint64_t>() + idx, nkeep * 8,
+                                  hipMemcpyDeviceToHost, c->stream));
+        wait = true;
+    }
+    if (wait) HIP_TRY(c, hipStreamSynchronize(c->stream));
+    *n += ncut;
+    return finish_resolve(c, s_open, end, keep, ncut);
 }
 
 void reset_stream(pbs_chunker* c) {
@@ -305,21 +377,14 @@ void reset_stream(pbs_chunker* c) {
     c->pend_head = 0;
 }
 
-// Scan new bytes [pos, pos + bl) (device source `dsrc`, host mirror `hsrc` or NULL)
-// and append their sorted candidates either to d_C after `np` pending entries
-// (to_device) or to the host pending list.  Returns the number of new candidates.
-int scan_new_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos,
-                   uint64_t bl, size_t np, bool to_device, uint32_t* nnew) {
+// pbs_chunker_scan path: scan new host bytes [pos, pos + bl) (uploaded to `dsrc`) and
+// append their sorted candidates to the host pending list.
+int scan_host_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos,
+                    uint64_t bl) {
     uint32_t ncand = 0;
     int rc = scan_candidates(c, dsrc, bl, pos, &ncand);
     if (rc) return rc;
-    if (to_device) {
-        // d_C = [pending (np) | new sorted (ncand)]; pending is uploaded by the caller
-        // after this (d_C may be reallocated here).
-        HIP_TRY(c, c->d_C.ensure(((size_t)np + ncand + 2) * 8));
-        rc = sort_candidates(c, ncand, c->d_C.as<uint64_t>() + np);
-        if (rc) return rc;
-    } else if (ncand) {
+    if (ncand) {
         HIP_TRY(c, c->d_C.ensure(((size_t)ncand + 2) * 8));
         rc = sort_candidates(c, ncand, c->d_C.as<uint64_t>());
         if (rc) return rc;
@@ -327,22 +392,10 @@ int scan_new_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uin
         c->pending.resize(old + ncand);
         HIP_TRY(c, hipMemcpyAsync(c->pending.data() + old, c->d_C.p, (size_t)ncand * 8,
                                   hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
-    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->prm.hash_cuts && bl) {  // ev[1] was recorded by scan_candidates
-        float ms = 0;
-        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
-        c->timing.exact_ms += ms;
-    }
-    if (hsrc)
-        update_carry(c, hsrc, bl);
-    else {
-        rc = update_carry_device(c, dsrc, bl);
-        if (rc) return rc;
-    }
+    update_carry(c, hsrc, bl);
     c->scanned_end = pos + bl;
-    *nnew = ncand;
     return PBS_OK;
 }
 
@@ -351,10 +404,10 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
     if (!c) return PBS_ERR_INVALID;
     if (!n_out || (len && !data) || (!out && cap)) return fail(c, PBS_ERR_INVALID);
     *n_out = 0;
-    if (cap < pbs_chunker_max_cuts(len)) return fail(c, PBS_ERR_CAPACITY);
+    if (cap < pbs_chunker_cuts_bound(c, len)) return fail(c, PBS_ERR_CAPACITY);
     HIP_TRY(c, hipSetDevice(c->device));
     c->timing = pbs_timing{};
-    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[5], c->stream));
     const uint64_t end = c->consumed + len;
     uint64_t pos = std::max(c->consumed, c->scanned_end);
     size_t n = 0;
@@ -366,9 +419,9 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
         size_t np = 0;
         while (c->pend_head + np < c->pending.size() && c->pending[c->pend_head + np] < rend) ++np;
         uint32_t nnew = 0;
+        const uint8_t* dsrc = nullptr;
+        const uint8_t* hsrc = nullptr;
         if (bl) {
-            const uint8_t* dsrc;
-            const uint8_t* hsrc = nullptr;
             if (device) {
                 dsrc = data + (pos - c->consumed);
             } else {
@@ -377,18 +430,34 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
                 HIP_TRY(c, hipMemcpyAsync(c->d_in.p, hsrc, bl, hipMemcpyHostToDevice, c->stream));
                 dsrc = c->d_in.as<uint8_t>();
             }
-            int rc = scan_new_bytes(c, dsrc, hsrc, pos, bl, np, true, &nnew);
+            int rc = scan_candidates(c, dsrc, bl, pos, &nnew);  // host sync: counts
             if (rc) return rc;
-        } else {
-            HIP_TRY(c, c->d_C.ensure(((size_t)np + 2) * 8));
+        }
+        const uint64_t m = (uint64_t)np + nnew;
+        if (m > 0xFFFFFFF0ull) return fail(c, PBS_ERR_NOMEM);
+        const bool small = m + 2 <= kSmallResolveMax;
+        // d_C = [pending (np) | new (nnew)]; the small resolve sorts the new ones itself
+        HIP_TRY(c, c->d_C.ensure((size_t)(m + 2) * 8));
+        if (!small && nnew) {
+            int rc = sort_candidates(c, nnew, c->d_C.as<uint64_t>() + np);
+            if (rc) return rc;
         }
         if (np)
             HIP_TRY(c, hipMemcpyAsync(c->d_C.p, c->pending.data() + c->pend_head, np * 8,
                                       hipMemcpyHostToDevice, c->stream));
-        const uint64_t m = (uint64_t)np + nnew;
-        if (m > 0xFFFFFFF0ull) return fail(c, PBS_ERR_NOMEM);
-        int rc = run_resolve(c, (uint32_t)m, rend, out, cap, &n);
+        // warm-up tail of this batch for the next one (lands with the resolve's sync)
+        const uint64_t tl = std::min<uint64_t>(bl, kWindow - 1);
+        uint8_t* tail = reinterpret_cast<uint8_t*>(c->h_small + 24);
+        if (tl && device)
+            HIP_TRY(c, hipMemcpyAsync(tail, dsrc + bl - tl, tl, hipMemcpyDeviceToHost, c->stream));
+        int rc = small ? run_resolve_small(c, c->d_cand.as<uint64_t>(), (uint32_t)np, nnew, rend,
+                                           out, cap, &n)
+                       : run_resolve(c, (uint32_t)m, rend, out, cap, &n);
         if (rc) return rc;
+        if (bl) {
+            update_carry(c, device ? tail : hsrc + bl - tl, tl);
+            c->scanned_end = pos + bl;
+        }
         pos += bl;
     }
     c->consumed = end;
@@ -399,10 +468,8 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
         }
         reset_stream(c);
     }
-    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
-    HIP_TRY(c, hipEventSynchronize(c->ev[3]));
-    float ms = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[4], c->ev[3]));
+    float ms = 0;  // ev[4] = end of the last resolve, already synchronized
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[5], c->ev[4]));
     c->timing.total_ms = ms;
     *n_out = n;
     return PBS_OK;
@@ -417,6 +484,8 @@ void destroy(pbs_chunker* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->h_cuts) (void)hipHostFree(c->h_cuts);
+    if (c->h_keep) (void)hipHostFree(c->h_keep);
     delete c;
 }
 
@@ -446,7 +515,12 @@ int pbs_device_count(void) {
     return n;
 }
 
-size_t pbs_chunker_max_cuts(size_t len) { return len / 65 + 2; }
+size_t pbs_chunker_max_cuts(size_t len) { return len / 65 + 3; }
+
+size_t pbs_chunker_cuts_bound(const pbs_chunker* c, size_t len) {
+    if (!c) return pbs_chunker_max_cuts(len);
+    return len / c->prm.min_eff + 3;
+}
 
 pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     int dummy;
@@ -466,6 +540,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
         return nullptr;
     }
     c->prm = prm;
+    if (const char* e = std::getenv("PBS_DEBUG_PHASES")) c->debug_phases = e[0] == '1';
     bool ok = hipGetDevice(&c->device) == hipSuccess;
     hipDeviceProp_t prop;
     if (ok && hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -473,7 +548,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     ok = ok && hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess;
     c->stream = c->own_stream;
     for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
-    ok = ok && hipHostMalloc((void**)&c->h_small, 64, hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipHostMalloc((void**)&c->h_small, kSmallBytes, hipHostMallocMapped) == hipSuccess;
     ok = ok && c->d_table.ensure(256 * 4) == hipSuccess;
     if (ok) {
         uint32_t t[256];
@@ -538,8 +613,7 @@ size_t pbs_chunker_scan(pbs_chunker* c, const uint8_t* data, size_t len) {
                 fail(c, PBS_ERR_HIP);
                 return SIZE_MAX;
             }
-            uint32_t nnew = 0;
-            if (scan_new_bytes(c, c->d_in.as<uint8_t>(), hsrc, pos, bl, 0, false, &nnew) != PBS_OK)
+            if (scan_host_bytes(c, c->d_in.as<uint8_t>(), hsrc, pos, bl) != PBS_OK)
                 return SIZE_MAX;
             pos += bl;
         }
@@ -576,6 +650,71 @@ int pbs_chunker_find_cuts(pbs_chunker* c, const uint8_t* data, size_t len, int i
 int pbs_chunker_find_cuts_device(pbs_chunker* c, const uint8_t* dev_data, size_t len,
                                  int is_final, uint64_t* out, size_t cap, size_t* n_out) {
     return find_cuts_impl(c, dev_data, len, is_final, out, cap, n_out, true);
+}
+
+int pbs_chunker_candidates_device(pbs_chunker* c, const uint8_t* dev, size_t len,
+                                  const uint8_t* pre, size_t pre_len, uint64_t base,
+                                  uint64_t* out_dev, size_t cap, size_t* n_out) {
+    if (!c) return PBS_ERR_INVALID;
+    if (!n_out || (len && !dev) || (pre_len && !pre) || (cap && !out_dev) ||
+        pre_len != std::min<uint64_t>(base, kWindow - 1))
+        return fail(c, PBS_ERR_INVALID);
+    *n_out = 0;
+    HIP_TRY(c, hipSetDevice(c->device));
+    c->timing = pbs_timing{};
+    // the handle's carry is the warm-up history of scan_candidates: swap the halo in
+    uint8_t saved[64];
+    const uint32_t saved_len = c->carry_len;
+    std::memcpy(saved, c->carry, saved_len);
+    std::memcpy(c->carry, pre, pre_len);
+    c->carry_len = (uint32_t)pre_len;
+    uint32_t n = 0;
+    int rc = scan_candidates(c, dev, len, base, &n);
+    std::memcpy(c->carry, saved, saved_len);
+    c->carry_len = saved_len;
+    if (rc) return rc;
+    *n_out = n;
+    if (n > cap) return fail(c, PBS_ERR_CAPACITY);
+    rc = sort_candidates(c, n, out_dev);
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return PBS_OK;
+}
+
+int pbs_chunker_resolve_device(pbs_chunker* c, const uint64_t* cand_dev, size_t n, uint64_t end,
+                               int is_final, uint64_t* out, size_t cap, size_t* n_out) {
+    if (!c) return PBS_ERR_INVALID;
+    if (!n_out || (n && !cand_dev) || (!out && cap)) return fail(c, PBS_ERR_INVALID);
+    *n_out = 0;
+    if (n > 0xFFFFFFF0ull) return fail(c, PBS_ERR_NOMEM);
+    if (cap < pbs_chunker_cuts_bound(c, end)) return fail(c, PBS_ERR_CAPACITY);
+    HIP_TRY(c, hipSetDevice(c->device));
+    reset_stream(c);
+    // keep the phase-A fields of a preceding candidates_device call
+    c->timing.resolve_ms = c->timing.total_ms = 0;
+    c->timing.cuts = 0;
+    HIP_TRY(c, hipEventRecord(c->ev[5], c->stream));
+    HIP_TRY(c, c->d_C.ensure((n + 2) * 8));
+    size_t k = 0;
+    int rc;
+    if (n + 2 <= kSmallResolveMax) {
+        rc = run_resolve_small(c, cand_dev, 0, (uint32_t)n, end, out, cap, &k);
+    } else {
+        if (n)
+            HIP_TRY(c, hipMemcpyAsync(c->d_C.p, cand_dev, n * 8, hipMemcpyDeviceToDevice, c->stream));
+        rc = run_resolve(c, (uint32_t)n, end, out, cap, &k);
+    }
+    if (rc) {
+        reset_stream(c);
+        return rc;
+    }
+    if (is_final && c->chunk_start < end) out[k++] = end;
+    reset_stream(c);
+    float ms = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[5], c->ev[4]));
+    c->timing.total_ms = ms;
+    *n_out = k;
+    return PBS_OK;
 }
 
 int pbs_candidates_host(const uint8_t* data, size_t len, size_t avg, uint64_t* out, size_t cap,

@@ -42,6 +42,17 @@ hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p,
                           uint32_t* jtmp, uint64_t* nforced, uint32_t* on, uint64_t* cnt,
                           uint64_t* off, void* scan_tmp, size_t scan_tmp_bytes, uint64_t* out,
                           uint64_t out_cap, uint64_t* res, hipStream_t stream);
+// Single-workgroup sort + resolve + emit for batches with np + nnew + 2 <= kSmallResolveMax
+// candidates (keys sorted in LDS).  C[0..np) holds the pending (sorted) candidates on
+// entry and C[0..m) all sorted candidates on exit.  Cuts go to out[] and, while they
+// fit, to the mapped pinned out_host[]; res/res_host = {ncut, s_open, idx}; the open
+// chunk's candidates C[idx..m) are copied to keep_host when m - idx <= keep_cap.
+constexpr uint32_t kSmallResolveMax = 16384;
+hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C, uint32_t np,
+                                const ResolveParams& p, uint32_t* nxt, uint64_t* nforced,
+                                uint64_t* out, uint64_t out_cap, uint64_t* out_host,
+                                uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
+                                uint64_t* res, uint64_t* res_host, hipStream_t stream);
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,
                       int kind, hipStream_t stream);
 

@@ -61,35 +61,61 @@ namespace pbs {
 // before this buffer); bytes before that do not exist and contribute nothing, as in
 // the reference's fill phase.  Position p is a candidate iff the window is full
 // (p + pre_len >= 63) and (H(p) & mask) >= minimum; it is written as base + p.
-// Exact hash at positions [B, B+128) of one block, window bytes [B-64, B+128).
-// Fast path (the whole window inside `data`, 16-byte aligned since B % 128 == 0): the
-// 192 bytes come in with 12 x 16-byte loads and the roll is fully unrolled from
-// registers.  Otherwise (stream head with `pre` bytes, ragged tail) a byte-wise loop.
-__device__ __forceinline__ void exact_block_fast(const uint8_t* __restrict__ data, uint64_t B,
-                                                 const uint32_t* tab, uint32_t mask,
-                                                 uint32_t minimum, uint64_t base,
-                                                 uint64_t* __restrict__ cand,
-                                                 uint32_t* __restrict__ ncand, uint32_t cand_cap) {
+// Exact hash at positions [B, B+128) of one block, window bytes [B-64, B+128).  The
+// 192 window bytes are loaded first (12 x 16-byte loads when the window lies inside
+// `data` 16-byte aligned -- B % 128 == 0 -- else independent byte loads from `data` and
+// `pre`; a byte-serial loop would pay one memory latency per byte), then the roll runs
+// fully unrolled from registers over the valid byte range [vlo, vhi) of the window;
+// bytes outside it (before the stream, after `len`) contribute nothing.  Hits go to
+// the 128-bit mask hit[] (bit j = position B + j).
+__device__ __forceinline__ void exact_block(const uint8_t* __restrict__ data, uint64_t len,
+                                            const uint8_t* __restrict__ pre, uint32_t pre_len,
+                                            uint64_t B, const uint32_t* tab, uint32_t mask,
+                                            uint32_t minimum, uint32_t (&hit)[4]) {
+    const int64_t q0 = (int64_t)B - 64;
+    const int64_t vlo = (q0 > -(int64_t)pre_len ? q0 : -(int64_t)pre_len) - q0;
+    const int64_t vhi = ((int64_t)len < q0 + 192 ? (int64_t)len : q0 + 192) - q0;
     uint32_t w[48];
-    const uint4* src = reinterpret_cast<const uint4*>(data + B - 64);
+    if (B >= 64 && B + kIter <= len && ((uintptr_t)(data + B - 64) & 15) == 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(data + B - 64);
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const uint4 v = src[k];
-        w[4 * k] = v.x;
-        w[4 * k + 1] = v.y;
-        w[4 * k + 2] = v.z;
-        w[4 * k + 3] = v.w;
+        for (int k = 0; k < 12; ++k) {
+            const uint4 v = src[k];
+            w[4 * k] = v.x;
+            w[4 * k + 1] = v.y;
+            w[4 * k + 2] = v.z;
+            w[4 * k + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 48; ++k) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int64_t q = q0 + 4 * k + b;
+                uint32_t byte = 0;
+                if (q >= 0 && q < (int64_t)len)
+                    byte = data[q];
+                else if (q < 0 && q >= -(int64_t)pre_len)
+                    byte = pre[pre_len + q];
+                v |= byte << (8 * b);
+            }
+            w[k] = v;
+        }
     }
     uint32_t h = 0;
 #pragma unroll
     for (int i = 0; i < 192; ++i) {
-        const uint32_t bin = (w[i >> 2] >> ((i & 3) * 8)) & 0xffu;
-        uint32_t x = tab[bin];
-        if (i >= 64) x ^= tab[(w[(i - 64) >> 2] >> (((i - 64) & 3) * 8)) & 0xffu];
+        uint32_t x = (i >= vlo && i < vhi) ? tab[(w[i >> 2] >> ((i & 3) * 8)) & 0xffu] : 0u;
+        if (i >= 64) {
+            const int o = i - 64;
+            if (o >= vlo && o < vhi) x ^= tab[(w[o >> 2] >> ((o & 3) * 8)) & 0xffu];
+        }
         h = ((h << 1) | (h >> 31)) ^ x;
-        if (i >= 64 && (h & mask) >= minimum) {
-            const uint32_t idx = atomicAdd(ncand, 1u);
-            if (idx < cand_cap) cand[idx] = base + B + (uint64_t)(i - 64);
+        const int64_t q = q0 + i;
+        if (i >= 64) {
+            const bool c = i < vhi && q + (int64_t)pre_len >= 63 && (h & mask) >= minimum;
+            hit[(i - 64) >> 5] |= (c ? 1u : 0u) << ((i - 64) & 31);
         }
     }
 }
@@ -107,40 +133,42 @@ __global__ __launch_bounds__(256) void scan_exact_kernel(
     const uint64_t ns = ns0 < susp_cap ? ns0 : susp_cap;
     const uint64_t total = ns + (uint64_t)(head ? 1 : 0) + ext_count;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += stride) {
-        uint64_t B;
-        if (w < ns)
-            B = susp[w];
-        else if (head && w == ns)
-            B = 0;
-        else
-            B = (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
-        if (B >= 64 && B + kIter <= len && ((uintptr_t)(data + B - 64) & 15) == 0) {
-            exact_block_fast(data, B, tab, mask, minimum, base, cand, ncand, cand_cap);
-            continue;
+    // one atomic per workgroup and round (a per-candidate atomic on the single counter
+    // serializes in L2: ~14k of them took ~130 us at 64 GiB / 4 MiB)
+    typedef hipcub::BlockScan<uint32_t, 256> Scan;
+    __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ uint32_t round_base;
+    for (uint64_t w0 = (uint64_t)blockIdx.x * blockDim.x; w0 < total; w0 += stride) {
+        const uint64_t w = w0 + threadIdx.x;
+        uint32_t hit[4] = {0u, 0u, 0u, 0u};
+        uint64_t B = 0;
+        if (w < total) {
+            if (w < ns)
+                B = susp[w];
+            else if (head && w == ns)
+                B = 0;
+            else
+                B = (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
+            exact_block(data, len, pre, pre_len, B, tab, mask, minimum, hit);
         }
-        const uint64_t end = B + kIter < len ? B + kIter : len;
-        uint32_t h = 0;
-        const int64_t q0 = (int64_t)B - 64;
-        for (int64_t q = q0; q < (int64_t)end; ++q) {
-            uint32_t tin = 0, tout = 0;
-            if (q >= 0)
-                tin = tab[data[q]];
-            else if (q >= -(int64_t)pre_len)
-                tin = tab[pre[pre_len + q]];
-            const int64_t r = q - 64;
-            if (r >= q0) {
-                if (r >= 0)
-                    tout = tab[data[r]];
-                else if (r >= -(int64_t)pre_len)
-                    tout = tab[pre[pre_len + r]];
-            }
-            h = ((h << 1) | (h >> 31)) ^ tin ^ tout;
-            if (q >= (int64_t)B && q + (int64_t)pre_len >= 63 && (h & mask) >= minimum) {
-                const uint32_t idx = atomicAdd(ncand, 1u);
-                if (idx < cand_cap) cand[idx] = base + (uint64_t)q;
+        const uint32_t k = __builtin_popcount(hit[0]) + __builtin_popcount(hit[1]) +
+                           __builtin_popcount(hit[2]) + __builtin_popcount(hit[3]);
+        uint32_t off, sum;
+        Scan(scan_tmp).ExclusiveSum(k, off, sum);
+        if (threadIdx.x == 0) round_base = sum ? atomicAdd(ncand, sum) : 0u;
+        __syncthreads();
+        uint32_t idx = round_base + off;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t m = hit[q];
+            while (m) {
+                const int bit = __builtin_ctz(m);
+                m &= m - 1;
+                if (idx < cand_cap) cand[idx] = base + B + (uint64_t)(q * 32 + bit);
+                ++idx;
             }
         }
+        __syncthreads();  // round_base / scan_tmp reuse
     }
 }
 
@@ -263,6 +291,285 @@ __global__ __launch_bounds__(256) void resolve_emit_kernel(
         res[1] = s_open;
         res[2] = lower_bound_u64(C, 0, m, s_open);
     }
+}
+
+// ---------------------------------------------------------------------------------
+// Phase B for small batches, one workgroup (the 64 GiB / 4 MiB-average stream has
+// ~14k candidates): the multi-kernel path above costs ~20 launches, a device-wide
+// radix sort and a device-wide scan; here the keys are sorted in LDS (bitonic), the
+// pointer doubling runs on 16-bit successor arrays in LDS, and the cut list is
+// written straight into mapped pinned host memory, so the host needs one sync.
+// Same node/slot semantics as resolve_next/double/count/emit.
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kSmallThreads = 1024;
+constexpr uint32_t kSmallBig = 64;        // nodes with many forced cuts, filled by the block
+constexpr uint32_t kSmallBigMin = 256;    // forced-cut run length handed to the block
+constexpr uint32_t kSmallJ = kSmallResolveMax + 16;  // u16 successor array stride (>= m + 2)
+
+constexpr uint32_t kSmallBuckets = 4096;
+constexpr uint32_t kSmallBucketMax = 64;
+
+__device__ __forceinline__ uint32_t small_bucket(uint64_t key, uint64_t lo, uint64_t span) {
+    return (uint32_t)(((key - lo) * kSmallBuckets) / span);  // key - lo < span <= 2^40
+}
+
+// Exclusive scan of one value per thread over the block (Hillis-Steele in `part`).
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t* part, uint64_t v, uint32_t tid) {
+    part[tid] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < kSmallThreads; d <<= 1) {
+        const uint64_t x = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    const uint64_t r = part[tid] - v;
+    __syncthreads();  // part is reused by the caller's next scan
+    return r;
+}
+
+__global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
+    const uint64_t* __restrict__ newc, uint32_t nnew, uint64_t* C, uint32_t np, ResolveParams p,
+    uint32_t* nxt, uint64_t* nforced, uint64_t* __restrict__ out, uint64_t out_cap,
+    uint64_t* __restrict__ out_host, uint64_t host_cap, uint64_t* __restrict__ keep_host,
+    uint64_t keep_cap, uint64_t* __restrict__ res, uint64_t* __restrict__ res_host) {
+    __shared__ uint64_t sk[kSmallResolveMax];  // keys; later reused for ja | jb | on
+    __shared__ uint64_t part[kSmallThreads];
+    __shared__ uint64_t big[kSmallBig][3];
+    __shared__ uint64_t open_info[3];
+    __shared__ uint32_t bcnt[kSmallBuckets];
+    __shared__ uint32_t nbig, bmax;
+    static_assert(2 * kSmallJ * 2 + kSmallJ <= sizeof(uint64_t) * kSmallResolveMax, "LDS reuse");
+
+    const uint32_t tid = threadIdx.x, T = kSmallThreads;
+    const uint32_t m = np + nnew;
+    const uint32_t none = m + 1;
+
+    // 1. sort the keys into LDS.  All keys lie in [s0, end) (pending >= chunk_start,
+    //    new < end), so a bucket sort over kSmallBuckets equal ranges of that span
+    //    (histogram, scan, scatter, insertion sort per bucket) is O(m); a bucket
+    //    holding more than kSmallBucketMax keys (skewed input) falls back to a
+    //    bitonic sort of the whole set.
+    const uint64_t t_start = wall_clock64();
+    const uint64_t span = p.end > p.s0 ? p.end - p.s0 : 1;
+    for (uint32_t b = tid; b < kSmallBuckets; b += T) bcnt[b] = 0;
+    if (tid == 0) {
+        nbig = 0;
+        bmax = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += T) {
+        const uint64_t key = i < np ? C[i] : newc[i - np];
+        atomicAdd(&bcnt[small_bucket(key, p.s0, span)], 1u);
+    }
+    __syncthreads();
+    const uint64_t t_hist = wall_clock64();
+    {
+        constexpr uint32_t per_b = kSmallBuckets / kSmallThreads;
+        uint32_t c[per_b], bsum = 0, bm = 0;
+#pragma unroll
+        for (int q = 0; q < (int)per_b; ++q) {
+            c[q] = bcnt[tid * per_b + q];
+            bsum += c[q];
+            bm = c[q] > bm ? c[q] : bm;
+        }
+        atomicMax(&bmax, bm);
+        const uint64_t before = block_exclusive_scan(part, bsum, tid);
+        uint32_t o = (uint32_t)before;
+#pragma unroll
+        for (int q = 0; q < (int)per_b; ++q) {
+            bcnt[tid * per_b + q] = o;  // bucket start
+            o += c[q];
+        }
+    }
+    __syncthreads();
+    const uint64_t t_bscan = wall_clock64();
+    uint64_t t_scatter = t_bscan;
+    if (bmax <= kSmallBucketMax) {
+        for (uint32_t i = tid; i < m; i += T) {
+            const uint64_t key = i < np ? C[i] : newc[i - np];
+            sk[atomicAdd(&bcnt[small_bucket(key, p.s0, span)], 1u)] = key;
+        }
+        __syncthreads();  // bcnt[b] = end of bucket b
+        t_scatter = wall_clock64();
+        for (uint32_t b = tid; b < kSmallBuckets; b += T) {
+            const uint32_t lo = b ? bcnt[b - 1] : 0u, hi = bcnt[b];
+            for (uint32_t i = lo + 1; i < hi; ++i) {
+                const uint64_t v = sk[i];
+                uint32_t k = i;
+                while (k > lo && sk[k - 1] > v) {
+                    sk[k] = sk[k - 1];
+                    --k;
+                }
+                sk[k] = v;
+            }
+        }
+        __syncthreads();
+    } else {
+        uint32_t N = 2;
+        while (N < m) N <<= 1;
+        for (uint32_t i = tid; i < N; i += T) sk[i] = i < np ? C[i] : (i < m ? newc[i - np] : ~0ull);
+        __syncthreads();
+        for (uint32_t k = 2; k <= N; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < N / 2; i += T) {
+                    const uint32_t a = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+                    const uint32_t b = a | j;
+                    const uint64_t x = sk[a], y = sk[b];
+                    if ((x > y) == ((a & k) == 0)) {
+                        sk[a] = y;
+                        sk[b] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+    const uint64_t t_sorted = wall_clock64();
+
+    // 2. sorted keys -> C; successor candidate and forced-cut count of every node
+    for (uint32_t i = tid; i < m; i += T) C[i] = sk[i];
+    for (uint32_t j = tid; j <= m; j += T) {
+        uint64_t s = (j == m) ? p.s0 : sk[j] + 1;
+        uint32_t i = (j == m) ? 0u : j + 1;
+        uint64_t nf = 0;
+        uint32_t r = none;
+        for (;;) {
+            const uint64_t lo = s + p.min_eff - 1, hi = s + p.max_eff - 1;
+            i = lower_bound_u64(sk, i, m, lo);
+            if (i < m && sk[i] <= hi) {
+                r = i;
+                break;
+            }
+            if (hi >= p.end) break;
+            uint64_t k;
+            if (i < m) {
+                k = (sk[i] - hi + p.max_eff - 1) / p.max_eff;
+            } else {
+                k = (p.end - s) / p.max_eff;
+                nf += k;
+                break;
+            }
+            nf += k;
+            s += k * p.max_eff;
+        }
+        nxt[j] = r;
+        nforced[j] = nf;
+    }
+    __syncthreads();
+    const uint64_t t_next = wall_clock64();
+
+    // 3. pointer doubling in LDS (marks only go 0 -> 1; see resolve_double_kernel)
+    uint16_t* ja = reinterpret_cast<uint16_t*>(sk);
+    uint16_t* jb = ja + kSmallJ;
+    uint8_t* on = reinterpret_cast<uint8_t*>(jb + kSmallJ);
+    const uint32_t n = m + 2;
+    for (uint32_t j = tid; j < n; j += T) {
+        ja[j] = (uint16_t)(j <= m ? nxt[j] : none);  // own writes from step 2
+        on[j] = j == m ? 1 : 0;
+    }
+    __syncthreads();
+    // each thread owns the contiguous nodes [d_lo, d_lo + kDblPer) (n <= T * kDblPer):
+    // all its gathers are issued before any result is used (one LDS latency per round)
+    constexpr uint32_t kDblPer = (kSmallJ + kSmallThreads - 1) / kSmallThreads;
+    const uint32_t d_lo = tid * kDblPer;
+    for (uint32_t span = 1; span < n; span <<= 1) {
+        uint32_t J[kDblPer], JJ[kDblPer];
+        uint8_t o[kDblPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kDblPer; ++q) {
+            const uint32_t j = d_lo + q;
+            J[q] = j < n ? ja[j] : 0u;
+            o[q] = j < n ? on[j] : 0;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kDblPer; ++q) JJ[q] = d_lo + q < n ? ja[J[q]] : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < kDblPer; ++q) {
+            if (d_lo + q < n) {
+                if (o[q]) on[J[q]] = 1;
+                jb[d_lo + q] = (uint16_t)JJ[q];
+            }
+        }
+        __syncthreads();
+        uint16_t* t = ja;
+        ja = jb;
+        jb = t;
+    }
+    const uint64_t t_doubled = wall_clock64();
+
+    // 4. per-thread contiguous slot ranges (slot 0 = start node m, slot j+1 = node j),
+    //    block-wide exclusive scan of the cut counts
+    const uint32_t slots = m + 1;
+    const uint32_t per = (slots + T - 1) / T;
+    const uint32_t s_lo = min(tid * per, slots), s_hi = min(s_lo + per, slots);
+    uint64_t sum = 0;
+    for (uint32_t sl = s_lo; sl < s_hi; ++sl) {
+        const uint32_t j = sl == 0 ? m : sl - 1;
+        if (on[j]) sum += nforced[j] + (nxt[j] != none ? 1u : 0u);
+    }
+    uint64_t o = block_exclusive_scan(part, sum, tid);
+    const uint64_t t_scanned = wall_clock64();
+
+    // 5. emit
+    for (uint32_t sl = s_lo; sl < s_hi; ++sl) {
+        const uint32_t j = sl == 0 ? m : sl - 1;
+        if (!on[j]) continue;
+        const uint64_t s = (j == m) ? p.s0 : C[j] + 1;
+        const uint64_t nf = nforced[j];
+        bool done = false;
+        if (nf >= kSmallBigMin) {
+            const uint32_t b = atomicAdd(&nbig, 1u);
+            if (b < kSmallBig) {
+                big[b][0] = s;
+                big[b][1] = o;
+                big[b][2] = nf;
+                done = true;
+            }
+        }
+        if (!done)
+            for (uint64_t t = 0; t < nf; ++t)
+                if (o + t < out_cap) out[o + t] = s + (t + 1) * p.max_eff;
+        if (nxt[j] != none) {
+            if (o + nf < out_cap) out[o + nf] = C[nxt[j]] + 1;
+            o += nf + 1;
+        } else {
+            open_info[0] = o + nf;              // cuts before the open chunk = all cuts
+            open_info[1] = s + nf * p.max_eff;  // start of the open chunk
+            o += nf;
+        }
+    }
+    __syncthreads();
+    const uint32_t nb = min(nbig, kSmallBig);
+    for (uint32_t b = 0; b < nb; ++b)
+        for (uint64_t t = tid; t < big[b][2]; t += T)
+            if (big[b][1] + t < out_cap) out[big[b][1] + t] = big[b][0] + (t + 1) * p.max_eff;
+    if (tid == 0) open_info[2] = lower_bound_u64(C, 0, m, open_info[1]);
+    __syncthreads();
+    const uint64_t t_emit = wall_clock64();
+    // cut list -> mapped pinned host memory, 16-byte coalesced stores
+    const uint64_t ncut = open_info[0];
+    if (ncut <= host_cap && ncut <= out_cap) {
+        const uint64_t pairs = ncut / 2;
+        const uint4* src = reinterpret_cast<const uint4*>(out);
+        uint4* dst = reinterpret_cast<uint4*>(out_host);
+        for (uint64_t i = tid; i < pairs; i += T) dst[i] = src[i];
+        if (tid == 0 && (ncut & 1)) out_host[ncut - 1] = out[ncut - 1];
+    }
+    const uint64_t idx = open_info[2];
+    if (tid < 3) {
+        res[tid] = open_info[tid];
+        res_host[tid] = open_info[tid];
+    }
+    if (tid == 0) {  // phase durations (100 MHz ticks), read by diagnostics only
+        const uint64_t t_end = wall_clock64();
+        const uint64_t ph[9] = {t_hist - t_start,    t_bscan - t_hist,     t_scatter - t_bscan,
+                                t_sorted - t_scatter, t_next - t_sorted,    t_doubled - t_next,
+                                t_scanned - t_doubled, t_emit - t_scanned,  t_end - t_emit};
+        for (int q = 0; q < 9; ++q) res_host[3 + q] = ph[q];
+    }
+    if (m - idx <= keep_cap)
+        for (uint64_t i = idx + tid; i < m; i += T) keep_host[i - idx] = C[i];
 }
 
 // ---------------------------------------------------------------------------------
@@ -404,6 +711,19 @@ hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p,
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(resolve_emit_kernel, dim3(blocks), dim3(256), 0, stream, C, m, p, nxt,
                        nforced, on, cnt, off, out, out_cap, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C, uint32_t np,
+                                const ResolveParams& p, uint32_t* nxt, uint64_t* nforced,
+                                uint64_t* out, uint64_t out_cap, uint64_t* out_host,
+                                uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
+                                uint64_t* res, uint64_t* res_host, hipStream_t stream) {
+    if ((uint64_t)np + nnew + 2 > kSmallResolveMax) return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(resolve_small_kernel, dim3(1), dim3(kSmallThreads), 0, stream, newc, nnew,
+                       C, np, p, nxt, nforced, out, out_cap, out_host, host_cap, keep_host,
+                       keep_cap, res, res_host);
     return hipGetLastError();
 }
 

@@ -38,7 +38,17 @@ __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
 // hand-scheduled roll128_asm_g4 (G = bytes per lgkmcnt wait).  PF > 0 adds an L2
 // "touch" DMA PF iterations ahead (measured slower; kept for the microbenchmark).
 // Design record of the variants measured against it: DESIGN.md "Kernel: scan_main".
-template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0>
+//
+// ZS (zero-run skip): the hash of any 64 equal bytes is 0 (rotations k and k+32 of the
+// same table word cancel), so a lane whose previous 128-byte block was all zero is in
+// the state {h = 0, every ring slot = T'[0]}; an all-zero block leaves that state
+// unchanged and holds no candidate (thr > 0), so the lane skips its roll (EXEC-masked;
+// a wave whose 64 lanes all skip branches over it).  Detecting it costs ~16 v_or3 per
+// 128 bytes.  Measured (profiles/r01/mb_zs_*.log): all-zero input reaches the
+// loads-only rate, but random and VM-image data get 2-3% SLOWER -- lanes 32 KiB apart
+// are almost never all in zero pages at once, and masked lanes save little -- so the
+// product runs ZS = 0.
+template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int ZS = 0>
 __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
     uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {
@@ -104,6 +114,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
 #pragma unroll
     for (int r = 0; r < 128; ++r) ring[r] = 0;
     uint32_t h = 0;
+    bool canon = false;  // ZS: lane state is {h = 0, ring = T'[0]} (last block all zero)
     issue(tile, 0);
     for (;;) {
         for (int it = 0; it < NIT; ++it) {
@@ -132,22 +143,33 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
             }
             if (it == 0) {
                 h = 0;
+                canon = false;
 #pragma unroll
                 for (int r = 64; r < 128; ++r) ring[r] = 0;
             }
-            uint32_t acc;
+            bool zero = false;
+            if constexpr (ZS != 0 && MODE != kModeLoadOnly) {
+                uint32_t z = 0;
+#pragma unroll
+                for (int k = 0; k < 32; ++k) z |= d[k];
+                zero = z == 0u;
+            }
+            uint32_t acc = 0;
             if constexpr (MODE == kModeLoadOnly) {
                 acc = 0;
 #pragma unroll
                 for (int k = 0; k < 32; ++k) acc ^= d[k];
                 acc = (acc == 0x9E3779B9u && lane == 65) ? 0xFFFFFFFFu : 0u;
-            } else if constexpr (G == 4) {
-                acc = roll128_asm_g4(d, ring, h, lanebase);
-            } else {
-                acc = roll128_asm(d, ring, h, lanebase);
+            } else if (!(canon && zero)) {
+                if constexpr (G == 4)
+                    acc = roll128_asm_g4(d, ring, h, lanebase);
+                else
+                    acc = roll128_asm(d, ring, h, lanebase);
             }
+            canon = zero;
             if (it == 0) {
                 if (tile == 0 && lane == 0) {
+                    canon = false;
                     h = 0;
 #pragma unroll
                     for (int r = 64; r < 128; ++r) ring[r] = 0;

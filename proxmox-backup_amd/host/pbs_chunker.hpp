@@ -60,7 +60,7 @@ class Chunker {
 
     // All chunk END offsets (absolute) decided inside `data`; with is_final the tail too.
     std::vector<uint64_t> find_cuts(const uint8_t* data, size_t len, bool is_final = false) {
-        std::vector<uint64_t> out(pbs_chunker_max_cuts(len));
+        std::vector<uint64_t> out(pbs_chunker_cuts_bound(h_, len));
         size_t n = 0;
         const int rc = pbs_chunker_find_cuts(h_, data, len, is_final ? 1 : 0, out.data(),
                                              out.size(), &n);

@@ -38,10 +38,12 @@ GEN_COUNTER, GEN_RANDOM, GEN_VMIMAGE = 0, 1, 2
 
 EXPORTED_SYMBOLS = (
     "pbs_chunker_new", "pbs_chunker_free", "pbs_chunker_scan", "pbs_chunker_find_cuts",
-    "pbs_chunker_find_cuts_device", "pbs_chunker_max_cuts", "pbs_chunker_stream_offset",
+    "pbs_chunker_find_cuts_device", "pbs_chunker_max_cuts", "pbs_chunker_cuts_bound",
+    "pbs_chunker_stream_offset",
     "pbs_chunker_chunk_start", "pbs_chunker_reset", "pbs_chunker_set_stream",
     "pbs_chunker_last_error", "pbs_strerror", "pbs_chunker_last_timing",
     "pbs_candidates_host", "pbs_generate_device", "pbs_device_count", "pbs_table_copy",
+    "pbs_chunker_candidates_device", "pbs_chunker_resolve_device",
 )
 
 
@@ -93,6 +95,7 @@ def lib():
         "pbs_chunker_find_cuts": ([p, p, sz, i, p, sz, ctypes.POINTER(sz)], i),
         "pbs_chunker_find_cuts_device": ([p, p, sz, i, p, sz, ctypes.POINTER(sz)], i),
         "pbs_chunker_max_cuts": ([sz], sz),
+        "pbs_chunker_cuts_bound": ([p, sz], sz),
         "pbs_chunker_stream_offset": ([p], u64),
         "pbs_chunker_chunk_start": ([p], u64),
         "pbs_chunker_reset": ([p], i),
@@ -104,6 +107,8 @@ def lib():
         "pbs_generate_device": ([p, sz, i, u64, u64, p], i),
         "pbs_device_count": ([], i),
         "pbs_table_copy": ([p], i),
+        "pbs_chunker_candidates_device": ([p, p, sz, p, sz, u64, p, sz, ctypes.POINTER(sz)], i),
+        "pbs_chunker_resolve_device": ([p, p, sz, u64, i, p, sz, ctypes.POINTER(sz)], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -185,10 +190,14 @@ class Chunker:
             raise ChunkerError(lib().pbs_chunker_last_error(self._h), "pbs_chunker_scan")
         return int(r)
 
+    def cuts_bound(self, length: int) -> int:
+        """Output capacity find_cuts needs for ``length`` bytes at this average."""
+        return int(lib().pbs_chunker_cuts_bound(self._h, length))
+
     def find_cuts(self, data, is_final: bool = False) -> np.ndarray:
         """Chunk END offsets (absolute) of every cut decided inside ``data``."""
         a = _as_u8(data)
-        cap = max_cuts(a.size)
+        cap = self.cuts_bound(a.size)
         out = np.empty(cap, dtype=np.uint64)
         n = ctypes.c_size_t(0)
         rc = lib().pbs_chunker_find_cuts(self._h, _ptr(a), a.size, int(bool(is_final)),
@@ -198,7 +207,7 @@ class Chunker:
 
     def find_cuts_device(self, dev_ptr: int, length: int, is_final: bool = False) -> np.ndarray:
         """Same over a device (HBM) buffer, e.g. ``tensor.data_ptr()``."""
-        cap = max_cuts(length)
+        cap = self.cuts_bound(length)
         out = np.empty(cap, dtype=np.uint64)
         n = ctypes.c_size_t(0)
         rc = lib().pbs_chunker_find_cuts_device(self._h, ctypes.c_void_p(dev_ptr), length,
@@ -206,6 +215,37 @@ class Chunker:
                                                ctypes.byref(n))
         self._check(rc, "pbs_chunker_find_cuts_device")
         return out[: n.value].copy()
+
+    def candidates_device(self, dev_ptr: int, length: int, pre: bytes, base: int,
+                          out_dev_ptr: int, cap: int) -> int:
+        """Phase A over device bytes [base, base+length) of a stream, given the
+        min(base, 63) stream bytes before them (``pre``): sorted absolute candidate
+        positions into the device array at ``out_dev_ptr`` (``cap`` u64 entries).
+        Returns their number; raises ChunkerError(PBS_ERR_CAPACITY) with
+        ``.needed`` set when cap is too small."""
+        pre = bytes(pre)
+        n = ctypes.c_size_t(0)
+        rc = lib().pbs_chunker_candidates_device(
+            self._h, ctypes.c_void_p(dev_ptr), length, pre if pre else None, len(pre), base,
+            ctypes.c_void_p(out_dev_ptr) if cap else None, cap, ctypes.byref(n))
+        if rc == PBS_ERR_CAPACITY:
+            e = ChunkerError(rc, "pbs_chunker_candidates_device")
+            e.needed = int(n.value)
+            raise e
+        self._check(rc, "pbs_chunker_candidates_device")
+        return int(n.value)
+
+    def resolve_device(self, cand_dev_ptr: int, n: int, end: int, is_final: bool = True) -> np.ndarray:
+        """Phase B: cut list of a stream of ``end`` bytes from its complete sorted
+        candidate list (device u64 array of ``n`` entries)."""
+        cap = self.cuts_bound(end)
+        out = np.empty(cap, dtype=np.uint64)
+        k = ctypes.c_size_t(0)
+        rc = lib().pbs_chunker_resolve_device(self._h, ctypes.c_void_p(cand_dev_ptr), n, end,
+                                              int(bool(is_final)), out.ctypes.data, cap,
+                                              ctypes.byref(k))
+        self._check(rc, "pbs_chunker_resolve_device")
+        return out[: k.value].copy()
 
     def set_stream(self, hip_stream: int):
         self._check(lib().pbs_chunker_set_stream(self._h, ctypes.c_void_p(hip_stream)),

@@ -19,6 +19,29 @@ __global__ void fill(uint64_t* p, uint64_t n) {
     }
 }
 
+__device__ __forceinline__ uint64_t sm64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// kind 1: the product's VM-image generator (40% zero 4 KiB pages, one 64 MiB zero
+// extent per GiB); kind 2: all zero
+__global__ void fill_kind(uint64_t* p, uint64_t n, int kind) {
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < n; w += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t v = 0;
+        if (kind == 1) {
+            const uint64_t seed = 0x5EED0003ull, x = w << 3, g = x >> 30;
+            const uint64_t ext = (sm64(seed ^ 0x4558544E54000000ull ^ g) & 15u) << 26;
+            const uint64_t in_g = x & ((1ull << 30) - 1);
+            if (!(in_g >= ext && in_g < ext + (1ull << 26)) &&
+                sm64(seed ^ 0x7A65726F50414745ull ^ (x >> 12)) % 100u >= 40u)
+                v = sm64(seed ^ 0x52414E44574F5244ull ^ w);
+        }
+        p[w] = v;
+    }
+}
+
 // plain coalesced streaming read (16 B/lane), the HBM reference point
 template <bool NT>
 __global__ __launch_bounds__(256) void stream_read(const uint4* __restrict__ p, uint64_t n, uint32_t* out) {
@@ -38,11 +61,16 @@ int main(int argc, char** argv) {
     double gib = argc > 1 ? atof(argv[1]) : 16.0;
     int reps = argc > 2 ? atoi(argv[2]) : 5;
     int only = argc > 3 ? atoi(argv[3]) : -1;  // run a single variant (for PMC collection)
+    int kind = argc > 4 ? atoi(argv[4]) : 0;   // 0 random, 1 vmimage-like, 2 zeros
     int vid = 0;
     uint64_t n = (uint64_t)(gib * (1ull << 30));
     n = n / (1ull << 20) * (1ull << 20);
     uint8_t* d; CK(hipMalloc(&d, n));
-    hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, (uint64_t*)d, n / 8);
+    if (kind == 0)
+        hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, (uint64_t*)d, n / 8);
+    else
+        hipLaunchKernelGGL(fill_kind, dim3(8192), dim3(256), 0, 0, (uint64_t*)d, n / 8, kind);
+    printf("data kind %d (%s)\n", kind, kind == 0 ? "random" : kind == 1 ? "vmimage" : "zeros");
     uint32_t *tab, *cnt; uint64_t* susp;
     CK(hipMalloc(&tab, 1024)); CK(hipMalloc(&cnt, 16)); CK(hipMalloc(&susp, 1 << 24));
     const uint64_t avg = 4ull << 20;
@@ -105,21 +133,22 @@ int main(int argc, char** argv) {
         char nm[96]; snprintf(nm, sizeof nm, "v2 SEG=%d W=%d mode=%d aux=%d susp=%u", SEG, NW, MODE, AUX, h_cnt); \
         report(nm, best);                                                                   \
     }
-#define RUN3(SEG, MODE, AUX, G, PF)                                                             \
+#define RUN3(SEG, MODE, AUX, G, PF) RUN3Z(SEG, MODE, AUX, G, PF, 1)
+#define RUN3Z(SEG, MODE, AUX, G, PF, ZS)                                                        \
     if (only < 0 || only == vid++) {                                                        \
         float best = 1e30f; uint32_t h_cnt = 0;                                             \
         const uint64_t tiles = n / (64ull * SEG);                                           \
         for (int r = 0; r < reps; ++r) {                                                    \
             CK(hipMemset(cnt, 0, 16));                                                      \
             CK(hipEventRecord(e0));                                                         \
-            hipLaunchKernelGGL((pbs::scan_main_kernel<SEG, MODE, AUX, G, PF>), dim3(cu), dim3(8 * 64), 0, 0, \
+            hipLaunchKernelGGL((pbs::scan_main_kernel<SEG, MODE, AUX, G, PF, ZS>), dim3(cu), dim3(8 * 64), 0, 0, \
                                d, tiles, tab, thr, susp, cnt, 1u << 21);                    \
             CK(hipGetLastError());                                                          \
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));                            \
             float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = ms < best ? ms : best;   \
             CK(hipMemcpy(&h_cnt, cnt, 4, hipMemcpyDeviceToHost));                           \
         }                                                                                   \
-        char nm[96]; snprintf(nm, sizeof nm, "v3 SEG=%d mode=%d aux=%d G=%d PF=%d susp=%u", SEG, MODE, AUX, G, PF, h_cnt); \
+        char nm[96]; snprintf(nm, sizeof nm, "v3 SEG=%d mode=%d G=%d PF=%d ZS=%d susp=%u", SEG, MODE, G, PF, ZS, h_cnt); \
         report(nm, best);                                                                   \
     }
 #define RUN4(SEG, MODE, AUX, G)                                                             \
@@ -173,11 +202,9 @@ int main(int argc, char** argv) {
         char nm[96]; snprintf(nm, sizeof nm, "v6 SEG=%d mode=%d aux=%d G=%d susp=%u", SEG, MODE, AUX, G, h_cnt); \
         report(nm, best);                                                                   \
     }
-    RUN3(32768, 0, 2, 4, 0)
-    RUN3(32768, 1, 2, 4, 0)
-    RUN3(32768, 2, 2, 4, 0)
-    RUN6(32768, 0, 2, 4)
-    RUN6(32768, 1, 2, 4)
-    RUN6(32768, 2, 2, 4)
+    RUN3Z(32768, 0, 2, 4, 0, 1)
+    RUN3Z(32768, 0, 2, 4, 0, 0)
+    RUN3Z(32768, 1, 2, 4, 0, 1)
+    RUN3Z(32768, 2, 2, 4, 0, 0)
     return 0;
 }

@@ -53,6 +53,25 @@ def test_strerror_and_max_cuts(pbschunk):
     assert "power of two" in pbschunk.strerror(pbschunk.PBS_ERR_NOT_POW2)
     assert pbschunk.max_cuts(0) >= 1
     assert pbschunk.max_cuts(65 * 1000) >= 1000
+    # without a handle the bound falls back to the any-average one
+    assert pbschunk.lib().pbs_chunker_cuts_bound(None, 65 * 1000) == pbschunk.max_cuts(65 * 1000)
+
+
+@pytest.mark.parametrize("avg", [64, 1024, 64 * KiB, 4 * MiB])
+def test_cuts_bound_holds_on_oracle_cuts(oracle, avg):
+    """pbs_chunker_cuts_bound(len) = len // max(avg/4, 65) + 3 covers the cuts any call
+    over a byte range can return (checked on the oracle's cut lists, any split)."""
+    import gen_np
+    n = 24 * MiB if avg >= 64 * KiB else 2 * MiB
+    data = gen_np.gen_vmimage(n, 0x5EED0003, 700 * MiB)
+    cuts = oracle.chunk_feed(avg, data).astype(np.int64)
+    ends = np.append(cuts, n) if cuts.size == 0 or cuts[-1] != n else cuts
+    min_eff = max(avg // 4, 65)
+    rng = np.random.default_rng(avg)
+    for _ in range(200):
+        a, b = sorted(rng.integers(0, n + 1, 2))
+        inside = int(((ends > a) & (ends <= b)).sum())
+        assert inside <= (b - a) // min_eff + 3, (a, b, inside)
 
 
 def test_non_power_of_two_rejected_like_reference(pbschunk):

@@ -36,6 +36,20 @@ def _golden_input(case):
 
 # ---------------------------------------------------------------- phase A (candidates)
 
+def _holes(n: int, seed: int, max_run: int = 20000) -> np.ndarray:
+    """Random bytes punched with zero runs of random length and alignment (the scan
+    kernel skips all-zero 128-byte blocks that follow an all-zero block)."""
+    rng = np.random.default_rng(seed)
+    d = gen_np.gen_random(n, seed)
+    pos = 0
+    while pos < n:
+        pos += int(rng.integers(1, 3000))
+        ln = int(rng.choice([int(rng.integers(1, max_run)), 64, 127, 128, 129, 255, 256, 257]))
+        d[pos:pos + ln] = 0
+        pos += ln
+    return d
+
+
 CAND_CASES = [
     # (name, maker, avg) -- sizes cover exact-only (< 1 MiB wave tile), several wave tiles
     # plus a ragged tail, and dense candidates (tiny averages) that overflow the first
@@ -52,6 +66,9 @@ CAND_CASES = [
     ("empty_64", lambda: np.zeros(0, np.uint8), 64),
     ("random_4M_avg2", lambda: gen_np.gen_random(4 * MiB, 9), 2),
     ("random_1M_avg1", lambda: gen_np.gen_random(1 * MiB, 9), 1),
+    ("holes_8M_256", lambda: _holes(8 * MiB + 5, 31), 256),
+    ("holes_24M_4096", lambda: _holes(24 * MiB, 32, 200000), 4096),
+    ("holes_6M_64", lambda: _holes(6 * MiB + 1, 33, 1000), 64),
 ]
 
 
@@ -128,6 +145,49 @@ def test_find_cuts_device(gpu, oracle):
     got = np.concatenate([g1, g2])
     assert np.array_equal(got[:-1], ref) and int(got[-1]) == n
     assert t["bytes"] == n - half and t["total_ms"] > 0
+
+
+def _zebra(n_runs: int, zero_run: int, rand_run: int, seed: int) -> np.ndarray:
+    """Zero runs (no candidates -> long forced-cut runs) between random runs."""
+    r = gen_np.gen_random(n_runs * rand_run, seed)
+    out = np.zeros(n_runs * (zero_run + rand_run), np.uint8)
+    for i in range(n_runs):
+        a = i * (zero_run + rand_run) + zero_run
+        out[a:a + rand_run] = r[i * rand_run:(i + 1) * rand_run]
+    return out
+
+
+# The resolve runs in one workgroup up to 16384 - 2 candidates (pending + new) and in the
+# multi-kernel sort + pointer-doubling path above that: sizes straddle the switch (random
+# bytes at avg 256 give ~3/512 candidates per byte), and forced-cut runs of >= 256 cuts
+# per node exercise the block-filled list, including more than its 64 entries.
+RESOLVE_CASES = [
+    ("random_2.5M_256", lambda: gen_np.gen_random(2 * MiB + 512 * KiB, 21), 256),
+    ("random_2.75M_256", lambda: gen_np.gen_random(2 * MiB + 768 * KiB + 13, 22), 256),
+    ("random_2.9M_256", lambda: gen_np.gen_random(2 * MiB + 920 * KiB, 23), 256),
+    ("random_6M_256", lambda: gen_np.gen_random(6 * MiB + 1, 24), 256),
+    ("zeros_1M_64", lambda: np.zeros(1 * MiB, np.uint8), 64),
+    ("zeros_9M_4096", lambda: np.zeros(9 * MiB + 3, np.uint8), 4096),
+    ("zebra_100x128K_64", lambda: _zebra(100, 128 * KiB, 4 * KiB, 25), 64),
+    ("zebra_30x8M_4096", lambda: _zebra(30, 8 * MiB, 64 * KiB, 26), 4096),
+]
+
+
+@pytest.mark.parametrize("name,mk,avg", RESOLVE_CASES, ids=[c[0] for c in RESOLVE_CASES])
+def test_resolve_paths(gpu, oracle, name, mk, avg):
+    data = mk()
+    ref = oracle.chunk_feed(avg, data)
+    if ref.size == 0 or int(ref[-1]) != data.size:  # the EOF tail chunk, if any
+        ref = np.append(ref, np.uint64(data.size))
+    with gpu.Chunker(avg) as c:
+        got = c.find_cuts(data, is_final=True)
+        t = c.last_timing()
+    assert np.array_equal(got, ref), (name, t["candidates"], got.size, ref.size)
+    # split in two calls: the open chunk's candidates come back as pending
+    h = data.size // 2 + 7
+    with gpu.Chunker(avg) as c:
+        got2 = np.concatenate([c.find_cuts(data[:h]), c.find_cuts(data[h:], is_final=True)])
+    assert np.array_equal(got2, got), name
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2])
