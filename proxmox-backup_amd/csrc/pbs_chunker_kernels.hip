@@ -296,10 +296,11 @@ __global__ __launch_bounds__(256) void resolve_emit_kernel(
 // ---------------------------------------------------------------------------------
 // Phase B for small batches, one workgroup (the 64 GiB / 4 MiB-average stream has
 // ~14k candidates): the multi-kernel path above costs ~20 launches, a device-wide
-// radix sort and a device-wide scan; here the keys are sorted in LDS (bitonic), the
-// pointer doubling runs on 16-bit successor arrays in LDS, and the cut list is
-// written straight into mapped pinned host memory, so the host needs one sync.
-// Same node/slot semantics as resolve_next/double/count/emit.
+// radix sort and a device-wide scan; here the keys are bucket-sorted in LDS, the
+// pointer doubling runs on 16-bit successor arrays in LDS, and the cut list is copied
+// straight into mapped pinned host memory, so the host needs one sync.  Same
+// node/slot semantics as resolve_next/double/count/emit.  One CU cannot hide latency
+// with parallel slack, so every phase issues its independent loads in batches.
 // ---------------------------------------------------------------------------------
 constexpr uint32_t kSmallThreads = 1024;
 constexpr uint32_t kSmallBig = 64;        // nodes with many forced cuts, filled by the block
@@ -307,10 +308,14 @@ constexpr uint32_t kSmallBigMin = 256;    // forced-cut run length handed to the
 constexpr uint32_t kSmallJ = kSmallResolveMax + 16;  // u16 successor array stride (>= m + 2)
 
 constexpr uint32_t kSmallBuckets = 4096;
-constexpr uint32_t kSmallBucketMax = 64;
+constexpr uint32_t kSmallBucketMax = 256;  // larger buckets (skewed input): bitonic fallback
+constexpr uint32_t kSmallPer = (kSmallJ + kSmallThreads - 1) / kSmallThreads;  // nodes per thread
+constexpr uint32_t kSmallChunk = 6;  // slots per batch of independent global loads
 
-__device__ __forceinline__ uint32_t small_bucket(uint64_t key, uint64_t lo, uint64_t span) {
-    return (uint32_t)(((key - lo) * kSmallBuckets) / span);  // key - lo < span <= 2^40
+// Buckets of 2^shift bytes from s0, shift = the smallest with span >> shift < kSmallBuckets
+// (a shift, not a 64-bit division: those are long software sequences on the GPU).
+__device__ __forceinline__ uint32_t small_bucket(uint64_t key, uint64_t lo, uint32_t shift) {
+    return (uint32_t)((key - lo) >> shift);
 }
 
 // Exclusive scan of one value per thread over the block (Hillis-Steele in `part`).
@@ -340,6 +345,7 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     __shared__ uint32_t bcnt[kSmallBuckets];
     __shared__ uint32_t nbig, bmax;
     static_assert(2 * kSmallJ * 2 + kSmallJ <= sizeof(uint64_t) * kSmallResolveMax, "LDS reuse");
+    static_assert(kSmallPer <= 32, "on-mask bits");
 
     const uint32_t tid = threadIdx.x, T = kSmallThreads;
     const uint32_t m = np + nnew;
@@ -352,6 +358,8 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     //    bitonic sort of the whole set.
     const uint64_t t_start = wall_clock64();
     const uint64_t span = p.end > p.s0 ? p.end - p.s0 : 1;
+    uint32_t bshift = 0;
+    while ((span >> bshift) >= kSmallBuckets) ++bshift;
     for (uint32_t b = tid; b < kSmallBuckets; b += T) bcnt[b] = 0;
     if (tid == 0) {
         nbig = 0;
@@ -360,7 +368,7 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     __syncthreads();
     for (uint32_t i = tid; i < m; i += T) {
         const uint64_t key = i < np ? C[i] : newc[i - np];
-        atomicAdd(&bcnt[small_bucket(key, p.s0, span)], 1u);
+        atomicAdd(&bcnt[small_bucket(key, p.s0, bshift)], 1u);
     }
     __syncthreads();
     const uint64_t t_hist = wall_clock64();
@@ -388,22 +396,22 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     if (bmax <= kSmallBucketMax) {
         for (uint32_t i = tid; i < m; i += T) {
             const uint64_t key = i < np ? C[i] : newc[i - np];
-            sk[atomicAdd(&bcnt[small_bucket(key, p.s0, span)], 1u)] = key;
+            sk[atomicAdd(&bcnt[small_bucket(key, p.s0, bshift)], 1u)] = key;
         }
         __syncthreads();  // bcnt[b] = end of bucket b
         t_scatter = wall_clock64();
-        for (uint32_t b = tid; b < kSmallBuckets; b += T) {
+        // final index of a key = its bucket's start + #smaller keys in the bucket
+        // (positions are distinct); placed through C, then reloaded
+        for (uint32_t i = tid; i < m; i += T) {
+            const uint64_t key = sk[i];
+            const uint32_t b = small_bucket(key, p.s0, bshift);
             const uint32_t lo = b ? bcnt[b - 1] : 0u, hi = bcnt[b];
-            for (uint32_t i = lo + 1; i < hi; ++i) {
-                const uint64_t v = sk[i];
-                uint32_t k = i;
-                while (k > lo && sk[k - 1] > v) {
-                    sk[k] = sk[k - 1];
-                    --k;
-                }
-                sk[k] = v;
-            }
+            uint32_t rank = 0;
+            for (uint32_t k = lo; k < hi; ++k) rank += sk[k] < key ? 1u : 0u;
+            C[lo + rank] = key;
         }
+        __syncthreads();
+        for (uint32_t i = tid; i < m; i += T) sk[i] = C[i];
         __syncthreads();
     } else {
         uint32_t N = 2;
@@ -426,9 +434,13 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
         }
     }
     const uint64_t t_sorted = wall_clock64();
+    const bool bucketed = bmax <= kSmallBucketMax;
 
-    // 2. sorted keys -> C; successor candidate and forced-cut count of every node
-    for (uint32_t i = tid; i < m; i += T) C[i] = sk[i];
+    // 2. sorted keys -> C; successor candidate and forced-cut count of every node.  The
+    //    search for the first key >= lo starts at lo's bucket (bucket b starts at the
+    //    end of bucket b-1), so it gallops over at most one bucket.
+    if (!bucketed)
+        for (uint32_t i = tid; i < m; i += T) C[i] = sk[i];
     for (uint32_t j = tid; j <= m; j += T) {
         uint64_t s = (j == m) ? p.s0 : sk[j] + 1;
         uint32_t i = (j == m) ? 0u : j + 1;
@@ -436,7 +448,16 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
         uint32_t r = none;
         for (;;) {
             const uint64_t lo = s + p.min_eff - 1, hi = s + p.max_eff - 1;
-            i = lower_bound_u64(sk, i, m, lo);
+            if (lo >= p.end) {
+                i = m;
+            } else {
+                if (bucketed) {
+                    const uint32_t b = small_bucket(lo, p.s0, bshift);
+                    const uint32_t bs = b ? bcnt[b - 1] : 0u;
+                    i = bs > i ? bs : i;
+                }
+                i = lower_bound_u64(sk, i, m, lo);
+            }
             if (i < m && sk[i] <= hi) {
                 r = i;
                 break;
@@ -469,26 +490,25 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
         on[j] = j == m ? 1 : 0;
     }
     __syncthreads();
-    // each thread owns the contiguous nodes [d_lo, d_lo + kDblPer) (n <= T * kDblPer):
+    // thread t owns nodes t + q*T (consecutive lanes, consecutive u16: conflict-free);
     // all its gathers are issued before any result is used (one LDS latency per round)
-    constexpr uint32_t kDblPer = (kSmallJ + kSmallThreads - 1) / kSmallThreads;
-    const uint32_t d_lo = tid * kDblPer;
-    for (uint32_t span = 1; span < n; span <<= 1) {
-        uint32_t J[kDblPer], JJ[kDblPer];
-        uint8_t o[kDblPer];
+    for (uint32_t rnd = 1; rnd < n; rnd <<= 1) {
+        uint32_t J[kSmallPer], JJ[kSmallPer];
+        uint32_t o = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < kDblPer; ++q) {
-            const uint32_t j = d_lo + q;
+        for (uint32_t q = 0; q < kSmallPer; ++q) {
+            const uint32_t j = tid + q * T;
             J[q] = j < n ? ja[j] : 0u;
-            o[q] = j < n ? on[j] : 0;
+            o |= (j < n && on[j]) ? (1u << q) : 0u;
         }
 #pragma unroll
-        for (uint32_t q = 0; q < kDblPer; ++q) JJ[q] = d_lo + q < n ? ja[J[q]] : 0u;
+        for (uint32_t q = 0; q < kSmallPer; ++q) JJ[q] = tid + q * T < n ? ja[J[q]] : 0u;
 #pragma unroll
-        for (uint32_t q = 0; q < kDblPer; ++q) {
-            if (d_lo + q < n) {
-                if (o[q]) on[J[q]] = 1;
-                jb[d_lo + q] = (uint16_t)JJ[q];
+        for (uint32_t q = 0; q < kSmallPer; ++q) {
+            const uint32_t j = tid + q * T;
+            if (j < n) {
+                if (o & (1u << q)) on[J[q]] = 1;
+                jb[j] = (uint16_t)JJ[q];
             }
         }
         __syncthreads();
@@ -504,19 +524,46 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     const uint32_t per = (slots + T - 1) / T;
     const uint32_t s_lo = min(tid * per, slots), s_hi = min(s_lo + per, slots);
     uint64_t sum = 0;
-    for (uint32_t sl = s_lo; sl < s_hi; ++sl) {
-        const uint32_t j = sl == 0 ? m : sl - 1;
-        if (on[j]) sum += nforced[j] + (nxt[j] != none ? 1u : 0u);
+    for (uint32_t c0 = s_lo; c0 < s_hi; c0 += kSmallChunk) {
+        uint64_t nfq[kSmallChunk];
+        uint32_t nxq[kSmallChunk];
+#pragma unroll
+        for (uint32_t q = 0; q < kSmallChunk; ++q) {
+            const uint32_t sl = c0 + q;
+            const uint32_t j = sl == 0 ? m : sl - 1;
+            const bool live = sl < s_hi && on[j];
+            nfq[q] = live ? nforced[j] : 0u;
+            nxq[q] = live ? nxt[j] : none;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kSmallChunk; ++q) sum += nfq[q] + (nxq[q] != none ? 1u : 0u);
     }
     uint64_t o = block_exclusive_scan(part, sum, tid);
     const uint64_t t_scanned = wall_clock64();
 
     // 5. emit
-    for (uint32_t sl = s_lo; sl < s_hi; ++sl) {
-        const uint32_t j = sl == 0 ? m : sl - 1;
-        if (!on[j]) continue;
-        const uint64_t s = (j == m) ? p.s0 : C[j] + 1;
-        const uint64_t nf = nforced[j];
+    for (uint32_t c0 = s_lo; c0 < s_hi; c0 += kSmallChunk) {
+      uint32_t jq[kSmallChunk], nxq[kSmallChunk];
+      uint64_t nfq[kSmallChunk], cj[kSmallChunk], cn[kSmallChunk];
+      uint32_t live = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < kSmallChunk; ++q) {
+          const uint32_t sl = c0 + q;
+          jq[q] = sl == 0 ? m : sl - 1;
+          const bool l = sl < s_hi && on[jq[q]];
+          live |= l ? (1u << q) : 0u;
+          nfq[q] = l ? nforced[jq[q]] : 0u;
+          nxq[q] = l ? nxt[jq[q]] : none;
+          cj[q] = (l && jq[q] != m) ? C[jq[q]] : 0u;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kSmallChunk; ++q) cn[q] = nxq[q] != none ? C[nxq[q]] : 0u;
+#pragma unroll
+      for (uint32_t q = 0; q < kSmallChunk; ++q) {
+        if (!(live & (1u << q))) continue;
+        const uint32_t j = jq[q];
+        const uint64_t s = (j == m) ? p.s0 : cj[q] + 1;
+        const uint64_t nf = nfq[q];
         bool done = false;
         if (nf >= kSmallBigMin) {
             const uint32_t b = atomicAdd(&nbig, 1u);
@@ -530,14 +577,15 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
         if (!done)
             for (uint64_t t = 0; t < nf; ++t)
                 if (o + t < out_cap) out[o + t] = s + (t + 1) * p.max_eff;
-        if (nxt[j] != none) {
-            if (o + nf < out_cap) out[o + nf] = C[nxt[j]] + 1;
+        if (nxq[q] != none) {
+            if (o + nf < out_cap) out[o + nf] = cn[q] + 1;
             o += nf + 1;
         } else {
             open_info[0] = o + nf;              // cuts before the open chunk = all cuts
             open_info[1] = s + nf * p.max_eff;  // start of the open chunk
             o += nf;
         }
+      }
     }
     __syncthreads();
     const uint32_t nb = min(nbig, kSmallBig);
