@@ -108,11 +108,14 @@ struct pbs_chunker {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     DevBuf d_table, d_pre, d_counters, d_susp, d_cand, d_C, d_sort_tmp, d_nxt, d_jtmp, d_nf, d_on,
-        d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in;
+        d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in, d_stage, d_hits;
     uint32_t susp_cap = 0, cand_cap = 0;
     uint64_t* h_small = nullptr;  // pinned + mapped: [0] counters, [8..19] results, [24..31] tail
     uint64_t* h_cuts = nullptr;   // pinned + mapped: cut list of the small resolve
     uint64_t* h_keep = nullptr;   // pinned + mapped: open-chunk candidates of the small resolve
+    uint64_t* h_cand = nullptr;   // pinned + mapped: candidates of a small scan() batch
+    uint8_t* h_stage = nullptr;   // pinned: carry | pending | input of a small batch
+    size_t h_stage_cap = 0;
     // events: 0/1 main scan, 2 exact end, 3/4 resolve, 5 call start
     hipEvent_t ev[6] = {};
     pbs_timing timing{};
@@ -314,32 +317,22 @@ int run_resolve(pbs_chunker* c, uint32_t m, uint64_t end, uint64_t* out, size_t 
     return finish_resolve(c, s_open, end, keep, ncut);
 }
 
-// Single-workgroup resolve (np + nnew + 2 <= kSmallResolveMax): pending candidates are
-// in d_C[0..np), the new unsorted ones in d_cand[0..nnew).  One host sync.
-int run_resolve_small(pbs_chunker* c, const uint64_t* newc, uint32_t np, uint32_t nnew,
-                      uint64_t end, uint64_t* out, size_t cap, size_t* n) {
-    const Params& p = c->prm;
-    const uint32_t m = np + nnew;
-    HIP_TRY(c, c->d_nxt.ensure(((size_t)m + 2) * 4));
-    HIP_TRY(c, c->d_nf.ensure(((size_t)m + 2) * 8));
-    HIP_TRY(c, c->d_res.ensure(32));
-    const uint64_t out_cap = cut_bound(c, m, end);
-    HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
+int ensure_small_host_bufs(pbs_chunker* c) {
     if (!c->h_cuts) HIP_TRY(c, hipHostMalloc((void**)&c->h_cuts, kHostCuts * 8, hipHostMallocMapped));
     if (!c->h_keep) HIP_TRY(c, hipHostMalloc((void**)&c->h_keep, kHostKeep * 8, hipHostMallocMapped));
-    uint64_t *cuts_dev = nullptr, *keep_dev = nullptr, *small_dev = nullptr;
-    HIP_TRY(c, hipHostGetDevicePointer((void**)&cuts_dev, c->h_cuts, 0));
-    HIP_TRY(c, hipHostGetDevicePointer((void**)&keep_dev, c->h_keep, 0));
-    HIP_TRY(c, hipHostGetDevicePointer((void**)&small_dev, c->h_small, 0));
-    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
-    ResolveParams rp{p.min_eff, p.max_eff, end, c->chunk_start};
-    HIP_TRY(c, launch_resolve_small(newc, nnew, c->d_C.as<uint64_t>(), np, rp,
-                                    c->d_nxt.as<uint32_t>(), c->d_nf.as<uint64_t>(),
-                                    c->d_cuts.as<uint64_t>(), out_cap, cuts_dev, kHostCuts,
-                                    keep_dev, kHostKeep, c->d_res.as<uint64_t>(), small_dev + 8,
-                                    c->stream));
-    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return PBS_OK;
+}
+
+template <class T>
+int mapped(pbs_chunker* c, T* host, T** dev) {
+    HIP_TRY(c, hipHostGetDevicePointer((void**)dev, host, 0));
+    return PBS_OK;
+}
+
+// After a single-workgroup resolve (synchronized): cut list and open-chunk candidates
+// from the mapped buffers (device copies when they did not fit).
+int small_finish(pbs_chunker* c, uint32_t m, uint64_t out_cap, uint64_t end, uint64_t* out,
+                 size_t cap, size_t* n) {
     const uint64_t ncut = c->h_small[8], s_open = c->h_small[9], idx = c->h_small[10];
     if (c->debug_phases)
         std::fprintf(stderr,
@@ -368,6 +361,116 @@ int run_resolve_small(pbs_chunker* c, const uint64_t* newc, uint32_t np, uint32_
     if (wait) HIP_TRY(c, hipStreamSynchronize(c->stream));
     *n += ncut;
     return finish_resolve(c, s_open, end, keep, ncut);
+}
+
+// Single-workgroup resolve (np + nnew + 2 <= kSmallResolveMax): pending candidates are
+// in d_C[0..np), the new unsorted ones in newc[0..nnew).  One host sync.
+int run_resolve_small(pbs_chunker* c, const uint64_t* newc, uint32_t np, uint32_t nnew,
+                      uint64_t end, uint64_t* out, size_t cap, size_t* n) {
+    const Params& p = c->prm;
+    const uint32_t m = np + nnew;
+    HIP_TRY(c, c->d_nxt.ensure(((size_t)m + 2) * 4));
+    HIP_TRY(c, c->d_nf.ensure(((size_t)m + 2) * 8));
+    HIP_TRY(c, c->d_res.ensure(32));
+    const uint64_t out_cap = cut_bound(c, m, end);
+    HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
+    int rc = ensure_small_host_bufs(c);
+    if (rc) return rc;
+    uint64_t *cuts_dev = nullptr, *keep_dev = nullptr, *small_dev = nullptr;
+    if ((rc = mapped(c, c->h_cuts, &cuts_dev)) || (rc = mapped(c, c->h_keep, &keep_dev)) ||
+        (rc = mapped(c, c->h_small, &small_dev)))
+        return rc;
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    ResolveParams rp{p.min_eff, p.max_eff, end, c->chunk_start};
+    HIP_TRY(c, launch_resolve_small(newc, nnew, c->d_C.as<uint64_t>(), np, rp,
+                                    c->d_nxt.as<uint32_t>(), c->d_nf.as<uint64_t>(),
+                                    c->d_cuts.as<uint64_t>(), out_cap, cuts_dev, kHostCuts,
+                                    keep_dev, kHostKeep, c->d_res.as<uint64_t>(), small_dev + 8,
+                                    c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return small_finish(c, m, out_cap, end, out, cap, n);
+}
+
+// Small batch (bl <= kFusedMaxBytes), stream bytes [pos, pos + bl) from host `hsrc` or
+// device `dsrc`: carry | pending (| host input) are staged in pinned memory and sent with
+// ONE H2D; scan_blocks_kernel + resolve_small_kernel<1> (resolve) or <2> (candidates
+// only, for scan()); one host sync.  *overflow: the batch holds too many candidates for
+// one workgroup -- nothing changed, the caller takes the regular path.
+int fused_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos,
+                uint64_t bl, size_t np, uint64_t rend, bool resolve, uint64_t* out, size_t cap,
+                size_t* n, bool* overflow) {
+    const Params& p = c->prm;
+    *overflow = false;
+    const size_t data_off = (64 + np * 8 + 15) & ~(size_t)15;
+    const size_t stage_bytes = data_off + (hsrc ? bl : 0);
+    if (stage_bytes > c->h_stage_cap) {
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_cap = 0;
+        const size_t want = std::max<size_t>(stage_bytes, kFusedMaxBytes + 64 + 8 * 1024 + 16);
+        HIP_TRY(c, hipHostMalloc((void**)&c->h_stage, want, hipHostMallocDefault));
+        c->h_stage_cap = want;
+    }
+    std::memcpy(c->h_stage + 64 - c->carry_len, c->carry, c->carry_len);
+    if (np) std::memcpy(c->h_stage + 64, c->pending.data() + c->pend_head, np * 8);
+    if (hsrc) std::memcpy(c->h_stage + data_off, hsrc, bl);
+    HIP_TRY(c, c->d_stage.ensure(stage_bytes));
+    HIP_TRY(c, hipMemcpyAsync(c->d_stage.p, c->h_stage, stage_bytes, hipMemcpyHostToDevice, c->stream));
+    const uint8_t* data = hsrc ? c->d_stage.as<uint8_t>() + data_off : dsrc;
+    const uint64_t nblk = (bl + kBlockBytes - 1) / kBlockBytes;
+    HIP_TRY(c, c->d_hits.ensure(std::max<uint64_t>(nblk, 1) * 16));
+    HIP_TRY(c, c->d_nxt.ensure((kSmallResolveMax + 2) * 4));
+    HIP_TRY(c, c->d_nf.ensure((kSmallResolveMax + 2) * 8));
+    HIP_TRY(c, c->d_C.ensure((kSmallResolveMax + 2) * 8));
+    HIP_TRY(c, c->d_res.ensure(32));
+    const uint64_t out_cap = cut_bound(c, kSmallResolveMax, rend);
+    HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
+    int rc = ensure_small_host_bufs(c);
+    if (rc) return rc;
+    if (!c->h_cand)
+        HIP_TRY(c, hipHostMalloc((void**)&c->h_cand, kSmallResolveMax * 8, hipHostMallocMapped));
+    uint64_t *cuts_dev = nullptr, *keep_dev = nullptr, *small_dev = nullptr, *cand_dev = nullptr;
+    if ((rc = mapped(c, c->h_cuts, &cuts_dev)) || (rc = mapped(c, c->h_keep, &keep_dev)) ||
+        (rc = mapped(c, c->h_small, &small_dev)) || (rc = mapped(c, c->h_cand, &cand_dev)))
+        return rc;
+    FusedScanArgs fa{data, bl, c->d_stage.as<uint8_t>() + 64 - c->carry_len, c->carry_len, pos,
+                     p.mask, p.minimum, c->d_hits.as<uint4>(), nblk,
+                     reinterpret_cast<const uint64_t*>(c->d_stage.as<uint8_t>() + 64), cand_dev,
+                     kSmallResolveMax};
+    ResolveParams rp{p.min_eff, p.max_eff, rend, c->chunk_start};
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(c, launch_scan_resolve_small(fa, resolve ? 1 : 0, c->d_C.as<uint64_t>(), (uint32_t)np,
+                                         rp, c->d_nxt.as<uint32_t>(), c->d_nf.as<uint64_t>(),
+                                         c->d_cuts.as<uint64_t>(), out_cap, cuts_dev, kHostCuts,
+                                         keep_dev, kHostKeep, c->d_res.as<uint64_t>(),
+                                         small_dev + 8, c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+    const uint64_t tl = std::min<uint64_t>(bl, kWindow - 1);
+    uint8_t* tail = reinterpret_cast<uint8_t*>(c->h_small + 24);
+    if (tl && !hsrc)
+        HIP_TRY(c, hipMemcpyAsync(tail, dsrc + bl - tl, tl, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->h_small[20]) {
+        *overflow = true;
+        return PBS_OK;
+    }
+    c->timing.bytes += bl;
+    if (resolve) {
+        const uint32_t m = (uint32_t)c->h_small[21];
+        c->timing.candidates += m - np;
+        rc = small_finish(c, m, out_cap, rend, out, cap, n);
+        if (rc) return rc;
+    } else {
+        const uint64_t k = c->h_small[8];
+        c->timing.candidates += k;
+        const size_t old = c->pending.size();
+        c->pending.resize(old + k);
+        std::memcpy(c->pending.data() + old, c->h_cand, k * 8);
+    }
+    update_carry(c, hsrc ? hsrc + bl - tl : tail, tl);
+    c->scanned_end = pos + bl;
+    return PBS_OK;
 }
 
 void reset_stream(pbs_chunker* c) {
@@ -421,6 +524,17 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
         uint32_t nnew = 0;
         const uint8_t* dsrc = nullptr;
         const uint8_t* hsrc = nullptr;
+        if (bl && bl <= kFusedMaxBytes && np + 2 <= kSmallResolveMax) {
+            bool overflow = false;
+            int rc = fused_batch(c, device ? data + (pos - c->consumed) : nullptr,
+                                 device ? nullptr : data + (pos - c->consumed), pos, bl, np, rend,
+                                 true, out, cap, &n, &overflow);
+            if (rc) return rc;
+            if (!overflow) {
+                pos += bl;
+                continue;
+            }
+        }
         if (bl) {
             if (device) {
                 dsrc = data + (pos - c->consumed);
@@ -468,7 +582,7 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
         }
         reset_stream(c);
     }
-    float ms = 0;  // ev[4] = end of the last resolve, already synchronized
+    float ms = 0;  // ev[4] = end of the last resolve (every path records it), synchronized
     HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[5], c->ev[4]));
     c->timing.total_ms = ms;
     *n_out = n;
@@ -480,6 +594,10 @@ void destroy(pbs_chunker* c) {
                       &c->d_sort_tmp, &c->d_nxt, &c->d_jtmp, &c->d_nf, &c->d_on, &c->d_cnt,
                       &c->d_off, &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in};
     for (DevBuf* b : bufs) b->release();
+    c->d_stage.release();
+    c->d_hits.release();
+    if (c->h_cand) (void)hipHostFree(c->h_cand);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -608,6 +726,17 @@ size_t pbs_chunker_scan(pbs_chunker* c, const uint8_t* data, size_t len) {
         while (pos < end) {
             const uint64_t bl = std::min<uint64_t>(end - pos, batch_max(c->prm));
             const uint8_t* hsrc = data + (pos - c->consumed);
+            if (bl <= kFusedMaxBytes) {
+                bool overflow = false;
+                size_t dummy = 0;
+                if (fused_batch(c, nullptr, hsrc, pos, bl, 0, pos + bl, false, nullptr, 0, &dummy,
+                                &overflow) != PBS_OK)
+                    return SIZE_MAX;
+                if (!overflow) {
+                    pos += bl;
+                    continue;
+                }
+            }
             if (c->d_in.ensure(bl) != hipSuccess ||
                 hipMemcpyAsync(c->d_in.p, hsrc, bl, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
                 fail(c, PBS_ERR_HIP);

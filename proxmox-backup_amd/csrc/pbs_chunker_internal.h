@@ -53,6 +53,32 @@ hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C
                                 uint64_t* out, uint64_t out_cap, uint64_t* out_host,
                                 uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
                                 uint64_t* res, uint64_t* res_host, hipStream_t stream);
+// Small-input path (scan_blocks_kernel + resolve_small_kernel<1|2>, two launches, no
+// host sync between): the input bytes `data[0..len)` (stream offset `base`, device
+// memory) with the pre_len <= 63 bytes before them in `pre` (device), the test
+// (h & mask) >= minimum, `hits` = device scratch of nblk = ceil(len/128) uint4 masks,
+// the pending candidates in `pend` (device or mapped), and for scan-only calls the
+// output array for the new candidates (mapped).
+struct FusedScanArgs {
+    const uint8_t* data;
+    uint64_t len;
+    const uint8_t* pre;
+    uint32_t pre_len;
+    uint64_t base;
+    uint32_t mask, minimum;
+    const uint4* hits;
+    uint64_t nblk;
+    const uint64_t* pend;
+    uint64_t* cand_out;
+    uint64_t cand_cap;
+};
+constexpr uint64_t kFusedMaxBytes = 1ull << 20;  // inputs up to this size take the fused path
+hipError_t launch_scan_resolve_small(const FusedScanArgs& fa, int resolve, uint64_t* C,
+                                     uint32_t np, const ResolveParams& p, uint32_t* nxt,
+                                     uint64_t* nforced, uint64_t* out, uint64_t out_cap,
+                                     uint64_t* out_host, uint64_t host_cap, uint64_t* keep_host,
+                                     uint64_t keep_cap, uint64_t* res, uint64_t* res_host,
+                                     hipStream_t stream);
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,
                       int kind, hipStream_t stream);
 

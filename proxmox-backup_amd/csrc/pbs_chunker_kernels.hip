@@ -172,6 +172,23 @@ __global__ __launch_bounds__(256) void scan_exact_kernel(
     }
 }
 
+// Every 128-byte block of a small input (the fused host path): hit mask per block.
+__global__ __launch_bounds__(256) void scan_blocks_kernel(const uint8_t* __restrict__ data,
+                                                          uint64_t len,
+                                                          const uint8_t* __restrict__ pre,
+                                                          uint32_t pre_len, uint32_t mask,
+                                                          uint32_t minimum, uint4* __restrict__ hits,
+                                                          uint64_t nblk) {
+    __shared__ uint32_t tab[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = kBuzhashTable[i];
+    __syncthreads();
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    uint32_t hit[4] = {0u, 0u, 0u, 0u};
+    exact_block(data, len, pre, pre_len, b * kIter, tab, mask, minimum, hit);
+    hits[b] = make_uint4(hit[0], hit[1], hit[2], hit[3]);
+}
+
 // ---------------------------------------------------------------------------------
 // Phase B: resolve the min/max rule over the sorted candidate list
 // ---------------------------------------------------------------------------------
@@ -319,7 +336,8 @@ __device__ __forceinline__ uint32_t small_bucket(uint64_t key, uint64_t lo, uint
 }
 
 // Exclusive scan of one value per thread over the block (Hillis-Steele in `part`).
-__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t* part, uint64_t v, uint32_t tid) {
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t* part, uint64_t v, uint32_t tid,
+                                                        uint64_t* total = nullptr) {
     part[tid] = v;
     __syncthreads();
     for (uint32_t d = 1; d < kSmallThreads; d <<= 1) {
@@ -329,15 +347,27 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t* part, uint64_
         __syncthreads();
     }
     const uint64_t r = part[tid] - v;
+    if (total) *total = part[kSmallThreads - 1];
     __syncthreads();  // part is reused by the caller's next scan
     return r;
 }
 
+// FUSED = 0: resolve `nnew` unsorted candidates (newc) after `np` sorted pending ones
+//            (C[0..np)).
+// FUSED = 1: small inputs (the host path's 256 KiB pieces): the kernel also scans the
+//            input itself -- every 128-byte block with exact_block, hits compacted in
+//            block order, so the keys come out sorted -- after the pending candidates
+//            (fa.pend), then resolves; one launch per call instead of ~10.
+// FUSED = 2: scan only; the sorted candidates go to fa.cand_out (mapped host memory).
+// More than kSmallResolveMax - 2 keys in a fused call: res_host[12] = 1 and nothing else
+// is written (the host reruns the call on the multi-kernel path).
+template <int FUSED>
 __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     const uint64_t* __restrict__ newc, uint32_t nnew, uint64_t* C, uint32_t np, ResolveParams p,
     uint32_t* nxt, uint64_t* nforced, uint64_t* __restrict__ out, uint64_t out_cap,
     uint64_t* __restrict__ out_host, uint64_t host_cap, uint64_t* __restrict__ keep_host,
-    uint64_t keep_cap, uint64_t* __restrict__ res, uint64_t* __restrict__ res_host) {
+    uint64_t keep_cap, uint64_t* __restrict__ res, uint64_t* __restrict__ res_host,
+    FusedScanArgs fa) {
     __shared__ uint64_t sk[kSmallResolveMax];  // keys; later reused for ja | jb | on
     __shared__ uint64_t part[kSmallThreads];
     __shared__ uint64_t big[kSmallBig][3];
@@ -348,17 +378,72 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     static_assert(kSmallPer <= 32, "on-mask bits");
 
     const uint32_t tid = threadIdx.x, T = kSmallThreads;
-    const uint32_t m = np + nnew;
+    uint32_t m = np + nnew;
+
+    const uint64_t t_start = wall_clock64();
+    uint64_t t_hist = t_start, t_bscan = t_start, t_scatter = t_start;
+    uint32_t bshift = 0;
+    if constexpr (FUSED != 0) {
+        // 1'. pending keys, then the candidates of the input's 128-byte blocks (hit masks
+        //     from scan_blocks_kernel), compacted in block order -- so already sorted.
+        //     Thread t owns the contiguous blocks [t*per, (t+1)*per).
+        for (uint32_t i = tid; i < np; i += T) sk[i] = fa.pend[i];
+        if (tid == 0) nbig = 0;
+        const uint32_t per = (uint32_t)((fa.nblk + T - 1) / T);
+        const uint64_t b_lo = min((uint64_t)tid * per, fa.nblk);
+        const uint64_t b_hi = min(b_lo + per, fa.nblk);
+        uint32_t k = 0;
+        for (uint64_t b = b_lo; b < b_hi; ++b) {
+            const uint4 hm = fa.hits[b];
+            k += __builtin_popcount(hm.x) + __builtin_popcount(hm.y) + __builtin_popcount(hm.z) +
+                 __builtin_popcount(hm.w);
+        }
+        uint64_t total;
+        uint32_t idx = np + (uint32_t)block_exclusive_scan(part, k, tid, &total);
+        if (np + total + 2 > kSmallResolveMax) {  // uniform
+            if (tid == 0) res_host[12] = 1;
+            return;
+        }
+        for (uint64_t b = b_lo; b < b_hi; ++b) {
+            const uint4 hm = fa.hits[b];
+            const uint32_t w4[4] = {hm.x, hm.y, hm.z, hm.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t mm = w4[q];
+                while (mm) {
+                    const int bit = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    sk[idx++] = fa.base + b * kBlockBytes + (uint64_t)(q * 32 + bit);
+                }
+            }
+        }
+        m = np + (uint32_t)total;
+        __syncthreads();
+        if constexpr (FUSED == 2) {
+            if (m - np <= fa.cand_cap)
+                for (uint32_t i = np + tid; i < m; i += T) fa.cand_out[i - np] = sk[i];
+            if (tid == 0) {
+                res_host[0] = m - np;
+                res_host[12] = 0;
+            }
+            return;
+        }
+        if (tid == 0) {
+            res_host[12] = 0;
+            res_host[13] = m;
+            bmax = kSmallBucketMax + 1;  // no bucket index: plain searches below
+        }
+        __syncthreads();
+    }
     const uint32_t none = m + 1;
+    if constexpr (FUSED == 0) {
 
     // 1. sort the keys into LDS.  All keys lie in [s0, end) (pending >= chunk_start,
     //    new < end), so a bucket sort over kSmallBuckets equal ranges of that span
     //    (histogram, scan, scatter, insertion sort per bucket) is O(m); a bucket
     //    holding more than kSmallBucketMax keys (skewed input) falls back to a
     //    bitonic sort of the whole set.
-    const uint64_t t_start = wall_clock64();
     const uint64_t span = p.end > p.s0 ? p.end - p.s0 : 1;
-    uint32_t bshift = 0;
     while ((span >> bshift) >= kSmallBuckets) ++bshift;
     for (uint32_t b = tid; b < kSmallBuckets; b += T) bcnt[b] = 0;
     if (tid == 0) {
@@ -371,7 +456,7 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
         atomicAdd(&bcnt[small_bucket(key, p.s0, bshift)], 1u);
     }
     __syncthreads();
-    const uint64_t t_hist = wall_clock64();
+    t_hist = wall_clock64();
     {
         constexpr uint32_t per_b = kSmallBuckets / kSmallThreads;
         uint32_t c[per_b], bsum = 0, bm = 0;
@@ -391,8 +476,8 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
         }
     }
     __syncthreads();
-    const uint64_t t_bscan = wall_clock64();
-    uint64_t t_scatter = t_bscan;
+    t_bscan = wall_clock64();
+    t_scatter = t_bscan;
     if (bmax <= kSmallBucketMax) {
         for (uint32_t i = tid; i < m; i += T) {
             const uint64_t key = i < np ? C[i] : newc[i - np];
@@ -433,6 +518,7 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
             }
         }
     }
+    }  // FUSED == 0
     const uint64_t t_sorted = wall_clock64();
     const bool bucketed = bmax <= kSmallBucketMax;
 
@@ -769,9 +855,33 @@ hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C
                                 uint64_t* res, uint64_t* res_host, hipStream_t stream) {
     if ((uint64_t)np + nnew + 2 > kSmallResolveMax) return hipErrorInvalidValue;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(resolve_small_kernel, dim3(1), dim3(kSmallThreads), 0, stream, newc, nnew,
-                       C, np, p, nxt, nforced, out, out_cap, out_host, host_cap, keep_host,
-                       keep_cap, res, res_host);
+    hipLaunchKernelGGL(resolve_small_kernel<0>, dim3(1), dim3(kSmallThreads), 0, stream, newc,
+                       nnew, C, np, p, nxt, nforced, out, out_cap, out_host, host_cap, keep_host,
+                       keep_cap, res, res_host, FusedScanArgs{});
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_resolve_small(const FusedScanArgs& fa, int resolve, uint64_t* C,
+                                     uint32_t np, const ResolveParams& p, uint32_t* nxt,
+                                     uint64_t* nforced, uint64_t* out, uint64_t out_cap,
+                                     uint64_t* out_host, uint64_t host_cap, uint64_t* keep_host,
+                                     uint64_t keep_cap, uint64_t* res, uint64_t* res_host,
+                                     hipStream_t stream) {
+    if ((uint64_t)np + 2 > kSmallResolveMax || fa.nblk * kBlockBytes > kFusedMaxBytes + kBlockBytes)
+        return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    if (fa.nblk)
+        hipLaunchKernelGGL(scan_blocks_kernel, dim3((unsigned)((fa.nblk + 255) / 256)), dim3(256), 0,
+                           stream, fa.data, fa.len, fa.pre, fa.pre_len, fa.mask, fa.minimum,
+                           const_cast<uint4*>(fa.hits), fa.nblk);
+    if (resolve)
+        hipLaunchKernelGGL(resolve_small_kernel<1>, dim3(1), dim3(kSmallThreads), 0, stream,
+                           nullptr, 0u, C, np, p, nxt, nforced, out, out_cap, out_host, host_cap,
+                           keep_host, keep_cap, res, res_host, fa);
+    else
+        hipLaunchKernelGGL(resolve_small_kernel<2>, dim3(1), dim3(kSmallThreads), 0, stream,
+                           nullptr, 0u, C, np, p, nxt, nforced, out, out_cap, out_host, host_cap,
+                           keep_host, keep_cap, res, res_host, fa);
     return hipGetLastError();
 }
 

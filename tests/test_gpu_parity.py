@@ -190,6 +190,41 @@ def test_resolve_paths(gpu, oracle, name, mk, avg):
     assert np.array_equal(got2, got), name
 
 
+# Batches of <= 1 MiB take the small-input path (block scan + one-workgroup resolve, one
+# sync); more than ~16K candidates in such a batch (avg 16/64) falls back to the
+# regular path; 1 MiB + 1 is the first size on the regular path.
+@pytest.mark.parametrize("avg,piece", [(4 * MiB, 256 * KiB), (64 * KiB, 64 * KiB + 3),
+                                       (256, 1 * MiB), (64, 1 * MiB), (16, 300 * KiB),
+                                       (4096, 1 * MiB + 1), (1 * MiB, 7)])
+def test_small_batches(gpu, oracle, avg, piece):
+    n = 6 * MiB + 11 if piece > 64 else 64 * KiB
+    data = gen_np.gen_vmimage(n, 0x5EED0003, 300 * MiB + 4093)
+    ref = oracle.chunk_feed(avg, data)
+    got = []
+    with gpu.Chunker(avg) as c:
+        for a in range(0, n, piece):
+            got.append(c.find_cuts(data[a:a + piece], is_final=a + piece >= n))
+    got = np.concatenate(got)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    assert np.array_equal(got, ref)
+
+
+def test_small_batches_device(gpu, oracle):
+    import torch
+    n, avg = 5 * MiB + 24, 256 * KiB
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n, gpu.GEN_VMIMAGE, 0x5EED0003, 96 * MiB)
+    ref = oracle.chunk_feed(avg, dev.cpu().numpy())
+    got = []
+    with gpu.Chunker(avg) as c:
+        c.set_stream(torch.cuda.current_stream().cuda_stream)
+        for a in range(0, n, 777 * KiB + 5):  # unaligned device pieces
+            b = min(n, a + 777 * KiB + 5)
+            got.append(c.find_cuts_device(dev.data_ptr() + a, b - a))
+    assert np.array_equal(np.concatenate(got), ref)
+
+
 @pytest.mark.parametrize("kind", [0, 1, 2])
 def test_device_generator_matches_oracle(gpu, oracle, kind):
     import torch
