@@ -418,7 +418,10 @@ int fused_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64
     HIP_TRY(c, c->d_stage.ensure(stage_bytes));
     HIP_TRY(c, hipMemcpyAsync(c->d_stage.p, c->h_stage, stage_bytes, hipMemcpyHostToDevice, c->stream));
     const uint8_t* data = hsrc ? c->d_stage.as<uint8_t>() + data_off : dsrc;
-    const uint64_t nblk = (bl + kBlockBytes - 1) / kBlockBytes;
+    // block grid on 16-byte-aligned addresses (scan_blocks_kernel): block b starts at
+    // stream offset pos - misalign + 128 b
+    const uint64_t misalign = (uintptr_t)data & 15;
+    const uint64_t nblk = (bl + misalign + kBlockBytes - 1) / kBlockBytes;
     HIP_TRY(c, c->d_hits.ensure(std::max<uint64_t>(nblk, 1) * 16));
     HIP_TRY(c, c->d_nxt.ensure((kSmallResolveMax + 2) * 4));
     HIP_TRY(c, c->d_nf.ensure((kSmallResolveMax + 2) * 8));
@@ -434,7 +437,8 @@ int fused_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64
     if ((rc = mapped(c, c->h_cuts, &cuts_dev)) || (rc = mapped(c, c->h_keep, &keep_dev)) ||
         (rc = mapped(c, c->h_small, &small_dev)) || (rc = mapped(c, c->h_cand, &cand_dev)))
         return rc;
-    FusedScanArgs fa{data, bl, c->d_stage.as<uint8_t>() + 64 - c->carry_len, c->carry_len, pos,
+    FusedScanArgs fa{data, bl, c->d_stage.as<uint8_t>() + 64 - c->carry_len, c->carry_len,
+                     pos - misalign,
                      p.mask, p.minimum, c->d_hits.as<uint4>(), nblk,
                      reinterpret_cast<const uint64_t*>(c->d_stage.as<uint8_t>() + 64), cand_dev,
                      kSmallResolveMax};

@@ -61,65 +61,99 @@ namespace pbs {
 // before this buffer); bytes before that do not exist and contribute nothing, as in
 // the reference's fill phase.  Position p is a candidate iff the window is full
 // (p + pre_len >= 63) and (H(p) & mask) >= minimum; it is written as base + p.
-// Exact hash at positions [B, B+128) of one block, window bytes [B-64, B+128).  The
-// 192 window bytes are loaded first (12 x 16-byte loads when the window lies inside
-// `data` 16-byte aligned -- B % 128 == 0 -- else independent byte loads from `data` and
-// `pre`; a byte-serial loop would pay one memory latency per byte), then the roll runs
-// fully unrolled from registers over the valid byte range [vlo, vhi) of the window;
-// bytes outside it (before the stream, after `len`) contribute nothing.  Hits go to
-// the 128-bit mask hit[] (bit j = position B + j).
-__device__ __forceinline__ void exact_block(const uint8_t* __restrict__ data, uint64_t len,
-                                            const uint8_t* __restrict__ pre, uint32_t pre_len,
-                                            uint64_t B, const uint32_t* tab, uint32_t mask,
-                                            uint32_t minimum, uint32_t (&hit)[4]) {
-    const int64_t q0 = (int64_t)B - 64;
-    const int64_t vlo = (q0 > -(int64_t)pre_len ? q0 : -(int64_t)pre_len) - q0;
-    const int64_t vhi = ((int64_t)len < q0 + 192 ? (int64_t)len : q0 + 192) - q0;
-    uint32_t w[48];
-    if (B >= 64 && B + kIter <= len && ((uintptr_t)(data + B - 64) & 15) == 0) {
-        const uint4* src = reinterpret_cast<const uint4*>(data + B - 64);
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const uint4 v = src[k];
-            w[4 * k] = v.x;
-            w[4 * k + 1] = v.y;
-            w[4 * k + 2] = v.z;
-            w[4 * k + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 48; ++k) {
-            uint32_t v = 0;
+// Exact hits of one 128-byte block, computed by ONE WAVE (B = block start relative to
+// `data`, may be negative on the aligned block grid; window = bytes [B-64, B+128)).
+// A per-thread roll is a 192-step dependent chain (~22k cycles for one block); instead
+// the window hash is a difference of prefix XORs:
+//   h(j) = rotl( P(j) ^ P(j-64), j mod 32 ),   P(j) = XOR_{i<=j} rotr( T[w_i], i mod 32 )
+// (rotl(T, j-i) = rotl(rotr(T, i), j), so the rotation of each term only depends on its
+// own index; window indices j, i).  Lane l < 48 owns window bytes [4l, 4l+4): one dword
+// load, 4 table lookups, a wave-wide prefix XOR (6 shuffles) and P(j-64) from lane l-16;
+// lanes 16..47 test positions j = 64..191, i.e. block positions 4(l-16)+k.
+// Bytes that do not exist (before the stream, after `len`) are read with clamped
+// addresses: a reportable position (q >= 0, q < len, q + pre_len >= 63) has all 64
+// window bytes in existence and its P-difference involves only them; the hit words are
+// clipped to reportable positions.  Returns the 4 hit words (bit j = position B + j),
+// uniform across the wave.  `pre` has 64 readable bytes; `len` >= 1.
+__device__ __forceinline__ uint4 exact_block_wave(const uint8_t* __restrict__ data, uint64_t len,
+                                                  const uint8_t* __restrict__ pre,
+                                                  uint32_t pre_len, int64_t B, const uint32_t* tab,
+                                                  uint32_t mask, uint32_t minimum, int lane) {
+    const int64_t q0 = B - 64;
+    const int64_t ilen = (int64_t)len, plen = (int64_t)pre_len;
+    uint32_t wv = 0;
+    if (lane < 48) {
+        const int64_t q = q0 + 4 * lane;
+        if (q >= 0 && q + 4 <= ilen && ((uintptr_t)(data + q) & 3) == 0) {
+            wv = *reinterpret_cast<const uint32_t*>(data + q);
+        } else {
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                const int64_t q = q0 + 4 * k + b;
-                uint32_t byte = 0;
-                if (q >= 0 && q < (int64_t)len)
-                    byte = data[q];
-                else if (q < 0 && q >= -(int64_t)pre_len)
-                    byte = pre[pre_len + q];
-                v |= byte << (8 * b);
+                const int64_t qq = q + b;
+                const uint32_t bd = data[qq < 0 ? 0 : (qq >= ilen ? ilen - 1 : qq)];
+                const int64_t qp = plen + qq;
+                const uint32_t bp = pre[qp < 0 ? 0 : (qp > 63 ? 63 : qp)];
+                wv |= (qq < 0 ? bp : bd) << (8 * b);
             }
-            w[k] = v;
         }
     }
-    uint32_t h = 0;
+    uint32_t u[4], acc = 0;
 #pragma unroll
-    for (int i = 0; i < 192; ++i) {
-        uint32_t x = (i >= vlo && i < vhi) ? tab[(w[i >> 2] >> ((i & 3) * 8)) & 0xffu] : 0u;
-        if (i >= 64) {
-            const int o = i - 64;
-            if (o >= vlo && o < vhi) x ^= tab[(w[o >> 2] >> ((o & 3) * 8)) & 0xffu];
-        }
-        h = ((h << 1) | (h >> 31)) ^ x;
-        const int64_t q = q0 + i;
-        if (i >= 64) {
-            const bool c = i < vhi && q + (int64_t)pre_len >= 63 && (h & mask) >= minimum;
-            hit[(i - 64) >> 5] |= (c ? 1u : 0u) << ((i - 64) & 31);
-        }
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = 4u * (uint32_t)lane + (uint32_t)k;
+        uint32_t t = tab[(wv >> (8 * k)) & 0xffu];
+        t = __builtin_amdgcn_alignbit(t, t, j & 31u);  // rotr(t, j)
+        acc ^= lane < 48 ? t : 0u;
+        u[k] = acc;
     }
+    uint32_t S = acc;  // inclusive prefix XOR over lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(S, d, 64);
+        if (lane >= d) S ^= v;
+    }
+    const uint32_t E = S ^ acc;  // exclusive
+    uint32_t nib = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t P = E ^ u[k];
+        const uint32_t Pm = __shfl(P, lane >= 16 ? lane - 16 : lane, 64);
+        const uint32_t j = 4u * (uint32_t)lane + (uint32_t)k;
+        uint32_t h = P ^ Pm;
+        h = __builtin_amdgcn_alignbit(h, h, (32u - (j & 31u)) & 31u);  // rotl(h, j)
+        nib |= ((h & mask) >= minimum ? 1u : 0u) << k;
+    }
+    const bool tester = lane >= 16 && lane < 48;
+    uint32_t v = tester ? nib << (4 * ((lane - 16) & 7)) : 0u;
+    v |= __shfl_xor(v, 1, 64);
+    v |= __shfl_xor(v, 2, 64);
+    v |= __shfl_xor(v, 4, 64);
+    uint4 hit = make_uint4(__shfl(v, 16, 64), __shfl(v, 24, 64), __shfl(v, 32, 64), __shfl(v, 40, 64));
+    const bool fast = B >= 64 && B + kIter <= ilen;
+    if (!fast) {
+        // reportable window indices [cmin, vhi): q >= 0, q + pre_len >= 63, q < len
+        int64_t cm = 64;
+        if (64 - B > cm) cm = 64 - B;
+        if (127 - plen - B > cm) cm = 127 - plen - B;
+        const int64_t hi = ilen - q0;
+        const int cmin = (int)(cm > 192 ? 192 : cm) - 64;  // bit range [cmin, chi)
+        const int chi = (int)(hi < 64 ? 64 : (hi > 192 ? 192 : hi)) - 64;
+        uint32_t hw[4] = {hit.x, hit.y, hit.z, hit.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int lo = cmin - 32 * q, up = chi - 32 * q;  // keep bits [lo, up) of word q
+            const uint32_t keep_lo = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
+            const uint32_t keep_hi = up >= 32 ? 0xFFFFFFFFu : (up <= 0 ? 0u : (0xFFFFFFFFu >> (32 - up)));
+            hw[q] &= keep_lo & keep_hi;
+        }
+        hit = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    }
+    return hit;
 }
 
+// One wave per work item (suspect blocks, the stream's first block with the carry bytes,
+// tail blocks past the last wave tile); 4 waves per workgroup, one atomic per workgroup
+// round for the output (per-candidate atomics on one counter serialise in L2).
 __global__ __launch_bounds__(256) void scan_exact_kernel(
     const uint8_t* __restrict__ data, uint64_t len, const uint8_t* __restrict__ pre,
     uint32_t pre_len, const uint64_t* __restrict__ susp, const uint32_t* __restrict__ nsusp,
@@ -127,20 +161,17 @@ __global__ __launch_bounds__(256) void scan_exact_kernel(
     uint32_t minimum, uint64_t base, uint64_t* __restrict__ cand, uint32_t* __restrict__ ncand,
     uint32_t cand_cap) {
     __shared__ uint32_t tab[256];
+    __shared__ uint32_t wcnt[4], wbase[4];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = kBuzhashTable[i];
     __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t ns0 = nsusp ? *nsusp : 0u;
     const uint64_t ns = ns0 < susp_cap ? ns0 : susp_cap;
     const uint64_t total = ns + (uint64_t)(head ? 1 : 0) + ext_count;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    // one atomic per workgroup and round (a per-candidate atomic on the single counter
-    // serializes in L2: ~14k of them took ~130 us at 64 GiB / 4 MiB)
-    typedef hipcub::BlockScan<uint32_t, 256> Scan;
-    __shared__ typename Scan::TempStorage scan_tmp;
-    __shared__ uint32_t round_base;
-    for (uint64_t w0 = (uint64_t)blockIdx.x * blockDim.x; w0 < total; w0 += stride) {
-        const uint64_t w = w0 + threadIdx.x;
-        uint32_t hit[4] = {0u, 0u, 0u, 0u};
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    for (uint64_t w0 = (uint64_t)blockIdx.x * 4; w0 < total; w0 += stride) {
+        const uint64_t w = w0 + wave;
+        uint4 hit = make_uint4(0u, 0u, 0u, 0u);
         uint64_t B = 0;
         if (w < total) {
             if (w < ns)
@@ -149,30 +180,40 @@ __global__ __launch_bounds__(256) void scan_exact_kernel(
                 B = 0;
             else
                 B = (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
-            exact_block(data, len, pre, pre_len, B, tab, mask, minimum, hit);
+            hit = exact_block_wave(data, len, pre, pre_len, (int64_t)B, tab, mask, minimum, lane);
         }
-        const uint32_t k = __builtin_popcount(hit[0]) + __builtin_popcount(hit[1]) +
-                           __builtin_popcount(hit[2]) + __builtin_popcount(hit[3]);
-        uint32_t off, sum;
-        Scan(scan_tmp).ExclusiveSum(k, off, sum);
-        if (threadIdx.x == 0) round_base = sum ? atomicAdd(ncand, sum) : 0u;
+        const uint32_t c0 = __builtin_popcount(hit.x), c1 = __builtin_popcount(hit.y),
+                       c2 = __builtin_popcount(hit.z), c3 = __builtin_popcount(hit.w);
+        if (lane == 0) wcnt[wave] = c0 + c1 + c2 + c3;
         __syncthreads();
-        uint32_t idx = round_base + off;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t m = hit[q];
+        if (threadIdx.x == 0) {
+            const uint32_t sum = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+            uint32_t b0 = sum ? atomicAdd(ncand, sum) : 0u;
+            for (int q = 0; q < 4; ++q) {
+                wbase[q] = b0;
+                b0 += wcnt[q];
+            }
+        }
+        __syncthreads();
+        if (lane < 4) {  // lane q writes the positions of hit word q
+            const uint32_t words[4] = {hit.x, hit.y, hit.z, hit.w};
+            const uint32_t before[4] = {0u, c0, c0 + c1, c0 + c1 + c2};
+            uint32_t m = words[lane];
+            uint32_t idx = wbase[wave] + before[lane];
             while (m) {
                 const int bit = __builtin_ctz(m);
                 m &= m - 1;
-                if (idx < cand_cap) cand[idx] = base + B + (uint64_t)(q * 32 + bit);
+                if (idx < cand_cap) cand[idx] = base + B + (uint64_t)(lane * 32 + bit);
                 ++idx;
             }
         }
-        __syncthreads();  // round_base / scan_tmp reuse
+        __syncthreads();  // wcnt / wbase reuse
     }
 }
 
-// Every 128-byte block of a small input (the fused host path): hit mask per block.
+// Every 128-byte block of a small input (the fused host path): hit mask per block, one
+// wave per block.  The block grid sits on 16-byte-aligned addresses: block b starts at
+// 128*b - misalign relative to `data` (misalign = data & 15).
 __global__ __launch_bounds__(256) void scan_blocks_kernel(const uint8_t* __restrict__ data,
                                                           uint64_t len,
                                                           const uint8_t* __restrict__ pre,
@@ -182,11 +223,13 @@ __global__ __launch_bounds__(256) void scan_blocks_kernel(const uint8_t* __restr
     __shared__ uint32_t tab[256];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = kBuzhashTable[i];
     __syncthreads();
-    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t b = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= nblk) return;
-    uint32_t hit[4] = {0u, 0u, 0u, 0u};
-    exact_block(data, len, pre, pre_len, b * kIter, tab, mask, minimum, hit);
-    hits[b] = make_uint4(hit[0], hit[1], hit[2], hit[3]);
+    const int lane = threadIdx.x & 63;
+    const int64_t misalign = (int64_t)((uintptr_t)data & 15);
+    const uint4 hit = exact_block_wave(data, len, pre, pre_len, (int64_t)(b * kIter) - misalign, tab,
+                                       mask, minimum, lane);
+    if (lane == 0) hits[b] = hit;
 }
 
 // ---------------------------------------------------------------------------------
@@ -799,9 +842,9 @@ hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* p
                              uint32_t* ncand, uint32_t cand_cap, uint64_t max_items,
                              hipStream_t stream) {
     (void)hipGetLastError();
-    uint64_t blocks = (max_items + 255) / 256;
+    uint64_t blocks = (max_items + 3) / 4;  // 4 waves per workgroup, one item per wave
     if (blocks < 1) blocks = 1;
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(scan_exact_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, data, len,
                        pre, pre_len, susp, nsusp, susp_cap, ext_first, ext_count, head, mask,
                        minimum, base, cand, ncand, cand_cap);
@@ -871,7 +914,7 @@ hipError_t launch_scan_resolve_small(const FusedScanArgs& fa, int resolve, uint6
         return hipErrorInvalidValue;
     (void)hipGetLastError();
     if (fa.nblk)
-        hipLaunchKernelGGL(scan_blocks_kernel, dim3((unsigned)((fa.nblk + 255) / 256)), dim3(256), 0,
+        hipLaunchKernelGGL(scan_blocks_kernel, dim3((unsigned)((fa.nblk + 3) / 4)), dim3(256), 0,
                            stream, fa.data, fa.len, fa.pre, fa.pre_len, fa.mask, fa.minimum,
                            const_cast<uint4*>(fa.hits), fa.nblk);
     if (resolve)
