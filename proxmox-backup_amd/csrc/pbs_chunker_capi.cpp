@@ -81,7 +81,16 @@ int make_params(uint64_t avg, Params* p) {
     p->hash_cuts = p->minimum <= p->mask;
     const int n = __builtin_popcount(p->mask);  // mask = 2^n - 1
     p->rot = (uint32_t)(32 - n) & 31u;
-    p->thr = p->hash_cuts ? (p->minimum << p->rot) : 0xFFFFFFFFu;
+    // scan_main_kernel's parity frame: odd bytes hold rotl(h, rot), even
+    // bytes rotl(h, rot + 1).  A candidate has bits 2..n-1 of h set and bits 1..0 != 0,
+    // so in both frames the top n-1 bits read >= 2^(n-1) - 3: one screening threshold
+    // (twice the exact candidate rate; scan_exact_kernel applies the exact test).
+    if (!p->hash_cuts)
+        p->thr = 0xFFFFFFFFu;
+    else if (n < 3)
+        p->thr = 0;  // every block is a suspect
+    else
+        p->thr = ((1u << (n - 1)) - 3u) << ((33u - (uint32_t)n) & 31u);
     return PBS_OK;
 }
 
@@ -166,7 +175,7 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
     const uint64_t blocks = (len + kBlockBytes - 1) / kBlockBytes;
     const uint64_t expected = len / p.avg * 3 / 2 + 1;
     const uint32_t want_s =
-        (uint32_t)std::min<uint64_t>(std::min<uint64_t>(blocks + 2, expected * 2 + 4096), 0xFFFFFFF0u);
+        (uint32_t)std::min<uint64_t>(std::min<uint64_t>(blocks + 2, expected * 4 + 4096), 0xFFFFFFF0u);
     const uint32_t want_c =
         (uint32_t)std::min<uint64_t>(std::min<uint64_t>(len + 1, expected * 2 + 8192), 0xFFFFFFF0u);
     c->susp_cap = std::max(c->susp_cap, want_s);
@@ -671,10 +680,13 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     c->stream = c->own_stream;
     for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&c->h_small, kSmallBytes, hipHostMallocMapped) == hipSuccess;
-    ok = ok && c->d_table.ensure(256 * 4) == hipSuccess;
+    ok = ok && c->d_table.ensure(512 * 4) == hipSuccess;
     if (ok) {
-        uint32_t t[256];
-        for (int i = 0; i < 256; ++i) t[i] = rotl32(kBuzhashTable[i], prm.rot);
+        uint32_t t[512];  // [T0 | T1] of the parity frame: even bytes rot + 1, odd bytes rot
+        for (int i = 0; i < 256; ++i) {
+            t[i] = rotl32(kBuzhashTable[i], prm.rot + 1);
+            t[256 + i] = rotl32(kBuzhashTable[i], prm.rot);
+        }
         ok = hipMemcpy(c->d_table.p, t, sizeof(t), hipMemcpyHostToDevice) == hipSuccess;
     }
     if (!ok) {

@@ -48,7 +48,11 @@ __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
 // loads-only rate, but random and VM-image data get 2-3% SLOWER -- lanes 32 KiB apart
 // are almost never all in zero pages at once, and masked lanes save little -- so the
 // product runs ZS = 0.
-template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int ZS = 0>
+// FR (hash frame): 1 = h' = rotl(h, 32-n) for every byte, table T' = rotl(T, 32-n)
+// replicated 64x (3.5 VALU/byte); 2 = parity frame of roll128_asm_f2 (3 VALU/byte), table
+// = [T0 | T1] (512 words) interleaved 32x per 256-byte row, thr = the screening threshold
+// of DESIGN.md "parity frame" (a necessary condition; scan_exact re-tests exactly).
+template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int ZS = 0, int FR = 2>
 __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
     uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {
@@ -60,13 +64,19 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int i = tid; i < kTableDwords; i += NW * 64) s_lds[i] = table_rot[i >> 6];
+    if constexpr (FR == 2) {
+        for (int i = tid; i < kTableDwords; i += NW * 64)
+            s_lds[i] = table_rot[((i >> 5) & 1) * 256 + (i >> 6)];
+    } else {
+        for (int i = tid; i < kTableDwords; i += NW * 64) s_lds[i] = table_rot[i >> 6];
+    }
     __syncthreads();
 
     uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
     uint8_t* touch_area = (uint8_t*)(s_lds + kTableDwords + NW * kStagePerWave / 4) + wave * 256;
     const uint32_t voff_touch = (uint32_t)lane * (uint32_t)SEG + 64u;
     const uint32_t lanebase = (uint32_t)lane * 4u;
+    const uint32_t lb0 = ((uint32_t)lane & 31u) * 4u, lb1 = lb0 + 128u;
     uint32_t voff[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -161,7 +171,13 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
                 for (int k = 0; k < 32; ++k) acc ^= d[k];
                 acc = (acc == 0x9E3779B9u && lane == 65) ? 0xFFFFFFFFu : 0u;
             } else if (!(canon && zero)) {
-                if constexpr (G == 4)
+                if constexpr (FR == 2 && G == 2)
+                    acc = roll128_asm_f2_g2p12(d, ring, h, lb0, lb1);
+                else if constexpr (FR == 2 && G == 3)
+                    acc = roll128_asm_f2_g2p10(d, ring, h, lb0, lb1);
+                else if constexpr (FR == 2)
+                    acc = roll128_asm_f2(d, ring, h, lb0, lb1);
+                else if constexpr (G == 4)
                     acc = roll128_asm_g4(d, ring, h, lanebase);
                 else
                     acc = roll128_asm(d, ring, h, lanebase);
@@ -187,6 +203,5 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
         if (tile >= ntiles) break;
     }
 }
-
 
 }  // namespace pbs

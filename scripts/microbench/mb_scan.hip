@@ -72,7 +72,8 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(fill_kind, dim3(8192), dim3(256), 0, 0, (uint64_t*)d, n / 8, kind);
     printf("data kind %d (%s)\n", kind, kind == 0 ? "random" : kind == 1 ? "vmimage" : "zeros");
     uint32_t *tab, *cnt; uint64_t* susp;
-    CK(hipMalloc(&tab, 1024)); CK(hipMalloc(&cnt, 16)); CK(hipMalloc(&susp, 1 << 24));
+    uint32_t* tab2;
+    CK(hipMalloc(&tab, 1024)); CK(hipMalloc(&tab2, 2048)); CK(hipMalloc(&cnt, 16)); CK(hipMalloc(&susp, 1 << 24));
     const uint64_t avg = 4ull << 20;
     const uint32_t mask = (uint32_t)(avg * 2 - 1), minimum = mask - 2;
     const int nb = __builtin_popcount(mask), rot = (32 - nb) & 31;
@@ -80,6 +81,10 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 256; ++i) t[i] = rotl(pbs::kBuzhashTable[i], rot);
     CK(hipMemcpy(tab, t.data(), 1024, hipMemcpyHostToDevice));
     const uint32_t thr = minimum << rot;
+    std::vector<uint32_t> t2(512);  // parity frame (FR 2): [rotl(T, rot+1) | rotl(T, rot)]
+    for (int i = 0; i < 256; ++i) { t2[i] = rotl(pbs::kBuzhashTable[i], (rot + 1) & 31); t2[256 + i] = t[i]; }
+    CK(hipMemcpy(tab2, t2.data(), 2048, hipMemcpyHostToDevice));
+    const uint32_t thr2 = ((1u << (nb - 1)) - 3u) << ((33 - nb) & 31);
     hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
     int cu = prop.multiProcessorCount;
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -134,21 +139,39 @@ int main(int argc, char** argv) {
         report(nm, best);                                                                   \
     }
 #define RUN3(SEG, MODE, AUX, G, PF) RUN3Z(SEG, MODE, AUX, G, PF, 1)
-#define RUN3Z(SEG, MODE, AUX, G, PF, ZS)                                                        \
+#define RUN3Z(SEG, MODE, AUX, G, PF, ZS) RUN3F(SEG, MODE, AUX, G, PF, ZS, 1)
+#define RUN3F(SEG, MODE, AUX, G, PF, ZS, FR)                                                    \
     if (only < 0 || only == vid++) {                                                        \
         float best = 1e30f; uint32_t h_cnt = 0;                                             \
         const uint64_t tiles = n / (64ull * SEG);                                           \
         for (int r = 0; r < reps; ++r) {                                                    \
             CK(hipMemset(cnt, 0, 16));                                                      \
             CK(hipEventRecord(e0));                                                         \
-            hipLaunchKernelGGL((pbs::scan_main_kernel<SEG, MODE, AUX, G, PF, ZS>), dim3(cu), dim3(8 * 64), 0, 0, \
-                               d, tiles, tab, thr, susp, cnt, 1u << 21);                    \
+            hipLaunchKernelGGL((pbs::scan_main_kernel<SEG, MODE, AUX, G, PF, ZS, FR>), dim3(cu), dim3(8 * 64), 0, 0, \
+                               d, tiles, FR == 2 ? tab2 : tab, FR == 2 ? thr2 : thr, susp, cnt, 1u << 21); \
             CK(hipGetLastError());                                                          \
             CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));                            \
             float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = ms < best ? ms : best;   \
             CK(hipMemcpy(&h_cnt, cnt, 4, hipMemcpyDeviceToHost));                           \
         }                                                                                   \
-        char nm[96]; snprintf(nm, sizeof nm, "v3 SEG=%d mode=%d G=%d PF=%d ZS=%d susp=%u", SEG, MODE, G, PF, ZS, h_cnt); \
+        char nm[96]; snprintf(nm, sizeof nm, "v3 SEG=%d mode=%d G=%d ZS=%d FR=%d susp=%u", SEG, MODE, G, ZS, FR, h_cnt); \
+        report(nm, best);                                                                   \
+    }
+#define RUNR96(SEG, MODE)                                                                   \
+    if (only < 0 || only == vid++) {                                                        \
+        float best = 1e30f; uint32_t h_cnt = 0;                                             \
+        const uint64_t tiles = n / (64ull * SEG);                                           \
+        for (int r = 0; r < reps; ++r) {                                                    \
+            CK(hipMemset(cnt, 0, 16));                                                      \
+            CK(hipEventRecord(e0));                                                         \
+            hipLaunchKernelGGL((pbs::scan_main_r96<SEG, MODE>), dim3(cu), dim3(pbs::kR96Waves * 64), 0, 0, \
+                               d, tiles, tab2, thr2, susp, cnt, 1u << 21);                  \
+            CK(hipGetLastError());                                                          \
+            CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));                            \
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = ms < best ? ms : best;   \
+            CK(hipMemcpy(&h_cnt, cnt, 4, hipMemcpyDeviceToHost));                           \
+        }                                                                                   \
+        char nm[96]; snprintf(nm, sizeof nm, "r96 SEG=%d mode=%d susp=%u", SEG, MODE, h_cnt); \
         report(nm, best);                                                                   \
     }
 #define RUN4(SEG, MODE, AUX, G)                                                             \
@@ -202,9 +225,14 @@ int main(int argc, char** argv) {
         char nm[96]; snprintf(nm, sizeof nm, "v6 SEG=%d mode=%d aux=%d G=%d susp=%u", SEG, MODE, AUX, G, h_cnt); \
         report(nm, best);                                                                   \
     }
-    RUN3Z(32768, 0, 2, 4, 0, 1)
-    RUN3Z(32768, 0, 2, 4, 0, 0)
-    RUN3Z(32768, 1, 2, 4, 0, 1)
-    RUN3Z(32768, 2, 2, 4, 0, 0)
+    RUN3F(32768, 0, 2, 4, 0, 0, 1)
+    RUN3F(32768, 0, 2, 4, 0, 0, 2)
+    RUNR96(32768, 0)
+    RUNR96(32768, 2)
+    RUNR96(32768, 1)
+    RUN3F(32768, 2, 2, 4, 0, 0, 2)
+    RUN3F(32768, 0, 2, 4, 0, 0, 1)
+    RUN3F(32768, 0, 2, 4, 0, 0, 2)
+    RUNR96(32768, 0)
     return 0;
 }

@@ -660,4 +660,132 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_v5(
     }
 }
 
+// ---------------------------------------------------------------------------------
+// R96 (measured slower, profiles/r01/fr2/mb_r96_*.log): 12 waves per CU (3 per SIMD), parity frame, 96-register ring.  The ring only
+// has to hold the 64 leave values plus the reads in flight, so 96 slots suffice; the
+// slot pattern then repeats every three 128-byte iterations (roll128_r96_p0..2).  That
+// frees the VGPRs for a third wave per SIMD (<= 168), and the LDS holds the 64 KiB
+// parity-frame table + 12 x 8 KiB stages = 160 KiB.  DMA offsets use one VGPR per
+// swizzle parity + SGPR soffsets (8j*SEG per instruction).
+constexpr int kR96Waves = 12;
+template <int SEG, int MODE = kModeFull, int AUX = 2>
+__global__ __launch_bounds__(kR96Waves * 64) void scan_main_r96(
+    const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
+    uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {
+    static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
+    constexpr int NW = kR96Waves;
+    __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < kTableDwords; i += NW * 64)
+        s_lds[i] = table_rot[((i >> 5) & 1) * 256 + (i >> 6)];
+    __syncthreads();
+
+    uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
+    const uint32_t lb0 = ((uint32_t)lane & 31u) * 4u, lb1 = lb0 + 128u;
+    // DMA j (0..7) covers segments 8j .. 8j+7: lane L reads segment 8j + (L>>3), chunk
+    // k = (L&7) ^ ((segment>>1)&7); (segment>>1)&7 = (4j + (L>>4)) & 7 depends on j's parity.
+    const uint32_t lsub = (uint32_t)lane >> 3;
+    const uint32_t voff_e = lsub * (uint32_t)SEG + ((((uint32_t)lane & 7u) ^ (((uint32_t)lane >> 4) & 7u)) << 4);
+    const uint32_t voff_o = lsub * (uint32_t)SEG + ((((uint32_t)lane & 7u) ^ ((4u + ((uint32_t)lane >> 4)) & 7u)) << 4);
+    const uint32_t rd_base = (uint32_t)lane * 128u;
+    const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
+
+    constexpr int NIT = SEG / kIter + 1;  // iteration 0 is the warm-up block [-128, 0)
+    const uint64_t nw = (uint64_t)gridDim.x * NW;
+    uint64_t tile = (uint64_t)blockIdx.x * NW + wave;
+    if (tile >= ntiles) return;
+
+    auto issue = [&](uint64_t t, int it) {
+        const uint8_t* tb = data + t * (64ull * SEG);
+        const bool first = (t == 0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(first ? tb : tb - kIter), 0, (int)(64u * SEG + kIter), 0x00020000);
+        const bool warm0 = first && it == 0;
+        const uint32_t soff = warm0 ? 0u : (uint32_t)it * kIter - (first ? (uint32_t)kIter : 0u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t vo = (j & 1) ? voff_o : voff_e;
+            uint32_t so = soff + (uint32_t)j * 8u * (uint32_t)SEG;
+            if (warm0) {  // tile 0's warm-up: the 128 bytes before each segment (segment 0: none)
+                if (j == 0) vo = vo >= (uint32_t)kIter ? vo - kIter : 0u;
+                else so -= kIter;
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, vo, so, 0, AUX);
+        }
+    };
+
+    uint32_t ring[96];
+#pragma unroll
+    for (int r = 0; r < 96; ++r) ring[r] = 0;
+    uint32_t h = 0;
+    int it = 0;
+    issue(tile, 0);
+    // One step = one 128-byte iteration in ring phase PH; the three phases are emitted as
+    // straight-line code so every ring slot keeps one register.
+    auto step = [&](auto PHC) -> bool {
+        constexpr int PH = decltype(PHC)::value;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t d[32];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint4 v = *(const uint4*)(stage + rd_base + (((uint32_t)k ^ rsw) << 4));
+            d[4 * k] = v.x;
+            d[4 * k + 1] = v.y;
+            d[4 * k + 2] = v.z;
+            d[4 * k + 3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint64_t nt = tile;
+        int nit = it + 1;
+        if (nit == NIT) {
+            nt = tile + nw;
+            nit = 0;
+        }
+        if (MODE != kModeComputeOnly && nt < ntiles) issue(nt, nit);
+        if (it == 0) {  // warm-up block: no leave values for its first 64 bytes
+            h = 0;
+#pragma unroll
+            for (int i = 0; i < 64; ++i) ring[(128 * PH + i + 32) % 96] = 0;
+        }
+        uint32_t acc = 0;
+        if constexpr (MODE == kModeLoadOnly) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) acc ^= d[k];
+            acc = (acc == 0x9E3779B9u && lane == 65) ? 0xFFFFFFFFu : 0u;
+        } else if constexpr (PH == 0) {
+            acc = roll128_r96_p0(d, ring, h, lb0, lb1);
+        } else if constexpr (PH == 1) {
+            acc = roll128_r96_p1(d, ring, h, lb0, lb1);
+        } else {
+            acc = roll128_r96_p2(d, ring, h, lb0, lb1);
+        }
+        if (it == 0) {
+            if (tile == 0 && lane == 0) {  // stream segment 0: no bytes before it
+                h = 0;
+#pragma unroll
+                for (int i = 0; i < 64; ++i) ring[(128 * (PH + 1) + i + 32) % 96] = 0;
+            }
+        } else if (acc >= thr) {
+            const uint64_t pos =
+                (tile * 64ull + (uint64_t)lane) * (uint64_t)SEG + (uint64_t)(it - 1) * kIter;
+            if (pos != 0) {
+                const uint32_t idx = atomicAdd(nsusp, 1u);
+                if (idx < cap) susp[idx] = pos;
+            }
+        }
+        tile = nt;
+        it = nit;
+        return tile < ntiles;
+    };
+    for (;;) {
+        if (!step(std::integral_constant<int, 0>{})) break;
+        if (!step(std::integral_constant<int, 1>{})) break;
+        if (!step(std::integral_constant<int, 2>{})) break;
+    }
+}
+
 }  // namespace pbs
