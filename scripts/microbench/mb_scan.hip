@@ -234,5 +234,6 @@ int main(int argc, char** argv) {
     RUN3F(32768, 0, 2, 4, 0, 0, 1)
     RUN3F(32768, 0, 2, 4, 0, 0, 2)
     RUNR96(32768, 0)
+    RUN3F(32768, 1, 2, 4, 0, 0, 2)
     return 0;
 }
