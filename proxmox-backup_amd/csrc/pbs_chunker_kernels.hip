@@ -152,63 +152,68 @@ __device__ __forceinline__ uint4 exact_block_wave(const uint8_t* __restrict__ da
 }
 
 // One wave per work item (suspect blocks, the stream's first block with the carry bytes,
-// tail blocks past the last wave tile); 4 waves per workgroup, one atomic per workgroup
-// round for the output (per-candidate atomics on one counter serialise in L2).
-__global__ __launch_bounds__(256) void scan_exact_kernel(
+// tail blocks past the last wave tile); 16 waves per workgroup, grid-stride over the
+// items.  Hits go to a per-workgroup LDS list (LDS atomics) that is flushed with ONE
+// global atomic per workgroup at the end: per-candidate (or per-round) atomics on the
+// single output counter serialise in L2 (~10 ns each; 4096 of them cost 40 us).
+constexpr int kExactWaves = 16;
+constexpr uint32_t kExactLds = 2048;  // candidates buffered per workgroup
+__global__ __launch_bounds__(kExactWaves * 64) void scan_exact_kernel(
     const uint8_t* __restrict__ data, uint64_t len, const uint8_t* __restrict__ pre,
     uint32_t pre_len, const uint64_t* __restrict__ susp, const uint32_t* __restrict__ nsusp,
     uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head, uint32_t mask,
     uint32_t minimum, uint64_t base, uint64_t* __restrict__ cand, uint32_t* __restrict__ ncand,
     uint32_t cand_cap) {
     __shared__ uint32_t tab[256];
-    __shared__ uint32_t wcnt[4], wbase[4];
+    __shared__ uint64_t lbuf[kExactLds];
+    __shared__ uint32_t lcnt, gbase;
     for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = kBuzhashTable[i];
+    if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t ns0 = nsusp ? *nsusp : 0u;
     const uint64_t ns = ns0 < susp_cap ? ns0 : susp_cap;
     const uint64_t total = ns + (uint64_t)(head ? 1 : 0) + ext_count;
-    const uint64_t stride = (uint64_t)gridDim.x * 4;
-    for (uint64_t w0 = (uint64_t)blockIdx.x * 4; w0 < total; w0 += stride) {
-        const uint64_t w = w0 + wave;
-        uint4 hit = make_uint4(0u, 0u, 0u, 0u);
-        uint64_t B = 0;
-        if (w < total) {
-            if (w < ns)
-                B = susp[w];
-            else if (head && w == ns)
-                B = 0;
-            else
-                B = (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
-            hit = exact_block_wave(data, len, pre, pre_len, (int64_t)B, tab, mask, minimum, lane);
-        }
-        const uint32_t c0 = __builtin_popcount(hit.x), c1 = __builtin_popcount(hit.y),
-                       c2 = __builtin_popcount(hit.z), c3 = __builtin_popcount(hit.w);
-        if (lane == 0) wcnt[wave] = c0 + c1 + c2 + c3;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t sum = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-            uint32_t b0 = sum ? atomicAdd(ncand, sum) : 0u;
-            for (int q = 0; q < 4; ++q) {
-                wbase[q] = b0;
-                b0 += wcnt[q];
-            }
-        }
-        __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * kExactWaves;
+    for (uint64_t w = (uint64_t)blockIdx.x * kExactWaves + wave; w < total; w += stride) {
+        uint64_t B;
+        if (w < ns)
+            B = susp[w];
+        else if (head && w == ns)
+            B = 0;
+        else
+            B = (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
+        const uint4 hit = exact_block_wave(data, len, pre, pre_len, (int64_t)B, tab, mask, minimum, lane);
         if (lane < 4) {  // lane q writes the positions of hit word q
             const uint32_t words[4] = {hit.x, hit.y, hit.z, hit.w};
-            const uint32_t before[4] = {0u, c0, c0 + c1, c0 + c1 + c2};
             uint32_t m = words[lane];
-            uint32_t idx = wbase[wave] + before[lane];
-            while (m) {
-                const int bit = __builtin_ctz(m);
-                m &= m - 1;
-                if (idx < cand_cap) cand[idx] = base + B + (uint64_t)(lane * 32 + bit);
-                ++idx;
+            const uint32_t c = __builtin_popcount(m);
+            if (c) {
+                // slots [idx, kExactLds) of the LDS list are all filled; what does not fit
+                // goes straight to the output with its own atomic
+                const uint32_t idx = atomicAdd(&lcnt, c);
+                const uint32_t inl = idx >= kExactLds ? 0u : (c < kExactLds - idx ? c : kExactLds - idx);
+                const uint32_t gidx = c > inl ? atomicAdd(ncand, c - inl) : 0u;
+                uint32_t k = 0;
+                while (m) {
+                    const int bit = __builtin_ctz(m);
+                    m &= m - 1;
+                    const uint64_t v = base + B + (uint64_t)(lane * 32 + bit);
+                    if (k < inl)
+                        lbuf[idx + k] = v;
+                    else if (gidx + (k - inl) < cand_cap)
+                        cand[gidx + (k - inl)] = v;
+                    ++k;
+                }
             }
         }
-        __syncthreads();  // wcnt / wbase reuse
     }
+    __syncthreads();
+    const uint32_t nl = lcnt < kExactLds ? lcnt : kExactLds;
+    if (threadIdx.x == 0) gbase = nl ? atomicAdd(ncand, nl) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
+        if (gbase + i < cand_cap) cand[gbase + i] = lbuf[i];
 }
 
 // Every 128-byte block of a small input (the fused host path): hit mask per block, one
@@ -842,10 +847,11 @@ hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* p
                              uint32_t* ncand, uint32_t cand_cap, uint64_t max_items,
                              hipStream_t stream) {
     (void)hipGetLastError();
-    uint64_t blocks = (max_items + 3) / 4;  // 4 waves per workgroup, one item per wave
+    // one item per wave; at most 2 workgroups per CU (one flush atomic each)
+    uint64_t blocks = (max_items + kExactWaves - 1) / kExactWaves;
     if (blocks < 1) blocks = 1;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(scan_exact_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, data, len,
+    if (blocks > 512) blocks = 512;
+    hipLaunchKernelGGL(scan_exact_kernel, dim3((unsigned)blocks), dim3(kExactWaves * 64), 0, stream, data, len,
                        pre, pre_len, susp, nsusp, susp_cap, ext_first, ext_count, head, mask,
                        minimum, base, cand, ncand, cand_cap);
     return hipGetLastError();

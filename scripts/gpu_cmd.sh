@@ -1,11 +1,6 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-# 101 stream_read nt, 100 stream_read, 9 v3 loads-only (8 waves), 1 FR2 full
-for v in 101 100 9 1; do
-  timeout -k 10 60 scripts/microbench/mb_scan 32 600 $v 1 > gpurun_out/pw_v$v.log 2>&1 &
-  pid=$!
-  sleep 1.0
-  for k in 1 2 3 4 5 6; do amd-smi metric -p -c -g 0 >> gpurun_out/pw_v$v.log 2>&1; sleep 0.2; done
-  wait $pid || exit 1
-done
-echo ok
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 > gpurun_out/pytest_gpu.log 2>&1 && \
+PBS_DEBUG_PHASES=1 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-inclusive-gib 0 > gpurun_out/bench_dbg.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $(pwd)/gpurun_out/prof2 -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-inclusive-gib 0 > gpurun_out/prof2.log 2>&1
+echo rc=$?
