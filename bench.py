@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=512)
     ap.add_argument("--host-inclusive-gib", type=float, default=4.0,
                     help="also time the host-buffer path (H2D + kernels + D2H) on this many GiB; 0 = skip")
+    ap.add_argument("--digest", type=int, default=0,
+                    help="also time the per-chunk SHA-256 stage (SURVEY 8(f)) over the stream's "
+                         "chunks (GPU), with hashlib on the host cores beside it")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per scan launch (written by profiles/collect_traffic.py)")
     return ap.parse_args()
@@ -105,6 +108,63 @@ def cpu_baseline(args, workload, seed, avg):
             "sample": f"{threads} x {args.cpu_sample_mib} MiB slices of the same {workload} stream, "
                       f"whole-buffer scan loop (oracle/chunker_oracle.c, gcc -O2); "
                       f"1 thread: {single:.3f} GiB/s; host CPU: {cpu}"}
+
+
+def digest_stage(args, buf, cuts, stream, reps: int = 3):
+    """Per-chunk SHA-256 of the whole device-resident stream (one lane per chunk, longest
+    chunks first), timed with HIP events on the launch stream; hashlib (OpenSSL) on the
+    host cores over a bounded sample of the same chunks as the CPU reference point."""
+    import hashlib
+
+    import numpy as np
+    import torch
+
+    import pbschunk
+
+    size = buf.numel()
+    bounds = np.concatenate([[0], cuts]).astype(np.uint64)
+    n = bounds.size - 1
+    lens = np.diff(bounds.astype(np.int64))
+    order = np.argsort(-lens, kind="stable").astype(np.int32)
+    bd = torch.from_numpy(bounds.view(np.int64)).to(buf.device)
+    od = torch.from_numpy(order).to(buf.device)
+    out = torch.empty(n * 32, dtype=torch.uint8, device=buf.device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    pbschunk.digest_chunks_async(buf.data_ptr(), size, bd.data_ptr(), od.data_ptr(), n,
+                                 out.data_ptr(), hip_stream=stream.cuda_stream)  # warm-up
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(reps):
+        ev[0].record(stream)
+        pbschunk.digest_chunks_async(buf.data_ptr(), size, bd.data_ptr(), od.data_ptr(), n,
+                                     out.data_ptr(), hip_stream=stream.cuda_stream)
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        ms.append(ev[0].elapsed_time(ev[1]))
+    t = min(ms) / 1e3
+    # host reference point: hashlib over the first chunks totalling ~1 GiB, 16 threads
+    take = int(np.searchsorted(np.cumsum(lens), 1 << 30)) + 1
+    take = max(1, min(n, take))
+    host = buf[: int(bounds[take])].cpu().numpy()
+    mv = memoryview(host)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    parts = [list(range(k, take, threads)) for k in range(threads)]
+
+    def work(ix):
+        for i in ix:
+            hashlib.sha256(mv[int(bounds[i]):int(bounds[i + 1])]).digest()
+
+    ths = [threading.Thread(target=work, args=(ix,)) for ix in parts]
+    t0 = time.perf_counter()
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    cpu_gib_s = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
+    return {"metric": "GiB/s SHA-256 digested (per chunk, device-resident)",
+            "value": round(size / (1 << 30) / t, 3), "ms": round(t * 1e3, 3), "chunks": n,
+            "max_chunk": int(lens.max()), "bound": "valu (one lane per chunk; serial per chunk)",
+            "cpu_baseline": {"value": round(cpu_gib_s, 3), "unit": "GiB/s", "cores": threads,
+                             "kind": "hashlib (OpenSSL)",
+                             "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"}}
 
 
 def main():
@@ -229,6 +289,8 @@ def main():
     }
     if host_incl is not None:
         out["host_inclusive_gib_s"] = round(host_incl, 3)
+    if args.digest and args.mode == "streams":
+        out["digest"] = digest_stage(args, buf, cuts, stream)
     if args.cpu_baseline and world == 1:
         del buf
         out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)

@@ -1,0 +1,72 @@
+/*
+ * pbs_digest.h -- C ABI of the per-chunk SHA-256 stage and the dynamic index image
+ * (the consumers right after the chunker).
+ *
+ * Reference interfaces replaced:
+ *  - chunk digest: `DataChunkBuilder::digest` / `compute_digest`
+ *    (pbs-datastore/src/data_blob.rs:516-536): `openssl::sha::sha256(data)`, or with a
+ *    crypt config `CryptConfig::compute_digest` (pbs-tools/src/crypt_config.rs:79-84):
+ *    SHA-256(data || id_key).  Called per chunk by the client upload stream
+ *    (pbs-client/src/backup_writer.rs:671-678) and by `DynamicChunkWriter`
+ *    (pbs-datastore/src/dynamic_index.rs:463-466).
+ *  - index: `DynamicIndexWriter::create` / `add_chunk` / `close`
+ *    (pbs-datastore/src/dynamic_index.rs:297-391): a 4096-byte header (magic
+ *    DYNAMIC_SIZED_CHUNK_INDEX_1_0, pbs-datastore/src/file_formats.rs:24, uuid, ctime,
+ *    index_csum) followed by 40-byte entries {end_le: u64, digest: [u8; 32]}
+ *    (dynamic_index.rs:28-68); index_csum = SHA-256(end1_le || digest1 || ...)
+ *    (dynamic_index.rs:373-391, and the client's own csum, backup_writer.rs:683-688).
+ *
+ * Chunk i of a stream is [bounds[i], bounds[i+1]) in absolute stream offsets; with the
+ * chunker's cut list `ends` (pbs_chunker_find_cuts*), bounds = {start, ends...}.
+ */
+#ifndef PBS_DIGEST_H
+#define PBS_DIGEST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBS_DIGEST_MAX_KEY 64 /* id_key is 32 bytes in the reference */
+
+/* SHA-256 of every chunk on the GPU.  `dev_data` (device) holds stream bytes
+ * [base, base + data_len); every chunk must lie inside it.  `bounds` (host, n + 1
+ * ascending absolute offsets), `key` (host, key_len <= PBS_DIGEST_MAX_KEY bytes
+ * appended to every chunk's message; NULL/0 for the plain digest).  Writes 32 * n
+ * digest bytes to host `digests` (chunk order).  Synchronous.  Returns PBS_OK or a
+ * PBS_ERR_* code (pbs_chunker.h). */
+int pbs_digest_chunks_device(const uint8_t *dev_data, size_t data_len, uint64_t base,
+                             const uint64_t *bounds, size_t n, const uint8_t *key,
+                             size_t key_len, uint8_t *digests, void *hip_stream);
+
+/* Device-only, asynchronous form for pipelines and the benchmark: `bounds_dev`
+ * (n + 1 offsets), `order_dev` (NULL or a permutation of 0..n-1: lane k hashes chunk
+ * order_dev[k]; pass the chunks sorted by length, longest first, so that the 64 lanes
+ * of a wave finish together), `digests_dev` (32 * n bytes) are device memory; `key`
+ * is host memory (copied into the launch). */
+int pbs_digest_chunks_async(const uint8_t *dev_data, size_t data_len, uint64_t base,
+                            const uint64_t *bounds_dev, const uint32_t *order_dev, size_t n,
+                            const uint8_t *key, size_t key_len, uint8_t *digests_dev,
+                            void *hip_stream);
+
+/* Host SHA-256 (FIPS 180-4), used for the index checksum (the reference's
+ * openssl::sha::Sha256 over 40-byte entries; a few hundred KiB per index). */
+void pbs_sha256(const uint8_t *data, size_t len, uint8_t out[32]);
+
+/* Size in bytes of a dynamic index image with n entries: 4096 + 40 n. */
+size_t pbs_didx_size(size_t n);
+
+/* Build the .didx image of n chunks (`ends`: chunk end offsets, `digests`: 32 n bytes)
+ * into `out` (cap >= pbs_didx_size(n)): header {magic, uuid[16], ctime (LE i64),
+ * index_csum, zeros}, then the entries.  `csum_out` (may be NULL) receives index_csum,
+ * what `DynamicIndexWriter::close` returns. */
+int pbs_didx_build(const uint64_t *ends, const uint8_t *digests, size_t n, const uint8_t uuid[16],
+                   int64_t ctime, uint8_t *out, size_t cap, uint8_t csum_out[32]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PBS_DIGEST_H */

@@ -135,3 +135,41 @@ def gen_vmimage(length: int, seed: int, offset: int = 0) -> np.ndarray:
 
 def splitmix64(x: int) -> int:
     return int(lib().ora_splitmix64(x & 0xFFFFFFFFFFFFFFFF))
+
+
+# ---- chunk digests and the dynamic index (checker only) ---------------
+# The digest is openssl::sha::sha256 in the reference (data_blob.rs:516-536); hashlib's
+# SHA-256 is the same FIPS 180-4 function.  With a crypt config the message is
+# chunk || id_key (pbs-tools/src/crypt_config.rs:79-84).
+
+def chunk_digests(data: np.ndarray, bounds, key: bytes = b"") -> np.ndarray:
+    import hashlib
+
+    b = [int(x) for x in bounds]
+    mv = memoryview(np.ascontiguousarray(data))
+    out = np.empty((max(0, len(b) - 1), 32), dtype=np.uint8)
+    for i in range(len(b) - 1):
+        h = hashlib.sha256(mv[b[i]:b[i + 1]])
+        if key:
+            h.update(key)
+        out[i] = np.frombuffer(h.digest(), dtype=np.uint8)
+    return out
+
+
+DIDX_MAGIC = bytes([28, 145, 78, 165, 25, 186, 179, 205])  # file_formats.rs:24
+
+
+def didx_image(ends, digests, uuid: bytes = bytes(16), ctime: int = 0):
+    """dynamic_index.rs:28-37 (header: magic, uuid, ctime i64 LE, index_csum, 4032 zero
+    bytes), :61-66 (entries {end_le u64, digest}), :373-391 (index_csum = SHA-256 over
+    the entries as written).  Returns (image, index_csum)."""
+    import hashlib
+    import struct
+
+    entries = b"".join(struct.pack("<Q", int(e)) + (d if isinstance(d, bytes) else
+                                                    bytes(np.asarray(d, dtype=np.uint8)))
+                       for e, d in zip(ends, digests))
+    csum = hashlib.sha256(entries).digest()
+    header = DIDX_MAGIC + bytes(uuid) + struct.pack("<q", int(ctime)) + csum
+    header += bytes(4096 - len(header))
+    return header + entries, csum

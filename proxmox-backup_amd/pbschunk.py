@@ -10,6 +10,11 @@ Mirrors, with the same names, argument meaning and error behaviour:
   * ``DynamicChunkWriter(sink, chunk_size)`` -- ``write(data) -> consumed`` / ``close()``
       pbs-datastore/src/dynamic_index.rs:397-523, with the digest/compress/index step
       replaced by a callback ``sink(chunk_end_offset, chunk_bytes)``.
+  * ``digest_chunks_device(...)`` -- per-chunk SHA-256 on the GPU,
+      ``DataChunkBuilder::digest`` (pbs-datastore/src/data_blob.rs:516-536; with a key,
+      ``CryptConfig::compute_digest``, pbs-tools/src/crypt_config.rs:79-84).
+  * ``DynamicIndexWriter(path)`` -- ``add_chunk(offset, digest)`` / ``close() -> csum``
+      pbs-datastore/src/dynamic_index.rs:297-391 (.didx image built by the C library).
 
 The hash scan always runs on the GPU through the HIP library; there is no CPU path.
 Loading fails loudly (``ChunkerLibraryError``) when the library is missing and handle
@@ -44,6 +49,9 @@ EXPORTED_SYMBOLS = (
     "pbs_chunker_last_error", "pbs_strerror", "pbs_chunker_last_timing",
     "pbs_candidates_host", "pbs_generate_device", "pbs_device_count", "pbs_table_copy",
     "pbs_chunker_candidates_device", "pbs_chunker_resolve_device",
+    # include/pbs_digest.h (chunk digests, dynamic index)
+    "pbs_digest_chunks_device", "pbs_digest_chunks_async", "pbs_sha256", "pbs_didx_size",
+    "pbs_didx_build",
 )
 
 
@@ -109,6 +117,11 @@ def lib():
         "pbs_table_copy": ([p], i),
         "pbs_chunker_candidates_device": ([p, p, sz, p, sz, u64, p, sz, ctypes.POINTER(sz)], i),
         "pbs_chunker_resolve_device": ([p, p, sz, u64, i, p, sz, ctypes.POINTER(sz)], i),
+        "pbs_digest_chunks_device": ([p, sz, u64, p, sz, p, sz, p, p], i),
+        "pbs_digest_chunks_async": ([p, sz, u64, p, p, sz, p, sz, p, p], i),
+        "pbs_sha256": ([p, sz, p], None),
+        "pbs_didx_size": ([sz], sz),
+        "pbs_didx_build": ([p, p, sz, p, ctypes.c_int64, p, sz, p], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -375,3 +388,142 @@ def generate_device(dev_ptr: int, length: int, kind: int, seed: int, offset: int
                                    offset, ctypes.c_void_p(hip_stream))
     if rc != PBS_OK:
         raise ChunkerError(rc, "pbs_generate_device")
+
+
+# ---- chunk digests and the dynamic index (include/pbs_digest.h) --------
+
+DIDX_MAGIC = bytes([28, 145, 78, 165, 25, 186, 179, 205])  # file_formats.rs:24
+DIDX_HEADER = 4096
+DIDX_ENTRY = 40
+
+
+def sha256(data) -> bytes:
+    """Host SHA-256 of the C library (the index checksum's hash)."""
+    a = _as_u8(data)
+    out = (ctypes.c_uint8 * 32)()
+    lib().pbs_sha256(_ptr(a), a.size, out)
+    return bytes(out)
+
+
+def _key_arg(key):
+    if key is None:
+        return None, 0
+    k = bytes(key)
+    if len(k) > 64:
+        raise ValueError("key longer than PBS_DIGEST_MAX_KEY (64)")
+    return ctypes.create_string_buffer(k, len(k) or 1), len(k)
+
+
+def digest_chunks_device(dev_ptr: int, data_len: int, bounds, base: int = 0, key=None,
+                         hip_stream: int = 0) -> np.ndarray:
+    """SHA-256 (on the GPU) of every chunk [bounds[i], bounds[i+1]) of the stream whose
+    bytes [base, base + data_len) are at device address dev_ptr; (n, 32) uint8 digests.
+    ``key``: the crypt config's id_key, appended to every chunk's message."""
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.uint64))
+    n = max(0, b.size - 1)
+    out = np.empty((n, 32), dtype=np.uint8)
+    if n == 0:
+        return out
+    kb, kl = _key_arg(key)
+    rc = lib().pbs_digest_chunks_device(ctypes.c_void_p(dev_ptr), data_len, base, b.ctypes.data, n,
+                                        kb, kl, out.ctypes.data, ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_digest_chunks_device")
+    return out
+
+
+def digest_chunks_async(dev_ptr: int, data_len: int, bounds_dev: int, order_dev: int, n: int,
+                        digests_dev: int, base: int = 0, key=None, hip_stream: int = 0):
+    """Device-only form (all pointers device memory; order_dev may be 0)."""
+    kb, kl = _key_arg(key)
+    rc = lib().pbs_digest_chunks_async(ctypes.c_void_p(dev_ptr), data_len, base,
+                                       ctypes.c_void_p(bounds_dev), ctypes.c_void_p(order_dev or None),
+                                       n, kb, kl, ctypes.c_void_p(digests_dev),
+                                       ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_digest_chunks_async")
+
+
+def didx_build(ends, digests, uuid: bytes = bytes(16), ctime: int = 0):
+    """.didx image (bytes) and index_csum of chunks with END offsets ``ends`` and
+    32-byte ``digests`` (dynamic_index.rs:28-68 header/entries, :373-391 csum)."""
+    e = np.ascontiguousarray(np.asarray(ends, dtype=np.uint64))
+    if isinstance(digests, (list, tuple)):
+        digests = np.frombuffer(b"".join(bytes(x) for x in digests), dtype=np.uint8)
+    d = np.ascontiguousarray(np.asarray(digests, dtype=np.uint8).reshape(-1, 32))
+    if d.shape[0] != e.size:
+        raise ValueError("ends and digests differ in length")
+    if len(uuid) != 16:
+        raise ValueError("uuid must be 16 bytes")
+    n = e.size
+    cap = int(lib().pbs_didx_size(n))
+    out = np.empty(cap, dtype=np.uint8)
+    csum = (ctypes.c_uint8 * 32)()
+    ub = ctypes.create_string_buffer(bytes(uuid), 16)
+    rc = lib().pbs_didx_build(e.ctypes.data if n else None, d.ctypes.data if n else None, n, ub,
+                              int(ctime), out.ctypes.data, cap, csum)
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_didx_build")
+    return out.tobytes(), bytes(csum)
+
+
+class DynamicIndexWriter:
+    """dynamic_index.rs:297-391: ``add_chunk(offset, digest)`` per chunk (offset = the
+    chunk's END offset, as DynamicChunkWriter passes it), ``close()`` writes the .didx
+    file (tmp file + rename) and returns index_csum.  uuid/ctime default to a random
+    uuid and the current time (Uuid::generate / epoch_i64 in the reference)."""
+
+    def __init__(self, path: str, uuid: Optional[bytes] = None, ctime: Optional[int] = None):
+        import time
+
+        self.path = path
+        self.uuid = bytes(uuid) if uuid is not None else os.urandom(16)
+        self.ctime = int(time.time()) if ctime is None else int(ctime)
+        self.ends = []
+        self.digests = []
+        self.closed = False
+
+    def add_chunk(self, offset: int, digest: bytes):
+        if self.closed:
+            raise RuntimeError(f"cannot write to closed dynamic index file {self.path!r}")
+        if len(digest) != 32:
+            raise ValueError("digest must be 32 bytes")
+        self.ends.append(int(offset))
+        self.digests.append(bytes(digest))
+
+    def close(self) -> bytes:
+        if self.closed:
+            raise RuntimeError(f"cannot close already closed archive index file {self.path!r}")
+        self.closed = True
+        image, csum = didx_build(self.ends, self.digests, self.uuid, self.ctime)
+        tmp = os.path.splitext(self.path)[0] + ".tmp_didx"
+        with open(tmp, "wb") as f:
+            f.write(image)
+        os.replace(tmp, self.path)
+        return csum
+
+
+def read_didx(image: bytes):
+    """Parse a .didx image: (uuid, ctime, index_csum, ends (u64), digests (n, 32))."""
+    if len(image) < DIDX_HEADER or image[:8] != DIDX_MAGIC:
+        raise ValueError("not a dynamic index image")
+    body = np.frombuffer(image, dtype=np.uint8, offset=DIDX_HEADER)
+    if body.size % DIDX_ENTRY:
+        raise ValueError("truncated entry")
+    ent = body.reshape(-1, DIDX_ENTRY)
+    ends = ent[:, :8].copy().view("<u8").reshape(-1)
+    ctime = int.from_bytes(image[24:32], "little", signed=True)
+    return image[8:24], ctime, image[32:64], ends, ent[:, 8:].copy()
+
+
+def index_stream_device(chunker: "Chunker", dev_ptr: int, length: int, key=None,
+                        hip_stream: int = 0, uuid: bytes = bytes(16), ctime: int = 0):
+    """The client's per-stream path on a device-resident stream: chunk boundaries
+    (GPU chunker), chunk digests (GPU SHA-256), then the .didx image and index_csum
+    (host).  Returns (ends, digests, csum, didx_bytes)."""
+    start = chunker.stream_offset
+    ends = chunker.find_cuts_device(dev_ptr, length, is_final=True)
+    bounds = np.concatenate([np.array([start], dtype=np.uint64), ends.astype(np.uint64)])
+    dig = digest_chunks_device(dev_ptr, length, bounds, base=start, key=key, hip_stream=hip_stream)
+    image, csum = didx_build(ends, dig, uuid, ctime)
+    return ends, dig, csum, image

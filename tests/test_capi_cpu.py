@@ -1,5 +1,5 @@
 """CPU-only checks of the C-ABI library (no compute calls): it loads, exports every
-symbol include/pbs_chunker.h declares, carries the right table, and fails loudly
+symbol include/*.h declares, carries the right table, and fails loudly
 without a device.  Plus the Python host mirror's caller logic (ChunkStream,
 DynamicChunkWriter) driven by the oracle chunker as a stand-in."""
 import hashlib
@@ -11,12 +11,13 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "pbs_chunker.h")
+HEADERS = sorted(os.path.join(ROOT, "include", h) for h in os.listdir(os.path.join(ROOT, "include"))
+                 if h.endswith(".h"))
 KiB, MiB = 1024, 1024 * 1024
 
 
 def declared_functions():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(pbs_[a-z0-9_]+)\s*\(", src)))
 

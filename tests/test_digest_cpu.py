@@ -1,0 +1,71 @@
+"""CPU checks of the 8(f) host pieces: the library's host SHA-256 (index checksum)
+against FIPS 180-4 known answers and hashlib, and the .didx image against the oracle's
+restatement of dynamic_index.rs (header layout, entries, index_csum)."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+# FIPS 180-4 / NIST CAVS known answers
+KAT = [
+    (b"", "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"),
+    (b"abc", "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"),
+    (b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq",
+     "248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"),
+    (b"a" * 1000000, "cdc76e5c9914fb9281a1c7e284d73e67f1809a48a497200e046d39ccc7112cd0"),
+]
+
+
+@pytest.mark.parametrize("msg,hexd", KAT, ids=["empty", "abc", "448bit", "million_a"])
+def test_host_sha256_known_answers(pbschunk, msg, hexd):
+    assert pbschunk.sha256(msg).hex() == hexd
+    assert hashlib.sha256(msg).hexdigest() == hexd  # the oracle's hash agrees too
+
+
+def test_host_sha256_lengths(pbschunk):
+    rng = np.random.default_rng(7)
+    for n in list(range(0, 200)) + [4095, 4096, 4097, 65536 + 13]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert pbschunk.sha256(d) == hashlib.sha256(d).digest(), n
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 1000])
+def test_didx_image_matches_oracle(pbschunk, oracle, n):
+    rng = np.random.default_rng(n)
+    ends = np.cumsum(rng.integers(65, 1 << 24, n)).astype(np.uint64)
+    dig = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    uuid = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    img, csum = pbschunk.didx_build(ends, dig, uuid, 1700000000 + n)
+    ref_img, ref_csum = oracle.didx_image(ends, dig, uuid, 1700000000 + n)
+    assert img == ref_img and csum == ref_csum
+    assert len(img) == 4096 + 40 * n
+    u, ct, c, e, d = pbschunk.read_didx(img)
+    assert u == uuid and ct == 1700000000 + n and c == csum
+    assert np.array_equal(e, ends) and np.array_equal(d, dig)
+
+
+def test_didx_negative_ctime_and_capacity(pbschunk, oracle):
+    img, _ = pbschunk.didx_build([5], [bytes(32)], bytes(16), -1)
+    assert img[24:32] == b"\xff" * 8
+    assert img == oracle.didx_image([5], [bytes(32)], bytes(16), -1)[0]
+
+
+def test_dynamic_index_writer_file(pbschunk, oracle, tmp_path):
+    path = str(tmp_path / "test.didx")
+    w = pbschunk.DynamicIndexWriter(path, uuid=bytes(range(16)), ctime=42)
+    ends, digs = [], []
+    for k in range(1, 6):
+        d = hashlib.sha256(str(k).encode()).digest()
+        w.add_chunk(k * 4096, d)
+        ends.append(k * 4096)
+        digs.append(np.frombuffer(d, np.uint8))
+    csum = w.close()
+    data = open(path, "rb").read()
+    ref, ref_csum = oracle.didx_image(ends, digs, bytes(range(16)), 42)
+    assert data == ref and csum == ref_csum
+    assert not os.path.exists(str(tmp_path / "test.tmp_didx"))
+    with pytest.raises(RuntimeError):
+        w.add_chunk(1, bytes(32))
+    with pytest.raises(RuntimeError):
+        w.close()

@@ -1,0 +1,132 @@
+"""GPU parity of the 8(f) stages: per-chunk SHA-256 on the device (one lane per chunk)
+against the oracle (hashlib, the FIPS 180-4 function the reference calls through
+openssl, data_blob.rs:516-536; keyed form crypt_config.rs:79-84), and the end-to-end
+device path chunk -> digest -> .didx against the oracle chunker + hashlib + the
+oracle's dynamic_index.rs restatement.  Bit-exact.
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+"""
+import numpy as np
+import pytest
+
+import gen_np
+
+pytestmark = pytest.mark.gpu
+KiB, MiB = 1024, 1024 * 1024
+
+
+def _dev(torch, host: np.ndarray, pad_front: int = 0):
+    """Device copy of `host` starting `pad_front` bytes into a fresh allocation (so the
+    stream start can be misaligned); returns (tensor, device pointer of byte 0)."""
+    t = torch.empty(host.size + pad_front, dtype=torch.uint8, device="cuda")
+    if host.size:
+        t[pad_front:] = torch.from_numpy(host).to("cuda")
+    return t, t.data_ptr() + pad_front
+
+
+@pytest.fixture(scope="module")
+def torch_dev(gpu):
+    import torch
+
+    torch.cuda.set_device(0)
+    return torch
+
+
+def test_edge_lengths_and_alignment(gpu, oracle, torch_dev):
+    """Chunk lengths around every padding boundary (55/56/63/64/119/120/...), each
+    start alignment 0..3, the last chunk ending exactly at the buffer end."""
+    lens = [0, 1, 2, 3, 4, 5, 31, 32, 54, 55, 56, 57, 63, 64, 65, 118, 119, 120, 121, 127,
+            128, 129, 191, 192, 193, 1000, 4095, 4096, 4097, 65536 + 7]
+    rng = np.random.default_rng(1)
+    for pad in range(4):
+        order = rng.permutation(len(lens))
+        bounds = np.concatenate([[0], np.cumsum([lens[i] for i in order])]).astype(np.uint64)
+        data = gen_np.gen_random(int(bounds[-1]), 0xD16E57 + pad)
+        t, ptr = _dev(torch_dev, data, pad)
+        got = gpu.digest_chunks_device(ptr, data.size, bounds)
+        ref = oracle.chunk_digests(data, bounds)
+        assert np.array_equal(got, ref), f"pad {pad}"
+        del t
+
+
+@pytest.mark.parametrize("klen", [1, 5, 32, 55, 56, 64])
+def test_keyed_digest(gpu, oracle, torch_dev, klen):
+    """SHA-256(chunk || id_key) (crypt_config.rs:79-84) for key lengths that move the
+    padding across block boundaries."""
+    key = bytes(range(100, 100 + klen))
+    lens = [0, 1, 7, 8, 9, 55, 56, 63, 64, 100, 4096 + 3]
+    bounds = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = gen_np.gen_random(int(bounds[-1]), 77 + klen)
+    t, ptr = _dev(torch_dev, data, 1)
+    got = gpu.digest_chunks_device(ptr, data.size, bounds, key=key)
+    assert np.array_equal(got, oracle.chunk_digests(data, bounds, key))
+
+
+def test_base_offset_and_subrange(gpu, oracle, torch_dev):
+    """Device buffer holding stream bytes [base, base + len): chunks addressed by
+    absolute offsets; only a sub-range of the buffer is chunked."""
+    data = gen_np.gen_random(3 * MiB + 11, 5)
+    base = 10 * MiB + 3
+    t, ptr = _dev(torch_dev, data)
+    rel = np.array([17, 100, 5000, 1 * MiB + 1, 2 * MiB + 999, 3 * MiB + 11], dtype=np.uint64)
+    got = gpu.digest_chunks_device(ptr, data.size, rel + np.uint64(base), base=base)
+    assert np.array_equal(got, oracle.chunk_digests(data, rel))
+    with pytest.raises(gpu.ChunkerError):  # a chunk outside the device range
+        gpu.digest_chunks_device(ptr, data.size, rel + np.uint64(base - 1000), base=base)
+
+
+@pytest.mark.parametrize("kind,avg", [("vmimage", 64 * KiB), ("random", 4 * MiB), ("zeros", 256 * KiB)])
+def test_chunker_to_didx_end_to_end(gpu, oracle, torch_dev, kind, avg):
+    """The client path on a device-resident stream: GPU cut list, GPU digests, .didx
+    image and index_csum -- all equal to the oracle chunker + hashlib + the oracle's
+    restatement of DynamicIndexWriter (incl. the forced 4*avg cuts of zero runs)."""
+    n = 24 * MiB + 333
+    if kind == "vmimage":
+        data = gen_np.gen_vmimage(n, 0x5EED0003, 0)
+    elif kind == "random":
+        data = gen_np.gen_random(n, 0x5EED0002)
+    else:
+        data = np.zeros(n, dtype=np.uint8)
+    t, ptr = _dev(torch_dev, data)
+    uuid = bytes(range(16))
+    with gpu.Chunker(avg) as c:
+        ends, dig, csum, image = gpu.index_stream_device(c, ptr, n, uuid=uuid, ctime=123)
+    ref_ends = oracle.chunk_feed(avg, data)
+    if ref_ends.size == 0 or int(ref_ends[-1]) != n:
+        ref_ends = np.append(ref_ends, np.uint64(n))
+    assert np.array_equal(ends, ref_ends)
+    bounds = np.concatenate([[0], ref_ends]).astype(np.uint64)
+    ref_dig = oracle.chunk_digests(data, bounds)
+    assert np.array_equal(dig, ref_dig)
+    ref_img, ref_csum = oracle.didx_image(ref_ends, ref_dig, uuid, 123)
+    assert csum == ref_csum and image == ref_img
+
+
+def test_large_chunks_sorted_lanes(gpu, oracle, torch_dev):
+    """Max-size (16 MiB) chunks beside tiny ones in one launch (the host orders lanes by
+    length), 64+ chunks so several waves run."""
+    rng = np.random.default_rng(3)
+    lens = [16 * MiB, 16 * MiB - 1, 1, 64, 9 * MiB + 5] + [int(x) for x in rng.integers(1, 300 * KiB, 90)]
+    bounds = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = gen_np.gen_vmimage(int(bounds[-1]), 11, 0)
+    t, ptr = _dev(torch_dev, data, 2)
+    got = gpu.digest_chunks_device(ptr, data.size, bounds)
+    assert np.array_equal(got, oracle.chunk_digests(data, bounds))
+
+
+def test_async_device_form(gpu, oracle, torch_dev):
+    """pbs_digest_chunks_async with device bounds/order/digests (the bench's form)."""
+    torch = torch_dev
+    lens = np.random.default_rng(9).integers(1, 100 * KiB, 40)
+    bounds = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = gen_np.gen_random(int(bounds[-1]), 9)
+    t, ptr = _dev(torch, data, 3)
+    n = bounds.size - 1
+    bd = torch.from_numpy(bounds.view(np.int64)).to("cuda")
+    order = torch.from_numpy(np.argsort(-(np.diff(bounds.astype(np.int64))), kind="stable").astype(np.int32)).to("cuda")
+    out = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    gpu.digest_chunks_async(ptr, data.size, bd.data_ptr(), order.data_ptr(), n, out.data_ptr(), hip_stream=s)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(n, 32)
+    assert np.array_equal(got, oracle.chunk_digests(data, bounds))
