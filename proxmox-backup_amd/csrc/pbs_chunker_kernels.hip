@@ -75,10 +75,11 @@ namespace pbs {
 // window bytes in existence and its P-difference involves only them; the hit words are
 // clipped to reportable positions.  Returns the 4 hit words (bit j = position B + j),
 // uniform across the wave.  `pre` has 64 readable bytes; `len` >= 1.
-__device__ __forceinline__ uint4 exact_block_wave(const uint8_t* __restrict__ data, uint64_t len,
-                                                  const uint8_t* __restrict__ pre,
-                                                  uint32_t pre_len, int64_t B, const uint32_t* tab,
-                                                  uint32_t mask, uint32_t minimum, int lane) {
+// exact_load: lane l's window dword (the memory half, issued ahead by the caller);
+// exact_hits: the hash and test (the compute half).
+__device__ __forceinline__ uint32_t exact_load(const uint8_t* __restrict__ data, uint64_t len,
+                                               const uint8_t* __restrict__ pre, uint32_t pre_len,
+                                               int64_t B, int lane) {
     const int64_t q0 = B - 64;
     const int64_t ilen = (int64_t)len, plen = (int64_t)pre_len;
     uint32_t wv = 0;
@@ -97,6 +98,14 @@ __device__ __forceinline__ uint4 exact_block_wave(const uint8_t* __restrict__ da
             }
         }
     }
+    return wv;
+}
+
+__device__ __forceinline__ uint4 exact_hits(uint32_t wv, uint64_t len, uint32_t pre_len, int64_t B,
+                                            const uint32_t* tab, uint32_t mask, uint32_t minimum,
+                                            int lane) {
+    const int64_t q0 = B - 64;
+    const int64_t ilen = (int64_t)len, plen = (int64_t)pre_len;
     uint32_t u[4], acc = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -151,6 +160,14 @@ __device__ __forceinline__ uint4 exact_block_wave(const uint8_t* __restrict__ da
     return hit;
 }
 
+__device__ __forceinline__ uint4 exact_block_wave(const uint8_t* __restrict__ data, uint64_t len,
+                                                  const uint8_t* __restrict__ pre,
+                                                  uint32_t pre_len, int64_t B, const uint32_t* tab,
+                                                  uint32_t mask, uint32_t minimum, int lane) {
+    const uint32_t wv = exact_load(data, len, pre, pre_len, B, lane);
+    return exact_hits(wv, len, pre_len, B, tab, mask, minimum, lane);
+}
+
 // One wave per work item (suspect blocks, the stream's first block with the carry bytes,
 // tail blocks past the last wave tile); 16 waves per workgroup, grid-stride over the
 // items.  Hits go to a per-workgroup LDS list (LDS atomics) that is flushed with ONE
@@ -175,37 +192,58 @@ __global__ __launch_bounds__(kExactWaves * 64) void scan_exact_kernel(
     const uint64_t ns = ns0 < susp_cap ? ns0 : susp_cap;
     const uint64_t total = ns + (uint64_t)(head ? 1 : 0) + ext_count;
     const uint64_t stride = (uint64_t)gridDim.x * kExactWaves;
-    for (uint64_t w = (uint64_t)blockIdx.x * kExactWaves + wave; w < total; w += stride) {
-        uint64_t B;
-        if (w < ns)
-            B = susp[w];
-        else if (head && w == ns)
-            B = 0;
-        else
-            B = (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
-        const uint4 hit = exact_block_wave(data, len, pre, pre_len, (int64_t)B, tab, mask, minimum, lane);
-        if (lane < 4) {  // lane q writes the positions of hit word q
-            const uint32_t words[4] = {hit.x, hit.y, hit.z, hit.w};
-            uint32_t m = words[lane];
-            const uint32_t c = __builtin_popcount(m);
-            if (c) {
-                // slots [idx, kExactLds) of the LDS list are all filled; what does not fit
-                // goes straight to the output with its own atomic
-                const uint32_t idx = atomicAdd(&lcnt, c);
-                const uint32_t inl = idx >= kExactLds ? 0u : (c < kExactLds - idx ? c : kExactLds - idx);
-                const uint32_t gidx = c > inl ? atomicAdd(ncand, c - inl) : 0u;
-                uint32_t k = 0;
-                while (m) {
-                    const int bit = __builtin_ctz(m);
-                    m &= m - 1;
-                    const uint64_t v = base + B + (uint64_t)(lane * 32 + bit);
-                    if (k < inl)
-                        lbuf[idx + k] = v;
-                    else if (gidx + (k - inl) < cand_cap)
-                        cand[gidx + (k - inl)] = v;
-                    ++k;
+    auto item = [&](uint64_t w) -> uint64_t {
+        if (w < ns) return susp[w];
+        if (head && w == ns) return 0;
+        return (ext_first + (w - ns - (head ? 1 : 0))) * (uint64_t)kIter;
+    };
+    // batches of 64 items per wave: lane j fetches the block position of item j up front,
+    // and the window of item j+1 is loaded while item j is hashed
+    for (uint64_t w0 = (uint64_t)blockIdx.x * kExactWaves + wave; w0 < total; w0 += 64 * stride) {
+        const uint64_t wj = w0 + (uint64_t)lane * stride;
+        const uint64_t Bj = wj < total ? item(wj) : 0;
+        const uint32_t Blo = (uint32_t)Bj, Bhi = (uint32_t)(Bj >> 32);
+        const uint64_t left = (total - w0 + stride - 1) / stride;
+        const int cnt = left < 64 ? (int)left : 64;
+        auto getB = [&](int j) -> uint64_t {
+            return (uint64_t)(uint32_t)__shfl((int)Blo, j, 64) |
+                   ((uint64_t)(uint32_t)__shfl((int)Bhi, j, 64) << 32);
+        };
+        uint64_t B = getB(0);
+        uint32_t wv = exact_load(data, len, pre, pre_len, (int64_t)B, lane);
+        for (int j = 0; j < cnt; ++j) {
+            uint64_t Bn = 0;
+            uint32_t wvn = 0;
+            if (j + 1 < cnt) {
+                Bn = getB(j + 1);
+                wvn = exact_load(data, len, pre, pre_len, (int64_t)Bn, lane);
+            }
+            const uint4 hit = exact_hits(wv, len, pre_len, (int64_t)B, tab, mask, minimum, lane);
+            if (lane < 4) {  // lane q writes the positions of hit word q
+                const uint32_t words[4] = {hit.x, hit.y, hit.z, hit.w};
+                uint32_t m = words[lane];
+                const uint32_t c = __builtin_popcount(m);
+                if (c) {
+                    // slots [idx, kExactLds) of the LDS list are all filled; what does not fit
+                    // goes straight to the output with its own atomic
+                    const uint32_t idx = atomicAdd(&lcnt, c);
+                    const uint32_t inl = idx >= kExactLds ? 0u : (c < kExactLds - idx ? c : kExactLds - idx);
+                    const uint32_t gidx = c > inl ? atomicAdd(ncand, c - inl) : 0u;
+                    uint32_t k = 0;
+                    while (m) {
+                        const int bit = __builtin_ctz(m);
+                        m &= m - 1;
+                        const uint64_t v = base + B + (uint64_t)(lane * 32 + bit);
+                        if (k < inl)
+                            lbuf[idx + k] = v;
+                        else if (gidx + (k - inl) < cand_cap)
+                            cand[gidx + (k - inl)] = v;
+                        ++k;
+                    }
                 }
             }
+            B = Bn;
+            wv = wvn;
         }
     }
     __syncthreads();
