@@ -157,67 +157,77 @@ uint64_t batch_max(const Params& p) {
 // Phase A over d_data[0..len) (stream offset `base`): scan_main_kernel flags blocks,
 // scan_exact_kernel writes exact candidate positions (unsorted) to c->d_cand.  The
 // handle's carry (the <= 63 stream bytes before `base`) is the warm-up history.
-int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t base,
-                    uint32_t* ncand_out) {
+// scan_launch only enqueues (counters -> h_small[0] as two u32); scan_collect reads them
+// after the caller's sync and reports whether the suspect/candidate capacities held.
+struct ScanPlan {
+    uint64_t ntiles = 0, ext_first = 0, ext_count = 0, blocks = 0;
+    int seg = 0, head = 0;
+};
+
+ScanPlan plan_scan(pbs_chunker* c, uint64_t len) {
     const Params& p = c->prm;
-    *ncand_out = 0;
-    if (!p.hash_cuts || len == 0) return PBS_OK;
-    HIP_TRY(c, c->d_pre.ensure(64));
-    if (c->carry_len)
-        HIP_TRY(c, hipMemcpyAsync(c->d_pre.p, c->carry, c->carry_len, hipMemcpyHostToDevice,
-                                  c->stream));
-    uint64_t ntiles = 0;
-    const int seg = scan_main_plan(len, c->cu, &ntiles);
-    const uint64_t covered = ntiles * 64ull * (uint64_t)seg;
-    const int head = ntiles > 0 ? 1 : 0;
-    const uint64_t ext_first = covered / kBlockBytes;
-    const uint64_t ext_count = (len - covered + kBlockBytes - 1) / kBlockBytes;
-    const uint64_t blocks = (len + kBlockBytes - 1) / kBlockBytes;
+    ScanPlan sp;
+    sp.seg = scan_main_plan(len, c->cu, &sp.ntiles);
+    const uint64_t covered = sp.ntiles * 64ull * (uint64_t)sp.seg;
+    sp.head = sp.ntiles > 0 ? 1 : 0;
+    sp.ext_first = covered / kBlockBytes;
+    sp.ext_count = (len - covered + kBlockBytes - 1) / kBlockBytes;
+    sp.blocks = (len + kBlockBytes - 1) / kBlockBytes;
     const uint64_t expected = len / p.avg * 3 / 2 + 1;
-    const uint32_t want_s =
-        (uint32_t)std::min<uint64_t>(std::min<uint64_t>(blocks + 2, expected * 4 + 4096), 0xFFFFFFF0u);
+    const uint32_t want_s = (uint32_t)std::min<uint64_t>(
+        std::min<uint64_t>(sp.blocks + 2, expected * 4 + 4096), 0xFFFFFFF0u);
     const uint32_t want_c =
         (uint32_t)std::min<uint64_t>(std::min<uint64_t>(len + 1, expected * 2 + 8192), 0xFFFFFFF0u);
     c->susp_cap = std::max(c->susp_cap, want_s);
     c->cand_cap = std::max(c->cand_cap, want_c);
-    uint32_t nsusp = 0, ncand = 0;
-    for (int attempt = 0;; ++attempt) {
-        HIP_TRY(c, c->d_susp.ensure((size_t)c->susp_cap * 8));
-        HIP_TRY(c, c->d_cand.ensure((size_t)c->cand_cap * 8));
-        HIP_TRY(c, c->d_counters.ensure(16));
-        HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 16, c->stream));
-        uint32_t* d_nsusp = c->d_counters.as<uint32_t>();
-        uint32_t* d_ncand = d_nsusp + 1;
-        HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
-        HIP_TRY(c, launch_scan_main(d_data, ntiles, seg, c->d_table.as<uint32_t>(), p.thr,
-                                    c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu,
-                                    c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
-        const uint64_t max_items = (uint64_t)c->susp_cap + 1 + ext_count;
-        HIP_TRY(c, launch_scan_exact(d_data, len, c->d_pre.as<uint8_t>(), c->carry_len,
-                                     c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, ext_first,
-                                     ext_count, head, p.mask, p.minimum, base,
-                                     c->d_cand.as<uint64_t>(), d_ncand, c->cand_cap, max_items,
-                                     c->stream));
-        HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
-        HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_counters.p, 8, hipMemcpyDeviceToHost,
+    return sp;
+}
+
+int scan_launch(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t base,
+                const ScanPlan& sp) {
+    const Params& p = c->prm;
+    HIP_TRY(c, c->d_pre.ensure(64));
+    if (c->carry_len)
+        HIP_TRY(c, hipMemcpyAsync(c->d_pre.p, c->carry, c->carry_len, hipMemcpyHostToDevice,
                                   c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        const uint32_t* cnt = reinterpret_cast<const uint32_t*>(c->h_small);
-        nsusp = cnt[0];
-        ncand = cnt[1];
-        bool again = false;
-        if (nsusp > c->susp_cap) {
-            c->susp_cap = (uint32_t)std::min<uint64_t>((uint64_t)nsusp * 2 + 1024, blocks + 2);
-            again = true;
-        }
-        if (ncand > c->cand_cap) {
-            c->cand_cap = (uint32_t)std::min<uint64_t>((uint64_t)ncand * 2 + 1024, 0xFFFFFFF0u);
-            again = true;
-        }
-        if (!again) break;
-        if (attempt > 4) return fail(c, PBS_ERR_NOMEM);
+    HIP_TRY(c, c->d_susp.ensure((size_t)c->susp_cap * 8));
+    HIP_TRY(c, c->d_cand.ensure((size_t)c->cand_cap * 8));
+    HIP_TRY(c, c->d_counters.ensure(16));
+    HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 16, c->stream));
+    uint32_t* d_nsusp = c->d_counters.as<uint32_t>();
+    uint32_t* d_ncand = d_nsusp + 1;
+    HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+    HIP_TRY(c, launch_scan_main(d_data, sp.ntiles, sp.seg, c->d_table.as<uint32_t>(), p.thr,
+                                c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu, c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
+    const uint64_t max_items = (uint64_t)c->susp_cap + 1 + sp.ext_count;
+    HIP_TRY(c, launch_scan_exact(d_data, len, c->d_pre.as<uint8_t>(), c->carry_len,
+                                 c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, sp.ext_first,
+                                 sp.ext_count, sp.head, p.mask, p.minimum, base,
+                                 c->d_cand.as<uint64_t>(), d_ncand, c->cand_cap, max_items,
+                                 c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_counters.p, 8, hipMemcpyDeviceToHost, c->stream));
+    return PBS_OK;
+}
+
+// After the sync: *ok = false (and the capacities grown) when a list overflowed.
+int scan_collect(pbs_chunker* c, uint64_t len, const ScanPlan& sp, uint32_t* nsusp_out,
+                 uint32_t* ncand_out, bool* ok) {
+    const uint32_t* cnt = reinterpret_cast<const uint32_t*>(c->h_small);
+    const uint32_t nsusp = cnt[0], ncand = cnt[1];
+    *ok = true;
+    if (nsusp > c->susp_cap) {
+        c->susp_cap = (uint32_t)std::min<uint64_t>((uint64_t)nsusp * 2 + 1024, sp.blocks + 2);
+        *ok = false;
     }
+    if (ncand > c->cand_cap) {
+        c->cand_cap = (uint32_t)std::min<uint64_t>((uint64_t)ncand * 2 + 1024, 0xFFFFFFF0u);
+        *ok = false;
+    }
+    *nsusp_out = nsusp;
+    *ncand_out = ncand;
+    if (!*ok) return PBS_OK;
     float ms = 0;
     HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     c->timing.scan_ms += ms;
@@ -226,8 +236,25 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
     c->timing.bytes += len;
     c->timing.suspects += nsusp;
     c->timing.candidates += ncand;
-    *ncand_out = ncand;
     return PBS_OK;
+}
+
+int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t base,
+                    uint32_t* ncand_out) {
+    *ncand_out = 0;
+    if (!c->prm.hash_cuts || len == 0) return PBS_OK;
+    const ScanPlan sp = plan_scan(c, len);
+    for (int attempt = 0;; ++attempt) {
+        int rc = scan_launch(c, d_data, len, base, sp);
+        if (rc) return rc;
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        uint32_t nsusp = 0;
+        bool ok = false;
+        rc = scan_collect(c, len, sp, &nsusp, ncand_out, &ok);
+        if (rc) return rc;
+        if (ok) return PBS_OK;
+        if (attempt > 4) return fail(c, PBS_ERR_NOMEM);
+    }
 }
 
 // Radix-sort c->d_cand[0..n) into dst (device).
@@ -515,6 +542,63 @@ int scan_host_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, ui
     return PBS_OK;
 }
 
+// One batch of the regular path with a single host sync (see find_cuts_impl).  *done:
+// the batch is resolved and the state advanced.  Otherwise *have_cands tells whether
+// c->d_cand holds the batch's *nnew candidates (too many for one workgroup: the caller
+// sorts them and runs the multi-kernel resolve) or a list overflowed (rescan).
+int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos,
+               uint64_t bl, size_t np, uint64_t rend, uint64_t* out, size_t cap, size_t* n,
+               bool* done, bool* have_cands, uint32_t* nnew) {
+    const Params& p = c->prm;
+    *done = *have_cands = false;
+    const ScanPlan sp = plan_scan(c, bl);
+    const uint32_t m_max = kSmallResolveMax - 2;
+    HIP_TRY(c, c->d_C.ensure((size_t)(m_max + 2) * 8));
+    if (np)
+        HIP_TRY(c, hipMemcpyAsync(c->d_C.p, c->pending.data() + c->pend_head, np * 8,
+                                  hipMemcpyHostToDevice, c->stream));
+    int rc = scan_launch(c, dsrc, bl, pos, sp);
+    if (rc) return rc;
+    const uint64_t tl = std::min<uint64_t>(bl, kWindow - 1);
+    uint8_t* tail = reinterpret_cast<uint8_t*>(c->h_small + 24);
+    if (tl && !hsrc)
+        HIP_TRY(c, hipMemcpyAsync(tail, dsrc + bl - tl, tl, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, c->d_nxt.ensure(((size_t)m_max + 2) * 4));
+    HIP_TRY(c, c->d_nf.ensure(((size_t)m_max + 2) * 8));
+    HIP_TRY(c, c->d_res.ensure(32));
+    const uint64_t out_cap = cut_bound(c, m_max, rend);
+    HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
+    if ((rc = ensure_small_host_bufs(c))) return rc;
+    uint64_t *cuts_dev = nullptr, *keep_dev = nullptr, *small_dev = nullptr;
+    if ((rc = mapped(c, c->h_cuts, &cuts_dev)) || (rc = mapped(c, c->h_keep, &keep_dev)) ||
+        (rc = mapped(c, c->h_small, &small_dev)))
+        return rc;
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    ResolveParams rp{p.min_eff, p.max_eff, rend, c->chunk_start};
+    HIP_TRY(c, launch_resolve_small(c->d_cand.as<uint64_t>(), 0, c->d_C.as<uint64_t>(),
+                                    (uint32_t)np, rp, c->d_nxt.as<uint32_t>(),
+                                    c->d_nf.as<uint64_t>(), c->d_cuts.as<uint64_t>(), out_cap,
+                                    cuts_dev, kHostCuts, keep_dev, kHostKeep,
+                                    c->d_res.as<uint64_t>(), small_dev + 8, c->stream,
+                                    c->d_counters.as<uint32_t>(), c->susp_cap, c->cand_cap));
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    uint32_t nsusp = 0;
+    bool ok = false;
+    if ((rc = scan_collect(c, bl, sp, &nsusp, nnew, &ok))) return rc;
+    if (!ok) return PBS_OK;  // a list overflowed (capacities grown): rescan
+    if (c->h_small[8 + 12] != 0) {  // resolve stood down: too many keys for one workgroup
+        *have_cands = true;
+        return PBS_OK;
+    }
+    rc = small_finish(c, (uint32_t)np + *nnew, out_cap, rend, out, cap, n);
+    if (rc) return rc;
+    update_carry(c, hsrc ? hsrc + bl - tl : tail, tl);
+    c->scanned_end = pos + bl;
+    *done = true;
+    return PBS_OK;
+}
+
 int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final, uint64_t* out,
                    size_t cap, size_t* n_out, bool device) {
     if (!c) return PBS_ERR_INVALID;
@@ -557,6 +641,22 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
                 HIP_TRY(c, hipMemcpyAsync(c->d_in.p, hsrc, bl, hipMemcpyHostToDevice, c->stream));
                 dsrc = c->d_in.as<uint8_t>();
             }
+        }
+        bool have_cands = false;
+        if (bl && c->prm.hash_cuts && np + 2 <= kSmallResolveMax) {
+            // Speculative single-sync batch: scan, exact and the one-workgroup resolve are
+            // enqueued back to back; the resolve reads the candidate count on the device
+            // and stands down (res flag) when the lists overflowed or hold too many keys.
+            bool done = false;
+            int rc = spec_batch(c, dsrc, hsrc, pos, bl, np, rend, out, cap, &n, &done, &have_cands,
+                                &nnew);
+            if (rc) return rc;
+            if (done) {
+                pos += bl;
+                continue;
+            }
+        }
+        if (bl && !have_cands) {
             int rc = scan_candidates(c, dsrc, bl, pos, &nnew);  // host sync: counts
             if (rc) return rc;
         }

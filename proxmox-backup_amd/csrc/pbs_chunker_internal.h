@@ -52,7 +52,9 @@ hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C
                                 const ResolveParams& p, uint32_t* nxt, uint64_t* nforced,
                                 uint64_t* out, uint64_t out_cap, uint64_t* out_host,
                                 uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
-                                uint64_t* res, uint64_t* res_host, hipStream_t stream);
+                                uint64_t* res, uint64_t* res_host, hipStream_t stream,
+                                const uint32_t* counts = nullptr, uint32_t susp_cap = 0,
+                                uint32_t cand_cap = 0);
 // Small-input path (scan_blocks_kernel + resolve_small_kernel<1|2>, two launches, no
 // host sync between): the input bytes `data[0..len)` (stream offset `base`, device
 // memory) with the pre_len <= 63 bytes before them in `pre` (device), the test
@@ -71,6 +73,11 @@ struct FusedScanArgs {
     const uint64_t* pend;
     uint64_t* cand_out;
     uint64_t cand_cap;
+    // FUSED = 0 with counts != nullptr (speculative single-sync path): nnew is read from
+    // counts[1] (scan_exact's candidate counter); counts[0] > susp_cap, counts[1] >
+    // cand_cap or too many keys -> res_host[12] = 1 and nothing else is written
+    const uint32_t* counts;
+    uint32_t susp_cap;
 };
 constexpr uint64_t kFusedMaxBytes = 1ull << 20;  // inputs up to this size take the fused path
 hipError_t launch_scan_resolve_small(const FusedScanArgs& fa, int resolve, uint64_t* C,

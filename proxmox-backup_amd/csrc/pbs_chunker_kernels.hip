@@ -24,6 +24,8 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "buzhash_table.h"
 #include "pbs_chunker_internal.h"
 #include "scan_main.h"  // scan_main_kernel (phase A main pass)
@@ -464,6 +466,16 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     static_assert(kSmallPer <= 32, "on-mask bits");
 
     const uint32_t tid = threadIdx.x, T = kSmallThreads;
+    if constexpr (FUSED == 0) {
+        if (fa.counts) {  // speculative: the candidate count is only known on the device
+            const uint32_t ns = fa.counts[0], nc = fa.counts[1];
+            const bool fits = ns <= fa.susp_cap && nc <= fa.cand_cap &&
+                              (uint64_t)np + nc + 2 <= kSmallResolveMax;
+            if (tid == 0) res_host[12] = fits ? 0u : 1u;
+            if (!fits) return;  // uniform
+            nnew = nc;
+        }
+    }
     uint32_t m = np + nnew;
 
     const uint64_t t_start = wall_clock64();
@@ -837,8 +849,10 @@ int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles) {
     // 128-byte warm-up per segment costs 128/SEG of the work and traffic
     const uint64_t waves = (uint64_t)cu * kWavesPerWG;
     int seg = 4096;
+    int cap = 32768;  // PBS_MAX_SEG: experiment knob (segment-length sweeps)
+    if (const char* e = std::getenv("PBS_MAX_SEG")) cap = std::atoi(e);
     for (int s : {32768, 16384, 8192}) {
-        if (len / (64ull * s) >= 2 * waves) {
+        if (s <= cap && len / (64ull * s) >= 2 * waves) {
             seg = s;
             break;
         }
@@ -939,12 +953,17 @@ hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C
                                 const ResolveParams& p, uint32_t* nxt, uint64_t* nforced,
                                 uint64_t* out, uint64_t out_cap, uint64_t* out_host,
                                 uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
-                                uint64_t* res, uint64_t* res_host, hipStream_t stream) {
-    if ((uint64_t)np + nnew + 2 > kSmallResolveMax) return hipErrorInvalidValue;
+                                uint64_t* res, uint64_t* res_host, hipStream_t stream,
+                                const uint32_t* counts, uint32_t susp_cap, uint32_t cand_cap) {
+    if ((uint64_t)np + (counts ? 0 : nnew) + 2 > kSmallResolveMax) return hipErrorInvalidValue;
     (void)hipGetLastError();
+    FusedScanArgs fa{};
+    fa.counts = counts;
+    fa.susp_cap = susp_cap;
+    fa.cand_cap = cand_cap;
     hipLaunchKernelGGL(resolve_small_kernel<0>, dim3(1), dim3(kSmallThreads), 0, stream, newc,
                        nnew, C, np, p, nxt, nforced, out, out_cap, out_host, host_cap, keep_host,
-                       keep_cap, res, res_host, FusedScanArgs{});
+                       keep_cap, res, res_host, fa);
     return hipGetLastError();
 }
 

@@ -155,7 +155,7 @@ int main(int argc, char** argv) {
             CK(hipMemcpy(&h_cnt, cnt, 4, hipMemcpyDeviceToHost));                           \
         }                                                                                   \
         char nm[96]; snprintf(nm, sizeof nm, "v3 SEG=%d mode=%d G=%d ZS=%d FR=%d susp=%u", SEG, MODE, G, ZS, FR, h_cnt); \
-        report(nm, best);                                                                   \
+        report(nm, best * (double)n / (double)(tiles * 64ull * SEG));                                                                   \
     }
 #define RUNR96(SEG, MODE)                                                                   \
     if (only < 0 || only == vid++) {                                                        \
@@ -225,15 +225,14 @@ int main(int argc, char** argv) {
         char nm[96]; snprintf(nm, sizeof nm, "v6 SEG=%d mode=%d aux=%d G=%d susp=%u", SEG, MODE, AUX, G, h_cnt); \
         report(nm, best);                                                                   \
     }
-    RUN3F(32768, 0, 2, 4, 0, 0, 1)
     RUN3F(32768, 0, 2, 4, 0, 0, 2)
-    RUNR96(32768, 0)
-    RUNR96(32768, 2)
-    RUNR96(32768, 1)
-    RUN3F(32768, 2, 2, 4, 0, 0, 2)
-    RUN3F(32768, 0, 2, 4, 0, 0, 1)
-    RUN3F(32768, 0, 2, 4, 0, 0, 2)
-    RUNR96(32768, 0)
+    RUN3F(32896, 0, 2, 4, 0, 0, 2)
+    RUN3F(33024, 0, 2, 4, 0, 0, 2)
+    RUN3F(33792, 0, 2, 4, 0, 0, 2)
+    RUN3F(30720, 0, 2, 4, 0, 0, 2)
     RUN3F(32768, 1, 2, 4, 0, 0, 2)
+    RUN3F(32896, 1, 2, 4, 0, 0, 2)
+    RUN3F(32768, 0, 2, 4, 0, 0, 2)
+    RUN3F(32896, 0, 2, 4, 0, 0, 2)
     return 0;
 }
