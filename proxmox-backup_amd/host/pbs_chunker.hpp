@@ -4,6 +4,9 @@
 //   pbs::Chunker            pbs-datastore/src/chunker.rs:18-186   (new / scan)
 //   pbs::ChunkStream        pbs-client/src/chunk_stream.rs:12-78  (pull iterator of chunks)
 //   pbs::DynamicChunkWriter pbs-datastore/src/dynamic_index.rs:397-523 (write / close)
+//   pbs::DynamicIndexWriter pbs-datastore/src/dynamic_index.rs:297-391 (add_chunk / close)
+//   pbs::digest_chunks_device  DataChunkBuilder::digest (data_blob.rs:516-536) per chunk, GPU
+//   pbs::sha256             openssl::sha::sha256 (host; index checksum)
 //
 // Same names, argument meaning and error behaviour as the reference: a non-power-of-two
 // average throws std::invalid_argument with the reference's panic text; `scan` is
@@ -11,8 +14,11 @@
 // shim in INTEGRATION.md panics at the same point).  The hash scan runs on the GPU.
 #pragma once
 
+#include <array>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
+#include <ctime>
 #include <functional>
 #include <optional>
 #include <stdexcept>
@@ -21,6 +27,7 @@
 #include <vector>
 
 #include "pbs_chunker.h"
+#include "pbs_digest.h"
 
 namespace pbs {
 
@@ -178,6 +185,73 @@ class DynamicChunkWriter {
     Chunker chunker_;
     std::vector<uint8_t> chunk_buffer_;
     uint64_t chunk_offset_ = 0, last_chunk_ = 0, chunk_count_ = 0;
+    bool closed_ = false;
+};
+
+using Digest = std::array<uint8_t, 32>;
+
+inline Digest sha256(const uint8_t* data, size_t len) {
+    Digest d;
+    pbs_sha256(data, len, d.data());
+    return d;
+}
+
+// SHA-256 of every chunk [bounds[i], bounds[i+1]) of a device-resident stream (stream
+// bytes [base, base + len) at dev), optionally keyed (SHA-256(chunk || id_key)).
+inline std::vector<Digest> digest_chunks_device(const uint8_t* dev, size_t len, uint64_t base,
+                                                const std::vector<uint64_t>& bounds,
+                                                const std::vector<uint8_t>& key = {},
+                                                void* hip_stream = nullptr) {
+    const size_t n = bounds.size() > 1 ? bounds.size() - 1 : 0;
+    std::vector<Digest> out(n);
+    if (!n) return out;
+    const int rc = pbs_digest_chunks_device(dev, len, base, bounds.data(), n,
+                                            key.empty() ? nullptr : key.data(), key.size(),
+                                            out[0].data(), hip_stream);
+    if (rc != PBS_OK) throw std::runtime_error(std::string("pbs_digest_chunks_device: ") + pbs_strerror(rc));
+    return out;
+}
+
+// DynamicIndexWriter (dynamic_index.rs:297-391): add_chunk(end offset, digest) per chunk,
+// close() writes the .didx file (tmp file + rename) and returns index_csum.
+class DynamicIndexWriter {
+  public:
+    explicit DynamicIndexWriter(std::string path, std::array<uint8_t, 16> uuid = {},
+                                int64_t ctime = (int64_t)std::time(nullptr))
+        : path_(std::move(path)), uuid_(uuid), ctime_(ctime) {}
+
+    void add_chunk(uint64_t offset, const Digest& digest) {
+        if (closed_) throw std::runtime_error("cannot write to closed dynamic index file " + path_);
+        ends_.push_back(offset);
+        digests_.insert(digests_.end(), digest.begin(), digest.end());
+    }
+
+    Digest close() {
+        if (closed_) throw std::runtime_error("cannot close already closed archive index file " + path_);
+        closed_ = true;
+        std::vector<uint8_t> image(pbs_didx_size(ends_.size()));
+        Digest csum;
+        const int rc = pbs_didx_build(ends_.data(), digests_.data(), ends_.size(), uuid_.data(),
+                                      ctime_, image.data(), image.size(), csum.data());
+        if (rc != PBS_OK) throw std::runtime_error(std::string("pbs_didx_build: ") + pbs_strerror(rc));
+        std::string tmp = path_;
+        const size_t dot = tmp.find_last_of('.');
+        tmp = (dot == std::string::npos ? tmp : tmp.substr(0, dot)) + ".tmp_didx";
+        std::FILE* f = std::fopen(tmp.c_str(), "wb");
+        if (!f) throw std::runtime_error("cannot create " + tmp);
+        const bool ok = std::fwrite(image.data(), 1, image.size(), f) == image.size();
+        if (std::fclose(f) != 0 || !ok) throw std::runtime_error("write failed: " + tmp);
+        if (std::rename(tmp.c_str(), path_.c_str()) != 0)
+            throw std::runtime_error("Atomic rename file " + path_ + " failed");
+        return csum;
+    }
+
+  private:
+    std::string path_;
+    std::array<uint8_t, 16> uuid_;
+    int64_t ctime_;
+    std::vector<uint64_t> ends_;
+    std::vector<uint8_t> digests_;
     bool closed_ = false;
 };
 

@@ -1,4 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-for k in 1 2 3; do timeout -k 10 120 scripts/microbench/mb_scan 32 5 -1 1 > gpurun_out/mb_seg_$k.log 2>&1 || exit 1; done
-echo ok
+timeout -k 10 600 python -u -m pytest tests/test_host_mirror_cpp.py -m gpu -x -q --timeout 300 > gpurun_out/pytest_mirror.log 2>&1
+echo rc=$?

@@ -4,6 +4,8 @@
 //   stream <ends...>    ChunkStream over pieces of `piece` bytes (chunk_stream.rs:40-77)
 //   writer <ends...>    DynamicChunkWriter via write_all (dynamic_index.rs:493-515)
 //   batch <ends...>     find_cuts(is_final)
+//   index <csum hex>    DynamicIndexWriter over the writer's chunks (host SHA-256
+//                       digests), written to $HOST_MIRROR_DIDX when set
 // usage: host_mirror <avg> <len> <seed> <piece>   (input: splitmix64 random stream)
 #include <cstdio>
 #include <cstdlib>
@@ -66,11 +68,22 @@ int main(int argc, char** argv) {
         }
         {
             std::vector<uint64_t> ends;
-            pbs::DynamicChunkWriter w([&](uint64_t end, const std::vector<uint8_t>&) { ends.push_back(end); }, avg);
+            const char* didx = std::getenv("HOST_MIRROR_DIDX");
+            pbs::DynamicIndexWriter index(didx ? didx : "/dev/null", {}, 1234);
+            pbs::DynamicChunkWriter w([&](uint64_t end, const std::vector<uint8_t>& chunk) {
+                ends.push_back(end);
+                index.add_chunk(end, pbs::sha256(chunk.data(), chunk.size()));
+            }, avg);
             for (size_t off = 0; off < len; off += piece)
                 w.write_all(data.data() + off, std::min(piece, len - off));
             w.close();
             print("writer", ends);
+            if (didx) {
+                const pbs::Digest csum = index.close();
+                std::printf("index ");
+                for (uint8_t b : csum) std::printf("%02x", b);
+                std::printf("\n");
+            }
         }
         {
             pbs::Chunker c(avg);

@@ -32,7 +32,9 @@ def test_host_mirror_compiles_and_fails_loudly_without_device(tmp_path, pbschunk
 @pytest.mark.parametrize("avg,n,piece", [(4096, 3 << 20, 65536), (65536, 9 << 20, 262144), (64, 200000, 1000)])
 def test_host_mirror_matches_oracle(tmp_path, gpu, oracle, avg, n, piece):
     exe = _build(tmp_path)
-    r = subprocess.run([exe, str(avg), str(n), "7", str(piece)], capture_output=True, text=True, check=True)
+    didx = str(tmp_path / "mirror.didx")
+    r = subprocess.run([exe, str(avg), str(n), "7", str(piece)], capture_output=True, text=True, check=True,
+                       env={**os.environ, "HOST_MIRROR_DIDX": didx})
     lines = {ln.split(" ", 1)[0]: ln.split()[1:] for ln in r.stdout.strip().splitlines()}
     data = oracle.gen_random(n, 7)
     ref = oracle.chunk_feed(avg, data).tolist()
@@ -41,3 +43,9 @@ def test_host_mirror_matches_oracle(tmp_path, gpu, oracle, avg, n, piece):
         ends = [int(x) for x in lines[tag]]
         assert ends[:-1] == ref and ends[-1] == n, tag
     assert "not a power of two" in " ".join(lines["badavg"])
+    # DynamicIndexWriter over the writer's chunks == the oracle's .didx restatement
+    wends = np.array([int(x) for x in lines["writer"]], dtype=np.uint64)
+    bounds = np.concatenate([[0], wends]).astype(np.uint64)
+    ref_img, ref_csum = oracle.didx_image(wends, oracle.chunk_digests(data, bounds), bytes(16), 1234)
+    assert lines["index"][0] == ref_csum.hex()
+    assert open(didx, "rb").read() == ref_img
