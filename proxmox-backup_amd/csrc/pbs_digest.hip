@@ -5,18 +5,21 @@
 //
 // SHA-256 is a serial chain of 64-byte compressions per message, so the parallelism is
 // the chunks: ONE LANE PER CHUNK.  A lane streams its chunk 64 bytes at a time from
-// HBM (5 dwordx4-class loads of the dword-aligned 68-byte window, issued one block
-// ahead of the compression that uses them), builds the big-endian message words with
-// one v_perm_b32 each (byte alignment and byte swap in one op, selector from the
-// chunk's start & 3), and runs the 64 rounds in registers.  Per block ~1.1 k VALU ops
-// (v_alignbit rotations, v_bitop3 for Ch/Maj/3-way XOR, v_add3): the kernel is
-// VALU-issue-bound per lane (~25 MB/s per lane at 2.4 GHz), not HBM-bound; a wave
-// therefore takes as long as its longest chunk, and the host orders the chunks by
-// length (longest first) so the 64 lanes of a wave finish together.
+// HBM (the dword-aligned 68-byte window, loaded one block ahead of its use), builds the
+// big-endian message words with one v_perm_b32 each (byte alignment and byte swap in
+// one op, selector from the chunk's start & 3), and runs the 64 rounds in registers
+// (v_alignbit rotations, v_bitop3 for Ch/Maj/3-way XOR, v_add3).  The product kernel
+// (sha256_chunks_split_kernel) gives the schedule and the rounds of each block to two
+// waves of one workgroup; the single-wave form (sha256_chunks_kernel, 1422
+// instructions per block) is kept for A/B runs.  Either way the kernel is
+// VALU-issue-bound along one chunk's chain, not HBM-bound: a workgroup takes as long as
+// its longest chunk, and the host orders the chunks by length (longest first) so the
+// 64 lanes finish together.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -165,6 +168,139 @@ __global__ __launch_bounds__(64) void sha256_chunks_kernel(const uint8_t* __rest
     for (int q = 0; q < 8; ++q) out[q] = __builtin_bswap32(st[q]);
 }
 
+
+// Two-wave form: the message schedule (48 sigma steps + K[t] per block, the data loads,
+// the tail/padding blocks) runs in wave 1 one block ahead of the 64 rounds in wave 0,
+// handed over through a double-buffered LDS array W[2][64 t][64 lanes] (lane-minor:
+// conflict-free); one s_barrier per block.  The rounds' wave is the critical path:
+// ~960 instructions per block instead of ~1420 for one wave doing both.
+constexpr int kShaWaves = 2;
+__global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
+    const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
+    const uint32_t* __restrict__ order, uint64_t n, DigestKey key, uint8_t* __restrict__ digests) {
+    __shared__ uint32_t sw[2][64][64];  // [buffer][t][lane]: W[t] + K[t]
+    __shared__ uint32_t s_blocks;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t k = (uint64_t)blockIdx.x * 64 + lane;
+    const bool live = k < n;
+    const uint64_t i = live ? (order ? order[k] : k) : 0;
+    const uint64_t s = live ? bounds[i] - base : 0, e = live ? bounds[i + 1] - base : 0;
+    const uint64_t len = e - s;
+    const uint64_t nfull = len >> 6;
+    const uint32_t rem = (uint32_t)(len & 63);
+    const uint32_t kl = key.len;
+    const uint32_t nb = (rem + kl + 1 + 8 + 63) / 64;  // tail blocks
+    const uint64_t total = live ? nfull + nb : 0;      // blocks of this lane
+    // the wave pair runs to the longest lane's block count
+    if (threadIdx.x == 0) s_blocks = 0;
+    __syncthreads();
+    if (wave == 0) atomicMax(&s_blocks, (uint32_t)total);
+    __syncthreads();
+    const uint32_t nblocks = s_blocks;
+
+    const uint8_t* p = data + s;
+    const uint32_t r = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t* pa = reinterpret_cast<const uint32_t*>(p - r);
+    const uint32_t sel = (r << 24) | ((r + 1) << 16) | ((r + 2) << 8) | (r + 3);
+    const uint64_t bits = (len + kl) * 8ull;
+    const uint8_t* tp = p + (nfull << 6);
+
+    // wave 1: message block b -> W + K into buffer b & 1
+    auto produce = [&](uint32_t b) {
+        uint32_t w[16];
+        if ((uint64_t)b < nfull) {
+            uint32_t d[17];
+            load_window(pa + 16 * (uint64_t)b, r != 0, d);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) w[q] = __builtin_amdgcn_perm(d[q + 1], d[q], sel);
+        } else if ((uint64_t)b < total) {
+            const uint32_t blk = (uint32_t)(b - nfull);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t t = blk * 64 + 4 * q + j;
+                    uint32_t byte;
+                    if (t < rem)
+                        byte = tp[t];
+                    else if (t < rem + kl)
+                        byte = key.bytes[t - rem];
+                    else if (t == rem + kl)
+                        byte = 0x80u;
+                    else if (t >= nb * 64 - 8)
+                        byte = (uint32_t)(bits >> (8 * (nb * 64 - 1 - t))) & 0xffu;
+                    else
+                        byte = 0;
+                    v = (v << 8) | byte;
+                }
+                w[q] = v;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) w[q] = 0;
+        }
+        uint32_t (*out)[64] = sw[b & 1];
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+            uint32_t wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                const uint32_t x = w[(t - 15) & 15], y = w[(t - 2) & 15];
+                const uint32_t s0 = xor3(rotr(x, 7), rotr(x, 18), x >> 3);
+                const uint32_t s1 = xor3(rotr(y, 17), rotr(y, 19), y >> 10);
+                wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+                w[t & 15] = wt;
+            }
+            out[t][lane] = wt + kK[t];
+        }
+    };
+
+    uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                      0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    if (wave == 1 && nblocks) produce(0);
+    __syncthreads();
+    for (uint32_t b = 0; b < nblocks; ++b) {
+        if (wave == 1) {
+            if (b + 1 < nblocks) produce(b + 1);
+        } else if ((uint64_t)b < total) {
+            const uint32_t (*in)[64] = sw[b & 1];
+            uint32_t a = st[0], bb = st[1], c = st[2], d = st[3], ee = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+            for (int t = 0; t < 64; ++t) {
+                const uint32_t S1 = xor3(rotr(ee, 6), rotr(ee, 11), rotr(ee, 25));
+                const uint32_t ch = __builtin_amdgcn_bitop3_b32(ee, f, g, 0xCA);
+                const uint32_t t1 = h + S1 + ch + in[t][lane];
+                const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+                const uint32_t maj = __builtin_amdgcn_bitop3_b32(a, bb, c, 0xE8);
+                h = g;
+                g = f;
+                f = ee;
+                ee = d + t1;
+                d = c;
+                c = bb;
+                bb = a;
+                a = t1 + S0 + maj;
+            }
+            st[0] += a;
+            st[1] += bb;
+            st[2] += c;
+            st[3] += d;
+            st[4] += ee;
+            st[5] += f;
+            st[6] += g;
+            st[7] += h;
+        }
+        __syncthreads();
+    }
+    if (wave == 0 && live) {
+        uint32_t* out = reinterpret_cast<uint32_t*>(digests + 32 * i);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) out[q] = __builtin_bswap32(st[q]);
+    }
+}
+
 }  // namespace
 }  // namespace pbs
 
@@ -183,8 +319,17 @@ extern "C" int pbs_digest_chunks_async(const uint8_t* dev_data, size_t data_len,
     if (key_len) std::memcpy(k.bytes, key, key_len);
     (void)hipGetLastError();
     const unsigned grid = (unsigned)((n + 63) / 64);
-    hipLaunchKernelGGL(sha256_chunks_kernel, dim3(grid), dim3(64), 0, (hipStream_t)hip_stream,
-                       dev_data, base, bounds_dev, order_dev, (uint64_t)n, k, digests_dev);
+    static const bool one_wave = [] {  // PBS_SHA_ONE_WAVE=1: the single-wave kernel (A/B runs)
+        const char* e = std::getenv("PBS_SHA_ONE_WAVE");
+        return e && e[0] == '1';
+    }();
+    if (one_wave)
+        hipLaunchKernelGGL(sha256_chunks_kernel, dim3(grid), dim3(64), 0, (hipStream_t)hip_stream,
+                           dev_data, base, bounds_dev, order_dev, (uint64_t)n, k, digests_dev);
+    else
+        hipLaunchKernelGGL(sha256_chunks_split_kernel, dim3(grid), dim3(64 * kShaWaves), 0,
+                           (hipStream_t)hip_stream, dev_data, base, bounds_dev, order_dev,
+                           (uint64_t)n, k, digests_dev);
     return hipGetLastError() == hipSuccess ? PBS_OK : PBS_ERR_HIP;
 }
 
