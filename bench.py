@@ -142,6 +142,13 @@ def digest_stage(args, buf, cuts, stream, reps: int = 3):
         torch.cuda.synchronize()
         ms.append(ev[0].elapsed_time(ev[1]))
     t = min(ms) / 1e3
+    # known-chunk test of the same digests (backup_writer.rs:677-697; no previous index:
+    # repeats inside the stream, e.g. the zero chunks, are the known ones)
+    flags = torch.empty(n, dtype=torch.uint8, device=buf.device)
+    t0 = time.perf_counter()
+    nknown = pbschunk.known_chunks_device(out.data_ptr(), n, 0, 0, flags.data_ptr(),
+                                          hip_stream=stream.cuda_stream)
+    known_ms = (time.perf_counter() - t0) * 1e3
     # host reference point: hashlib over the first chunks totalling ~1 GiB, 16 threads
     take = int(np.searchsorted(np.cumsum(lens), 1 << 30)) + 1
     take = max(1, min(n, take))
@@ -162,6 +169,7 @@ def digest_stage(args, buf, cuts, stream, reps: int = 3):
     return {"metric": "GiB/s SHA-256 digested (per chunk, device-resident)",
             "value": round(size / (1 << 30) / t, 3), "ms": round(t * 1e3, 3), "chunks": n,
             "max_chunk": int(lens.max()), "bound": "valu (one lane per chunk; serial per chunk)",
+            "known_chunks": nknown, "known_ms": round(known_ms, 3),
             "cpu_baseline": {"value": round(cpu_gib_s, 3), "unit": "GiB/s", "cores": threads,
                              "kind": "hashlib (OpenSSL)",
                              "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"}}

@@ -51,6 +51,17 @@ int pbs_digest_chunks_async(const uint8_t *dev_data, size_t data_len, uint64_t b
                             const uint8_t *key, size_t key_len, uint8_t *digests_dev,
                             void *hip_stream);
 
+/* Known-chunk test of the upload stream (pbs-client/src/backup_writer.rs:677-697):
+ * chunk i is "known" -- uploaded as a reference, not as data -- iff its digest is in the
+ * previous backup's index (`known_chunks`, filled from the downloaded index,
+ * backup_writer.rs:524-547) or equals the digest of an earlier chunk of this stream
+ * (the reference inserts every new digest into the same set, :697).  `digests_dev` (32 n
+ * bytes) and `known_dev` (32 k bytes, sorted ascending as byte strings, duplicates
+ * allowed) are device memory; writes is_known_dev[i] = 0/1 (device, n bytes).
+ * Synchronous on `hip_stream`; *n_known (host, may be NULL) receives the count. */
+int pbs_known_chunks_device(const uint8_t *digests_dev, size_t n, const uint8_t *known_dev,
+                            size_t k, uint8_t *is_known_dev, size_t *n_known, void *hip_stream);
+
 /* Host SHA-256 (FIPS 180-4), used for the index checksum (the reference's
  * openssl::sha::Sha256 over 40-byte entries; a few hundred KiB per index). */
 void pbs_sha256(const uint8_t *data, size_t len, uint8_t out[32]);

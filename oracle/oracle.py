@@ -173,3 +173,17 @@ def didx_image(ends, digests, uuid: bytes = bytes(16), ctime: int = 0):
     header = DIDX_MAGIC + bytes(uuid) + struct.pack("<q", int(ctime)) + csum
     header += bytes(4096 - len(header))
     return header + entries, csum
+
+
+def known_chunks(digests, known) -> np.ndarray:
+    """backup_writer.rs:677-697: a chunk is known iff its digest is in the set (the
+    previous index's digests, :524-547); every new digest joins the set (:697)."""
+    seen = {bytes(d) for d in known}
+    out = np.zeros(len(digests), dtype=np.uint8)
+    for i, d in enumerate(digests):
+        b = bytes(d)
+        if b in seen:
+            out[i] = 1
+        else:
+            seen.add(b)
+    return out

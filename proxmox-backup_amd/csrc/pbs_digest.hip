@@ -16,6 +16,7 @@
 // its longest chunk, and the host orders the chunks by length (longest first) so the
 // 64 lanes finish together.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
 #include <algorithm>
@@ -301,6 +302,80 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Known-chunk test (backup_writer.rs:677-697), see pbs_digest.h.  The digests are
+// radix-sorted by their first 8 bytes (big-endian, i.e. byte-string order) with the
+// chunk index as value; the sort is stable, so each run of equal prefixes lists its
+// chunks in stream order.  A chunk is a repeat iff an earlier chunk of its run has the
+// same full digest: compared with the run's first element (the usual case: all equal),
+// else (a 64-bit prefix shared by different digests) against every earlier run member.
+// Membership in the previous index: binary search over the sorted known digests.
+__device__ __forceinline__ int cmp32(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b) {
+    const uint4* x = reinterpret_cast<const uint4*>(a);
+    const uint4* y = reinterpret_cast<const uint4*>(b);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint4 u = x[q], v = y[q];
+        const uint32_t uu[4] = {u.x, u.y, u.z, u.w}, vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (uu[w] != vv[w]) {
+                const uint32_t bu = __builtin_bswap32(uu[w]), bv = __builtin_bswap32(vv[w]);
+                return bu < bv ? -1 : 1;
+            }
+    }
+    return 0;
+}
+
+__global__ void digest_prefix_kernel(const uint8_t* __restrict__ dig, uint64_t n,
+                                     uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(dig + 32 * i);
+    key[i] = ((uint64_t)__builtin_bswap32(d[0]) << 32) | __builtin_bswap32(d[1]);
+    idx[i] = (uint32_t)i;
+}
+
+__global__ void run_head_kernel(const uint64_t* __restrict__ key, uint64_t n, uint32_t* __restrict__ head) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    head[p] = (p == 0 || key[p] != key[p - 1]) ? (uint32_t)p : 0u;
+}
+
+__global__ void known_kernel(const uint8_t* __restrict__ dig, uint64_t n,
+                             const uint32_t* __restrict__ sidx, const uint32_t* __restrict__ rstart,
+                             const uint8_t* __restrict__ known, uint64_t k,
+                             uint8_t* __restrict__ is_known, unsigned int* __restrict__ count) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t i = sidx[p];
+    const uint8_t* di = dig + 32ull * i;
+    bool rep = false;
+    const uint32_t r0 = rstart[p];
+    if (r0 != p) {
+        if (cmp32(dig + 32ull * sidx[r0], di) == 0) {
+            rep = true;
+        } else {
+            for (uint32_t q = r0 + 1; q < p && !rep; ++q) rep = cmp32(dig + 32ull * sidx[q], di) == 0;
+        }
+    }
+    bool in_known = false;
+    if (!rep && k) {
+        uint64_t lo = 0, hi = k;  // first known >= di
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (cmp32(known + 32 * mid, di) < 0)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        in_known = lo < k && cmp32(known + 32 * lo, di) == 0;
+    }
+    const bool kn = rep || in_known;
+    is_known[i] = kn ? 1 : 0;
+    if (kn) atomicAdd(count, 1u);
+}
+
 }  // namespace
 }  // namespace pbs
 
@@ -369,5 +444,67 @@ extern "C" int pbs_digest_chunks_device(const uint8_t* dev_data, size_t data_len
     if (d_bounds) (void)hipFree(d_bounds);
     if (d_order) (void)hipFree(d_order);
     if (d_dig) (void)hipFree(d_dig);
+    return rc;
+}
+
+extern "C" int pbs_known_chunks_device(const uint8_t* digests_dev, size_t n, const uint8_t* known_dev,
+                                       size_t k, uint8_t* is_known_dev, size_t* n_known,
+                                       void* hip_stream) {
+    if (n_known) *n_known = 0;
+    if (n == 0) return PBS_OK;
+    if (!digests_dev || !is_known_dev || (k && !known_dev) || n > 0xFFFFFFF0u) return PBS_ERR_INVALID;
+    hipStream_t st = (hipStream_t)hip_stream;
+    uint64_t *key = nullptr, *skey = nullptr;
+    uint32_t *idx = nullptr, *sidx = nullptr, *head = nullptr, *rstart = nullptr;
+    unsigned int* cnt = nullptr;
+    void* tmp = nullptr;
+    int rc = PBS_OK;
+    size_t tb_sort = 0, tb_scan = 0;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (hipMalloc(&key, n * 8) != hipSuccess || hipMalloc(&skey, n * 8) != hipSuccess ||
+        hipMalloc(&idx, n * 4) != hipSuccess || hipMalloc(&sidx, n * 4) != hipSuccess ||
+        hipMalloc(&head, n * 4) != hipSuccess || hipMalloc(&rstart, n * 4) != hipSuccess ||
+        hipMalloc(&cnt, 4) != hipSuccess) {
+        rc = PBS_ERR_NOMEM;
+        goto done;
+    }
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, key, skey, idx, sidx, (int)n, 0, 64, st) != hipSuccess ||
+        hipcub::DeviceScan::InclusiveScan(nullptr, tb_scan, head, rstart, hipcub::Max(), (int)n, st) != hipSuccess ||
+        hipMalloc(&tmp, std::max(tb_sort, tb_scan)) != hipSuccess) {
+        rc = PBS_ERR_NOMEM;
+        goto done;
+    }
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(digest_prefix_kernel, dim3(grid), dim3(256), 0, st, digests_dev, (uint64_t)n, key, idx);
+    tb_sort = std::max(tb_sort, tb_scan);
+    tb_scan = tb_sort;
+    if (hipcub::DeviceRadixSort::SortPairs(tmp, tb_sort, key, skey, idx, sidx, (int)n, 0, 64, st) != hipSuccess) {
+        rc = PBS_ERR_HIP;
+        goto done;
+    }
+    hipLaunchKernelGGL(run_head_kernel, dim3(grid), dim3(256), 0, st, skey, (uint64_t)n, head);
+    if (hipcub::DeviceScan::InclusiveScan(tmp, tb_scan, head, rstart, hipcub::Max(), (int)n, st) != hipSuccess ||
+        hipMemsetAsync(cnt, 0, 4, st) != hipSuccess) {
+        rc = PBS_ERR_HIP;
+        goto done;
+    }
+    hipLaunchKernelGGL(known_kernel, dim3(grid), dim3(256), 0, st, digests_dev, (uint64_t)n, sidx, rstart,
+                       known_dev, (uint64_t)k, is_known_dev, cnt);
+    if (hipGetLastError() != hipSuccess) {
+        rc = PBS_ERR_HIP;
+        goto done;
+    }
+    {
+        unsigned int h = 0;
+        if (hipMemcpyAsync(&h, cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            rc = PBS_ERR_HIP;
+            goto done;
+        }
+        if (n_known) *n_known = h;
+    }
+done:
+    for (void* q : {(void*)key, (void*)skey, (void*)idx, (void*)sidx, (void*)head, (void*)rstart, (void*)cnt, tmp})
+        if (q) (void)hipFree(q);
     return rc;
 }

@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "pbs_chunker_candidates_device", "pbs_chunker_resolve_device",
     # include/pbs_digest.h (chunk digests, dynamic index)
     "pbs_digest_chunks_device", "pbs_digest_chunks_async", "pbs_sha256", "pbs_didx_size",
-    "pbs_didx_build",
+    "pbs_didx_build", "pbs_known_chunks_device",
 )
 
 
@@ -122,6 +122,7 @@ def lib():
         "pbs_sha256": ([p, sz, p], None),
         "pbs_didx_size": ([sz], sz),
         "pbs_didx_build": ([p, p, sz, p, ctypes.c_int64, p, sz, p], i),
+        "pbs_known_chunks_device": ([p, sz, p, sz, p, ctypes.POINTER(sz), p], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -442,6 +443,20 @@ def digest_chunks_async(dev_ptr: int, data_len: int, bounds_dev: int, order_dev:
                                        ctypes.c_void_p(hip_stream))
     if rc != PBS_OK:
         raise ChunkerError(rc, "pbs_digest_chunks_async")
+
+
+def known_chunks_device(digests_dev: int, n: int, known_dev: int, k: int, is_known_dev: int,
+                        hip_stream: int = 0) -> int:
+    """backup_writer.rs:677-697 on the GPU: is_known[i] = digest i is in the previous
+    index (known_dev: k sorted 32-byte digests) or repeats an earlier chunk's digest.
+    All pointers device memory; returns the number of known chunks."""
+    cnt = ctypes.c_size_t(0)
+    rc = lib().pbs_known_chunks_device(ctypes.c_void_p(digests_dev), n, ctypes.c_void_p(known_dev or None),
+                                       k, ctypes.c_void_p(is_known_dev), ctypes.byref(cnt),
+                                       ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_known_chunks_device")
+    return int(cnt.value)
 
 
 def didx_build(ends, digests, uuid: bytes = bytes(16), ctime: int = 0):

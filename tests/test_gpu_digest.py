@@ -130,3 +130,38 @@ def test_async_device_form(gpu, oracle, torch_dev):
     torch.cuda.synchronize()
     got = out.cpu().numpy().reshape(n, 32)
     assert np.array_equal(got, oracle.chunk_digests(data, bounds))
+
+
+def _known_case(rng, n, k, prefix_clash=False):
+    dig = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    # repeats inside the stream (runs and scattered), like the zero chunks of an image
+    for _ in range(n // 5):
+        a, b = rng.integers(0, n, 2)
+        dig[max(a, b)] = dig[min(a, b)]
+    dig[n // 2: n // 2 + 40] = dig[n // 2]
+    if prefix_clash:  # same first 8 bytes, different digests (forces the slow path)
+        dig[10:30, :8] = dig[3, :8]
+        dig[25] = dig[12]
+    prev = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+    if k:
+        prev[: k // 3] = dig[rng.integers(0, n, k // 3)]
+    known = np.unique(prev.view("S32").reshape(-1)).view(np.uint8).reshape(-1, 32) if k else prev
+    return dig, known
+
+
+@pytest.mark.parametrize("n,k,clash", [(1, 0, False), (500, 0, False), (5000, 300, False),
+                                       (3000, 1000, True), (20000, 5000, True)])
+def test_known_chunks(gpu, oracle, torch_dev, n, k, clash):
+    """Known-chunk flags (previous index + repeats within the stream) equal the
+    reference's HashSet walk."""
+    torch = torch_dev
+    rng = np.random.default_rng(n + k)
+    dig, known = _known_case(rng, n, k, clash)
+    d = torch.from_numpy(dig.reshape(-1)).to("cuda")
+    kn = torch.from_numpy(known.reshape(-1).copy()).to("cuda") if k else None
+    out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cnt = gpu.known_chunks_device(d.data_ptr(), n, kn.data_ptr() if k else 0, known.shape[0] if k else 0,
+                                  out.data_ptr(), hip_stream=torch.cuda.current_stream().cuda_stream)
+    ref = oracle.known_chunks(dig, known if k else [])
+    got = out.cpu().numpy()
+    assert np.array_equal(got, ref) and cnt == int(ref.sum())
