@@ -450,6 +450,8 @@ int fused_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64
     }
     std::memcpy(c->h_stage + 64 - c->carry_len, c->carry, c->carry_len);
     if (np) std::memcpy(c->h_stage + 64, c->pending.data() + c->pend_head, np * 8);
+    // one pinned staging copy + ONE H2D beats a second H2D straight from the caller's
+    // pageable buffer for pieces <= 256 KiB (34 vs 49 us per 64 KiB piece) and ties above
     if (hsrc) std::memcpy(c->h_stage + data_off, hsrc, bl);
     HIP_TRY(c, c->d_stage.ensure(stage_bytes));
     HIP_TRY(c, hipMemcpyAsync(c->d_stage.p, c->h_stage, stage_bytes, hipMemcpyHostToDevice, c->stream));

@@ -97,15 +97,18 @@ class ChunkStream {
 
     std::optional<std::vector<uint8_t>> next() {
         for (;;) {
-            if (scan_pos_ < buffer_.size()) {
-                const size_t boundary =
-                    chunker_.scan(buffer_.data() + scan_pos_, buffer_.size() - scan_pos_);
+            const size_t avail = buffer_.size() - head_;
+            if (scan_pos_ < avail) {
+                const uint8_t* base = buffer_.data() + head_;
+                const size_t boundary = chunker_.scan(base + scan_pos_, avail - scan_pos_);
                 const size_t chunk_size = scan_pos_ + boundary;
                 if (boundary == 0) {
-                    scan_pos_ = buffer_.size();
-                } else if (chunk_size <= buffer_.size()) {
-                    std::vector<uint8_t> out(buffer_.begin(), buffer_.begin() + chunk_size);
-                    buffer_.erase(buffer_.begin(), buffer_.begin() + chunk_size);
+                    scan_pos_ = avail;
+                } else if (chunk_size <= avail) {
+                    // BytesMut::split_to (chunk_stream.rs:51) is O(1): advance a head
+                    // offset instead of moving the remainder
+                    std::vector<uint8_t> out(base, base + chunk_size);
+                    head_ += chunk_size;
                     scan_pos_ = 0;
                     return out;
                 } else {
@@ -115,10 +118,15 @@ class ChunkStream {
             std::vector<uint8_t> piece;
             if (!source_(piece)) {
                 scan_pos_ = 0;
-                if (buffer_.empty()) return std::nullopt;
-                std::vector<uint8_t> out;
-                out.swap(buffer_);
+                if (head_ == buffer_.size()) return std::nullopt;
+                std::vector<uint8_t> out(buffer_.begin() + (ptrdiff_t)head_, buffer_.end());
+                buffer_.clear();
+                head_ = 0;
                 return out;
+            }
+            if (head_ && head_ * 2 >= buffer_.size()) {  // compact before growing
+                buffer_.erase(buffer_.begin(), buffer_.begin() + (ptrdiff_t)head_);
+                head_ = 0;
             }
             buffer_.insert(buffer_.end(), piece.begin(), piece.end());
         }
@@ -128,7 +136,8 @@ class ChunkStream {
     Source source_;
     Chunker chunker_;
     std::vector<uint8_t> buffer_;
-    size_t scan_pos_ = 0;
+    size_t head_ = 0;      // bytes of buffer_ already handed out
+    size_t scan_pos_ = 0;  // relative to head_
 };
 
 // DynamicChunkWriter: `write` returns the bytes consumed (the caller re-submits the

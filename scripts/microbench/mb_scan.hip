@@ -226,13 +226,10 @@ int main(int argc, char** argv) {
         report(nm, best);                                                                   \
     }
     RUN3F(32768, 0, 2, 4, 0, 0, 2)
-    RUN3F(32896, 0, 2, 4, 0, 0, 2)
-    RUN3F(33024, 0, 2, 4, 0, 0, 2)
-    RUN3F(33792, 0, 2, 4, 0, 0, 2)
-    RUN3F(30720, 0, 2, 4, 0, 0, 2)
-    RUN3F(32768, 1, 2, 4, 0, 0, 2)
-    RUN3F(32896, 1, 2, 4, 0, 0, 2)
+    RUN3F(32768, 0, 2, 4, 0, 1, 2)
     RUN3F(32768, 0, 2, 4, 0, 0, 2)
-    RUN3F(32896, 0, 2, 4, 0, 0, 2)
+    RUN3F(32768, 0, 2, 4, 0, 1, 2)
+    RUN3F(32768, 0, 2, 4, 0, 0, 1)
+    RUN3F(32768, 0, 2, 4, 0, 1, 1)
     return 0;
 }
