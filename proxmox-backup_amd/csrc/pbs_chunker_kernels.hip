@@ -410,12 +410,12 @@ __global__ __launch_bounds__(256) void resolve_emit_kernel(
 constexpr uint32_t kSmallThreads = 1024;
 constexpr uint32_t kSmallBig = 64;        // nodes with many forced cuts, filled by the block
 constexpr uint32_t kSmallBigMin = 256;    // forced-cut run length handed to the block
-constexpr uint32_t kSmallJ = kSmallResolveMax + 16;  // u16 successor array stride (>= m + 2)
+constexpr uint32_t kSmallJ = kSmallResolveMax;  // u16 successor array stride (>= m + 2)
 
 constexpr uint32_t kSmallBuckets = 4096;
 constexpr uint32_t kSmallBucketMax = 256;  // larger buckets (skewed input): bitonic fallback
 constexpr uint32_t kSmallPer = (kSmallJ + kSmallThreads - 1) / kSmallThreads;  // nodes per thread
-constexpr uint32_t kSmallChunk = 6;  // slots per batch of independent global loads
+constexpr uint32_t kSmallChunk = 10;  // slots per batch of independent global loads
 
 // Buckets of 2^shift bytes from s0, shift = the smallest with span >> shift < kSmallBuckets
 // (a shift, not a 64-bit division: those are long software sequences on the GPU).
@@ -426,16 +426,30 @@ __device__ __forceinline__ uint32_t small_bucket(uint64_t key, uint64_t lo, uint
 // Exclusive scan of one value per thread over the block (Hillis-Steele in `part`).
 __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t* part, uint64_t v, uint32_t tid,
                                                         uint64_t* total = nullptr) {
-    part[tid] = v;
-    __syncthreads();
-    for (uint32_t d = 1; d < kSmallThreads; d <<= 1) {
-        const uint64_t x = tid >= d ? part[tid - d] : 0;
-        __syncthreads();
-        part[tid] += x;
-        __syncthreads();
+    // wave-level inclusive scan by shuffles, then the 16 wave totals (3 barriers instead
+    // of 20 for a Hillis-Steele pass over LDS)
+    constexpr uint32_t W = kSmallThreads / 64;
+    const uint32_t lane = tid & 63, w = tid >> 6;
+    unsigned long long x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
     }
-    const uint64_t r = part[tid] - v;
-    if (total) *total = part[kSmallThreads - 1];
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        unsigned long long t = lane < W ? part[lane] : 0ull;
+#pragma unroll
+        for (int d = 1; d < (int)W; d <<= 1) {
+            const unsigned long long y = __shfl_up(t, d, 64);
+            if (lane >= (uint32_t)d) t += y;
+        }
+        if (lane < W) part[lane] = t;  // inclusive wave prefixes
+    }
+    __syncthreads();
+    const uint64_t r = (w ? part[w - 1] : 0ull) + x - v;
+    if (total) *total = part[W - 1];
     __syncthreads();  // part is reused by the caller's next scan
     return r;
 }
@@ -456,13 +470,14 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     uint64_t* __restrict__ out_host, uint64_t host_cap, uint64_t* __restrict__ keep_host,
     uint64_t keep_cap, uint64_t* __restrict__ res, uint64_t* __restrict__ res_host,
     FusedScanArgs fa) {
-    __shared__ uint64_t sk[kSmallResolveMax];  // keys; later reused for ja | jb | on
+    __shared__ __attribute__((aligned(16))) uint64_t sk[kSmallResolveMax];  // keys; later ja | jb | on | nx16 | nf8
     __shared__ uint64_t part[kSmallThreads];
     __shared__ uint64_t big[kSmallBig][3];
     __shared__ uint64_t open_info[3];
     __shared__ uint32_t bcnt[kSmallBuckets];
     __shared__ uint32_t nbig, bmax;
-    static_assert(2 * kSmallJ * 2 + kSmallJ <= sizeof(uint64_t) * kSmallResolveMax, "LDS reuse");
+    // after the sort, sk holds ja | jb (u16) | on (u8) | nx16 (u16) | nf8 (u8)
+    static_assert(3 * kSmallJ * 2 + 2 * kSmallJ <= sizeof(uint64_t) * kSmallResolveMax, "LDS reuse");
     static_assert(kSmallPer <= 32, "on-mask bits");
 
     const uint32_t tid = threadIdx.x, T = kSmallThreads;
@@ -668,33 +683,52 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     uint16_t* ja = reinterpret_cast<uint16_t*>(sk);
     uint16_t* jb = ja + kSmallJ;
     uint8_t* on = reinterpret_cast<uint8_t*>(jb + kSmallJ);
+    // successor and forced-cut count kept in LDS for the emit step (nf8 = 255: see nforced)
+    uint16_t* nx16 = reinterpret_cast<uint16_t*>(on + kSmallJ);
+    uint8_t* nf8 = reinterpret_cast<uint8_t*>(nx16 + kSmallJ);
     const uint32_t n = m + 2;
-    for (uint32_t j = tid; j < n; j += T) {
-        ja[j] = (uint16_t)(j <= m ? nxt[j] : none);  // own writes from step 2
+    // every slot of the arrays is initialised: nodes >= n point to the sink (m + 1, a
+    // self-loop) and are never marked, so the rounds below need no bounds checks
+    for (uint32_t j = tid; j < kSmallJ; j += T) {
+        const uint32_t x = j <= m ? nxt[j] : none;  // own writes from step 2
+        const uint64_t f = j <= m ? nforced[j] : 0;
+        ja[j] = (uint16_t)x;
+        nx16[j] = (uint16_t)x;
+        nf8[j] = (uint8_t)(f < 255 ? f : 255);
         on[j] = j == m ? 1 : 0;
     }
     __syncthreads();
-    // thread t owns nodes t + q*T (consecutive lanes, consecutive u16: conflict-free);
-    // all its gathers are issued before any result is used (one LDS latency per round)
+    // thread t owns the 16 consecutive nodes [16t, 16t + 16): its successors and marks
+    // come in with two ds_read_b128 + one ds_read_b128, the 16 gathers are issued before
+    // any is used (one LDS latency per round), the new successors leave with two
+    // ds_write_b128
+    static_assert(kSmallPer == 16 && kSmallJ == kSmallPer * kSmallThreads, "doubling layout");
+    const uint32_t j0 = tid * kSmallPer;
     for (uint32_t rnd = 1; rnd < n; rnd <<= 1) {
-        uint32_t J[kSmallPer], JJ[kSmallPer];
-        uint32_t o = 0;
+        const uint4 a0 = *reinterpret_cast<const uint4*>(ja + j0);
+        const uint4 a1 = *reinterpret_cast<const uint4*>(ja + j0 + 8);
+        const uint4 ov = *reinterpret_cast<const uint4*>(on + j0);
+        const uint32_t aw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w};
+        uint32_t J[16], JJ[16];
 #pragma unroll
-        for (uint32_t q = 0; q < kSmallPer; ++q) {
-            const uint32_t j = tid + q * T;
-            J[q] = j < n ? ja[j] : 0u;
-            o |= (j < n && on[j]) ? (1u << q) : 0u;
-        }
+        for (int q = 0; q < 16; ++q) J[q] = (aw[q >> 1] >> (16 * (q & 1))) & 0xffffu;
 #pragma unroll
-        for (uint32_t q = 0; q < kSmallPer; ++q) JJ[q] = tid + q * T < n ? ja[J[q]] : 0u;
+        for (int q = 0; q < 16; ++q) JJ[q] = ja[J[q]];
 #pragma unroll
-        for (uint32_t q = 0; q < kSmallPer; ++q) {
-            const uint32_t j = tid + q * T;
-            if (j < n) {
-                if (o & (1u << q)) on[J[q]] = 1;
-                jb[j] = (uint16_t)JJ[q];
-            }
-        }
+        for (int q = 0; q < 16; ++q)
+            if ((ow[q >> 2] >> (8 * (q & 3))) & 0xffu) on[J[q]] = 1;
+        uint4 b0, b1;
+        b0.x = JJ[0] | (JJ[1] << 16);
+        b0.y = JJ[2] | (JJ[3] << 16);
+        b0.z = JJ[4] | (JJ[5] << 16);
+        b0.w = JJ[6] | (JJ[7] << 16);
+        b1.x = JJ[8] | (JJ[9] << 16);
+        b1.y = JJ[10] | (JJ[11] << 16);
+        b1.z = JJ[12] | (JJ[13] << 16);
+        b1.w = JJ[14] | (JJ[15] << 16);
+        *reinterpret_cast<uint4*>(jb + j0) = b0;
+        *reinterpret_cast<uint4*>(jb + j0 + 8) = b1;
         __syncthreads();
         uint16_t* t = ja;
         ja = jb;
@@ -716,8 +750,9 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
             const uint32_t sl = c0 + q;
             const uint32_t j = sl == 0 ? m : sl - 1;
             const bool live = sl < s_hi && on[j];
-            nfq[q] = live ? nforced[j] : 0u;
-            nxq[q] = live ? nxt[j] : none;
+            const uint32_t f8 = live ? nf8[j] : 0u;
+            nfq[q] = f8 == 255 ? nforced[j] : f8;
+            nxq[q] = live ? nx16[j] : none;
         }
 #pragma unroll
         for (uint32_t q = 0; q < kSmallChunk; ++q) sum += nfq[q] + (nxq[q] != none ? 1u : 0u);
@@ -736,8 +771,9 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
           jq[q] = sl == 0 ? m : sl - 1;
           const bool l = sl < s_hi && on[jq[q]];
           live |= l ? (1u << q) : 0u;
-          nfq[q] = l ? nforced[jq[q]] : 0u;
-          nxq[q] = l ? nxt[jq[q]] : none;
+          const uint32_t f8 = l ? nf8[jq[q]] : 0u;
+          nfq[q] = f8 == 255 ? nforced[jq[q]] : f8;
+          nxq[q] = l ? nx16[jq[q]] : none;
           cj[q] = (l && jq[q] != m) ? C[jq[q]] : 0u;
       }
 #pragma unroll
@@ -776,7 +812,18 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     for (uint32_t b = 0; b < nb; ++b)
         for (uint64_t t = tid; t < big[b][2]; t += T)
             if (big[b][1] + t < out_cap) out[big[b][1] + t] = big[b][0] + (t + 1) * p.max_eff;
-    if (tid == 0) open_info[2] = lower_bound_u64(C, 0, m, open_info[1]);
+    __syncthreads();  // open_info[1] (the open chunk's start) is set
+    {
+        // index of the first candidate >= the open chunk's start: C is sorted, so it is the
+        // number of smaller keys (one round of independent loads instead of a serial
+        // gallop + binary search through L2)
+        const uint64_t key = open_info[1];
+        uint64_t cnt = 0;
+        for (uint32_t i = tid; i < m; i += T) cnt += C[i] < key ? 1u : 0u;
+        uint64_t below = 0;
+        (void)block_exclusive_scan(part, cnt, tid, &below);
+        if (tid == 0) open_info[2] = below;
+    }
     __syncthreads();
     const uint64_t t_emit = wall_clock64();
     // cut list -> mapped pinned host memory, 16-byte coalesced stores
