@@ -16,10 +16,10 @@
 //            j); the nodes on the chain from the stream start are marked by pointer
 //            doubling, then emitted with an exclusive scan.
 //
-// No MFMA: this is a byte scan bound by HBM bandwidth.  The per-byte work is one
-// v_perm_b32 (LDS address), one ds_read_b32 (replicated table), one v_alignbit_b32
-// (rotl 1), one v_bitop3_b32 (3-input XOR; gfx950 has no v_xor3_b32) and half a
-// v_max3_u32.
+// No MFMA: this is a byte scan bound by HBM bandwidth (and, on MI355X, by board power:
+// DESIGN.md section 6).  The per-byte work of the main scan is one v_perm_b32 (LDS
+// address), one ds_read_b32 (replicated table), 1.5 hash ops (v_bitop3_b32 3-input XOR,
+// a v_alignbit_b32 rotate every second byte) and half a v_max3_u32.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -42,19 +42,21 @@ namespace pbs {
 // (global_load_lds_dwordx4), each covering 8 full 128-byte lines.
 //
 // LDS (128 KiB per workgroup):
-//   table  [0, 64 KiB):  T'[b] replicated 64x, byte address b*256 + lane*4, so a
-//                        wave64 ds_read_b32 of random bytes is bank-conflict-free
-//                        (bank = lane mod 32) and the address is ONE v_perm_b32.
+//   table  [0, 64 KiB):  row b (256 B) = T0[b] x 32 | T1[b] x 32, byte address
+//                        b*256 + u*128 + (lane&31)*4 for byte parity u: ds_read_b32
+//                        banks by (a/4) mod 32 per 32-lane half, so a wave64 read of
+//                        random bytes is conflict-free and the address is ONE
+//                        v_perm_b32 of the data dword and a per-parity lane base.
 //   stage  [64, 128 KiB): 8 KiB per wave.  Chunk k (16 B) of lane l's 128-byte block
 //                        sits at l*128 + ((k ^ ((l>>1)&7)) * 16): the XOR swizzle
 //                        makes the per-lane ds_read_b128 conflict-free.
 //
-// Hash representation.  h' = rotl(h, rot) with rot = 32 - popcount(mask), so the
-// mask bits sit at the top of the word and the test (h & mask) >= mask-2 becomes
-// the unsigned compare h' >= thr, thr = (mask-2) << rot.  Rotation commutes with
-// the recurrence, so the table is pre-rotated: T'[b] = rotl(T[b], rot).  The max
-// over a 128-byte block (v_max3_u32) flags the rare blocks that hold a candidate;
-// those blocks are re-evaluated exactly by scan_exact_kernel.
+// Hash representation (parity frame): byte i of a lane's block
+// keeps g_i = rotl(h_i, c - (i & 1)), c = 33 - popcount(mask); odd bytes need only the
+// 3-input XOR with T1 = rotl(T, c-1), even bytes a rotate by 2 and the XOR with
+// T0 = rotl(T, c).  In both frames a candidate's top n-1 bits read >= 2^(n-1) - 3, so
+// the max over a 128-byte block (v_max3_u32) against one threshold flags the rare
+// blocks that may hold a candidate; scan_exact_kernel re-evaluates them exactly.
 
 // ---------------------------------------------------------------------------------
 // Phase A, exact evaluation of 128-byte blocks (suspect blocks, stream head, tail)
@@ -599,17 +601,33 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
         __syncthreads();  // bcnt[b] = end of bucket b
         t_scatter = wall_clock64();
         // final index of a key = its bucket's start + #smaller keys in the bucket
-        // (positions are distinct); placed through C, then reloaded
-        for (uint32_t i = tid; i < m; i += T) {
-            const uint64_t key = sk[i];
-            const uint32_t b = small_bucket(key, p.s0, bshift);
-            const uint32_t lo = b ? bcnt[b - 1] : 0u, hi = bcnt[b];
-            uint32_t rank = 0;
-            for (uint32_t k = lo; k < hi; ++k) rank += sk[k] < key ? 1u : 0u;
-            C[lo + rank] = key;
+        // (positions are distinct); kept in registers until every thread has ranked,
+        // then placed in LDS (and in C, which the later steps read)
+        static_assert(kSmallPer * kSmallThreads >= kSmallResolveMax, "keys per thread");
+        uint64_t kq[kSmallPer];
+        uint32_t dq[kSmallPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kSmallPer; ++q) {
+            const uint32_t i = tid + q * T;
+            kq[q] = 0;
+            dq[q] = ~0u;
+            if (i < m) {
+                const uint64_t key = sk[i];
+                const uint32_t b = small_bucket(key, p.s0, bshift);
+                const uint32_t lo = b ? bcnt[b - 1] : 0u, hi = bcnt[b];
+                uint32_t rank = 0;
+                for (uint32_t k = lo; k < hi; ++k) rank += sk[k] < key ? 1u : 0u;
+                kq[q] = key;
+                dq[q] = lo + rank;
+            }
         }
         __syncthreads();
-        for (uint32_t i = tid; i < m; i += T) sk[i] = C[i];
+#pragma unroll
+        for (uint32_t q = 0; q < kSmallPer; ++q)
+            if (dq[q] != ~0u) {
+                sk[dq[q]] = kq[q];
+                C[dq[q]] = kq[q];
+            }
         __syncthreads();
     } else {
         uint32_t N = 2;
