@@ -12,9 +12,10 @@
 //                         up to kSmallResolveMax candidates one workgroup sorts and
 //                         resolves in LDS and writes the cuts into mapped pinned memory;
 //                         above that a hipcub radix sort + the multi-kernel resolve
-// Steps 1-3 run on the handle's HIP stream with two host syncs per batch (candidate
-// counts, then results); only the counts, the cut list, the open chunk's candidates
-// and the 63-byte warm-up tail come back to the host.
+// Steps 1-3 run on the handle's HIP stream with ONE host sync per batch (spec_batch:
+// the one-workgroup resolve reads the candidate count on the device and stands down
+// when it does not fit; the host then takes the two-sync path); only the counts, the
+// cut list, the open chunk's candidates and the 63-byte warm-up tail come back.
 //
 // `Chunker::scan` semantics (stateful, 0 or the boundary relative to the slice) are
 // kept by tracking absolute offsets: consumed (caller position), chunk_start (open
