@@ -259,13 +259,16 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
 }
 
 // Radix-sort c->d_cand[0..n) into dst (device).
-int sort_candidates(pbs_chunker* c, uint32_t n, uint64_t* dst) {
+int sort_candidates(pbs_chunker* c, uint32_t n, uint64_t* dst, uint64_t key_end) {
     if (n == 0) return PBS_OK;
+    // keys are stream offsets < key_end: radix passes only over the bits in use
+    // (36 bits for a 64 GiB stream: 5 passes instead of 8)
+    const int end_bit = key_end > 1 ? 64 - __builtin_clzll(key_end - 1) : 1;
     size_t tb = 0;
-    HIP_TRY(c, sort_u64(nullptr, &tb, c->d_cand.as<uint64_t>(), dst, n, c->stream));
+    HIP_TRY(c, sort_u64(nullptr, &tb, c->d_cand.as<uint64_t>(), dst, n, end_bit, c->stream));
     HIP_TRY(c, c->d_sort_tmp.ensure(tb));
     tb = c->d_sort_tmp.cap;
-    HIP_TRY(c, sort_u64(c->d_sort_tmp.p, &tb, c->d_cand.as<uint64_t>(), dst, n, c->stream));
+    HIP_TRY(c, sort_u64(c->d_sort_tmp.p, &tb, c->d_cand.as<uint64_t>(), dst, n, end_bit, c->stream));
     return PBS_OK;
 }
 
@@ -532,7 +535,7 @@ int scan_host_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, ui
     if (rc) return rc;
     if (ncand) {
         HIP_TRY(c, c->d_C.ensure(((size_t)ncand + 2) * 8));
-        rc = sort_candidates(c, ncand, c->d_C.as<uint64_t>());
+        rc = sort_candidates(c, ncand, c->d_C.as<uint64_t>(), pos + bl);
         if (rc) return rc;
         const size_t old = c->pending.size();
         c->pending.resize(old + ncand);
@@ -669,7 +672,7 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
         // d_C = [pending (np) | new (nnew)]; the small resolve sorts the new ones itself
         HIP_TRY(c, c->d_C.ensure((size_t)(m + 2) * 8));
         if (!small && nnew) {
-            int rc = sort_candidates(c, nnew, c->d_C.as<uint64_t>() + np);
+            int rc = sort_candidates(c, nnew, c->d_C.as<uint64_t>() + np, pos + bl);
             if (rc) return rc;
         }
         if (np)
@@ -923,7 +926,7 @@ int pbs_chunker_candidates_device(pbs_chunker* c, const uint8_t* dev, size_t len
     if (rc) return rc;
     *n_out = n;
     if (n > cap) return fail(c, PBS_ERR_CAPACITY);
-    rc = sort_candidates(c, n, out_dev);
+    rc = sort_candidates(c, n, out_dev, base + len);
     if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return PBS_OK;
@@ -981,7 +984,7 @@ int pbs_candidates_host(const uint8_t* data, size_t len, size_t avg, uint64_t* o
         if (!rc && n > cap) rc = PBS_ERR_CAPACITY;
         if (!rc && n) {
             if (c->d_C.ensure((size_t)n * 8) != hipSuccess) rc = PBS_ERR_HIP;
-            if (!rc) rc = sort_candidates(c, n, c->d_C.as<uint64_t>());
+            if (!rc) rc = sort_candidates(c, n, c->d_C.as<uint64_t>(), len);
             if (!rc && (hipMemcpyAsync(out, c->d_C.p, (size_t)n * 8, hipMemcpyDeviceToHost,
                                        c->stream) != hipSuccess ||
                         hipStreamSynchronize(c->stream) != hipSuccess))

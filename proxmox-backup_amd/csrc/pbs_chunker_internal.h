@@ -35,7 +35,7 @@ hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* p
                              uint32_t* ncand, uint32_t cand_cap, uint64_t max_items,
                              hipStream_t stream);
 hipError_t sort_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
-                    hipStream_t stream);
+                    int end_bit, hipStream_t stream);
 hipError_t exclusive_sum_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
                              uint32_t n, hipStream_t stream);
 hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p, uint32_t* nxt,

@@ -975,8 +975,8 @@ hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* p
 }
 
 hipError_t sort_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
-                    hipStream_t stream) {
-    return hipcub::DeviceRadixSort::SortKeys(tmp, *tmp_bytes, in, out, (int)n, 0, 64, stream);
+                    int end_bit, hipStream_t stream) {
+    return hipcub::DeviceRadixSort::SortKeys(tmp, *tmp_bytes, in, out, (int)n, 0, end_bit, stream);
 }
 
 hipError_t exclusive_sum_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
