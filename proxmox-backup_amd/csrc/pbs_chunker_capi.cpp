@@ -82,16 +82,18 @@ int make_params(uint64_t avg, Params* p) {
     p->hash_cuts = p->minimum <= p->mask;
     const int n = __builtin_popcount(p->mask);  // mask = 2^n - 1
     p->rot = (uint32_t)(32 - n) & 31u;
-    // scan_main_kernel's parity frame: odd bytes hold rotl(h, rot), even
-    // bytes rotl(h, rot + 1).  A candidate has bits 2..n-1 of h set and bits 1..0 != 0,
-    // so in both frames the top n-1 bits read >= 2^(n-1) - 3: one screening threshold
-    // (twice the exact candidate rate; scan_exact_kernel applies the exact test).
-    if (!p->hash_cuts)
+    if (!p->hash_cuts) {
         p->thr = 0xFFFFFFFFu;
-    else if (n < 3)
-        p->thr = 0;  // every block is a suspect
-    else
-        p->thr = ((1u << (n - 1)) - 3u) << ((33u - (uint32_t)n) & 31u);
+    } else if (kScanFrame == 1) {
+        // h' = rotl(h, rot): the mask bits sit on top, (h & mask) >= mask-2 <=> h' >= thr
+        p->thr = p->minimum << p->rot;
+    } else {
+        // parity frame: odd bytes hold rotl(h, rot), even bytes
+        // rotl(h, rot + 1).  A candidate has bits 2..n-1 of h set and bits 1..0 != 0, so in
+        // both frames the top n-1 bits read >= 2^(n-1) - 3: one screening threshold (twice
+        // the exact candidate rate; scan_exact_kernel applies the exact test)
+        p->thr = n < 3 ? 0u : ((1u << (n - 1)) - 3u) << ((33u - (uint32_t)n) & 31u);
+    }
     return PBS_OK;
 }
 
@@ -788,9 +790,10 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     ok = ok && hipHostMalloc((void**)&c->h_small, kSmallBytes, hipHostMallocMapped) == hipSuccess;
     ok = ok && c->d_table.ensure(512 * 4) == hipSuccess;
     if (ok) {
-        uint32_t t[512];  // [T0 | T1] of the parity frame: even bytes rot + 1, odd bytes rot
+        // frame 1: T' = rotl(T, rot); frame 2: [T0 | T1], even bytes rot + 1, odd bytes rot
+        uint32_t t[512];
         for (int i = 0; i < 256; ++i) {
-            t[i] = rotl32(kBuzhashTable[i], prm.rot + 1);
+            t[i] = rotl32(kBuzhashTable[i], kScanFrame == 1 ? prm.rot : prm.rot + 1);
             t[256 + i] = rotl32(kBuzhashTable[i], prm.rot);
         }
         ok = hipMemcpy(c->d_table.p, t, sizeof(t), hipMemcpyHostToDevice) == hipSuccess;

@@ -936,19 +936,19 @@ hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
     const dim3 gd(g), bd(kWavesPerWG * 64);
     switch (seg) {
         case 32768:
-            hipLaunchKernelGGL((scan_main_kernel<32768>), gd, bd, 0, stream, data, ntiles,
+            hipLaunchKernelGGL((scan_main_kernel<32768, kModeFull, 2, 4, 0, 0, kScanFrame>), gd, bd, 0, stream, data, ntiles,
                                table_rot, thr, susp, nsusp, cap);
             break;
         case 16384:
-            hipLaunchKernelGGL((scan_main_kernel<16384>), gd, bd, 0, stream, data, ntiles,
+            hipLaunchKernelGGL((scan_main_kernel<16384, kModeFull, 2, 4, 0, 0, kScanFrame>), gd, bd, 0, stream, data, ntiles,
                                table_rot, thr, susp, nsusp, cap);
             break;
         case 8192:
-            hipLaunchKernelGGL((scan_main_kernel<8192>), gd, bd, 0, stream, data, ntiles,
+            hipLaunchKernelGGL((scan_main_kernel<8192, kModeFull, 2, 4, 0, 0, kScanFrame>), gd, bd, 0, stream, data, ntiles,
                                table_rot, thr, susp, nsusp, cap);
             break;
         case 4096:
-            hipLaunchKernelGGL((scan_main_kernel<4096>), gd, bd, 0, stream, data, ntiles,
+            hipLaunchKernelGGL((scan_main_kernel<4096, kModeFull, 2, 4, 0, 0, kScanFrame>), gd, bd, 0, stream, data, ntiles,
                                table_rot, thr, susp, nsusp, cap);
             break;
         default:

@@ -49,10 +49,12 @@ __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
 // are almost never all in zero pages at once, and masked lanes save little -- so the
 // product runs ZS = 0.
 // FR (hash frame): 1 = h' = rotl(h, 32-n) for every byte, table T' = rotl(T, 32-n)
-// replicated 64x (3.5 VALU/byte); 2 = parity frame of roll128_asm_f2 (3 VALU/byte), table
-// = [T0 | T1] (512 words) interleaved 32x per 256-byte row, thr = the screening threshold
-// of DESIGN.md "parity frame" (a necessary condition; scan_exact re-tests exactly).
-template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int ZS = 0, int FR = 2>
+// replicated 64x (3.5 VALU/byte), exact block test -- the product (kScanFrame); 2 =
+// parity frame of roll128_asm_f2 (3 VALU/byte), table = [T0 | T1] (512 words)
+// interleaved 32x per 256-byte row, thr = the screening threshold of DESIGN.md section 6
+// (a necessary condition; scan_exact re-tests exactly): faster hash-only (7.7-8.0 vs
+// 7.2 TB/s) but 2-4 % slower in the full, power-limited kernel (profiles/r01/fr2/).
+template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int ZS = 0, int FR = 1>
 __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
     uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {

@@ -225,11 +225,13 @@ int main(int argc, char** argv) {
         char nm[96]; snprintf(nm, sizeof nm, "v6 SEG=%d mode=%d aux=%d G=%d susp=%u", SEG, MODE, AUX, G, h_cnt); \
         report(nm, best);                                                                   \
     }
-    RUN3F(32768, 0, 2, 4, 0, 0, 2)
-    RUN3F(32768, 0, 2, 4, 0, 1, 2)
-    RUN3F(32768, 0, 2, 4, 0, 0, 2)
-    RUN3F(32768, 0, 2, 4, 0, 1, 2)
     RUN3F(32768, 0, 2, 4, 0, 0, 1)
-    RUN3F(32768, 0, 2, 4, 0, 1, 1)
+    RUN3F(32768, 0, 2, 4, 0, 0, 2)
+    RUN3F(32768, 0, 2, 4, 0, 0, 1)
+    RUN3F(32768, 0, 2, 4, 0, 0, 2)
+    RUN3F(32768, 0, 2, 4, 0, 0, 1)
+    RUN3F(32768, 0, 2, 4, 0, 0, 2)
+    RUN3F(32768, 0, 2, 4, 0, 0, 1)
+    RUN3F(32768, 0, 2, 4, 0, 0, 2)
     return 0;
 }
