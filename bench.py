@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--digest", type=int, default=0,
                     help="also time the per-chunk SHA-256 stage (SURVEY 8(f)) over the stream's "
                          "chunks (GPU), with hashlib on the host cores beside it")
+    ap.add_argument("--pipeline-gib", type=float, default=0.0,
+                    help="also time the host-stream pipeline (copy -> chunk -> SHA-256 per chunk, "
+                         "pbs_pipeline_host) over this many GiB of a pageable host copy of the "
+                         "stream, with the oracle + hashlib on the host cores beside it")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per scan launch (written by profiles/collect_traffic.py)")
     return ap.parse_args()
@@ -173,6 +177,54 @@ def digest_stage(args, buf, cuts, stream, reps: int = 3):
             "cpu_baseline": {"value": round(cpu_gib_s, 3), "unit": "GiB/s", "cores": threads,
                              "kind": "hashlib (OpenSSL)",
                              "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"}}
+
+
+def pipeline_stage(args, buf, piece: int = 1 << 30):
+    """a pageable host copy of the stream's first --pipeline-gib GiB
+    through pbs_pipeline_host (copy thread -> HBM, chunker on CU-masked stream, per-chunk
+    SHA-256 on the other CUs, overlapped), end to end; the CPU path beside it: the oracle
+    chunker + hashlib per chunk on the host cores over a bounded sample."""
+    import hashlib
+
+    import numpy as np
+
+    import pbschunk
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    n = int(args.pipeline_gib * (1 << 30)) // 8 * 8
+    host = buf[:n].cpu().numpy()  # pageable, untimed
+    pbschunk.pipeline_host(host[: 64 << 20], args.avg, piece=16 << 20)  # warm-up
+    t0 = time.perf_counter()
+    ends, dig, t = pbschunk.pipeline_host(host, args.avg, piece=piece)
+    wall = time.perf_counter() - t0
+    # CPU path: threads chunk their own slice and hash its chunks (hashlib/OpenSSL)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    per = (256 << 20)
+
+    def work(k):
+        sl = host[k * per:(k + 1) * per]
+        cuts = oracle.chunk_feed(args.avg, sl)
+        b = np.concatenate([[0], cuts, [sl.size]]).astype(np.int64)
+        mv = memoryview(sl)
+        for i in range(b.size - 1):
+            if b[i + 1] > b[i]:
+                hashlib.sha256(mv[b[i]:b[i + 1]]).digest()
+
+    nth = min(threads, max(1, n // per))
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(nth)]
+    c0 = time.perf_counter()
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    cpu = nth * per / (1 << 30) / (time.perf_counter() - c0)
+    return {"metric": "GiB/s host stream -> chunk boundaries + SHA-256 per chunk (end to end)",
+            "value": round(n / (1 << 30) / wall, 3), "bytes": n, "piece": piece,
+            "chunks": int(ends.size), "timing_ms": {k: round(v, 2) for k, v in t.items()
+                                                     if k.endswith("_ms")},
+            "cpu_baseline": {"value": round(cpu, 3), "unit": "GiB/s", "cores": nth,
+                             "kind": "port (oracle chunker) + hashlib",
+                             "sample": f"{nth} x 256 MiB slices: chunk_feed then sha256 per chunk"}}
 
 
 def main():
@@ -304,6 +356,8 @@ def main():
         out["host_inclusive_gib_s"] = round(host_incl, 3)
     if args.digest and args.mode == "streams":
         out["digest"] = digest_stage(args, buf, cuts, stream)
+    if args.pipeline_gib > 0 and args.mode == "streams" and world == 1:
+        out["pipeline"] = pipeline_stage(args, buf)
     if args.cpu_baseline and world == 1:
         del buf
         out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)

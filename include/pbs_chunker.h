@@ -92,6 +92,10 @@ int pbs_chunker_reset(pbs_chunker *c);
 /* Run the handle's kernels on this hipStream_t (NULL = the handle's own stream). */
 int pbs_chunker_set_stream(pbs_chunker *c, void *hip_stream);
 
+/* Number of CUs the persistent scan kernel sizes its grid for (default: all of the
+ * device); set it to the CU count of a CU-masked stream given to set_stream. */
+int pbs_chunker_set_cu_count(pbs_chunker *c, int cus);
+
 /* Error of the last failed call on this handle, and a message for any code. */
 int pbs_chunker_last_error(const pbs_chunker *c);
 const char *pbs_strerror(int code);

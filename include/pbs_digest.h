@@ -62,6 +62,26 @@ int pbs_digest_chunks_async(const uint8_t *dev_data, size_t data_len, uint64_t b
 int pbs_known_chunks_device(const uint8_t *digests_dev, size_t n, const uint8_t *known_dev,
                             size_t k, uint8_t *is_known_dev, size_t *n_known, void *hip_stream);
 
+/* Client upload path on a host-resident stream (ChunkStream
+ * pbs-client/src/chunk_stream.rs:40-77 + the per-chunk digest of the upload stream,
+ * backup_writer.rs:671-678): a copy thread moves `host` (pageable, `len` bytes) to HBM
+ * in `piece`-byte pieces; the chunker cuts every resident piece on CUs
+ * [digest_cus, n) and the chunks each piece completes are digested on CU-masked
+ * streams over CUs [0, digest_cus) while the next pieces copy.  Writes the chunk END
+ * offsets (`ends`, the tail included) and their 32-byte digests (SHA-256(chunk || key))
+ * in chunk order; cap >= pbs_chunker_cuts_bound for the average.  Needs `len` bytes of
+ * device memory.  Synchronous. */
+typedef struct {
+    double total_ms; /* first copy issued .. digests on the host */
+    double h2d_ms;   /* copy thread: all pieces issued and landed */
+    double chunk_ms; /* main thread inside the chunker calls */
+    double drain_ms; /* last piece chunked .. digests on the host */
+    uint64_t bytes, chunks, pieces;
+} pbs_pipeline_timing;
+int pbs_pipeline_host(size_t avg, const uint8_t *host, size_t len, size_t piece,
+                      const uint8_t *key, size_t key_len, int digest_cus, uint64_t *ends,
+                      uint8_t *digests, size_t cap, size_t *n_out, pbs_pipeline_timing *timing);
+
 /* Host SHA-256 (FIPS 180-4), used for the index checksum (the reference's
  * openssl::sha::Sha256 over 40-byte entries; a few hundred KiB per index). */
 void pbs_sha256(const uint8_t *data, size_t len, uint8_t out[32]);

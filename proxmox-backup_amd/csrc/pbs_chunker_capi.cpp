@@ -817,6 +817,12 @@ int pbs_chunker_reset(pbs_chunker* c) {
     return PBS_OK;
 }
 
+int pbs_chunker_set_cu_count(pbs_chunker* c, int cus) {
+    if (!c || cus < 1) return PBS_ERR_INVALID;
+    c->cu = cus;
+    return PBS_OK;
+}
+
 int pbs_chunker_set_stream(pbs_chunker* c, void* hip_stream) {
     if (!c) return PBS_ERR_INVALID;
     c->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->own_stream;

@@ -1,0 +1,226 @@
+// Client upload path on a host-resident stream: ChunkStream's
+// chunking (pbs-client/src/chunk_stream.rs:40-77) and the per-chunk digest of the upload
+// stream (pbs-client/src/backup_writer.rs:671-678), overlapped on one MI355X:
+//
+//   copy thread   pageable host pieces -> HBM (hipMemcpyAsync on its own stream; the DMA
+//                 engines, no CUs)
+//   main thread   chunker over each resident piece (find_cuts_device on a stream
+//                 CU-masked to CUs [digest_cus, n)); the completed chunks go to per-chunk
+//                 SHA-256 launches on four digest streams CU-masked to CUs [0, digest_cus)
+//
+// The CU split keeps the persistent scan kernel and the long-running digest workgroups
+// apart: a scan workgroup (130 KiB LDS, 2 x 208 VGPRs per SIMD) cannot share a CU with a
+// digest workgroup, and a digest launch lasts as long as its longest chunk's serial
+// hash (~0.6 s for a 16 MiB chunk), so without the split a scan launch would wait for it.
+// The chunks are digested in a few large launches (a quarter of the stream, at most
+// 16 GiB each), which overlap on the four digest streams and with the later copies.  C ABI:
+// include/pbs_digest.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <thread>
+#include <vector>
+
+#include "pbs_chunker.h"
+#include "pbs_digest.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double ms_since(Clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+hipError_t masked_stream(hipStream_t* s, int first, int count, int ncu) {
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    for (int cu = first; cu < first + count && cu < ncu; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
+constexpr int kDigestStreams = 4;
+
+}  // namespace
+
+extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, size_t piece,
+                                 const uint8_t* key, size_t key_len, int digest_cus,
+                                 uint64_t* ends, uint8_t* digests, size_t cap, size_t* n_out,
+                                 pbs_pipeline_timing* timing) {
+    if (!n_out || (len && !host) || piece == 0 || (cap && (!ends || !digests)) ||
+        key_len > PBS_DIGEST_MAX_KEY || (key_len && !key))
+        return PBS_ERR_INVALID;
+    *n_out = 0;
+    if (timing) std::memset(timing, 0, sizeof(*timing));
+    if (len == 0) return PBS_OK;
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return PBS_ERR_NO_DEVICE;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 16)
+        return PBS_ERR_HIP;
+    const int dig = std::min(std::max(digest_cus, 4), ncu - 8);
+    int err = PBS_OK;
+    pbs_chunker* c = pbs_chunker_new(avg, &err);
+    if (!c) return err;
+    if (cap < pbs_chunker_cuts_bound(c, len)) {
+        pbs_chunker_free(c);
+        return PBS_ERR_CAPACITY;
+    }
+    const size_t npieces = (len + piece - 1) / piece;
+    hipStream_t s_copy = nullptr, s_scan = nullptr, s_dig[kDigestStreams] = {};
+    uint8_t* d_data = nullptr;
+    uint8_t* d_dig = nullptr;
+    uint64_t* d_bounds = nullptr;
+    uint32_t* d_order = nullptr;
+    std::vector<hipEvent_t> ev_copied(npieces, nullptr);
+    int rc = PBS_OK;
+    auto hip_ok = [&](hipError_t e) {
+        if (e != hipSuccess && rc == PBS_OK) rc = PBS_ERR_HIP;
+        return e == hipSuccess;
+    };
+    bool ok = hip_ok(hipStreamCreateWithFlags(&s_copy, hipStreamNonBlocking)) &&
+              hip_ok(masked_stream(&s_scan, dig, ncu - dig, ncu));
+    for (auto& s : s_dig) ok = ok && hip_ok(masked_stream(&s, 0, dig, ncu));
+    for (auto& e : ev_copied) ok = ok && hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // device: the stream, the digests, and per-launch bounds/order (<= cap + npieces + 1)
+    if (ok && (hipMalloc(&d_data, len) != hipSuccess || hipMalloc(&d_dig, cap * 32) != hipSuccess ||
+               hipMalloc(&d_bounds, (cap + npieces + 1) * 8) != hipSuccess ||
+               hipMalloc(&d_order, std::max<size_t>(cap, 1) * 4) != hipSuccess)) {
+        ok = false;
+        rc = PBS_ERR_NOMEM;
+    }
+    ok = ok && pbs_chunker_set_stream(c, s_scan) == PBS_OK &&
+         pbs_chunker_set_cu_count(c, ncu - dig) == PBS_OK;
+    if (!ok && rc == PBS_OK) rc = PBS_ERR_HIP;
+
+    const Clock::time_point t0 = Clock::now();
+    std::atomic<size_t> copied{0};
+    std::atomic<bool> copy_failed{false};
+    std::mutex mu;
+    std::condition_variable cv;
+    double h2d_ms = 0;
+    std::thread copier;
+    if (ok) {
+        copier = std::thread([&] {
+            const Clock::time_point tc = Clock::now();
+            for (size_t k = 0; k < npieces; ++k) {
+                const size_t off = k * piece, n = std::min(piece, len - off);
+                if (hipMemcpyAsync(d_data + off, host + off, n, hipMemcpyHostToDevice, s_copy) !=
+                        hipSuccess ||
+                    hipEventRecord(ev_copied[k], s_copy) != hipSuccess) {
+                    copy_failed = true;
+                    break;
+                }
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    copied = k + 1;
+                }
+                cv.notify_one();
+            }
+            (void)hipStreamSynchronize(s_copy);
+            h2d_ms = ms_since(tc);
+            cv.notify_one();
+        });
+    }
+
+    double chunk_ms = 0, last_chunk_at = 0;
+    size_t n = 0, nb = 0, launches = 0, launched = 0;
+    uint64_t start = 0;  // start of the first chunk not yet digested
+    // bytes of completed chunks per digest launch: a quarter of the stream, at most 16 GiB
+    const uint64_t dbatch = std::max<uint64_t>(std::min<uint64_t>(len / 4, 16ull << 30), piece);
+    std::vector<uint64_t> tmp(ok ? pbs_chunker_cuts_bound(c, std::min(piece, len)) + 1 : 0);
+    std::vector<std::vector<uint64_t>> hb;  // host bounds/order stay alive until the end
+    std::vector<std::vector<uint32_t>> ho;
+    for (size_t k = 0; ok && rc == PBS_OK && k < npieces; ++k) {
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return copied.load() > k || copy_failed.load(); });
+        }
+        if (copy_failed) {
+            rc = PBS_ERR_HIP;
+            break;
+        }
+        const size_t off = k * piece, pn = std::min(piece, len - off);
+        if (!hip_ok(hipStreamWaitEvent(s_scan, ev_copied[k], 0))) break;
+        const Clock::time_point tk = Clock::now();
+        size_t m = 0;
+        const int r = pbs_chunker_find_cuts_device(c, d_data + off, pn, k + 1 == npieces, tmp.data(),
+                                                   tmp.size(), &m);
+        chunk_ms += ms_since(tk);
+        if (r != PBS_OK) {
+            rc = r;
+            break;
+        }
+        if (n + m > cap) {
+            rc = PBS_ERR_CAPACITY;
+            break;
+        }
+        if (m) {
+            std::memcpy(ends + n, tmp.data(), m * 8);
+            n += m;
+        }
+        // digest the chunks completed since the last launch once they cover dbatch bytes
+        // (or at the end): a launch lasts as long as its longest chunk's serial hash, so
+        // few large launches, overlapping on the digest streams, keep the CUs busy
+        const uint64_t done_to = n ? ends[n - 1] : 0;
+        const bool last = k + 1 == npieces;
+        if (n > launched && (done_to - start >= dbatch || last)) {
+            const size_t mm = n - launched;
+            hb.emplace_back(mm + 1);
+            ho.emplace_back(mm);
+            std::vector<uint64_t>& b = hb.back();
+            std::vector<uint32_t>& o = ho.back();
+            b[0] = start;
+            std::memcpy(b.data() + 1, ends + launched, mm * 8);
+            std::iota(o.begin(), o.end(), 0u);
+            std::stable_sort(o.begin(), o.end(), [&](uint32_t x, uint32_t y) {
+                return b[x + 1] - b[x] > b[y + 1] - b[y];
+            });
+            hipStream_t sd = s_dig[launches % kDigestStreams];
+            if (!hip_ok(hipMemcpyAsync(d_bounds + nb, b.data(), (mm + 1) * 8, hipMemcpyHostToDevice, sd)) ||
+                !hip_ok(hipMemcpyAsync(d_order + launched, o.data(), mm * 4, hipMemcpyHostToDevice, sd)))
+                break;
+            const int dr = pbs_digest_chunks_async(d_data, len, 0, d_bounds + nb, d_order + launched, mm,
+                                                   key, key_len, d_dig + 32 * launched, sd);
+            if (dr != PBS_OK) {
+                rc = dr;
+                break;
+            }
+            ++launches;
+            nb += mm + 1;
+            launched = n;
+            start = done_to;
+        }
+        last_chunk_at = ms_since(t0);
+    }
+    if (copier.joinable()) copier.join();
+    if (rc == PBS_OK && ok) {
+        for (auto& s : s_dig) hip_ok(hipStreamSynchronize(s));
+        if (rc == PBS_OK && n) hip_ok(hipMemcpy(digests, d_dig, n * 32, hipMemcpyDeviceToHost));
+    }
+    const double total = ms_since(t0);
+    if (timing) {
+        timing->total_ms = total;
+        timing->h2d_ms = h2d_ms;
+        timing->chunk_ms = chunk_ms;
+        timing->drain_ms = total - last_chunk_at;
+        timing->bytes = len;
+        timing->chunks = n;
+        timing->pieces = npieces;
+    }
+    *n_out = n;
+    for (auto& e : ev_copied)
+        if (e) (void)hipEventDestroy(e);
+    for (void* p : {(void*)d_data, (void*)d_dig, (void*)d_bounds, (void*)d_order})
+        if (p) (void)hipFree(p);
+    pbs_chunker_free(c);  // before its stream goes away
+    if (s_copy) (void)hipStreamDestroy(s_copy);
+    if (s_scan) (void)hipStreamDestroy(s_scan);
+    for (auto& s : s_dig)
+        if (s) (void)hipStreamDestroy(s);
+    return rc;
+}

@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "pbs_chunker_candidates_device", "pbs_chunker_resolve_device",
     # include/pbs_digest.h (chunk digests, dynamic index)
     "pbs_digest_chunks_device", "pbs_digest_chunks_async", "pbs_sha256", "pbs_didx_size",
-    "pbs_didx_build", "pbs_known_chunks_device",
+    "pbs_didx_build", "pbs_known_chunks_device", "pbs_pipeline_host", "pbs_chunker_set_cu_count",
 )
 
 
@@ -71,6 +71,17 @@ class Timing(ctypes.Structure):
         ("resolve_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
         ("bytes", ctypes.c_uint64), ("suspects", ctypes.c_uint64),
         ("candidates", ctypes.c_uint64), ("cuts", ctypes.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class PipelineTiming(ctypes.Structure):
+    _fields_ = [
+        ("total_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
+        ("chunk_ms", ctypes.c_double), ("drain_ms", ctypes.c_double),
+        ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64), ("pieces", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -123,6 +134,9 @@ def lib():
         "pbs_didx_size": ([sz], sz),
         "pbs_didx_build": ([p, p, sz, p, ctypes.c_int64, p, sz, p], i),
         "pbs_known_chunks_device": ([p, sz, p, sz, p, ctypes.POINTER(sz), p], i),
+        "pbs_pipeline_host": ([sz, p, sz, sz, p, sz, i, p, p, sz, ctypes.POINTER(sz),
+                               ctypes.POINTER(PipelineTiming)], i),
+        "pbs_chunker_set_cu_count": ([p, i], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -264,6 +278,9 @@ class Chunker:
     def set_stream(self, hip_stream: int):
         self._check(lib().pbs_chunker_set_stream(self._h, ctypes.c_void_p(hip_stream)),
                     "pbs_chunker_set_stream")
+
+    def set_cu_count(self, cus: int):
+        self._check(lib().pbs_chunker_set_cu_count(self._h, cus), "pbs_chunker_set_cu_count")
 
     def reset(self):
         self._check(lib().pbs_chunker_reset(self._h), "pbs_chunker_reset")
@@ -542,3 +559,21 @@ def index_stream_device(chunker: "Chunker", dev_ptr: int, length: int, key=None,
     dig = digest_chunks_device(dev_ptr, length, bounds, base=start, key=key, hip_stream=hip_stream)
     image, csum = didx_build(ends, dig, uuid, ctime)
     return ends, dig, csum, image
+
+
+def pipeline_host(data, avg: int, piece: int = 1 << 30, key=None, digest_cus: int = 64):
+    """pbs_pipeline_host: chunk END offsets, (n, 32) digests and the timing dict of the
+    overlapped copy -> chunk -> digest path over a host buffer."""
+    a = _as_u8(data)
+    with Chunker(avg) as c:
+        cap = c.cuts_bound(a.size) + 1
+    ends = np.empty(cap, dtype=np.uint64)
+    dig = np.empty((cap, 32), dtype=np.uint8)
+    n = ctypes.c_size_t(0)
+    t = PipelineTiming()
+    kb, kl = _key_arg(key)
+    rc = lib().pbs_pipeline_host(avg, _ptr(a), a.size, piece, kb, kl, digest_cus, ends.ctypes.data,
+                                 dig.ctypes.data, cap, ctypes.byref(n), ctypes.byref(t))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_pipeline_host")
+    return ends[: n.value].copy(), dig[: n.value].copy(), t.as_dict()

@@ -165,3 +165,23 @@ def test_known_chunks(gpu, oracle, torch_dev, n, k, clash):
     ref = oracle.known_chunks(dig, known if k else [])
     got = out.cpu().numpy()
     assert np.array_equal(got, ref) and cnt == int(ref.sum())
+
+
+@pytest.mark.parametrize("kind,avg,piece,key", [
+    ("vmimage", 1 << 20, 8 << 20, None),          # chunks shorter than a piece
+    ("vmimage", 4 << 20, 5 << 20 | 3, b"k" * 32),  # 16 MiB chunks spanning pieces, keyed
+    ("random", 64 << 10, 1 << 20, None),           # many chunks per piece
+])
+def test_pipeline_host(gpu, oracle, kind, avg, piece, key):
+    """Overlapped copy -> chunk -> digest over a pageable host buffer (pbs_pipeline_host)
+    equals the oracle chunker + hashlib, with chunks straddling the copy pieces."""
+    n = 100 * MiB + 77
+    data = gen_np.gen_vmimage(n, 0x5EED0003, 0) if kind == "vmimage" else gen_np.gen_random(n, 21)
+    ends, dig, t = gpu.pipeline_host(data, avg, piece=piece, key=key, digest_cus=32)
+    ref = oracle.chunk_feed(avg, data)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    assert np.array_equal(ends, ref)
+    bounds = np.concatenate([[0], ref]).astype(np.uint64)
+    assert np.array_equal(dig, oracle.chunk_digests(data, bounds, key or b""))
+    assert t["chunks"] == ref.size and t["bytes"] == n
