@@ -308,12 +308,25 @@ class ChunkStream:
         self.chunker = Chunker(chunk_size if chunk_size is not None else 4 * 1024 * 1024)
         self.buffer = bytearray()
         self.scan_pos = 0
+        self.eof = False
+        # bytes gathered per device scan: each scan is a host->device round trip, so
+        # scanning every small read piece would be latency-bound; the cuts are those of
+        # the whole stream either way, only latency changes (0 = scan every piece)
+        self.min_scan = 4 * 1024 * 1024
 
     def __iter__(self) -> Iterator[bytes]:
         return self
 
+    def _pull(self) -> None:
+        try:
+            self.buffer += bytes(next(self.input))
+        except StopIteration:
+            self.eof = True
+
     def __next__(self) -> bytes:
         while True:
+            while not self.eof and len(self.buffer) - self.scan_pos < max(self.min_scan, 1):
+                self._pull()
             if self.scan_pos < len(self.buffer):
                 boundary = self.chunker.scan(memoryview(self.buffer)[self.scan_pos:])
                 chunk_size = self.scan_pos + boundary
@@ -326,16 +339,13 @@ class ChunkStream:
                     return result
                 else:
                     raise RuntimeError("got unexpected chunk boundary from chunker")
-            try:
-                data = next(self.input)
-            except StopIteration:
-                self.scan_pos = 0
-                if self.buffer:
-                    result = bytes(self.buffer)
-                    self.buffer = bytearray()
-                    return result
-                raise
-            self.buffer += bytes(data)
+                continue
+            self.scan_pos = 0
+            if self.buffer:
+                result = bytes(self.buffer)
+                self.buffer = bytearray()
+                return result
+            raise StopIteration
 
 
 class DynamicChunkWriter:

@@ -2,6 +2,7 @@
 // reference's callers do, and prints the chunk END offsets per caller, one line each:
 //   scan <ends...>      Chunker::scan loop of test_chunker1's test2 (chunker.rs:246-257)
 //   stream <ends...>    ChunkStream over pieces of `piece` bytes (chunk_stream.rs:40-77)
+//   stream0 <ends...>   the same, scanning every piece as it arrives (min_scan 0)
 //   writer <ends...>    DynamicChunkWriter via write_all (dynamic_index.rs:493-515)
 //   batch <ends...>     find_cuts(is_final)
 //   index <csum hex>    DynamicIndexWriter over the writer's chunks (host SHA-256
@@ -49,7 +50,7 @@ int main(int argc, char** argv) {
             }
             print("scan", ends);
         }
-        {
+        for (size_t min_scan : {(size_t)0, (size_t)4 << 20}) {
             size_t off = 0;
             pbs::ChunkStream s([&](std::vector<uint8_t>& out) {
                 if (off >= len) return false;
@@ -58,13 +59,14 @@ int main(int argc, char** argv) {
                 off += n;
                 return true;
             }, avg);
+            s.set_min_scan(min_scan);
             std::vector<uint64_t> ends;
             uint64_t total = 0;
             while (auto ch = s.next()) {
                 total += ch->size();
                 ends.push_back(total);
             }
-            print("stream", ends);
+            print(min_scan ? "stream" : "stream0", ends);
         }
         {
             std::vector<uint64_t> ends;

@@ -99,9 +99,11 @@ def test_chunk_stream_logic(monkeypatch, pbschunk, oracle):
     _patch_chunker(monkeypatch, pbschunk, oracle)
     data = oracle.gen_random(3 * MiB + 17, 21)
     ref = oracle.chunk_feed(64 * KiB, data)
-    for piece in (1000, 64 * KiB, 256 * KiB):
+    for piece, min_scan in ((1000, 0), (1000, 300 * KiB), (64 * KiB, 4 * MiB), (256 * KiB, 0), (256 * KiB, 1)):
         pieces = [data[i:i + piece].tobytes() for i in range(0, data.size, piece)]
-        chunks = list(pbschunk.ChunkStream(pieces, 64 * KiB))
+        cs = pbschunk.ChunkStream(pieces, 64 * KiB)
+        cs.min_scan = min_scan  # coalescing pieces per scan must not move a cut
+        chunks = list(cs)
         ends = np.cumsum([len(c) for c in chunks])
         assert b"".join(chunks) == data.tobytes()
         assert np.array_equal(ends[:-1], ref) or np.array_equal(ends, ref)

@@ -293,11 +293,14 @@ def test_test_chunk_speed_loop(gpu, oracle):
                 pos += k
 
 
-def test_chunk_stream_and_writer(gpu, oracle):
+@pytest.mark.parametrize("min_scan", [0, 4 * MiB])
+def test_chunk_stream_and_writer(gpu, oracle, min_scan):
     data = gen_np.gen_vmimage(20 * MiB + 5, 0x5EED0003, 510 * MiB)
     ref = oracle.chunk_feed(1 * MiB, data)
     pieces = [data[i:i + 256 * KiB].tobytes() for i in range(0, data.size, 256 * KiB)]
-    chunks = list(gpu.ChunkStream(pieces, 1 * MiB))
+    cs = gpu.ChunkStream(pieces, 1 * MiB)
+    cs.min_scan = min_scan
+    chunks = list(cs)
     ends = np.cumsum([len(ch) for ch in chunks])
     assert b"".join(chunks) == data.tobytes()
     assert np.array_equal(ends[:-1], ref) and ends[-1] == data.size

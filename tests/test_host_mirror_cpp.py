@@ -39,7 +39,7 @@ def test_host_mirror_matches_oracle(tmp_path, gpu, oracle, avg, n, piece):
     data = oracle.gen_random(n, 7)
     ref = oracle.chunk_feed(avg, data).tolist()
     assert [int(x) for x in lines["scan"]] == ref
-    for tag in ("stream", "writer", "batch"):
+    for tag in ("stream", "stream0", "writer", "batch"):
         ends = [int(x) for x in lines[tag]]
         assert ends[:-1] == ref and ends[-1] == n, tag
     assert "not a power of two" in " ".join(lines["badavg"])
