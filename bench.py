@@ -170,12 +170,61 @@ def digest_stage(args, buf, cuts, stream, reps: int = 3):
     [x.start() for x in ths]
     [x.join() for x in ths]
     cpu_gib_s = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
+    crc = crc_stage(args, buf, bd, od, n, bounds, take, threads, stream, reps)
     return {"metric": "GiB/s SHA-256 digested (per chunk, device-resident)",
             "value": round(size / (1 << 30) / t, 3), "ms": round(t * 1e3, 3), "chunks": n,
             "max_chunk": int(lens.max()), "bound": "valu (one lane per chunk; serial per chunk)",
             "known_chunks": nknown, "known_ms": round(known_ms, 3),
             "cpu_baseline": {"value": round(cpu_gib_s, 3), "unit": "GiB/s", "cores": threads,
                              "kind": "hashlib (OpenSSL)",
+                             "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"},
+            "blob_crc": crc}
+
+
+def crc_stage(args, buf, bd, od, n, bounds, take, threads, stream, reps):
+    """SURVEY 8(f) rank 4: DataBlob::compute_crc (CRC-32) of every chunk on the device
+    (256 lanes per chunk, HBM-bound), HIP events on the launch stream; zlib.crc32 (the
+    same CRC-32) on the host cores over the digest stage's sample."""
+    import zlib
+
+    import torch
+
+    import pbschunk
+
+    size = buf.numel()
+    out = torch.empty(n, dtype=torch.int32, device=buf.device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    pbschunk.crc32_chunks_async(buf.data_ptr(), size, bd.data_ptr(), od.data_ptr(), n, out.data_ptr(),
+                                hip_stream=stream.cuda_stream)  # warm-up
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(reps):
+        ev[0].record(stream)
+        pbschunk.crc32_chunks_async(buf.data_ptr(), size, bd.data_ptr(), od.data_ptr(), n, out.data_ptr(),
+                                    hip_stream=stream.cuda_stream)
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        ms.append(ev[0].elapsed_time(ev[1]))
+    t = min(ms) / 1e3
+    host = buf[: int(bounds[take])].cpu().numpy()
+    mv = memoryview(host)
+    parts = [list(range(k, take, threads)) for k in range(threads)]
+
+    def work(ix):
+        for i in ix:
+            zlib.crc32(mv[int(bounds[i]):int(bounds[i + 1])])
+
+    ths = [threading.Thread(target=work, args=(ix,)) for ix in parts]
+    t0 = time.perf_counter()
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    cpu = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
+    return {"metric": "GiB/s blob CRC-32 (per chunk, device-resident)",
+            "value": round(size / (1 << 30) / t, 3), "ms": round(t * 1e3, 3),
+            "roofline": {"bound": "hbm", "achieved": round(size / t / 1e9, 1), "peak": 8000.0,
+                         "unit": "GB/s", "frac": round(size / t / 8e12, 4)},
+            "cpu_baseline": {"value": round(cpu, 3), "unit": "GiB/s", "cores": threads,
+                             "kind": "zlib.crc32 (same CRC-32 as crc32fast)",
                              "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"}}
 
 

@@ -1,0 +1,58 @@
+/*
+ * pbs_blob.h -- C ABI of the per-chunk blob CRC stage (SURVEY.md section 8(f) rank 4:
+ * the client-side per-chunk work after the digest).
+ *
+ * Reference interfaces replaced:
+ *  - `DataBlob::compute_crc` (pbs-datastore/src/data_blob.rs:70-75):
+ *    crc32fast::Hasher over the blob payload -- the chunk bytes for an uncompressed blob,
+ *    set by `DataBlob::encode` (data_blob.rs:87-179; set_crc :64-67) and checked by
+ *    `DataBlob::verify_crc` (:78-84) on every load/verify.  crc32fast (Cargo.toml:111,
+ *    "1") computes CRC-32/ISO-HDLC: reflected polynomial 0xEDB88320, init and final
+ *    XOR 0xFFFFFFFF -- the same function as zlib's crc32.
+ *  - the uncompressed blob layout (pbs-datastore/src/file_formats.rs:9 and :36-45):
+ *    magic UNCOMPRESSED_BLOB_MAGIC_1_0 (8 bytes) || crc (u32 LE) || data.
+ *
+ * Chunk i of a stream is [bounds[i], bounds[i+1]) in absolute stream offsets, as in
+ * pbs_digest.h.
+ */
+#ifndef PBS_BLOB_H
+#define PBS_BLOB_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBS_BLOB_HEADER_SIZE 12 /* DataBlobHeader: magic[8] + crc[4] */
+
+/* CRC-32 of every chunk on the GPU.  `dev_data` (device) holds stream bytes
+ * [base, base + data_len); `bounds` (host, n + 1 ascending absolute offsets); writes n
+ * CRCs to host `crcs` (chunk order).  Synchronous.  Returns PBS_OK or PBS_ERR_*. */
+int pbs_crc32_chunks_device(const uint8_t *dev_data, size_t data_len, uint64_t base,
+                            const uint64_t *bounds, size_t n, uint32_t *crcs, void *hip_stream);
+
+/* Device-only, asynchronous form: `bounds_dev` (n + 1 offsets), `order_dev` (NULL or a
+ * permutation of 0..n-1; workgroup k takes chunk order_dev[k] -- longest first balances
+ * the tail), `crcs_dev` (n u32) are device memory. */
+int pbs_crc32_chunks_async(const uint8_t *dev_data, size_t data_len, uint64_t base,
+                           const uint64_t *bounds_dev, const uint32_t *order_dev, size_t n,
+                           uint32_t *crcs_dev, void *hip_stream);
+
+/* Host CRC-32 (crc32fast::Hasher::update/finalize): continue `crc` (0 to start) over
+ * `data`. */
+uint32_t pbs_crc32(uint32_t crc, const uint8_t *data, size_t len);
+
+/* Uncompressed DataBlob image of `data` with its precomputed CRC (from
+ * pbs_crc32_chunks_*): magic || crc LE || data into `out` (cap >= len + 12).  Returns
+ * the bytes written (len + 12) or 0 if `cap` is too small or len exceeds MAX_BLOB_SIZE
+ * (128 MiB, data_blob.rs:13 / :92). */
+size_t pbs_blob_encode_uncompressed(const uint8_t *data, size_t len, uint32_t crc, uint8_t *out,
+                                    size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PBS_BLOB_H */

@@ -187,3 +187,29 @@ def known_chunks(digests, known) -> np.ndarray:
         else:
             seen.add(b)
     return out
+
+
+# ---- the blob CRC (checker only) --------------------------------
+# DataBlob::compute_crc (data_blob.rs:70-75) is crc32fast::Hasher (Cargo.toml:111,
+# crc32fast "1"), whose published algorithm is CRC-32/ISO-HDLC: reflected polynomial
+# 0xEDB88320, init 0xFFFFFFFF, final XOR 0xFFFFFFFF, check value CRC("123456789") =
+# 0xCBF43926 -- the same function as zlib.crc32 (crc32fast's own tests compare against
+# it).  An uncompressed blob is UNCOMPRESSED_BLOB_MAGIC_1_0 || crc LE || data
+# (file_formats.rs:9, :36-45; data_blob.rs:159-174).
+
+UNCOMPRESSED_BLOB_MAGIC = bytes([66, 171, 56, 7, 190, 131, 112, 161])  # file_formats.rs:9
+
+
+def chunk_crcs(data: np.ndarray, bounds) -> np.ndarray:
+    import zlib
+
+    b = [int(x) for x in bounds]
+    mv = memoryview(np.ascontiguousarray(data))
+    return np.array([zlib.crc32(mv[b[i]:b[i + 1]]) for i in range(len(b) - 1)], dtype=np.uint32)
+
+
+def blob_uncompressed(chunk: bytes) -> bytes:
+    import struct
+    import zlib
+
+    return UNCOMPRESSED_BLOB_MAGIC + struct.pack("<I", zlib.crc32(chunk)) + bytes(chunk)

@@ -52,6 +52,8 @@ EXPORTED_SYMBOLS = (
     # include/pbs_digest.h (chunk digests, dynamic index)
     "pbs_digest_chunks_device", "pbs_digest_chunks_async", "pbs_sha256", "pbs_didx_size",
     "pbs_didx_build", "pbs_known_chunks_device", "pbs_pipeline_host", "pbs_chunker_set_cu_count",
+    # include/pbs_blob.h (blob CRC)
+    "pbs_crc32_chunks_device", "pbs_crc32_chunks_async", "pbs_crc32", "pbs_blob_encode_uncompressed",
 )
 
 
@@ -137,6 +139,10 @@ def lib():
         "pbs_pipeline_host": ([sz, p, sz, sz, p, sz, i, p, p, sz, ctypes.POINTER(sz),
                                ctypes.POINTER(PipelineTiming)], i),
         "pbs_chunker_set_cu_count": ([p, i], i),
+        "pbs_crc32_chunks_device": ([p, sz, u64, p, sz, p, p], i),
+        "pbs_crc32_chunks_async": ([p, sz, u64, p, p, sz, p, p], i),
+        "pbs_crc32": ([ctypes.c_uint32, p, sz], ctypes.c_uint32),
+        "pbs_blob_encode_uncompressed": ([p, sz, ctypes.c_uint32, p, sz], sz),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -470,6 +476,52 @@ def digest_chunks_async(dev_ptr: int, data_len: int, bounds_dev: int, order_dev:
                                        ctypes.c_void_p(hip_stream))
     if rc != PBS_OK:
         raise ChunkerError(rc, "pbs_digest_chunks_async")
+
+
+def crc32(data, crc: int = 0) -> int:
+    """Host CRC-32 of the C library (crc32fast::Hasher: continue ``crc`` over data)."""
+    a = _as_u8(data)
+    return int(lib().pbs_crc32(crc, _ptr(a), a.size))
+
+
+def crc32_chunks_device(dev_ptr: int, data_len: int, bounds, base: int = 0, hip_stream: int = 0) -> np.ndarray:
+    """DataBlob::compute_crc (data_blob.rs:70-75) on the GPU for every chunk
+    [bounds[i], bounds[i+1]) of the stream whose bytes [base, base + data_len) are at
+    device address dev_ptr; uint32 CRCs in chunk order."""
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.uint64))
+    n = max(0, b.size - 1)
+    out = np.empty(n, dtype=np.uint32)
+    if n == 0:
+        return out
+    rc = lib().pbs_crc32_chunks_device(ctypes.c_void_p(dev_ptr), data_len, base, b.ctypes.data, n,
+                                       out.ctypes.data, ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_crc32_chunks_device")
+    return out
+
+
+def crc32_chunks_async(dev_ptr: int, data_len: int, bounds_dev: int, order_dev: int, n: int, crcs_dev: int,
+                       base: int = 0, hip_stream: int = 0):
+    """Device-only form (all pointers device memory; order_dev may be 0)."""
+    rc = lib().pbs_crc32_chunks_async(ctypes.c_void_p(dev_ptr), data_len, base, ctypes.c_void_p(bounds_dev),
+                                      ctypes.c_void_p(order_dev or None), n, ctypes.c_void_p(crcs_dev),
+                                      ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_crc32_chunks_async")
+
+
+UNCOMPRESSED_BLOB_MAGIC_1_0 = bytes([66, 171, 56, 7, 190, 131, 112, 161])  # file_formats.rs:9
+
+
+def blob_encode_uncompressed(data, crc: int) -> bytes:
+    """DataBlob::encode(data, None, compress=false) (data_blob.rs:159-174) with the CRC
+    from crc32_chunks_device: magic || crc LE || data."""
+    a = _as_u8(data)
+    out = np.empty(a.size + 12, dtype=np.uint8)
+    n = lib().pbs_blob_encode_uncompressed(_ptr(a), a.size, crc, out.ctypes.data, out.size)
+    if n != a.size + 12:
+        raise ValueError(f"data blob too large ({a.size} bytes).")
+    return out.tobytes()
 
 
 def known_chunks_device(digests_dev: int, n: int, known_dev: int, k: int, is_known_dev: int,

@@ -1,7 +1,4 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/examples; export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_examples.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_examples.log 2>&1 && \
-timeout -k 10 200 examples/test_chunk_speed > gpurun_out/examples/test_chunk_speed.txt 2>&1 && \
-timeout -k 10 200 examples/test_chunk_speed2 > gpurun_out/examples/test_chunk_speed2.txt 2>&1 && \
-timeout -k 10 200 examples/test_chunk_size > gpurun_out/examples/test_chunk_size.txt 2>&1
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/blob; export TMPDIR=/tmp
+timeout -k 10 500 python bench.py --steps 2 --warmup 1 --cpu-baseline 0 --host-inclusive-gib 0 --digest 1 > gpurun_out/blob/bench_digest.log 2>&1
 echo rc=$?
