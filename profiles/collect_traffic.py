@@ -20,6 +20,7 @@ ap.add_argument("pmc_dir")
 ap.add_argument("--size-gib", type=float, default=64.0)
 ap.add_argument("--avg", type=int, default=4 * 1024 * 1024)
 ap.add_argument("--workload", default="vmimage")
+ap.add_argument("--kernel", default="scan_main_kernel", help="kernel-name substring (e.g. crc32_chunks_kernel)")
 ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "traffic_latest.json"))
 a = ap.parse_args()
 
@@ -27,13 +28,13 @@ files = glob.glob(os.path.join(a.pmc_dir, "**", "*counter_collection.csv"), recu
 per_dispatch = {}
 for f in files:
     for row in csv.DictReader(open(f)):
-        if "scan_main_kernel" not in row.get("Kernel_Name", "") or row.get("Counter_Name") != "FETCH_SIZE":
+        if a.kernel not in row.get("Kernel_Name", "") or row.get("Counter_Name") != "FETCH_SIZE":
             continue
         key = (f, row.get("Dispatch_Id"))
         per_dispatch[key] = per_dispatch.get(key, 0.0) + float(row["Counter_Value"])
 vals = sorted(per_dispatch.values())
 if not vals:
-    raise SystemExit("no scan_main_kernel FETCH_SIZE rows found")
+    raise SystemExit(f"no {a.kernel} FETCH_SIZE rows found")
 kib = statistics.median(vals)
 size = int(a.size_gib * (1 << 30)) // 8 * 8
 out = {"size": size, "avg": a.avg, "workload": a.workload, "dispatches": len(vals),
