@@ -172,14 +172,19 @@ __global__ __launch_bounds__(64) void sha256_chunks_kernel(const uint8_t* __rest
 
 // Two-wave form: the message schedule (48 sigma steps + K[t] per block, the data loads,
 // the tail/padding blocks) runs in wave 1 one block ahead of the 64 rounds in wave 0,
-// handed over through a double-buffered LDS array W[2][64 t][64 lanes] (lane-minor:
-// conflict-free); one s_barrier per block.  The rounds' wave is the critical path:
+// handed over through a double-buffered LDS array W[2][16][64 lanes] of 4-word groups
+// (one ds_write_b128 / ds_read_b128 per 4 rounds, lane-minor: conflict-free); one
+// s_barrier per block.  The producer loads block b + 1's data while it schedules
+// block b, so no HBM latency sits on the per-block critical path.  The rounds' wave is the critical path:
 // ~960 instructions per block instead of ~1420 for one wave doing both.
 constexpr int kShaWaves = 2;
+#ifdef PBS_SHA_PROBE
+__device__ uint64_t g_sha_probe[5];
+#endif
 __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint32_t* __restrict__ order, uint64_t n, DigestKey key, uint8_t* __restrict__ digests) {
-    __shared__ uint32_t sw[2][64][64];  // [buffer][t][lane]: W[t] + K[t]
+    __shared__ uint4 sw[2][16][64];  // [buffer][t / 4][lane]: W[t] + K[t] for 4 t (b128 per lane)
     __shared__ uint32_t s_blocks;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t k = (uint64_t)blockIdx.x * 64 + lane;
@@ -206,12 +211,18 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
     const uint64_t bits = (len + kl) * 8ull;
     const uint8_t* tp = p + (nfull << 6);
 
-    // wave 1: message block b -> W + K into buffer b & 1
+    // wave 1: message block b -> W + K into buffer b & 1.  The data window of block b
+    // was loaded during the previous block's period (`pre`); the loads of block b + 1
+    // are issued here, before the schedule, so HBM latency hides behind a block period.
+    uint32_t pre[17];
+    if (wave == 1 && nfull) load_window(pa, r != 0, pre);
     auto produce = [&](uint32_t b) {
         uint32_t w[16];
         if ((uint64_t)b < nfull) {
             uint32_t d[17];
-            load_window(pa + 16 * (uint64_t)b, r != 0, d);
+#pragma unroll
+            for (int q = 0; q < 17; ++q) d[q] = pre[q];
+            if ((uint64_t)b + 1 < nfull) load_window(pa + 16 * ((uint64_t)b + 1), r != 0, pre);
 #pragma unroll
             for (int q = 0; q < 16; ++q) w[q] = __builtin_amdgcn_perm(d[q + 1], d[q], sel);
         } else if ((uint64_t)b < total) {
@@ -241,7 +252,8 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
 #pragma unroll
             for (int q = 0; q < 16; ++q) w[q] = 0;
         }
-        uint32_t (*out)[64] = sw[b & 1];
+        uint4 (*out)[64] = sw[b & 1];
+        uint32_t o[4];
 #pragma unroll
         for (int t = 0; t < 64; ++t) {
             uint32_t wt;
@@ -254,7 +266,8 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
                 wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
                 w[t & 15] = wt;
             }
-            out[t][lane] = wt + kK[t];
+            o[t & 3] = wt + kK[t];
+            if ((t & 3) == 3) out[t >> 2][lane] = make_uint4(o[0], o[1], o[2], o[3]);
         }
     };
 
@@ -262,17 +275,26 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
                       0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     if (wave == 1 && nblocks) produce(0);
     __syncthreads();
+#ifdef PBS_SHA_PROBE  // scripts/microbench/mb_sha.hip: cycles of each wave's work vs the barrier
+    uint64_t pr_work = 0, pr_wait = 0;
+#endif
     for (uint32_t b = 0; b < nblocks; ++b) {
+#ifdef PBS_SHA_PROBE
+        const uint64_t c0 = clock64();
+#endif
         if (wave == 1) {
             if (b + 1 < nblocks) produce(b + 1);
         } else if ((uint64_t)b < total) {
-            const uint32_t (*in)[64] = sw[b & 1];
+            const uint4 (*in)[64] = sw[b & 1];
             uint32_t a = st[0], bb = st[1], c = st[2], d = st[3], ee = st[4], f = st[5], g = st[6], h = st[7];
+            uint4 kw4 = in[0][lane];
 #pragma unroll
             for (int t = 0; t < 64; ++t) {
+                const uint32_t kw = (t & 3) == 0 ? kw4.x : (t & 3) == 1 ? kw4.y : (t & 3) == 2 ? kw4.z : kw4.w;
+                if ((t & 3) == 3 && t < 63) kw4 = in[(t >> 2) + 1][lane];
                 const uint32_t S1 = xor3(rotr(ee, 6), rotr(ee, 11), rotr(ee, 25));
                 const uint32_t ch = __builtin_amdgcn_bitop3_b32(ee, f, g, 0xCA);
-                const uint32_t t1 = h + S1 + ch + in[t][lane];
+                const uint32_t t1 = h + S1 + ch + kw;
                 const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
                 const uint32_t maj = __builtin_amdgcn_bitop3_b32(a, bb, c, 0xE8);
                 h = g;
@@ -293,8 +315,22 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
             st[6] += g;
             st[7] += h;
         }
+#ifdef PBS_SHA_PROBE
+        const uint64_t c1 = clock64();
         __syncthreads();
+        pr_work += c1 - c0;
+        pr_wait += clock64() - c1;
+#else
+        __syncthreads();
+#endif
     }
+#ifdef PBS_SHA_PROBE
+    if (blockIdx.x == 0 && lane == 0) {
+        g_sha_probe[wave * 2] = pr_work;
+        g_sha_probe[wave * 2 + 1] = pr_wait;
+        g_sha_probe[4] = nblocks;
+    }
+#endif
     if (wave == 0 && live) {
         uint32_t* out = reinterpret_cast<uint32_t*>(digests + 32 * i);
 #pragma unroll

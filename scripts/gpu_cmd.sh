@@ -1,4 +1,4 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/blob; export TMPDIR=/tmp
-timeout -k 10 500 python bench.py --steps 2 --warmup 1 --cpu-baseline 0 --host-inclusive-gib 0 --digest 1 > gpurun_out/blob/bench_digest.log 2>&1
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/sha; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_digest.py tests/test_gpu_blob.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/sha/pytest.log 2>&1
 echo rc=$?
