@@ -165,12 +165,13 @@ uint64_t batch_max(const Params& p) {
 struct ScanPlan {
     uint64_t ntiles = 0, ext_first = 0, ext_count = 0, blocks = 0;
     int seg = 0, head = 0;
+    bool dyn = false;  // dynamic tile order (scan_main_plan)
 };
 
 ScanPlan plan_scan(pbs_chunker* c, uint64_t len) {
     const Params& p = c->prm;
     ScanPlan sp;
-    sp.seg = scan_main_plan(len, c->cu, &sp.ntiles);
+    sp.seg = scan_main_plan(len, c->cu, &sp.ntiles, &sp.dyn);
     const uint64_t covered = sp.ntiles * 64ull * (uint64_t)sp.seg;
     sp.head = sp.ntiles > 0 ? 1 : 0;
     sp.ext_first = covered / kBlockBytes;
@@ -201,7 +202,8 @@ int scan_launch(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t ba
     uint32_t* d_ncand = d_nsusp + 1;
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, launch_scan_main(d_data, sp.ntiles, sp.seg, c->d_table.as<uint32_t>(), p.thr,
-                                c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu, c->stream));
+                                c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu, c->stream,
+                                d_nsusp + 2, sp.dyn));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     const uint64_t max_items = (uint64_t)c->susp_cap + 1 + sp.ext_count;
     HIP_TRY(c, launch_scan_exact(d_data, len, c->d_pre.as<uint8_t>(), c->carry_len,

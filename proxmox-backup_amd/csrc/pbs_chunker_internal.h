@@ -28,10 +28,11 @@ struct ResolveParams {
 
 // Segment bytes per lane for a scan of `len` bytes (a wave tile = 64 segments) and
 // the number of full wave tiles; bytes past ntiles*64*seg are the tail.
-int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles);
+int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn);
 hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
-                            uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream);
+                            uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream,
+                            uint32_t* tile_ctr = nullptr, bool dynamic = false);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
                              uint32_t pre_len, const uint64_t* susp, const uint32_t* nsusp,
                              uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head,

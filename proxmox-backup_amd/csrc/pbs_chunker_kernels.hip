@@ -909,51 +909,70 @@ __global__ __launch_bounds__(256) void gen_kernel(uint64_t* __restrict__ out, ui
 // ---------------------------------------------------------------------------------
 // Host-side launchers (called from pbs_chunker_capi.cpp)
 // ---------------------------------------------------------------------------------
-int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles) {
-    // largest segment that still gives every wave >= 2 tiles (load balance); the
-    // 128-byte warm-up per segment costs 128/SEG of the work and traffic
+int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn) {
+    // Tile order: dynamic (waves draw tiles from a counter, so waves on faster CUs take
+    // more) once every wave gets >= 16 tiles of 16 KiB segments; measured same-process
+    // A/B on MI355X (scripts/ab_dyn.py, profiles/r01/dyn/): 64 GiB 11.13 -> 10.55 ms
+    // (static 32 KiB -> dynamic 16 KiB), 64 GiB at 256 KiB 11.85 -> 11.02; at 1-8 GiB
+    // (2-4 tiles per wave) static is 2-3 % faster.  Static: the largest segment that
+    // still gives every wave >= 2 tiles; the 128-byte warm-up per segment costs 128/SEG
+    // of the work and traffic.
     const uint64_t waves = (uint64_t)cu * kWavesPerWG;
-    int seg = 4096;
-    int cap = 32768;  // PBS_MAX_SEG: experiment knob (segment-length sweeps)
+    int cap = 32768;  // PBS_MAX_SEG / PBS_SCAN_DYN: experiment knobs (A/B sweeps)
     if (const char* e = std::getenv("PBS_MAX_SEG")) cap = std::atoi(e);
-    for (int s : {32768, 16384, 8192}) {
-        if (s <= cap && len / (64ull * s) >= 2 * waves) {
-            seg = s;
-            break;
+    bool d = len / (64ull * 16384) >= 16 * waves;
+    if (const char* e = std::getenv("PBS_SCAN_DYN")) d = e[0] == '1';
+    int seg = 0;
+    if (d) {
+        for (int s : {16384, 8192})
+            if (s <= cap && len / (64ull * s) >= 2 * waves) {
+                seg = s;
+                break;
+            }
+    }
+    if (seg == 0) {
+        d = false;
+        seg = 4096;
+        for (int s : {32768, 16384, 8192}) {
+            if (s <= cap && len / (64ull * s) >= 2 * waves) {
+                seg = s;
+                break;
+            }
         }
     }
+    *dyn = d;
     *ntiles = len / (64ull * seg);
     return seg;
 }
 
 hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
-                            uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream) {
+                            uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream,
+                            uint32_t* tile_ctr, bool dynamic) {
     if (ntiles == 0) return hipSuccess;
     (void)hipGetLastError();  // launch errors below must not be confused with stale ones
     const uint64_t need = (ntiles + kWavesPerWG - 1) / kWavesPerWG;
     const int g = (uint64_t)grid < need ? grid : (int)need;
     const dim3 gd(g), bd(kWavesPerWG * 64);
+    const bool dyn = tile_ctr && dynamic;  // tile_ctr: a zeroed device counter
+#define PBS_SCAN_CASE(S)                                                                          \
+    case S:                                                                                       \
+        if (dyn)                                                                                  \
+            hipLaunchKernelGGL((scan_main_kernel<S, kModeFull, 2, 4, 0, 0, kScanFrame, 1>), gd, bd, 0, \
+                               stream, data, ntiles, table_rot, thr, susp, nsusp, cap, tile_ctr);   \
+        else                                                                                      \
+            hipLaunchKernelGGL((scan_main_kernel<S, kModeFull, 2, 4, 0, 0, kScanFrame, 0>), gd, bd, 0, \
+                               stream, data, ntiles, table_rot, thr, susp, nsusp, cap, nullptr);    \
+        break;
     switch (seg) {
-        case 32768:
-            hipLaunchKernelGGL((scan_main_kernel<32768, kModeFull, 2, 4, 0, 0, kScanFrame>), gd, bd, 0, stream, data, ntiles,
-                               table_rot, thr, susp, nsusp, cap);
-            break;
-        case 16384:
-            hipLaunchKernelGGL((scan_main_kernel<16384, kModeFull, 2, 4, 0, 0, kScanFrame>), gd, bd, 0, stream, data, ntiles,
-                               table_rot, thr, susp, nsusp, cap);
-            break;
-        case 8192:
-            hipLaunchKernelGGL((scan_main_kernel<8192, kModeFull, 2, 4, 0, 0, kScanFrame>), gd, bd, 0, stream, data, ntiles,
-                               table_rot, thr, susp, nsusp, cap);
-            break;
-        case 4096:
-            hipLaunchKernelGGL((scan_main_kernel<4096, kModeFull, 2, 4, 0, 0, kScanFrame>), gd, bd, 0, stream, data, ntiles,
-                               table_rot, thr, susp, nsusp, cap);
-            break;
+        PBS_SCAN_CASE(32768)
+        PBS_SCAN_CASE(16384)
+        PBS_SCAN_CASE(8192)
+        PBS_SCAN_CASE(4096)
         default:
             return hipErrorInvalidValue;
     }
+#undef PBS_SCAN_CASE
     return hipGetLastError();
 }
 

@@ -54,10 +54,16 @@ __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
 // interleaved 32x per 256-byte row, thr = the screening threshold of DESIGN.md section 6
 // (a necessary condition; scan_exact re-tests exactly): faster hash-only (7.7-8.0 vs
 // 7.2 TB/s) but 2-4 % slower in the full, power-limited kernel (profiles/r01/fr2/).
-template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int ZS = 0, int FR = 1>
+// DYN (tile order): 0 = static, wave w takes tiles w, w + nw, ...; 1 = the first nw tiles
+// static, then each wave takes its next tile from a device counter (one atomic per
+// 2 MiB tile, issued at the tile's first iteration, read at its last), so waves on
+// faster CUs take more tiles.
+template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int ZS = 0, int FR = 1,
+          int DYN = 0>
 __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
-    uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap) {
+    uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap,
+    uint32_t* __restrict__ tile_ctr = nullptr) {
     static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
     constexpr int NW = kWavesPerWG;
     // + 256 B per wave: landing area of the L2 "touch" DMAs (PF > 0)
@@ -127,8 +133,18 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     for (int r = 0; r < 128; ++r) ring[r] = 0;
     uint32_t h = 0;
     bool canon = false;  // ZS: lane state is {h = 0, ring = T'[0]} (last block all zero)
+    uint32_t dyn_v = 0;  // DYN: counter value drawn for the tile after this one
+    auto next_tile = [&]() -> uint64_t {
+        if constexpr (DYN != 0)
+            return nw + (uint64_t)__builtin_amdgcn_readfirstlane(dyn_v);
+        else
+            return tile + nw;
+    };
     issue(tile, 0);
     for (;;) {
+        if constexpr (DYN != 0) {
+            if (lane == 0) dyn_v = atomicAdd(tile_ctr, 1u);
+        }
         for (int it = 0; it < NIT; ++it) {
             if (PF > 0 && it + PF < NIT)
                 asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // the touch may stay in flight
@@ -148,7 +164,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
                 uint64_t nt = tile;
                 int nit = it + 1;
                 if (nit == NIT) {
-                    nt = tile + nw;
+                    nt = next_tile();
                     nit = 0;
                 }
                 if (MODE != kModeComputeOnly && nt < ntiles) issue(nt, nit);
@@ -201,7 +217,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
                 }
             }
         }
-        tile += nw;
+        tile = next_tile();
         if (tile >= ntiles) break;
     }
 }

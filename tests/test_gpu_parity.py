@@ -347,13 +347,20 @@ def _oracle_two_phase_parallel(oracle, data: np.ndarray, avg: int, threads: int 
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("gib,kind,avg", [(8, 1, 4 * MiB), (6, 2, 256 * KiB), (3, 1, 64 * KiB)],
-                         ids=["config2-8GiB-random-4M", "6GiB-vm-256K", "3GiB-random-64K"])
-def test_full_size_in_hbm(gpu, oracle, gib, kind, avg):
-    """BASELINE config 2 (8 GiB random already in HBM, 4 MiB average) and two sizes that
-    select the other scan_main segment lengths (16 KiB, 8 KiB): the full cut list is
-    diffed against the (multi-threaded two-phase) oracle."""
+@pytest.mark.parametrize("gib,kind,avg,dyn", [(8, 1, 4 * MiB, None), (6, 2, 256 * KiB, None),
+                                             (3, 1, 64 * KiB, None), (64, 2, 4 * MiB, None),
+                                             (6, 2, 4 * MiB, "1"), (3, 1, 64 * KiB, "1")],
+                         ids=["config2-8GiB-random-4M", "6GiB-vm-256K", "3GiB-random-64K",
+                              "config3-64GiB-vm-4M", "6GiB-vm-4M-dynamic", "3GiB-random-64K-dynamic"])
+def test_full_size_in_hbm(gpu, oracle, monkeypatch, gib, kind, avg, dyn):
+    """BASELINE config 2 (8 GiB random already in HBM, 4 MiB average), the headline
+    config 3 (64 GiB VM image, 4 MiB: 16 KiB segments in the dynamic tile order), and
+    sizes that select the other scan_main segment lengths (16 KiB, 8 KiB) in both tile
+    orders (PBS_SCAN_DYN forces the dynamic one): the full cut list is diffed against
+    the (multi-threaded two-phase) oracle."""
     import torch
+    if dyn is not None:
+        monkeypatch.setenv("PBS_SCAN_DYN", dyn)
     n = gib * GiB
     seed = 0x5EED0002 if kind == 1 else 0x5EED0003
     dev = torch.empty(n, dtype=torch.uint8, device="cuda")
