@@ -913,8 +913,9 @@ int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn) {
     // Tile order: dynamic (waves draw tiles from a counter, so waves on faster CUs take
     // more) once every wave gets >= 16 tiles of 16 KiB segments; measured same-process
     // A/B on MI355X (scripts/ab_dyn.py, profiles/r01/dyn/): 64 GiB 11.13 -> 10.55 ms
-    // (static 32 KiB -> dynamic 16 KiB), 64 GiB at 256 KiB 11.85 -> 11.02; at 1-8 GiB
-    // (2-4 tiles per wave) static is 2-3 % faster.  Static: the largest segment that
+    // (static 32 KiB -> dynamic 16 KiB; 10.92 -> 10.66 on another box, where dynamic
+    // 8 KiB / 4 KiB took 10.86 / 11.26: more warm-up re-reads), 64 GiB at 256 KiB
+    // 11.85 -> 11.02; at 1-8 GiB (2-4 tiles per wave) static is 2-3 % faster.  Static: the largest segment that
     // still gives every wave >= 2 tiles; the 128-byte warm-up per segment costs 128/SEG
     // of the work and traffic.
     const uint64_t waves = (uint64_t)cu * kWavesPerWG;
