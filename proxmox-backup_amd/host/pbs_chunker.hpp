@@ -7,6 +7,8 @@
 //   pbs::DynamicIndexWriter pbs-datastore/src/dynamic_index.rs:297-391 (add_chunk / close)
 //   pbs::digest_chunks_device  DataChunkBuilder::digest (data_blob.rs:516-536) per chunk, GPU
 //   pbs::sha256             openssl::sha::sha256 (host; index checksum)
+//   pbs::crc32_chunks_device DataBlob::compute_crc (data_blob.rs:70-75) per chunk, GPU
+//   pbs::crc32 / pbs::blob_encode_uncompressed  crc32fast::Hasher, DataBlob::encode(.., false)
 //
 // Same names, argument meaning and error behaviour as the reference: a non-power-of-two
 // average throws std::invalid_argument with the reference's panic text; `scan` is
@@ -28,6 +30,7 @@
 #include <vector>
 
 #include "pbs_chunker.h"
+#include "pbs_blob.h"
 #include "pbs_digest.h"
 
 namespace pbs {
@@ -236,6 +239,32 @@ inline std::vector<Digest> digest_chunks_device(const uint8_t* dev, size_t len, 
                                             key.empty() ? nullptr : key.data(), key.size(),
                                             out[0].data(), hip_stream);
     if (rc != PBS_OK) throw std::runtime_error(std::string("pbs_digest_chunks_device: ") + pbs_strerror(rc));
+    return out;
+}
+
+// CRC-32 (crc32fast) of every chunk [bounds[i], bounds[i+1]) of a device-resident stream:
+// the blob CRC of an uncompressed chunk blob (DataBlob::compute_crc, data_blob.rs:70-75).
+inline std::vector<uint32_t> crc32_chunks_device(const uint8_t* dev, size_t len, uint64_t base,
+                                                 const std::vector<uint64_t>& bounds,
+                                                 void* hip_stream = nullptr) {
+    const size_t n = bounds.size() > 1 ? bounds.size() - 1 : 0;
+    std::vector<uint32_t> out(n);
+    if (!n) return out;
+    const int rc = pbs_crc32_chunks_device(dev, len, base, bounds.data(), n, out.data(), hip_stream);
+    if (rc != PBS_OK) throw std::runtime_error(std::string("pbs_crc32_chunks_device: ") + pbs_strerror(rc));
+    return out;
+}
+
+// Host CRC-32, continuable like crc32fast::Hasher::update (crc = 0 to start).
+inline uint32_t crc32(const uint8_t* data, size_t len, uint32_t crc = 0) { return pbs_crc32(crc, data, len); }
+
+// DataBlob::encode(data, None, compress = false) (data_blob.rs:159-174) with a known CRC:
+// UNCOMPRESSED_BLOB_MAGIC_1_0 || crc LE || data; throws above MAX_BLOB_SIZE like the
+// reference's bail! (data_blob.rs:92-94).
+inline std::vector<uint8_t> blob_encode_uncompressed(const uint8_t* data, size_t len, uint32_t crc) {
+    std::vector<uint8_t> out(len + PBS_BLOB_HEADER_SIZE);
+    if (pbs_blob_encode_uncompressed(data, len, crc, out.data(), out.size()) != out.size())
+        throw std::invalid_argument("data blob too large (" + std::to_string(len) + " bytes).");
     return out;
 }
 

@@ -5,6 +5,8 @@
 //   stream0 <ends...>   the same, scanning every piece as it arrives (min_scan 0)
 //   writer <ends...>    DynamicChunkWriter via write_all (dynamic_index.rs:493-515)
 //   batch <ends...>     find_cuts(is_final)
+//   crc <crcs...>       host CRC-32 of the writer's chunks (DataBlob::compute_crc)
+//   blob0 <hex>         first 16 bytes of the first chunk's uncompressed blob
 //   index <csum hex>    DynamicIndexWriter over the writer's chunks (host SHA-256
 //                       digests), written to $HOST_MIRROR_DIDX when set
 // usage: host_mirror <avg> <len> <seed> <piece>   (input: splitmix64 random stream)
@@ -72,14 +74,23 @@ int main(int argc, char** argv) {
             std::vector<uint64_t> ends;
             const char* didx = std::getenv("HOST_MIRROR_DIDX");
             pbs::DynamicIndexWriter index(didx ? didx : "/dev/null", {}, 1234);
+            std::vector<uint64_t> crcs;
+            std::vector<uint8_t> blob0;
             pbs::DynamicChunkWriter w([&](uint64_t end, const std::vector<uint8_t>& chunk) {
                 ends.push_back(end);
                 index.add_chunk(end, pbs::sha256(chunk.data(), chunk.size()));
+                crcs.push_back(pbs::crc32(chunk.data(), chunk.size()));
+                if (blob0.empty())
+                    blob0 = pbs::blob_encode_uncompressed(chunk.data(), chunk.size(), (uint32_t)crcs.back());
             }, avg);
             for (size_t off = 0; off < len; off += piece)
                 w.write_all(data.data() + off, std::min(piece, len - off));
             w.close();
             print("writer", ends);
+            print("crc", crcs);
+            std::printf("blob0 ");
+            for (size_t k = 0; k < blob0.size() && k < 16; ++k) std::printf("%02x", blob0[k]);
+            std::printf("\n");
             if (didx) {
                 const pbs::Digest csum = index.close();
                 std::printf("index ");

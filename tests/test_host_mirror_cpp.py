@@ -48,4 +48,8 @@ def test_host_mirror_matches_oracle(tmp_path, gpu, oracle, avg, n, piece):
     bounds = np.concatenate([[0], wends]).astype(np.uint64)
     ref_img, ref_csum = oracle.didx_image(wends, oracle.chunk_digests(data, bounds), bytes(16), 1234)
     assert lines["index"][0] == ref_csum.hex()
+    # host CRC-32 of the writer's chunks and the first uncompressed blob's header
+    assert [int(x) for x in lines["crc"]] == oracle.chunk_crcs(data, bounds).tolist()
+    first = data[:int(wends[0])].tobytes()
+    assert lines["blob0"][0] == oracle.blob_uncompressed(first)[:16].hex()
     assert open(didx, "rb").read() == ref_img
