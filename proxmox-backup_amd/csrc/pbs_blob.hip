@@ -20,8 +20,11 @@
 // 0xFFFFFFFF is the same as XOR-ing 0xFF into the first four message bytes, which the
 // lanes holding them do at load time (chunks shorter than 4 bytes: one lane, serially).
 // Only bytes inside [start, end) are ever read: words crossing either end are gathered
-// byte by byte.  The workgroups are persistent and stride over the chunks (longest
-// first), so the 17 KiB of tables are staged into LDS once per workgroup.
+// byte by byte.  The workgroups are persistent (the 17 KiB of tables are staged into LDS
+// once per workgroup) and take the chunks longest first: the first gridDim.x
+// statically, then each draws its next chunk from a per-stream device counter, so
+// workgroups on faster CUs take more (64 GiB / 4 MiB: 11.01 -> 10.66 ms against the
+// static stride, profiles/r01/blob/ab_crc_dynamic.log; PBS_CRC_DYN=0 restores it).
 //
 // Roofline: HBM, L bytes read per chunk; per 16 bytes one dwordx4 load, 16 ds_read_b32
 // and ~40 VALU (byte extract, address, XOR).
@@ -29,6 +32,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -102,6 +106,20 @@ const CrcTables* device_tables(int dev) {
     return d;
 }
 
+// work counter of the dynamic chunk order, one per (device, stream): launches on one
+// stream are serialized, so each can reset and use it
+unsigned long long* stream_counter(int dev, hipStream_t st) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, unsigned long long*> ctrs;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = ctrs.find({dev, st});
+    if (it != ctrs.end()) return it->second;
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    ctrs[{dev, st}] = d;
+    return d;
+}
+
 // byte p of the chunk's message: zero outside [as, ae), the first four bytes XOR 0xFF
 __device__ __forceinline__ uint32_t msg_byte(uintptr_t p, uintptr_t as, uintptr_t ae) {
     if (p < as || p >= ae) return 0;
@@ -140,17 +158,23 @@ __device__ __forceinline__ uint32_t row_step(const uint32_t* tf, uint32_t r, uin
 __global__ __launch_bounds__(kCrcThreads) void crc32_chunks_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint32_t* __restrict__ order, uint64_t n, const CrcTables* __restrict__ tab,
-    uint32_t* __restrict__ out) {
+    uint32_t* __restrict__ out, unsigned long long* __restrict__ next_ctr) {
     __shared__ __attribute__((aligned(16))) uint32_t tf[16 * 256];
     __shared__ uint32_t tb[256];
     __shared__ uint32_t red[kCrcThreads / 64];
+    __shared__ uint64_t s_next;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < 16 * 256 / 4; i += kCrcThreads)
         reinterpret_cast<uint4*>(tf)[i] = reinterpret_cast<const uint4*>(tab->tf)[i];
     tb[tid] = tab->t[tid];
     __syncthreads();
 
-    for (uint64_t k = blockIdx.x; k < n; k += gridDim.x) {
+    // chunk order: the first gridDim.x statically, then (next_ctr) each workgroup draws
+    // its next chunk from a counter, so workgroups on faster CUs take more
+    for (uint64_t k = blockIdx.x; k < n;) {
+        if (next_ctr) {
+            if (tid == 0) s_next = gridDim.x + atomicAdd(next_ctr, 1ull);
+        }
         const uint64_t ci = order ? order[k] : k;
         const uint64_t s = bounds[ci] - base, e = bounds[ci + 1] - base;
         if (e - s < 4) {  // shorter than the init register: serially, one lane
@@ -158,6 +182,13 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_chunks_kernel(
                 uint32_t r = 0xFFFFFFFFu;
                 for (uint64_t p = s; p < e; ++p) r = (r >> 8) ^ tb[(r ^ data[p]) & 0xFFu];
                 out[ci] = ~r;
+            }
+            if (next_ctr) {
+                __syncthreads();
+                k = s_next;
+                __syncthreads();
+            } else {
+                k += gridDim.x;
             }
             continue;
         }
@@ -204,7 +235,13 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_chunks_kernel(
             for (int i = 0; i < kCrcThreads / 64; ++i) x ^= red[i];
             out[ci] = ~x;
         }
-        __syncthreads();  // red is reused by the next chunk
+        __syncthreads();  // red (and s_next) are reused by the next chunk
+        if (next_ctr) {
+            k = s_next;
+            __syncthreads();
+        } else {
+            k += gridDim.x;
+        }
     }
 }
 
@@ -226,8 +263,15 @@ extern "C" int pbs_crc32_chunks_async(const uint8_t* dev_data, size_t data_len, 
     if (!tab) return PBS_ERR_NOMEM;
     (void)hipGetLastError();
     const unsigned grid = (unsigned)std::min<uint64_t>(n, (uint64_t)ncu * kCrcGroupsPerCu);
+    const char* e = std::getenv("PBS_CRC_DYN");  // A/B knob
+    unsigned long long* ctr = nullptr;
+    if (n > grid && !(e && e[0] == '0')) {
+        ctr = stream_counter(dev, (hipStream_t)hip_stream);
+        if (!ctr) return PBS_ERR_NOMEM;
+        if (hipMemsetAsync(ctr, 0, sizeof(*ctr), (hipStream_t)hip_stream) != hipSuccess) return PBS_ERR_HIP;
+    }
     hipLaunchKernelGGL(crc32_chunks_kernel, dim3(grid), dim3(kCrcThreads), 0, (hipStream_t)hip_stream,
-                       dev_data, base, bounds_dev, order_dev, (uint64_t)n, tab, crcs_dev);
+                       dev_data, base, bounds_dev, order_dev, (uint64_t)n, tab, crcs_dev, ctr);
     return hipGetLastError() == hipSuccess ? PBS_OK : PBS_ERR_HIP;
 }
 
