@@ -165,14 +165,15 @@ uint64_t batch_max(const Params& p) {
 struct ScanPlan {
     uint64_t ntiles = 0, ext_first = 0, ext_count = 0, blocks = 0;
     int seg = 0, head = 0;
-    bool dyn = false;  // dynamic tile order (scan_main_plan)
+    bool dyn = false;        // dynamic tile order (scan_main_plan)
+    uint64_t t_big = 0;      // tiles >= t_big are small (segments of seg / 4)
 };
 
 ScanPlan plan_scan(pbs_chunker* c, uint64_t len) {
     const Params& p = c->prm;
     ScanPlan sp;
-    sp.seg = scan_main_plan(len, c->cu, &sp.ntiles, &sp.dyn);
-    const uint64_t covered = sp.ntiles * 64ull * (uint64_t)sp.seg;
+    sp.seg = scan_main_plan(len, c->cu, &sp.ntiles, &sp.dyn, &sp.t_big);
+    const uint64_t covered = scan_main_covered(sp.ntiles, sp.t_big, sp.seg);
     sp.head = sp.ntiles > 0 ? 1 : 0;
     sp.ext_first = covered / kBlockBytes;
     sp.ext_count = (len - covered + kBlockBytes - 1) / kBlockBytes;
@@ -203,7 +204,7 @@ int scan_launch(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t ba
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, launch_scan_main(d_data, sp.ntiles, sp.seg, c->d_table.as<uint32_t>(), p.thr,
                                 c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu, c->stream,
-                                d_nsusp + 2, sp.dyn));
+                                d_nsusp + 2, sp.dyn, sp.t_big));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     const uint64_t max_items = (uint64_t)c->susp_cap + 1 + sp.ext_count;
     HIP_TRY(c, launch_scan_exact(d_data, len, c->d_pre.as<uint8_t>(), c->carry_len,

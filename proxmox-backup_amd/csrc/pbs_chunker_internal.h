@@ -28,11 +28,14 @@ struct ResolveParams {
 
 // Segment bytes per lane for a scan of `len` bytes (a wave tile = 64 segments) and
 // the number of full wave tiles; bytes past ntiles*64*seg are the tail.
-int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn);
+int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn, uint64_t* t_big);
+// bytes covered by the plan's tiles (tiles >= t_big are small: 64 * seg / 4 bytes)
+uint64_t scan_main_covered(uint64_t ntiles, uint64_t t_big, int seg);
 hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
                             uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream,
-                            uint32_t* tile_ctr = nullptr, bool dynamic = false);
+                            uint32_t* tile_ctr = nullptr, bool dynamic = false,
+                            uint64_t t_big = ~0ull);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
                              uint32_t pre_len, const uint64_t* susp, const uint32_t* nsusp,
                              uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head,

@@ -909,7 +909,7 @@ __global__ __launch_bounds__(256) void gen_kernel(uint64_t* __restrict__ out, ui
 // ---------------------------------------------------------------------------------
 // Host-side launchers (called from pbs_chunker_capi.cpp)
 // ---------------------------------------------------------------------------------
-int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn) {
+int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn, uint64_t* t_big) {
     // Tile order: dynamic (waves draw tiles from a counter, so waves on faster CUs take
     // more) once every wave gets >= 16 tiles of 16 KiB segments; measured same-process
     // A/B on MI355X (scripts/ab_dyn.py, profiles/r01/dyn/): 64 GiB 11.13 -> 10.55 ms
@@ -943,13 +943,28 @@ int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn) {
     }
     *dyn = d;
     *ntiles = len / (64ull * seg);
+    *t_big = *ntiles;
+    // dynamic order: end with 2 small tiles (segments of seg / 4) per wave, so the waves
+    // finish within a quarter tile of each other (PBS_SCAN_SMALL=0: no small tiles)
+    const char* es = std::getenv("PBS_SCAN_SMALL");
+    if (d && !(es && es[0] == '0')) {
+        const uint64_t big = 64ull * seg, small = big / 4, small_bytes = 2 * waves * small;
+        if (len > small_bytes + big) {
+            *t_big = (len - small_bytes) / big;
+            *ntiles = *t_big + (len - *t_big * big) / small;
+        }
+    }
     return seg;
+}
+
+uint64_t scan_main_covered(uint64_t ntiles, uint64_t t_big, int seg) {
+    return t_big >= ntiles ? ntiles * 64ull * seg : t_big * 64ull * seg + (ntiles - t_big) * 16ull * seg;
 }
 
 hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
                             uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream,
-                            uint32_t* tile_ctr, bool dynamic) {
+                            uint32_t* tile_ctr, bool dynamic, uint64_t t_big) {
     if (ntiles == 0) return hipSuccess;
     (void)hipGetLastError();  // launch errors below must not be confused with stale ones
     const uint64_t need = (ntiles + kWavesPerWG - 1) / kWavesPerWG;
@@ -960,7 +975,8 @@ hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
     case S:                                                                                       \
         if (dyn)                                                                                  \
             hipLaunchKernelGGL((scan_main_kernel<S, kModeFull, 2, 4, 0, 0, kScanFrame, 1>), gd, bd, 0, \
-                               stream, data, ntiles, table_rot, thr, susp, nsusp, cap, tile_ctr);   \
+                               stream, data, ntiles, table_rot, thr, susp, nsusp, cap, tile_ctr,    \
+                               t_big);                                                             \
         else                                                                                      \
             hipLaunchKernelGGL((scan_main_kernel<S, kModeFull, 2, 4, 0, 0, kScanFrame, 0>), gd, bd, 0, \
                                stream, data, ntiles, table_rot, thr, susp, nsusp, cap, nullptr);    \
@@ -1088,3 +1104,12 @@ hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t wo
 }
 
 }  // namespace pbs
+
+#ifdef PBS_SCAN_PROBE
+// probe build only (scripts/microbench/scan_probe.py): the per-wave finish times of the
+// last scan_main launch, wall_clock64 ticks (100 MHz)
+extern "C" int pbs_scan_probe_read(uint64_t* out) {  // 2 * 4096: finish, then start times
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pbs::g_scan_probe), sizeof(pbs::g_scan_probe)) == hipSuccess
+               ? 0 : -1;
+}
+#endif

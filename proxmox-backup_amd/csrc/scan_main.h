@@ -56,15 +56,25 @@ __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
 // 7.2 TB/s) but 2-4 % slower in the full, power-limited kernel (profiles/r01/fr2/).
 // DYN (tile order): 0 = static, wave w takes tiles w, w + nw, ...; 1 = the first nw tiles
 // static, then each wave takes its next tile from a device counter (one atomic per
-// 2 MiB tile, issued at the tile's first iteration, read at its last), so waves on
-// faster CUs take more tiles.
+// tile, issued at the tile's first iteration, read at its last), so waves on faster CUs
+// take more tiles -- and tiles t >= t_big are "small" (segments of SEG / 4), so the
+// waves also finish together: the last tiles are a quarter as long.  Measured per-wave
+// finish times (scripts/microbench/scan_probe.py): static order 7.4-11.2 ms for the
+// 64 GiB stream (the older wave of a SIMD wins the issue arbitration), dynamic
+// 10.3-10.7 ms.
+#ifdef PBS_SCAN_PROBE
+constexpr int kScanProbeMax = 4096;
+__device__ uint64_t g_scan_probe[2 * kScanProbeMax];  // finish times, then start times
+#endif
 template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int ZS = 0, int FR = 1,
           int DYN = 0>
 __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
     uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap,
-    uint32_t* __restrict__ tile_ctr = nullptr) {
+    uint32_t* __restrict__ tile_ctr = nullptr, uint64_t t_big = ~0ull) {
     static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
+    constexpr int SEG2 = SEG / 4;  // DYN: segment length of the small tiles (t >= t_big)
+    static_assert(SEG2 % kIter == 0, "small segment must be a multiple of the iteration size");
     constexpr int NW = kWavesPerWG;
     // + 256 B per wave: landing area of the L2 "touch" DMAs (PF > 0)
     __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4 + NW * 64];
@@ -92,12 +102,23 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
         const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
         voff[j] = l * (uint32_t)SEG + k * 16u;
     }
+    uint32_t voff2[8];  // DYN: the same offsets for small tiles
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t l = 8u * j + ((uint32_t)lane >> 3);
+        const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
+        voff2[j] = l * (uint32_t)SEG2 + k * 16u;
+    }
     const uint32_t rd_base = (uint32_t)lane * 128u;
     const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
 
     constexpr int NIT = SEG / kIter + 1;  // iteration 0 is the warm-up block [-128, 0)
     const uint64_t nw = (uint64_t)gridDim.x * NW;
     uint64_t tile = (uint64_t)blockIdx.x * NW + wave;
+#ifdef PBS_SCAN_PROBE
+    if (lane == 0 && blockIdx.x * NW + wave < kScanProbeMax)
+        g_scan_probe[kScanProbeMax + blockIdx.x * NW + wave] = wall_clock64();
+#endif
     if (tile >= ntiles) return;
 
     // Tile t > 0: base = tile start - 128, iteration offset it*128 (the warm-up block of
@@ -105,19 +126,33 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     // warm-up iteration (it == 0) uses explicit per-lane offsets voff - 128 (segment 0
     // has no bytes before it: it reads offset 0 and its warm-up state is discarded).
     // Offsets must not wrap: the buffer unit range-checks voffset + soffset unwrapped.
+    // byte offset of tile t and whether it is a small one (wave-uniform)
+    auto tile_off = [&](uint64_t t) -> uint64_t {
+        if (DYN != 0 && t >= t_big) return t_big * (64ull * SEG) + (t - t_big) * (64ull * SEG2);
+        return t * (64ull * SEG);
+    };
     auto issue = [&](uint64_t t, int it) {
-        const uint8_t* tb = data + t * (64ull * SEG);
+        const bool sm = DYN != 0 && t >= t_big;
+        const uint8_t* tb = data + tile_off(t);
         const bool first = (t == 0);
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(first ? tb : tb - kIter), 0, (int)(64u * SEG + kIter), 0x00020000);
+            (void*)(first ? tb : tb - kIter), 0, (int)(64u * (sm ? SEG2 : SEG) + kIter), 0x00020000);
         const bool warm0 = first && it == 0;
         const uint32_t soff = warm0 ? 0u : (uint32_t)it * kIter - (first ? (uint32_t)kIter : 0u);
+        if (sm) {  // small tiles are never tile 0
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t vo = warm0 ? (voff[j] >= (uint32_t)kIter ? voff[j] - kIter : 0u) : voff[j];
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, vo, soff, 0,
-                AUX);
+            for (int j = 0; j < 8; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, voff2[j], soff,
+                    0, AUX);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t vo = warm0 ? (voff[j] >= (uint32_t)kIter ? voff[j] - kIter : 0u) : voff[j];
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, vo, soff, 0,
+                    AUX);
+            }
         }
         if constexpr (PF > 0) {
             // pull the 64 lines of iteration it+PF into L2 (4 bytes per lane, dummy LDS)
@@ -145,7 +180,11 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
         if constexpr (DYN != 0) {
             if (lane == 0) dyn_v = atomicAdd(tile_ctr, 1u);
         }
-        for (int it = 0; it < NIT; ++it) {
+        const bool small = DYN != 0 && tile >= t_big;
+        const int nit_cur = small ? SEG2 / kIter + 1 : NIT;
+        const uint64_t toff = tile_off(tile);
+        const uint32_t seg_cur = small ? (uint32_t)SEG2 : (uint32_t)SEG;
+        for (int it = 0; it < nit_cur; ++it) {
             if (PF > 0 && it + PF < NIT)
                 asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // the touch may stay in flight
             else
@@ -163,7 +202,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
             {
                 uint64_t nt = tile;
                 int nit = it + 1;
-                if (nit == NIT) {
+                if (nit == nit_cur) {
                     nt = next_tile();
                     nit = 0;
                 }
@@ -210,7 +249,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
                 }
             } else if (acc >= thr) {
                 const uint64_t pos =
-                    (tile * 64ull + (uint64_t)lane) * (uint64_t)SEG + (uint64_t)(it - 1) * kIter;
+                    toff + (uint64_t)lane * seg_cur + (uint64_t)(it - 1) * kIter;
                 if (pos != 0) {
                     const uint32_t idx = atomicAdd(nsusp, 1u);
                     if (idx < cap) susp[idx] = pos;
@@ -220,6 +259,10 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
         tile = next_tile();
         if (tile >= ntiles) break;
     }
+#ifdef PBS_SCAN_PROBE  // scripts/microbench/scan_probe.py: per-wave finish time
+    if (lane == 0 && blockIdx.x * NW + wave < kScanProbeMax)
+        g_scan_probe[blockIdx.x * NW + wave] = wall_clock64();
+#endif
 }
 
 }  // namespace pbs

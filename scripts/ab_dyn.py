@@ -1,6 +1,6 @@
 """A/B of scan_main tile orders (PBS_SCAN_DYN) and segment caps (PBS_MAX_SEG), same
 process, same VM-image buffer, modes alternating; cut lists must agree.
-usage: ab_dyn.py <GiB> <avg> <mode> [<mode> ...]   mode = "<dyn 0|1>:<max seg>"."""
+usage: ab_dyn.py <GiB> <avg> <mode> [<mode> ...]   mode = "<dyn 0|1>:<max seg>[:<small tiles 0|1>]"."""
 import os
 import sys
 
@@ -24,9 +24,10 @@ res = {m: [] for m in modes}
 ref = None
 for rep in range(10):
     for m in modes:
-        dyn, seg = m.split(":")
-        os.environ["PBS_SCAN_DYN"] = dyn
-        os.environ["PBS_MAX_SEG"] = seg
+        f = m.split(":")
+        os.environ["PBS_SCAN_DYN"] = f[0]
+        os.environ["PBS_MAX_SEG"] = f[1]
+        os.environ["PBS_SCAN_SMALL"] = f[2] if len(f) > 2 else "1"
         cuts = ch.find_cuts_device(buf.data_ptr(), size, is_final=True)
         t = ch.last_timing()
         if ref is None:
