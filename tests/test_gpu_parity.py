@@ -349,9 +349,11 @@ def _oracle_two_phase_parallel(oracle, data: np.ndarray, avg: int, threads: int 
 @pytest.mark.slow
 @pytest.mark.parametrize("gib,kind,avg,dyn", [(8, 1, 4 * MiB, None), (6, 2, 256 * KiB, None),
                                              (3, 1, 64 * KiB, None), (64, 2, 4 * MiB, None),
-                                             (6, 2, 4 * MiB, "1"), (3, 1, 64 * KiB, "1")],
+                                             (6, 2, 4 * MiB, "1"), (3, 1, 64 * KiB, "1"),
+                                             (1.5, 2, 1 * MiB, "1")],
                          ids=["config2-8GiB-random-4M", "6GiB-vm-256K", "3GiB-random-64K",
-                              "config3-64GiB-vm-4M", "6GiB-vm-4M-dynamic", "3GiB-random-64K-dynamic"])
+                              "config3-64GiB-vm-4M", "6GiB-vm-4M-dynamic", "3GiB-random-64K-dynamic",
+                              "1.5GiB+ragged-vm-1M-dynamic"])
 def test_full_size_in_hbm(gpu, oracle, monkeypatch, gib, kind, avg, dyn):
     """BASELINE config 2 (8 GiB random already in HBM, 4 MiB average), the headline
     config 3 (64 GiB VM image, 4 MiB: 16 KiB segments in the dynamic tile order), and
@@ -361,14 +363,15 @@ def test_full_size_in_hbm(gpu, oracle, monkeypatch, gib, kind, avg, dyn):
     import torch
     if dyn is not None:
         monkeypatch.setenv("PBS_SCAN_DYN", dyn)
-    n = gib * GiB
+    n = int(gib * GiB) + (12345 if gib != int(gib) else 0)  # ragged: the tail after the small tiles
     seed = 0x5EED0002 if kind == 1 else 0x5EED0003
-    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
-    gpu.generate_device(dev.data_ptr(), n, kind, seed, 0)
+    n8 = (n + 7) // 8 * 8  # the generator writes whole words
+    dev = torch.empty(n8, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n8, kind, seed, 0)
     with gpu.Chunker(avg) as c:
         got = c.find_cuts_device(dev.data_ptr(), n, is_final=False)
         t = c.last_timing()
-    host = dev.cpu().numpy()
+    host = dev[:n].cpu().numpy()
     del dev
     cand, ref = _oracle_two_phase_parallel(oracle, host, avg)
     assert t["candidates"] == cand.size
