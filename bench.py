@@ -105,7 +105,7 @@ def cpu_baseline(args, workload, seed, avg):
     [t.start() for t in ths]
     [t.join() for t in ths]
     agg = threads * n / (1 << 30) / (time.perf_counter() - t0)
-    cpu = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": ") \
+    cpu = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].split(":", 1)[-1].strip() \
         if os.path.exists("/proc/cpuinfo") else "unknown"
     del bufs
     return {"value": round(agg, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
