@@ -231,9 +231,11 @@ def crc_stage(args, buf, bd, od, n, bounds, take, threads, stream, reps):
 def pipeline_stage(args, buf, piece: int = 1 << 30):
     """a pageable host copy of the stream's first --pipeline-gib GiB
     through pbs_pipeline_host (copy thread -> HBM, chunker on CU-masked stream, per-chunk
-    SHA-256 on the other CUs, overlapped), end to end; the CPU path beside it: the oracle
-    chunker + hashlib per chunk on the host cores over a bounded sample."""
+    SHA-256 and blob CRC-32 on the other CUs, overlapped), end to end; the CPU path beside
+    it: the oracle chunker + hashlib + zlib.crc32 per chunk on the host cores over a
+    bounded sample."""
     import hashlib
+    import zlib
 
     import numpy as np
 
@@ -244,9 +246,9 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
 
     n = int(args.pipeline_gib * (1 << 30)) // 8 * 8
     host = buf[:n].cpu().numpy()  # pageable, untimed
-    pbschunk.pipeline_host(host[: 64 << 20], args.avg, piece=16 << 20)  # warm-up
+    pbschunk.pipeline_host(host[: 64 << 20], args.avg, piece=16 << 20, crc=True)  # warm-up
     t0 = time.perf_counter()
-    ends, dig, t = pbschunk.pipeline_host(host, args.avg, piece=piece)
+    ends, dig, crcs, t = pbschunk.pipeline_host(host, args.avg, piece=piece, crc=True)
     wall = time.perf_counter() - t0
     # CPU path: threads chunk their own slice and hash its chunks (hashlib/OpenSSL)
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -260,6 +262,7 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
         for i in range(b.size - 1):
             if b[i + 1] > b[i]:
                 hashlib.sha256(mv[b[i]:b[i + 1]]).digest()
+                zlib.crc32(mv[b[i]:b[i + 1]])
 
     nth = min(threads, max(1, n // per))
     ths = [threading.Thread(target=work, args=(k,)) for k in range(nth)]
@@ -267,13 +270,13 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
     [x.start() for x in ths]
     [x.join() for x in ths]
     cpu = nth * per / (1 << 30) / (time.perf_counter() - c0)
-    return {"metric": "GiB/s host stream -> chunk boundaries + SHA-256 per chunk (end to end)",
+    return {"metric": "GiB/s host stream -> chunk boundaries + SHA-256 + blob CRC-32 per chunk (end to end)",
             "value": round(n / (1 << 30) / wall, 3), "bytes": n, "piece": piece,
             "chunks": int(ends.size), "timing_ms": {k: round(v, 2) for k, v in t.items()
                                                      if k.endswith("_ms")},
             "cpu_baseline": {"value": round(cpu, 3), "unit": "GiB/s", "cores": nth,
-                             "kind": "port (oracle chunker) + hashlib",
-                             "sample": f"{nth} x 256 MiB slices: chunk_feed then sha256 per chunk"}}
+                             "kind": "port (oracle chunker) + hashlib + zlib.crc32",
+                             "sample": f"{nth} x 256 MiB slices: chunk_feed then sha256 + crc32 per chunk"}}
 
 
 def main():

@@ -69,7 +69,9 @@ int pbs_known_chunks_device(const uint8_t *digests_dev, size_t n, const uint8_t 
  * [digest_cus, n) and the chunks each piece completes are digested on CU-masked
  * streams over CUs [0, digest_cus) while the next pieces copy.  Writes the chunk END
  * offsets (`ends`, the tail included) and their 32-byte digests (SHA-256(chunk || key))
- * in chunk order; cap >= pbs_chunker_cuts_bound for the average.  Needs `len` bytes of
+ * in chunk order, and with `crcs` != NULL each chunk's CRC-32 (the uncompressed blob's
+ * DataBlob::compute_crc, include/pbs_blob.h; computed right after each digest launch on
+ * the same stream); cap >= pbs_chunker_cuts_bound for the average.  Needs `len` bytes of
  * device memory.  Synchronous. */
 typedef struct {
     double total_ms; /* first copy issued .. digests on the host */
@@ -80,7 +82,8 @@ typedef struct {
 } pbs_pipeline_timing;
 int pbs_pipeline_host(size_t avg, const uint8_t *host, size_t len, size_t piece,
                       const uint8_t *key, size_t key_len, int digest_cus, uint64_t *ends,
-                      uint8_t *digests, size_t cap, size_t *n_out, pbs_pipeline_timing *timing);
+                      uint8_t *digests, uint32_t *crcs, size_t cap, size_t *n_out,
+                      pbs_pipeline_timing *timing);
 
 /* Host SHA-256 (FIPS 180-4), used for the index checksum (the reference's
  * openssl::sha::Sha256 over 40-byte entries; a few hundred KiB per index). */

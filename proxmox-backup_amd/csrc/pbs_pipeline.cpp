@@ -27,6 +27,7 @@
 #include <thread>
 #include <vector>
 
+#include "pbs_blob.h"
 #include "pbs_chunker.h"
 #include "pbs_digest.h"
 
@@ -50,8 +51,8 @@ constexpr int kDigestStreams = 4;
 
 extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, size_t piece,
                                  const uint8_t* key, size_t key_len, int digest_cus,
-                                 uint64_t* ends, uint8_t* digests, size_t cap, size_t* n_out,
-                                 pbs_pipeline_timing* timing) {
+                                 uint64_t* ends, uint8_t* digests, uint32_t* crcs, size_t cap,
+                                 size_t* n_out, pbs_pipeline_timing* timing) {
     if (!n_out || (len && !host) || piece == 0 || (cap && (!ends || !digests)) ||
         key_len > PBS_DIGEST_MAX_KEY || (key_len && !key))
         return PBS_ERR_INVALID;
@@ -76,6 +77,7 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     uint8_t* d_dig = nullptr;
     uint64_t* d_bounds = nullptr;
     uint32_t* d_order = nullptr;
+    uint32_t* d_crc = nullptr;
     std::vector<hipEvent_t> ev_copied(npieces, nullptr);
     int rc = PBS_OK;
     auto hip_ok = [&](hipError_t e) {
@@ -89,7 +91,8 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     // device: the stream, the digests, and per-launch bounds/order (<= cap + npieces + 1)
     if (ok && (hipMalloc(&d_data, len) != hipSuccess || hipMalloc(&d_dig, cap * 32) != hipSuccess ||
                hipMalloc(&d_bounds, (cap + npieces + 1) * 8) != hipSuccess ||
-               hipMalloc(&d_order, std::max<size_t>(cap, 1) * 4) != hipSuccess)) {
+               hipMalloc(&d_order, std::max<size_t>(cap, 1) * 4) != hipSuccess ||
+               (crcs && hipMalloc(&d_crc, std::max<size_t>(cap, 1) * 4) != hipSuccess))) {
         ok = false;
         rc = PBS_ERR_NOMEM;
     }
@@ -190,6 +193,14 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
                 rc = dr;
                 break;
             }
+            if (crcs) {  // the blob CRC of the same chunks, behind the digests on that stream
+                const int cr = pbs_crc32_chunks_async(d_data, len, 0, d_bounds + nb, d_order + launched, mm,
+                                                      d_crc + launched, sd);
+                if (cr != PBS_OK) {
+                    rc = cr;
+                    break;
+                }
+            }
             ++launches;
             nb += mm + 1;
             launched = n;
@@ -201,6 +212,7 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     if (rc == PBS_OK && ok) {
         for (auto& s : s_dig) hip_ok(hipStreamSynchronize(s));
         if (rc == PBS_OK && n) hip_ok(hipMemcpy(digests, d_dig, n * 32, hipMemcpyDeviceToHost));
+        if (rc == PBS_OK && n && crcs) hip_ok(hipMemcpy(crcs, d_crc, n * 4, hipMemcpyDeviceToHost));
     }
     const double total = ms_since(t0);
     if (timing) {
@@ -215,7 +227,7 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     *n_out = n;
     for (auto& e : ev_copied)
         if (e) (void)hipEventDestroy(e);
-    for (void* p : {(void*)d_data, (void*)d_dig, (void*)d_bounds, (void*)d_order})
+    for (void* p : {(void*)d_data, (void*)d_dig, (void*)d_bounds, (void*)d_order, (void*)d_crc})
         if (p) (void)hipFree(p);
     pbs_chunker_free(c);  // before its stream goes away
     if (s_copy) (void)hipStreamDestroy(s_copy);

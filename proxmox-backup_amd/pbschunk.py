@@ -136,7 +136,7 @@ def lib():
         "pbs_didx_size": ([sz], sz),
         "pbs_didx_build": ([p, p, sz, p, ctypes.c_int64, p, sz, p], i),
         "pbs_known_chunks_device": ([p, sz, p, sz, p, ctypes.POINTER(sz), p], i),
-        "pbs_pipeline_host": ([sz, p, sz, sz, p, sz, i, p, p, sz, ctypes.POINTER(sz),
+        "pbs_pipeline_host": ([sz, p, sz, sz, p, sz, i, p, p, p, sz, ctypes.POINTER(sz),
                                ctypes.POINTER(PipelineTiming)], i),
         "pbs_chunker_set_cu_count": ([p, i], i),
         "pbs_crc32_chunks_device": ([p, sz, u64, p, sz, p, p], i),
@@ -623,19 +623,24 @@ def index_stream_device(chunker: "Chunker", dev_ptr: int, length: int, key=None,
     return ends, dig, csum, image
 
 
-def pipeline_host(data, avg: int, piece: int = 1 << 30, key=None, digest_cus: int = 64):
+def pipeline_host(data, avg: int, piece: int = 1 << 30, key=None, digest_cus: int = 64, crc: bool = False):
     """pbs_pipeline_host: chunk END offsets, (n, 32) digests and the timing dict of the
-    overlapped copy -> chunk -> digest path over a host buffer."""
+    overlapped copy -> chunk -> digest path over a host buffer; with crc=True also the
+    per-chunk blob CRC-32s: (ends, digests, crcs, timing)."""
     a = _as_u8(data)
     with Chunker(avg) as c:
         cap = c.cuts_bound(a.size) + 1
     ends = np.empty(cap, dtype=np.uint64)
     dig = np.empty((cap, 32), dtype=np.uint8)
+    crcs = np.empty(cap, dtype=np.uint32) if crc else None
     n = ctypes.c_size_t(0)
     t = PipelineTiming()
     kb, kl = _key_arg(key)
     rc = lib().pbs_pipeline_host(avg, _ptr(a), a.size, piece, kb, kl, digest_cus, ends.ctypes.data,
-                                 dig.ctypes.data, cap, ctypes.byref(n), ctypes.byref(t))
+                                 dig.ctypes.data, crcs.ctypes.data if crc else None, cap, ctypes.byref(n),
+                                 ctypes.byref(t))
     if rc != PBS_OK:
         raise ChunkerError(rc, "pbs_pipeline_host")
+    if crc:
+        return ends[: n.value].copy(), dig[: n.value].copy(), crcs[: n.value].copy(), t.as_dict()
     return ends[: n.value].copy(), dig[: n.value].copy(), t.as_dict()

@@ -177,11 +177,15 @@ def test_pipeline_host(gpu, oracle, kind, avg, piece, key):
     equals the oracle chunker + hashlib, with chunks straddling the copy pieces."""
     n = 100 * MiB + 77
     data = gen_np.gen_vmimage(n, 0x5EED0003, 0) if kind == "vmimage" else gen_np.gen_random(n, 21)
-    ends, dig, t = gpu.pipeline_host(data, avg, piece=piece, key=key, digest_cus=32)
+    ends, dig, crcs, t = gpu.pipeline_host(data, avg, piece=piece, key=key, digest_cus=32, crc=True)
     ref = oracle.chunk_feed(avg, data)
     if ref.size == 0 or int(ref[-1]) != n:
         ref = np.append(ref, np.uint64(n))
     assert np.array_equal(ends, ref)
     bounds = np.concatenate([[0], ref]).astype(np.uint64)
     assert np.array_equal(dig, oracle.chunk_digests(data, bounds, key or b""))
+    assert np.array_equal(crcs, oracle.chunk_crcs(data, bounds))  # the blob CRCs
     assert t["chunks"] == ref.size and t["bytes"] == n
+    # without the CRC output: same cut list and digests
+    ends2, dig2, _ = gpu.pipeline_host(data, avg, piece=piece, key=key, digest_cus=32)
+    assert np.array_equal(ends2, ends) and np.array_equal(dig2, dig)
