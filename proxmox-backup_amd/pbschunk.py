@@ -623,6 +623,38 @@ def index_stream_device(chunker: "Chunker", dev_ptr: int, length: int, key=None,
     return ends, dig, csum, image
 
 
+def upload_stream_host(data, avg: int, known=None, key=None, piece: int = 1 << 30,
+                       uuid: bytes = bytes(16), ctime: int = 0) -> dict:
+    """The client's upload of one dynamic-index stream from a host buffer, up to the
+    network (pbs-client/src/backup_writer.rs:638-700 upload_chunk_info_stream /
+    :683-688 index csum): chunk (ChunkStream), digest every chunk, mark it known when
+    its digest is in ``known`` (the previous index's digests, :524-547) or repeats an
+    earlier chunk of this stream (:697), and build the .didx image.  Chunking, digests,
+    the blob CRCs and the known-chunk test run on the GPU (pipeline_host,
+    known_chunks_device).  Returns a dict: ends, digests, crcs, known (uint8 mask),
+    csum, didx (bytes), and new_chunks = [(start, length, crc), ...] -- the chunks whose
+    uncompressed blob (blob_encode_uncompressed) would be uploaded."""
+    import torch
+
+    ends, dig, crcs, _ = pipeline_host(data, avg, piece=piece, key=key, crc=True)
+    n = ends.size
+    d_dig = torch.from_numpy(dig.reshape(-1)).to("cuda")
+    flags = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+    kd = np.zeros((0, 32), dtype=np.uint8)
+    if known is not None and len(known):
+        kd = np.frombuffer(b"".join(sorted(bytes(x) for x in known)), dtype=np.uint8).reshape(-1, 32)
+    d_known = torch.from_numpy(kd.reshape(-1).copy()).to("cuda") if kd.size else None
+    torch.cuda.synchronize()
+    known_chunks_device(d_dig.data_ptr(), n, d_known.data_ptr() if d_known is not None else 0,
+                        kd.shape[0], flags.data_ptr())
+    mask = flags[:n].cpu().numpy()
+    image, csum = didx_build(ends, dig, uuid, ctime)
+    starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64) if n else np.zeros(0, np.uint64)
+    new = [(int(starts[i]), int(ends[i] - starts[i]), int(crcs[i])) for i in range(n) if not mask[i]]
+    return {"ends": ends, "digests": dig, "crcs": crcs, "known": mask, "csum": csum, "didx": image,
+            "new_chunks": new}
+
+
 def pipeline_host(data, avg: int, piece: int = 1 << 30, key=None, digest_cus: int = 64, crc: bool = False):
     """pbs_pipeline_host: chunk END offsets, (n, 32) digests and the timing dict of the
     overlapped copy -> chunk -> digest path over a host buffer; with crc=True also the

@@ -1,4 +1,4 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/pipeprof; export TMPDIR=/tmp
-timeout -s KILL 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pipeprof/p -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline 0 --host-inclusive-gib 0 --pipeline-gib 64 > gpurun_out/pipeprof/bench.log 2>&1
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_digest.py -m gpu -x -v --timeout 300 --timeout-method thread -k "upload or pipeline" > gpurun_out/pytest_upload.log 2>&1
 echo rc=$?

@@ -189,3 +189,30 @@ def test_pipeline_host(gpu, oracle, kind, avg, piece, key):
     # without the CRC output: same cut list and digests
     ends2, dig2, _ = gpu.pipeline_host(data, avg, piece=piece, key=key, digest_cus=32)
     assert np.array_equal(ends2, ends) and np.array_equal(dig2, dig)
+
+
+@pytest.mark.parametrize("prev", [0, 5, 40])
+def test_upload_stream_host(gpu, oracle, prev):
+    """backup_writer.rs:638-700 end to end from a host buffer: cut list, digests, blob
+    CRCs, the known-chunk mask against a previous index holding some of this stream's
+    digests (plus unrelated ones) and repeats inside the stream, and the .didx image."""
+    n = 48 * MiB + 5
+    data = gen_np.gen_vmimage(n, 0x5EED0003, 0)
+    ref_ends = oracle.chunk_feed(1 * MiB, data)
+    if ref_ends.size == 0 or int(ref_ends[-1]) != n:
+        ref_ends = np.append(ref_ends, np.uint64(n))
+    bounds = np.concatenate([[0], ref_ends]).astype(np.uint64)
+    ref_dig = oracle.chunk_digests(data, bounds)
+    rng = np.random.default_rng(prev)
+    pick = rng.choice(ref_dig.shape[0], size=min(prev, ref_dig.shape[0]), replace=False)
+    known = [bytes(ref_dig[i]) for i in pick] + [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(prev)]
+    out = gpu.upload_stream_host(data, 1 * MiB, known=known, piece=16 * MiB, uuid=bytes(range(16)), ctime=77)
+    assert np.array_equal(out["ends"], ref_ends)
+    assert np.array_equal(out["digests"], ref_dig)
+    assert np.array_equal(out["crcs"], oracle.chunk_crcs(data, bounds))
+    ref_known = oracle.known_chunks(ref_dig, known)
+    assert np.array_equal(out["known"], ref_known)
+    img, csum = oracle.didx_image(ref_ends, ref_dig, bytes(range(16)), 77)
+    assert out["didx"] == img and out["csum"] == csum
+    new = [(int(bounds[i]), int(bounds[i + 1] - bounds[i])) for i in range(ref_known.size) if not ref_known[i]]
+    assert [(s, l) for s, l, _ in out["new_chunks"]] == new
