@@ -189,7 +189,7 @@ ScanPlan plan_scan(pbs_chunker* c, uint64_t len) {
 }
 
 int scan_launch(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t base,
-                const ScanPlan& sp) {
+                const ScanPlan& sp, bool copy_counts = true) {
     const Params& p = c->prm;
     HIP_TRY(c, c->d_pre.ensure(64));
     if (c->carry_len)
@@ -213,7 +213,9 @@ int scan_launch(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t ba
                                  c->d_cand.as<uint64_t>(), d_ncand, c->cand_cap, max_items,
                                  c->stream));
     HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_counters.p, 8, hipMemcpyDeviceToHost, c->stream));
+    // (the speculative batch has resolve_small write them instead: one copy less)
+    if (copy_counts)
+        HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_counters.p, 8, hipMemcpyDeviceToHost, c->stream));
     return PBS_OK;
 }
 
@@ -568,12 +570,10 @@ int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     if (np)
         HIP_TRY(c, hipMemcpyAsync(c->d_C.p, c->pending.data() + c->pend_head, np * 8,
                                   hipMemcpyHostToDevice, c->stream));
-    int rc = scan_launch(c, dsrc, bl, pos, sp);
+    int rc = scan_launch(c, dsrc, bl, pos, sp, false);
     if (rc) return rc;
     const uint64_t tl = std::min<uint64_t>(bl, kWindow - 1);
-    uint8_t* tail = reinterpret_cast<uint8_t*>(c->h_small + 24);
-    if (tl && !hsrc)
-        HIP_TRY(c, hipMemcpyAsync(tail, dsrc + bl - tl, tl, hipMemcpyDeviceToHost, c->stream));
+    uint8_t* tail = reinterpret_cast<uint8_t*>(c->h_small + 24);  // written by resolve_small
     HIP_TRY(c, c->d_nxt.ensure(((size_t)m_max + 2) * 4));
     HIP_TRY(c, c->d_nf.ensure(((size_t)m_max + 2) * 8));
     HIP_TRY(c, c->d_res.ensure(32));
@@ -591,7 +591,11 @@ int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
                                     c->d_nf.as<uint64_t>(), c->d_cuts.as<uint64_t>(), out_cap,
                                     cuts_dev, kHostCuts, keep_dev, kHostKeep,
                                     c->d_res.as<uint64_t>(), small_dev + 8, c->stream,
-                                    c->d_counters.as<uint32_t>(), c->susp_cap, c->cand_cap));
+                                    c->d_counters.as<uint32_t>(), c->susp_cap, c->cand_cap,
+                                    reinterpret_cast<uint32_t*>(small_dev),
+                                    hsrc ? nullptr : dsrc + bl - tl,
+                                    hsrc ? nullptr : reinterpret_cast<uint8_t*>(small_dev + 24),
+                                    hsrc ? 0u : (uint32_t)tl));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     uint32_t nsusp = 0;

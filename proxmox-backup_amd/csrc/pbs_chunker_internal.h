@@ -62,7 +62,9 @@ hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C
                                 uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
                                 uint64_t* res, uint64_t* res_host, hipStream_t stream,
                                 const uint32_t* counts = nullptr, uint32_t susp_cap = 0,
-                                uint32_t cand_cap = 0);
+                                uint32_t cand_cap = 0, uint32_t* counts_host = nullptr,
+                                const uint8_t* tail_src = nullptr, uint8_t* tail_host = nullptr,
+                                uint32_t tail_len = 0);
 // Small-input path (scan_blocks_kernel + resolve_small_kernel<1|2>, two launches, no
 // host sync between): the input bytes `data[0..len)` (stream offset `base`, device
 // memory) with the pre_len <= 63 bytes before them in `pre` (device), the test
@@ -86,6 +88,13 @@ struct FusedScanArgs {
     // cand_cap or too many keys -> res_host[12] = 1 and nothing else is written
     const uint32_t* counts;
     uint32_t susp_cap;
+    // speculative path, written before the stand-down test (saves two D2H copies): the
+    // two counters to counts_host, the tail_len <= 63 bytes at tail_src (the warm-up
+    // history of the next call) to tail_host; both mapped host memory, may be null
+    uint32_t* counts_host;
+    const uint8_t* tail_src;
+    uint8_t* tail_host;
+    uint32_t tail_len;
 };
 constexpr uint64_t kFusedMaxBytes = 1ull << 20;  // inputs up to this size take the fused path
 hipError_t launch_scan_resolve_small(const FusedScanArgs& fa, int resolve, uint64_t* C,

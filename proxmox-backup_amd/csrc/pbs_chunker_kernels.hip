@@ -486,6 +486,8 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     if constexpr (FUSED == 0) {
         if (fa.counts) {  // speculative: the candidate count is only known on the device
             const uint32_t ns = fa.counts[0], nc = fa.counts[1];
+            if (fa.counts_host && tid < 2) fa.counts_host[tid] = tid ? nc : ns;
+            if (fa.tail_host && tid < fa.tail_len) fa.tail_host[tid] = fa.tail_src[tid];
             const bool fits = ns <= fa.susp_cap && nc <= fa.cand_cap &&
                               (uint64_t)np + nc + 2 <= kSmallResolveMax;
             if (tid == 0) res_host[12] = fits ? 0u : 1u;
@@ -1055,13 +1057,19 @@ hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C
                                 uint64_t* out, uint64_t out_cap, uint64_t* out_host,
                                 uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
                                 uint64_t* res, uint64_t* res_host, hipStream_t stream,
-                                const uint32_t* counts, uint32_t susp_cap, uint32_t cand_cap) {
+                                const uint32_t* counts, uint32_t susp_cap, uint32_t cand_cap,
+                                uint32_t* counts_host, const uint8_t* tail_src, uint8_t* tail_host,
+                                uint32_t tail_len) {
     if ((uint64_t)np + (counts ? 0 : nnew) + 2 > kSmallResolveMax) return hipErrorInvalidValue;
     (void)hipGetLastError();
     FusedScanArgs fa{};
     fa.counts = counts;
     fa.susp_cap = susp_cap;
     fa.cand_cap = cand_cap;
+    fa.counts_host = counts_host;
+    fa.tail_src = tail_src;
+    fa.tail_host = tail_host;
+    fa.tail_len = tail_len;
     hipLaunchKernelGGL(resolve_small_kernel<0>, dim3(1), dim3(kSmallThreads), 0, stream, newc,
                        nnew, C, np, p, nxt, nforced, out, out_cap, out_host, host_cap, keep_host,
                        keep_cap, res, res_host, fa);
