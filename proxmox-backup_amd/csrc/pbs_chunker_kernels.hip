@@ -350,17 +350,25 @@ __global__ __launch_bounds__(256) void resolve_next_kernel(const uint64_t* __res
     on[j] = (j == m) ? 1u : 0u;
 }
 
-// One pointer-doubling round: J_{t+1} = J_t o J_t, and every marked node marks its
-// 2^t-th successor.  Races on `on` are benign (marks only ever go 0 -> 1, and any
-// node marked is on the chain).
-__global__ __launch_bounds__(256) void resolve_double_kernel(uint32_t n, const uint32_t* __restrict__ jin,
-                                                             uint32_t* __restrict__ jout,
-                                                             uint32_t* on) {
+// Pointer doubling, three rounds per launch.  One round: J_{t+1} = J_t o J_t, and every
+// marked node marks its 2^t-th successor (after round t the chain's first 2^(t+1) nodes
+// are marked).  Here, from J_t and the marks of the first 2^t nodes, every marked node
+// marks its i * 2^t-th successors (i = 1..7, gathered along J_t) and J_{t+3} = J_t^8:
+// the same result as three rounds with a third of the launches.  Races on `on` are
+// benign: marks only go 0 -> 1, and any node marked is on the chain.
+__global__ __launch_bounds__(256) void resolve_double3_kernel(uint32_t n, const uint32_t* __restrict__ jin,
+                                                              uint32_t* __restrict__ jout,
+                                                              uint32_t* on) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
-    const uint32_t J = jin[j];
-    if (on[j]) on[J] = 1u;
-    jout[j] = jin[J];
+    const bool mk = on[j] != 0u;
+    uint32_t x = j;
+#pragma unroll
+    for (int i = 1; i <= 8; ++i) {
+        x = jin[x];
+        if (mk && i < 8) on[x] = 1u;
+    }
+    jout[j] = x;
 }
 
 __device__ __forceinline__ uint32_t slot_of(uint32_t j, uint32_t m) { return j == m ? 0u : j + 1u; }
@@ -699,7 +707,7 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     __syncthreads();
     const uint64_t t_next = wall_clock64();
 
-    // 3. pointer doubling in LDS (marks only go 0 -> 1; see resolve_double_kernel)
+    // 3. pointer doubling in LDS (marks only go 0 -> 1; see resolve_double3_kernel)
     uint16_t* ja = reinterpret_cast<uint16_t*>(sk);
     uint16_t* jb = ja + kSmallJ;
     uint8_t* on = reinterpret_cast<uint8_t*>(jb + kSmallJ);
@@ -1036,8 +1044,8 @@ hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p,
     if (e != hipSuccess) return e;
     uint32_t* ja = jtmp;
     uint32_t* jb = jtmp + n;
-    for (uint32_t span = 1; span < n; span <<= 1) {
-        hipLaunchKernelGGL(resolve_double_kernel, dim3(blocks), dim3(256), 0, stream, n, ja, jb, on);
+    for (uint64_t span = 1; span < n; span <<= 3) {  // three rounds per launch
+        hipLaunchKernelGGL(resolve_double3_kernel, dim3(blocks), dim3(256), 0, stream, n, ja, jb, on);
         uint32_t* t = ja;
         ja = jb;
         jb = t;
