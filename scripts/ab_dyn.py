@@ -16,7 +16,9 @@ avg = int(sys.argv[2])
 modes = sys.argv[3:] or ["0:32768", "1:32768"]
 st = torch.cuda.current_stream()
 buf = torch.empty(size, dtype=torch.uint8, device="cuda")
-pbschunk.generate_device(buf.data_ptr(), size, pbschunk.GEN_VMIMAGE, 0x5EED0003, 0, st.cuda_stream)
+kind = os.environ.get("AB_WORKLOAD", "vmimage")
+pbschunk.generate_device(buf.data_ptr(), size, pbschunk.GEN_RANDOM if kind == "random" else pbschunk.GEN_VMIMAGE,
+                         0x5EED0002 if kind == "random" else 0x5EED0003, 0, st.cuda_stream)
 ch = pbschunk.Chunker(avg)
 ch.set_stream(st.cuda_stream)
 torch.cuda.synchronize()

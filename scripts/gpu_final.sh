@@ -18,6 +18,6 @@ step rocprof_digest 400 rocprofv3 --kernel-trace --stats -d "$R/$O/prof_digest" 
 step pmc_crc 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/$O/pmc_crc" -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline 0 --host-inclusive-gib 0 --digest 1 || exit 1
 python profiles/collect_traffic.py "$O/pmc_crc" --kernel crc32_chunks_kernel --out "$O/traffic_crc.json" > "$O/collect_crc.log" 2>&1
 step examples 300 bash -c "make -s -C examples && examples/test_chunk_speed && examples/test_chunk_speed2 | tail -3 && examples/test_chunk_size | tail -3" || exit 1
-step c2 300 python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-inclusive-gib 0 --size-gib 8 --workload random || exit 1
-step c5 300 python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-inclusive-gib 0 --avg 262144 || exit 1
+step c2 300 python bench.py --steps 50 --warmup 30 --cpu-baseline 0 --host-inclusive-gib 0 --size-gib 8 --workload random || exit 1
+step c5 300 python bench.py --steps 10 --warmup 3 --cpu-baseline 0 --host-inclusive-gib 0 --avg 262144 || exit 1
 echo done
