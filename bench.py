@@ -32,7 +32,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size-gib", type=float, default=64.0)
     ap.add_argument("--avg", type=int, default=4 * 1024 * 1024)
     ap.add_argument("--workload", choices=list(GEN), default="vmimage")
