@@ -106,8 +106,9 @@ const CrcTables* device_tables(int dev) {
     return d;
 }
 
-// work counter of the dynamic chunk order, one per (device, stream): launches on one
-// stream are serialized, so each can reset and use it
+// counters of the dynamic chunk order, one pair per (device, stream): {next chunk, done
+// workgroups}.  Zero when allocated; the last workgroup of each launch zeroes them again,
+// so launches need no reset of their own.
 unsigned long long* stream_counter(int dev, hipStream_t st) {
     static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, unsigned long long*> ctrs;
@@ -115,7 +116,11 @@ unsigned long long* stream_counter(int dev, hipStream_t st) {
     auto it = ctrs.find({dev, st});
     if (it != ctrs.end()) return it->second;
     unsigned long long* d = nullptr;
-    if (hipMalloc(&d, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    if (hipMalloc(&d, 2 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    if (hipMemset(d, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
     ctrs[{dev, st}] = d;
     return d;
 }
@@ -243,6 +248,14 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_chunks_kernel(
             k += gridDim.x;
         }
     }
+    if (next_ctr && tid == 0) {  // the last workgroup out zeroes the counters
+        __threadfence();
+        if (atomicAdd(&next_ctr[1], 1ull) == gridDim.x - 1) {
+            next_ctr[0] = 0;
+            next_ctr[1] = 0;
+            __threadfence();
+        }
+    }
 }
 
 }  // namespace
@@ -268,7 +281,6 @@ extern "C" int pbs_crc32_chunks_async(const uint8_t* dev_data, size_t data_len, 
     if (n > grid && !(e && e[0] == '0')) {
         ctr = stream_counter(dev, (hipStream_t)hip_stream);
         if (!ctr) return PBS_ERR_NOMEM;
-        if (hipMemsetAsync(ctr, 0, sizeof(*ctr), (hipStream_t)hip_stream) != hipSuccess) return PBS_ERR_HIP;
     }
     hipLaunchKernelGGL(crc32_chunks_kernel, dim3(grid), dim3(kCrcThreads), 0, (hipStream_t)hip_stream,
                        dev_data, base, bounds_dev, order_dev, (uint64_t)n, tab, crcs_dev, ctr);
