@@ -98,7 +98,10 @@ const CrcTables* device_tables(int dev) {
     }
     CrcTables* d = nullptr;
     if (hipMalloc(&d, sizeof(CrcTables)) != hipSuccess) return nullptr;
-    if (hipMemcpy(d, &host, sizeof(CrcTables), hipMemcpyHostToDevice) != hipSuccess) {
+    // landed before any launch on a non-blocking stream (which does not wait for the
+    // null stream the copy runs on)
+    if (hipMemcpy(d, &host, sizeof(CrcTables), hipMemcpyHostToDevice) != hipSuccess ||
+        hipStreamSynchronize(nullptr) != hipSuccess) {
         (void)hipFree(d);
         return nullptr;
     }
@@ -117,7 +120,10 @@ unsigned long long* stream_counter(int dev, hipStream_t st) {
     if (it != ctrs.end()) return it->second;
     unsigned long long* d = nullptr;
     if (hipMalloc(&d, 2 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
-    if (hipMemset(d, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
+    // zeroed on THAT stream: a plain hipMemset runs on the null stream, which a
+    // non-blocking stream (torch's) does not wait for -- the first launch could read
+    // the fresh allocation's garbage (tests/test_gpu_blob.py::test_back_to_back_...)
+    if (hipMemsetAsync(d, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) {
         (void)hipFree(d);
         return nullptr;
     }

@@ -803,7 +803,10 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
             t[i] = rotl32(kBuzhashTable[i], kScanFrame == 1 ? prm.rot : prm.rot + 1);
             t[256 + i] = rotl32(kBuzhashTable[i], prm.rot);
         }
-        ok = hipMemcpy(c->d_table.p, t, sizeof(t), hipMemcpyHostToDevice) == hipSuccess;
+        // landed before any launch on the handle's stream, which may be a non-blocking
+        // stream that does not wait for the null stream
+        ok = hipMemcpy(c->d_table.p, t, sizeof(t), hipMemcpyHostToDevice) == hipSuccess &&
+             hipStreamSynchronize(nullptr) == hipSuccess;
     }
     if (!ok) {
         destroy(c);

@@ -113,3 +113,28 @@ def test_async_form_and_order(gpu, oracle, torch_dev):
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32)
     assert np.array_equal(got, oracle.chunk_crcs(data, bounds))
+
+
+def test_back_to_back_launches_one_stream(gpu, oracle, torch_dev):
+    """The dynamic chunk order's counters reset themselves at the end of each launch:
+    three launches of different sizes queued back to back on one stream (and one on a
+    second stream), one sync, all results exact."""
+    torch = torch_dev
+    rng = np.random.default_rng(9)
+    data = gen_np.gen_random(96 * MiB, 17)
+    t, ptr = _dev(torch, data)
+    s2 = torch.cuda.Stream()
+    runs = []
+    for k, (nchunks, stream) in enumerate([(5000, 0), (20000, 0), (300, 0), (7000, s2.cuda_stream)]):
+        lens = rng.integers(1, 4000, size=nchunks)
+        bounds = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + np.uint64(k * 1000)
+        assert int(bounds[-1]) <= data.size
+        b_dev = torch.from_numpy(bounds.view(np.int64)).to("cuda")
+        out = torch.zeros(nchunks, dtype=torch.int32, device="cuda")
+        runs.append((bounds, b_dev, out, stream, nchunks))
+    torch.cuda.synchronize()  # inputs in place; then the four launches without a sync between
+    for bounds, b_dev, out, stream, nchunks in runs:
+        gpu.crc32_chunks_async(ptr, data.size, b_dev.data_ptr(), 0, nchunks, out.data_ptr(), hip_stream=stream)
+    torch.cuda.synchronize()
+    for bounds, _, out, _, _ in runs:
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle.chunk_crcs(data, bounds))
