@@ -89,7 +89,11 @@ uint64_t pbs_chunker_chunk_start(const pbs_chunker *c);
 /* Start a new stream with the same average (what `Chunker::new` would give). */
 int pbs_chunker_reset(pbs_chunker *c);
 
-/* Run the handle's kernels on this hipStream_t (NULL = the handle's own stream). */
+/* Run the handle's kernels on this hipStream_t (NULL = the handle's own stream).  The
+ * handle's own stream is non-blocking: it does not wait for work on the null stream or
+ * any other stream, so device input written there (find_cuts_device, the sharded entry
+ * points) must be complete before the call -- synchronize, or set the producing stream
+ * here (what bench.py and the tests do with torch's current stream). */
 int pbs_chunker_set_stream(pbs_chunker *c, void *hip_stream);
 
 /* Number of CUs the persistent scan kernel sizes its grid for (default: all of the
