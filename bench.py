@@ -11,10 +11,19 @@ collective; an all-reduce (RCCL) of the per-rank elapsed time (MAX) and byte cou
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size-gib 64] [--avg 4194304]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+``--gpus N`` without a launcher (no WORLD_SIZE in the environment) starts N rank
+processes itself (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set per child, 127.0.0.1) before
+anything touches the GPU, and fails (exit 2) when fewer than N devices are visible or
+when WORLD_SIZE disagrees with --gpus.  ``--cpu-standin`` runs the same launch,
+barrier and MAX/SUM aggregation with gloo and the CPU oracle as the step (tests only:
+its line says so and is never a GPU measurement).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -40,8 +49,16 @@ def parse():
                     help="streams: one independent stream per GPU (config 4); "
                          "sharded: one stream split over the GPUs")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-sample-mib", type=int, default=512)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (0 = nproc: every CPU this process may run on)")
+    ap.add_argument("--cpu-sample-mib", type=int, default=512,
+                    help="bytes each CPU-baseline thread chunks (windows of one shared sample)")
+    ap.add_argument("--cpu-config1", type=int, default=1,
+                    help="also time BASELINE config 1 on the CPU (1 GiB LE-u32 counter @ 64 KiB, "
+                         "1 GiB random @ 4 MiB; 1 thread and nproc threads)")
+    ap.add_argument("--cpu-standin", action="store_true",
+                    help="TEST ONLY: gloo + the CPU oracle as the step (exercises the N-rank "
+                         "launcher and aggregation without a GPU)")
     ap.add_argument("--host-inclusive-gib", type=float, default=4.0,
                     help="also time the host-buffer path (H2D + kernels + D2H) on this many GiB; 0 = skip")
     ap.add_argument("--digest", type=int, default=0,
@@ -75,43 +92,96 @@ def aggregate(elapsed: float, nbytes: int, dist, device):
     return float(mx.item()), float(tot.item())
 
 
-def cpu_baseline(args, workload, seed, avg):
-    """The oracle (faithful C restatement of chunker.rs) on the host cores, on a bounded
-    sample of the same stream: `threads` threads each chunk their own sample slice."""
+def cpu_info():
+    """(CPUs this process may run on = nproc, cgroup CPU quota or None, CPU model)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = f.read().split("model name")[1].split("\n")[0].split(":", 1)[-1].strip()
+    except (OSError, IndexError):
+        pass
+    return n, quota, model
+
+
+def cpu_threads(args) -> int:
+    return args.cpu_threads if args.cpu_threads > 0 else cpu_info()[0]
+
+
+def time_oracle(oracle, avg: int, sample, per: int, threads: int):
+    """The oracle (gcc -O2 restatement of chunker.rs) on the host cores: one thread over
+    sample[:per], then `threads` threads each over its own `per`-byte window of the
+    shared read-only sample (windows start at different offsets: independent streams,
+    bounded memory).  Returns (1-thread GiB/s, aggregate GiB/s)."""
+    t0 = time.perf_counter()
+    oracle.chunk_feed(avg, sample[:per])
+    single = per / (1 << 30) / (time.perf_counter() - t0)
+    span = sample.size - per
+    offs = [(t * span // max(1, threads)) // 4096 * 4096 for t in range(threads)]
+    ths = [threading.Thread(target=oracle.chunk_feed, args=(avg, sample[o:o + per])) for o in offs]
+    t0 = time.perf_counter()
+    [t.start() for t in ths]
+    [t.join() for t in ths]  # ctypes releases the GIL
+    agg = threads * per / (1 << 30) / (time.perf_counter() - t0)
+    return single, agg
+
+
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
     import oracle
+    return oracle
 
-    n = args.cpu_sample_mib * 1024 * 1024
-    gen = {"counter": lambda o: oracle.gen_counter(n, o),
-           "random": lambda o: oracle.gen_random(n, seed, o),
-           "vmimage": lambda o: oracle.gen_vmimage(n, seed, o)}[workload]
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    bufs = [None] * threads
 
-    def mk(t):
-        bufs[t] = gen(t * n)
-
-    ths = [threading.Thread(target=mk, args=(t,)) for t in range(threads)]
-    [t.start() for t in ths]
-    [t.join() for t in ths]
-    # single thread, one slice
-    t0 = time.perf_counter()
-    oracle.chunk_feed(avg, bufs[0])
-    single = n / (1 << 30) / (time.perf_counter() - t0)
-    # all threads, independent slices (ctypes releases the GIL)
-    ths = [threading.Thread(target=oracle.chunk_feed, args=(avg, bufs[t])) for t in range(threads)]
-    t0 = time.perf_counter()
-    [t.start() for t in ths]
-    [t.join() for t in ths]
-    agg = threads * n / (1 << 30) / (time.perf_counter() - t0)
-    cpu = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].split(":", 1)[-1].strip() \
-        if os.path.exists("/proc/cpuinfo") else "unknown"
-    del bufs
+def cpu_baseline(args, workload, seed, avg):
+    """The oracle on the host cores on a bounded sample of the same stream (bench's
+    workload, seed, average): nproc threads by default (--cpu-threads)."""
+    oracle = _oracle()
+    per = args.cpu_sample_mib << 20
+    gen = {"counter": lambda n: oracle.gen_counter(n, 0),
+           "random": lambda n: oracle.gen_random(n, seed, 0),
+           "vmimage": lambda n: oracle.gen_vmimage(n, seed, 0)}[workload]
+    sample = gen(2 * per)
+    threads = cpu_threads(args)
+    single, agg = time_oracle(oracle, avg, sample, per, threads)
+    n, quota, model = cpu_info()
+    del sample
     return {"value": round(agg, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{threads} x {args.cpu_sample_mib} MiB slices of the same {workload} stream, "
-                      f"whole-buffer scan loop (oracle/chunker_oracle.c, gcc -O2); "
-                      f"1 thread: {single:.3f} GiB/s; host CPU: {cpu}"}
+            "sample": f"{threads} threads x {args.cpu_sample_mib} MiB windows of one "
+                      f"{2 * args.cpu_sample_mib} MiB {workload} sample (seed {hex(seed)}), "
+                      f"whole-buffer scan loop (oracle/chunker_oracle.c, gcc -O2); 1 thread: "
+                      f"{single:.3f} GiB/s; nproc {n}, os.cpu_count {os.cpu_count()}, cgroup "
+                      f"quota {quota if quota is not None else 'none'} CPUs; host CPU: {model}",
+            "single_thread_gib_s": round(single, 3)}
+
+
+def cpu_config1(args):
+    """BASELINE config 1 (CPU only): the reference's "pseudo-random" buffer -- 1 GiB
+    LE-u32 counter, byte[4i+j] = (i >> 8j) & 0xff (examples/test_chunk_speed.rs:8-14) --
+    at its 64 KiB average (:15), and 1 GiB seeded random at the 4 MiB default; the
+    oracle with 1 thread over the whole GiB and nproc threads over 512 MiB windows."""
+    oracle = _oracle()
+    threads = cpu_threads(args)
+    out = {"unit": "GiB/s", "threads": threads,
+           "reference_published": "about 830MB/s: ChunkStream over 1 GiB of /dev/urandom at "
+                                  "4 MiB (examples/test_chunk_speed2.rs:13)"}
+    for name, mk, avg in (("counter_1GiB_avg64K", lambda: oracle.gen_counter(1 << 30, 0), 64 << 10),
+                          ("random_1GiB_avg4M", lambda: oracle.gen_random(1 << 30, 0x5EED0001, 0), 4 << 20)):
+        buf = mk()
+        t0 = time.perf_counter()
+        cuts = oracle.chunk_feed(avg, buf)
+        one = buf.size / (1 << 30) / (time.perf_counter() - t0)
+        _, agg = time_oracle(oracle, avg, buf, 512 << 20, threads)
+        out[name] = {"1_thread": round(one, 3), "aggregate": round(agg, 3), "chunks": int(cuts.size)}
+        del buf
+    return out
 
 
 def digest_stage(args, buf, cuts, stream, reps: int = 3):
@@ -158,7 +228,7 @@ def digest_stage(args, buf, cuts, stream, reps: int = 3):
     take = max(1, min(n, take))
     host = buf[: int(bounds[take])].cpu().numpy()
     mv = memoryview(host)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = cpu_threads(args)
     parts = [list(range(k, take, threads)) for k in range(threads)]
 
     def work(ix):
@@ -241,8 +311,7 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
 
     import pbschunk
 
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+    oracle = _oracle()
 
     n = int(args.pipeline_gib * (1 << 30)) // 8 * 8
     host = buf[:n].cpu().numpy()  # pageable, untimed
@@ -251,7 +320,7 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
     ends, dig, crcs, t = pbschunk.pipeline_host(host, args.avg, piece=piece, crc=True)
     wall = time.perf_counter() - t0
     # CPU path: threads chunk their own slice and hash its chunks (hashlib/OpenSSL)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = cpu_threads(args)
     per = (256 << 20)
 
     def work(k):
@@ -279,14 +348,134 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
                              "sample": f"{nth} x 256 MiB slices: chunk_feed then sha256 + crc32 per chunk"}}
 
 
+def free_port() -> int:
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: N rank processes of this script (one per GPU),
+    started before anything touches the GPU; returns the job's exit code.  A rank that
+    fails ends the others (they would wait in the barrier)."""
+    n = args.gpus
+    if not args.cpu_standin:
+        import torch
+        have = torch.cuda.device_count()  # counts devices without initialising HIP
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc, live = 0, list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in live:
+                    q.kill()  # our own children, by PID
+        time.sleep(0.1)
+    return rc
+
+
+def timed_steps(step, args, dist, sync, after=None):
+    """W untimed warm-up steps, then exactly K steps bracketed by a barrier + device sync
+    on both sides.  Returns (this rank's elapsed seconds, last step's result)."""
+    for _ in range(args.warmup):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = step()
+        if after:
+            after(res)
+    sync()
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0, res
+
+
+def per_rank_records(rec: dict, dist, world: int):
+    if dist is None:
+        return [rec]
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return out
+
+
+def base_line(args, metric, value, world, elapsed, scaling, dtype, data, config):
+    return {"metric": metric, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 4), "higher_is_better": True,
+            "scaling": scaling, "vs_baseline": None, "dtype": dtype, "data": data, "config": config}
+
+
+def standin_main(args, world: int, rank: int):
+    """TEST ONLY (--cpu-standin): the launcher, barrier and MAX/SUM aggregation of the GPU
+    path with gloo, every rank chunking its own stream (seed + rank) with the CPU oracle."""
+    import torch
+
+    oracle = _oracle()
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    size = int(args.size_gib * (1 << 30)) // 8 * 8
+    seed = stream_seed(args.workload, rank)
+    buf = {"counter": lambda: oracle.gen_counter(size, 0),
+           "random": lambda: oracle.gen_random(size, seed, 0),
+           "vmimage": lambda: oracle.gen_vmimage(size, seed, 0)}[args.workload]()
+    elapsed, cuts = timed_steps(lambda: oracle.chunk_feed(args.avg, buf), args, dist, lambda: None)
+    recs = per_rank_records({"rank": rank, "seed": seed, "elapsed_s": elapsed, "bytes": size,
+                             "chunks": int(cuts.size)}, dist, world)
+    mx, total = aggregate(elapsed, size, dist, torch.device("cpu"))
+    if rank == 0:
+        out = base_line(args, "STAND-IN (CPU oracle over gloo, not a GPU measurement): GiB/s chunked",
+                        total * args.steps / (1 << 30) / mx, world, mx, "weak", "u8",
+                        f"synthetic ({args.workload}, seed {hex(SEEDS[args.workload])}+rank)",
+                        {"workload": f"{args.workload}-{args.size_gib:g}GiB-avg{args.avg}",
+                         "stream_bytes_per_rank": size})
+        out["stand_in"] = True
+        out["per_rank"] = recs
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cpu_standin:
+        standin_main(args, world, rank)
+        return
     import numpy as np
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.device_count() < max(world, local + 1):
+        print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible",
+              file=sys.stderr)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -305,16 +494,16 @@ def main():
     if args.mode == "sharded":
         import shard
         seed = SEEDS[args.workload]  # one stream; this rank generates its range of it
-        base, local = shard.shard_ranges(size, world)[rank]
-        buf = torch.empty(local, dtype=torch.uint8, device=dev)
-        pbschunk.generate_device(buf.data_ptr(), local, GEN[args.workload], seed, base,
+        base, local_len = shard.shard_ranges(size, world)[rank]
+        buf = torch.empty(local_len, dtype=torch.uint8, device=dev)
+        pbschunk.generate_device(buf.data_ptr(), local_len, GEN[args.workload], seed, base,
                                  stream.cuda_stream)
         torch.cuda.synchronize()
-        ptr, tail = buf.data_ptr(), buf[max(0, local - shard.HALO):]
+        ptr, tail = buf.data_ptr(), buf[max(0, local_len - shard.HALO):]
 
         def step():
-            return shard.chunk_sharded(ch, ptr, local, base, size, tail, dist, rank, world, dev)
-        work_bytes = local
+            return shard.chunk_sharded(ch, ptr, local_len, base, size, tail, dist, rank, world, dev)
+        work_bytes = local_len
     else:
         seed = stream_seed(args.workload, rank)
         buf = torch.empty(size, dtype=torch.uint8, device=dev)
@@ -327,36 +516,34 @@ def main():
             return ch.find_cuts_device(ptr, size, is_final=True)
         work_bytes = size
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    scan_ms, ncuts, cand = [], 0, 0
-    for _ in range(args.steps):
-        cuts = step()
+    scan_ms, last = [], {}
+
+    def after(cuts):
         t = ch.last_timing()
         scan_ms.append(t["scan_ms"])
-        ncuts, cand = int(cuts.size), int(t["candidates"])
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+        last.update(t, ncuts=int(cuts.size))
+
+    elapsed, cuts = timed_steps(step, args, dist, torch.cuda.synchronize, after)
+    recs = per_rank_records({"rank": rank, "seed": seed, "elapsed_s": round(elapsed, 6),
+                             "bytes": work_bytes, "chunks": last.get("ncuts", 0)}, dist, world)
     elapsed, total_bytes = aggregate(elapsed, work_bytes, dist, dev)
 
-    step_s = elapsed / max(1, args.steps)
     value = total_bytes * args.steps / (1 << 30) / elapsed
     avg_scan_s = float(np.mean(scan_ms)) / 1e3 if scan_ms else float("nan")
     achieved = work_bytes / avg_scan_s / 1e9  # algorithmic bytes (input read once) per launch
-    traffic = None
+    traffic, traffic_note = None, "no PMC record"
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if (tj.get("size") == work_bytes and tj.get("avg") == args.avg
-                and tj.get("workload") == args.workload and args.mode == "streams"):
+        bid = pbschunk.build_id()
+        if tj.get("build_id") != bid:
+            traffic_note = f"PMC record is of build {tj.get('build_id')}, this is {bid}: not reported"
+        elif not (tj.get("size") == work_bytes and tj.get("avg") == args.avg
+                  and tj.get("workload") == args.workload and args.mode == "streams"):
+            traffic_note = "PMC record is of another workload"
+        else:
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_note = f"rocprofv3 FETCH_SIZE x 1024 x 2, build {bid}"
     except (OSError, ValueError):
         pass
 
@@ -381,29 +568,23 @@ def main():
     metric = METRIC if default_cfg else (
         f"GiB/s chunked (device-resident), {args.avg >> 10} KiB mean, {args.size_gib:g} GiB "
         f"{args.workload} stream ({args.mode}); boundaries bit-exact")
-    out = {
-        "metric": metric,
-        "value": round(value, 3),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(step_s * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak" if args.mode == "streams" else "strong",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": f"synthetic ({args.workload} generator, seed {hex(SEEDS[args.workload])}+rank, "
-                f"generated in HBM before timing)",
-        "config": {"workload": f"{args.workload}-{args.size_gib:g}GiB-avg{args.avg}",
-                   "stream_bytes_per_gpu": work_bytes, "avg_chunk": args.avg,
-                   "parallelism": (f"independent stream per GPU x{world}" if args.mode == "streams"
-                                   else f"one stream sharded over {world} GPU(s)"),
-                   "chunks_per_stream": ncuts, "candidates_per_stream": cand},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "scan_main_kernel", "avg_launch_ms": round(avg_scan_s * 1e3, 4)},
-    }
+    out = base_line(
+        args, metric, value, world, elapsed, "weak" if args.mode == "streams" else "strong", "u8",
+        f"synthetic ({args.workload} generator, seed {hex(SEEDS[args.workload])}+rank, "
+        f"generated in HBM before timing)",
+        {"workload": f"{args.workload}-{args.size_gib:g}GiB-avg{args.avg}",
+         "stream_bytes_per_gpu": work_bytes, "avg_chunk": args.avg,
+         "parallelism": (f"independent stream per GPU x{world}" if args.mode == "streams"
+                         else f"one stream sharded over {world} GPU(s)"),
+         "chunks_per_stream": last.get("ncuts", 0),
+         "candidates_per_stream": int(last.get("candidates", 0))})
+    out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                       "traffic_note": traffic_note, "kernel": "scan_main_kernel",
+                       "avg_launch_ms": round(avg_scan_s * 1e3, 4)}
+    out["build_id"] = pbschunk.build_id()
+    if world > 1:
+        out["per_rank"] = recs
     if host_incl is not None:
         out["host_inclusive_gib_s"] = round(host_incl, 3)
     if args.digest and args.mode == "streams":
@@ -413,6 +594,8 @@ def main():
     if args.cpu_baseline and world == 1:
         del buf
         out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)
+        if args.cpu_config1:
+            out["cpu_config1"] = cpu_config1(args)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

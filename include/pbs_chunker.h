@@ -161,6 +161,11 @@ int pbs_device_count(void);
 /* Copy of the library's Buzhash table (256 entries), for the digest check. */
 int pbs_table_copy(uint32_t *out256);
 
+/* Digest (16 hex digits) of the sources this library was built from (csrc/ and
+ * include/); bench.py reports a PMC traffic record only when it was measured on the
+ * same build. */
+const char *pbs_build_id(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,9 @@
 """Derive HBM read bytes per scan_main_kernel launch from a rocprofv3 --pmc FETCH_SIZE
 run of bench.py and write profiles/traffic_latest.json (read by bench.py).
 
+The record carries the library's build id (pbs_build_id, a digest of its sources):
+bench.py reports the traffic only for the same build.
+
 FETCH_SIZE is in KiB; on gfx950 it reports exactly half the bytes of a wide coalesced
 streaming read (MI355X_MICROARCH.md "HBM"), so bytes = FETCH_SIZE * 1024 * 2.
 
@@ -14,6 +17,9 @@ import glob
 import json
 import os
 import statistics
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "proxmox-backup_amd"))
 
 ap = argparse.ArgumentParser()
 ap.add_argument("pmc_dir")
@@ -37,7 +43,9 @@ if not vals:
     raise SystemExit(f"no {a.kernel} FETCH_SIZE rows found")
 kib = statistics.median(vals)
 size = int(a.size_gib * (1 << 30)) // 8 * 8
-out = {"size": size, "avg": a.avg, "workload": a.workload, "dispatches": len(vals),
+import pbschunk  # noqa: E402  (the library the PMC run loaded: no device call)
+
+out = {"build_id": pbschunk.build_id(), "kernel": a.kernel, "size": size, "avg": a.avg, "workload": a.workload, "dispatches": len(vals),
        "fetch_size_kib_median": kib, "hbm_bytes_per_launch": int(kib * 1024 * 2),
        "ratio_to_algorithmic": kib * 1024 * 2 / size,
        "note": "FETCH_SIZE x 1024 x 2 (gfx950 half-count correction), median over dispatches"}

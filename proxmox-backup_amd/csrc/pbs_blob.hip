@@ -41,6 +41,7 @@
 
 #include "pbs_blob.h"
 #include "pbs_chunker.h"
+#include "pbs_chunker_internal.h"
 
 namespace pbs {
 namespace {
@@ -96,40 +97,58 @@ const CrcTables* device_tables(int dev) {
         make_tables(host);
         made = true;
     }
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     CrcTables* d = nullptr;
-    if (hipMalloc(&d, sizeof(CrcTables)) != hipSuccess) return nullptr;
+    bool ok = hipMalloc(&d, sizeof(CrcTables)) == hipSuccess;
     // landed before any launch on a non-blocking stream (which does not wait for the
     // null stream the copy runs on)
-    if (hipMemcpy(d, &host, sizeof(CrcTables), hipMemcpyHostToDevice) != hipSuccess ||
-        hipStreamSynchronize(nullptr) != hipSuccess) {
+    if (ok && (hipMemcpy(d, &host, sizeof(CrcTables), hipMemcpyHostToDevice) != hipSuccess ||
+               hipStreamSynchronize(nullptr) != hipSuccess)) {
         (void)hipFree(d);
-        return nullptr;
+        ok = false;
     }
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ok) return nullptr;
     tabs[dev] = d;
     return d;
 }
 
-// counters of the dynamic chunk order, one pair per (device, stream): {next chunk, done
-// workgroups}.  Zero when allocated; the last workgroup of each launch zeroes them again,
-// so launches need no reset of their own.
-unsigned long long* stream_counter(int dev, hipStream_t st) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, unsigned long long*> ctrs;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = ctrs.find({dev, st});
-    if (it != ctrs.end()) return it->second;
+// counter of the dynamic chunk order, one per stream, allocated on the stream's own
+// device and zeroed by a 8-byte memset on that stream before every launch (launches on
+// one stream are ordered, so a counter is never shared by two running launches, and an
+// aborted launch cannot leave a stale value behind).  release_stream_counter() frees
+// a stream's entry before the stream is destroyed (pbs_pipeline.cpp).
+std::mutex g_ctr_mu;
+std::map<hipStream_t, unsigned long long*> g_ctrs;
+
+unsigned long long* stream_counter(hipStream_t st, int dev) {
+    std::lock_guard<std::mutex> g(g_ctr_mu);
+    auto it = g_ctrs.find(st);
+    if (it != g_ctrs.end()) return it->second;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     unsigned long long* d = nullptr;
-    if (hipMalloc(&d, 2 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
-    // zeroed on THAT stream: a plain hipMemset runs on the null stream, which a
-    // non-blocking stream (torch's) does not wait for -- the first launch could read
-    // the fresh allocation's garbage (tests/test_gpu_blob.py::test_back_to_back_...)
-    if (hipMemsetAsync(d, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) {
-        (void)hipFree(d);
-        return nullptr;
-    }
-    ctrs[{dev, st}] = d;
+    const bool ok = hipMalloc(&d, sizeof(unsigned long long)) == hipSuccess;
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ok) return nullptr;
+    g_ctrs[st] = d;
     return d;
 }
+
+}  // namespace
+
+void release_stream_counter(hipStream_t st) {
+    std::lock_guard<std::mutex> g(g_ctr_mu);
+    auto it = g_ctrs.find(st);
+    if (it == g_ctrs.end()) return;
+    (void)hipFree(it->second);
+    g_ctrs.erase(it);
+}
+
+namespace {
 
 // byte p of the chunk's message: zero outside [as, ae), the first four bytes XOR 0xFF
 __device__ __forceinline__ uint32_t msg_byte(uintptr_t p, uintptr_t as, uintptr_t ae) {
@@ -254,14 +273,6 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_chunks_kernel(
             k += gridDim.x;
         }
     }
-    if (next_ctr && tid == 0) {  // the last workgroup out zeroes the counters
-        __threadfence();
-        if (atomicAdd(&next_ctr[1], 1ull) == gridDim.x - 1) {
-            next_ctr[0] = 0;
-            next_ctr[1] = 0;
-            __threadfence();
-        }
-    }
 }
 
 }  // namespace
@@ -274,8 +285,11 @@ extern "C" int pbs_crc32_chunks_async(const uint8_t* dev_data, size_t data_len, 
                                       uint32_t* crcs_dev, void* hip_stream) {
     if (n == 0) return PBS_OK;
     if (!bounds_dev || !crcs_dev || (data_len && !dev_data)) return PBS_ERR_INVALID;
+    // the stream's own device (not the calling thread's current one) holds the tables and
+    // the counter
+    const hipStream_t st = (hipStream_t)hip_stream;
     int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
+    if (hipStreamGetDevice(st, &dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return PBS_ERR_NO_DEVICE;
     const CrcTables* tab = device_tables(dev);
@@ -285,8 +299,9 @@ extern "C" int pbs_crc32_chunks_async(const uint8_t* dev_data, size_t data_len, 
     const char* e = std::getenv("PBS_CRC_DYN");  // A/B knob
     unsigned long long* ctr = nullptr;
     if (n > grid && !(e && e[0] == '0')) {
-        ctr = stream_counter(dev, (hipStream_t)hip_stream);
+        ctr = stream_counter(st, dev);
         if (!ctr) return PBS_ERR_NOMEM;
+        if (hipMemsetAsync(ctr, 0, sizeof(unsigned long long), st) != hipSuccess) return PBS_ERR_HIP;
     }
     hipLaunchKernelGGL(crc32_chunks_kernel, dim3(grid), dim3(kCrcThreads), 0, (hipStream_t)hip_stream,
                        dev_data, base, bounds_dev, order_dev, (uint64_t)n, tab, crcs_dev, ctr);

@@ -121,7 +121,9 @@ struct pbs_chunker {
     hipStream_t stream = nullptr;
     DevBuf d_table, d_pre, d_counters, d_susp, d_cand, d_C, d_sort_tmp, d_nxt, d_jtmp, d_nf, d_on,
         d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in, d_stage, d_hits;
-    uint32_t susp_cap = 0, cand_cap = 0;
+    uint64_t susp_cap = 0, cand_cap = 0;
+    uint64_t batch_limit = 0;  // bytes per batch (0 = batch_max); shrunk when a batch is too dense
+    bool too_dense = false;    // the last scan found more than kMaxBatchCand candidates
     uint64_t* h_small = nullptr;  // pinned + mapped: [0] counters, [8..19] results, [24..31] tail
     uint64_t* h_cuts = nullptr;   // pinned + mapped: cut list of the small resolve
     uint64_t* h_keep = nullptr;   // pinned + mapped: open-chunk candidates of the small resolve
@@ -151,10 +153,15 @@ constexpr uint64_t kHostCuts = 1ull << 20;  // h_cuts entries (8 MiB)
 constexpr uint64_t kHostKeep = 1ull << 16;  // h_keep entries
 constexpr size_t kSmallBytes = 256;         // h_small bytes
 
-uint64_t batch_max(const Params& p) {
-    // keep 32-bit candidate counters safe for tiny averages
-    if (p.avg >= 4096) return 1ull << 40;
-    return 1ull << 30;
+// Candidates one batch may hold (the lists and the multi-kernel resolve's node arrays,
+// ~60 B per candidate, stay < 8 GiB).  Candidates are bounded by the bytes, not by the
+// average: data whose window hash passes the test with a short period makes every
+// period-th byte one, so a denser batch is redone at a quarter of its length.
+constexpr uint64_t kMaxBatchCand = 1ull << 27;
+
+uint64_t batch_max(const pbs_chunker* c) {
+    const uint64_t cap = c->prm.avg >= 4096 ? 1ull << 40 : 1ull << 30;
+    return c->batch_limit ? std::min(cap, c->batch_limit) : cap;
 }
 
 // Phase A over d_data[0..len) (stream offset `base`): scan_main_kernel flags blocks,
@@ -179,10 +186,9 @@ ScanPlan plan_scan(pbs_chunker* c, uint64_t len) {
     sp.ext_count = (len - covered + kBlockBytes - 1) / kBlockBytes;
     sp.blocks = (len + kBlockBytes - 1) / kBlockBytes;
     const uint64_t expected = len / p.avg * 3 / 2 + 1;
-    const uint32_t want_s = (uint32_t)std::min<uint64_t>(
-        std::min<uint64_t>(sp.blocks + 2, expected * 4 + 4096), 0xFFFFFFF0u);
-    const uint32_t want_c =
-        (uint32_t)std::min<uint64_t>(std::min<uint64_t>(len + 1, expected * 2 + 8192), 0xFFFFFFF0u);
+    const uint64_t want_s = std::min<uint64_t>(sp.blocks + 2, expected * 4 + 4096);
+    const uint64_t want_c =
+        std::min<uint64_t>(std::min<uint64_t>(len + 1, expected * 2 + 8192), kMaxBatchCand);
     c->susp_cap = std::max(c->susp_cap, want_s);
     c->cand_cap = std::max(c->cand_cap, want_c);
     return sp;
@@ -197,16 +203,17 @@ int scan_launch(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t ba
                                   c->stream));
     HIP_TRY(c, c->d_susp.ensure((size_t)c->susp_cap * 8));
     HIP_TRY(c, c->d_cand.ensure((size_t)c->cand_cap * 8));
-    HIP_TRY(c, c->d_counters.ensure(16));
-    HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 16, c->stream));
-    uint32_t* d_nsusp = c->d_counters.as<uint32_t>();
-    uint32_t* d_ncand = d_nsusp + 1;
+    // counters: [0] suspects, [1] candidates (u64), [2] scan_main's tile counter (u32)
+    HIP_TRY(c, c->d_counters.ensure(24));
+    HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 24, c->stream));
+    unsigned long long* d_nsusp = c->d_counters.as<unsigned long long>();
+    unsigned long long* d_ncand = d_nsusp + 1;
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, launch_scan_main(d_data, sp.ntiles, sp.seg, c->d_table.as<uint32_t>(), p.thr,
                                 c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu, c->stream,
-                                d_nsusp + 2, sp.dyn, sp.t_big));
+                                reinterpret_cast<uint32_t*>(d_nsusp + 2), sp.dyn, sp.t_big));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
-    const uint64_t max_items = (uint64_t)c->susp_cap + 1 + sp.ext_count;
+    const uint64_t max_items = c->susp_cap + 1 + sp.ext_count;
     HIP_TRY(c, launch_scan_exact(d_data, len, c->d_pre.as<uint8_t>(), c->carry_len,
                                  c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, sp.ext_first,
                                  sp.ext_count, sp.head, p.mask, p.minimum, base,
@@ -215,22 +222,28 @@ int scan_launch(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t ba
     HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
     // (the speculative batch has resolve_small write them instead: one copy less)
     if (copy_counts)
-        HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_counters.p, 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream));
     return PBS_OK;
 }
 
 // After the sync: *ok = false (and the capacities grown) when a list overflowed.
-int scan_collect(pbs_chunker* c, uint64_t len, const ScanPlan& sp, uint32_t* nsusp_out,
-                 uint32_t* ncand_out, bool* ok) {
-    const uint32_t* cnt = reinterpret_cast<const uint32_t*>(c->h_small);
-    const uint32_t nsusp = cnt[0], ncand = cnt[1];
+int scan_collect(pbs_chunker* c, uint64_t len, const ScanPlan& sp, uint64_t* nsusp_out,
+                 uint64_t* ncand_out, bool* ok) {
+    const uint64_t nsusp = c->h_small[0], ncand = c->h_small[1];
     *ok = true;
+    if (ncand > kMaxBatchCand) {  // the caller redoes the batch shorter (too_dense)
+        c->too_dense = true;
+        *ok = false;
+        *nsusp_out = nsusp;
+        *ncand_out = ncand;
+        return PBS_OK;
+    }
     if (nsusp > c->susp_cap) {
-        c->susp_cap = (uint32_t)std::min<uint64_t>((uint64_t)nsusp * 2 + 1024, sp.blocks + 2);
+        c->susp_cap = std::min<uint64_t>(nsusp * 2 + 1024, sp.blocks + 2);
         *ok = false;
     }
     if (ncand > c->cand_cap) {
-        c->cand_cap = (uint32_t)std::min<uint64_t>((uint64_t)ncand * 2 + 1024, 0xFFFFFFF0u);
+        c->cand_cap = std::min<uint64_t>(ncand * 2 + 1024, kMaxBatchCand);
         *ok = false;
     }
     *nsusp_out = nsusp;
@@ -248,7 +261,7 @@ int scan_collect(pbs_chunker* c, uint64_t len, const ScanPlan& sp, uint32_t* nsu
 }
 
 int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t base,
-                    uint32_t* ncand_out) {
+                    uint64_t* ncand_out) {
     *ncand_out = 0;
     if (!c->prm.hash_cuts || len == 0) return PBS_OK;
     const ScanPlan sp = plan_scan(c, len);
@@ -256,26 +269,28 @@ int scan_candidates(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_
         int rc = scan_launch(c, d_data, len, base, sp);
         if (rc) return rc;
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        uint32_t nsusp = 0;
+        uint64_t nsusp = 0;
         bool ok = false;
         rc = scan_collect(c, len, sp, &nsusp, ncand_out, &ok);
         if (rc) return rc;
         if (ok) return PBS_OK;
+        if (c->too_dense) return PBS_OK;  // caller shrinks the batch
         if (attempt > 4) return fail(c, PBS_ERR_NOMEM);
     }
 }
 
 // Radix-sort c->d_cand[0..n) into dst (device).
-int sort_candidates(pbs_chunker* c, uint32_t n, uint64_t* dst, uint64_t key_end) {
+int sort_candidates(pbs_chunker* c, uint64_t n, uint64_t* dst, uint64_t key_end) {
     if (n == 0) return PBS_OK;
     // keys are stream offsets < key_end: radix passes only over the bits in use
     // (36 bits for a 64 GiB stream: 5 passes instead of 8)
     const int end_bit = key_end > 1 ? 64 - __builtin_clzll(key_end - 1) : 1;
     size_t tb = 0;
-    HIP_TRY(c, sort_u64(nullptr, &tb, c->d_cand.as<uint64_t>(), dst, n, end_bit, c->stream));
+    HIP_TRY(c, sort_u64(nullptr, &tb, c->d_cand.as<uint64_t>(), dst, (uint32_t)n, end_bit, c->stream));
     HIP_TRY(c, c->d_sort_tmp.ensure(tb));
     tb = c->d_sort_tmp.cap;
-    HIP_TRY(c, sort_u64(c->d_sort_tmp.p, &tb, c->d_cand.as<uint64_t>(), dst, n, end_bit, c->stream));
+    HIP_TRY(c, sort_u64(c->d_sort_tmp.p, &tb, c->d_cand.as<uint64_t>(), dst, (uint32_t)n, end_bit,
+                        c->stream));
     return PBS_OK;
 }
 
@@ -537,9 +552,10 @@ void reset_stream(pbs_chunker* c) {
 // append their sorted candidates to the host pending list.
 int scan_host_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos,
                     uint64_t bl) {
-    uint32_t ncand = 0;
+    uint64_t ncand = 0;
     int rc = scan_candidates(c, dsrc, bl, pos, &ncand);
     if (rc) return rc;
+    if (c->too_dense) return PBS_OK;  // nothing changed: the caller redoes a shorter batch
     if (ncand) {
         HIP_TRY(c, c->d_C.ensure(((size_t)ncand + 2) * 8));
         rc = sort_candidates(c, ncand, c->d_C.as<uint64_t>(), pos + bl);
@@ -561,7 +577,7 @@ int scan_host_bytes(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, ui
 // sorts them and runs the multi-kernel resolve) or a list overflowed (rescan).
 int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos,
                uint64_t bl, size_t np, uint64_t rend, uint64_t* out, size_t cap, size_t* n,
-               bool* done, bool* have_cands, uint32_t* nnew) {
+               bool* done, bool* have_cands, uint64_t* nnew) {
     const Params& p = c->prm;
     *done = *have_cands = false;
     const ScanPlan sp = plan_scan(c, bl);
@@ -591,17 +607,17 @@ int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
                                     c->d_nf.as<uint64_t>(), c->d_cuts.as<uint64_t>(), out_cap,
                                     cuts_dev, kHostCuts, keep_dev, kHostKeep,
                                     c->d_res.as<uint64_t>(), small_dev + 8, c->stream,
-                                    c->d_counters.as<uint32_t>(), c->susp_cap, c->cand_cap,
-                                    reinterpret_cast<uint32_t*>(small_dev),
+                                    c->d_counters.as<unsigned long long>(), c->susp_cap,
+                                    c->cand_cap, small_dev,
                                     hsrc ? nullptr : dsrc + bl - tl,
                                     hsrc ? nullptr : reinterpret_cast<uint8_t*>(small_dev + 24),
                                     hsrc ? 0u : (uint32_t)tl));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    uint32_t nsusp = 0;
+    uint64_t nsusp = 0;
     bool ok = false;
     if ((rc = scan_collect(c, bl, sp, &nsusp, nnew, &ok))) return rc;
-    if (!ok) return PBS_OK;  // a list overflowed (capacities grown): rescan
+    if (!ok) return PBS_OK;  // a list overflowed (capacities grown) or too dense: rescan
     if (c->h_small[8 + 12] != 0) {  // resolve stood down: too many keys for one workgroup
         *have_cands = true;
         return PBS_OK;
@@ -629,11 +645,12 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
     bool first = true;
     while (pos < end || first) {
         first = false;
-        const uint64_t bl = std::min<uint64_t>(end > pos ? end - pos : 0, batch_max(c->prm));
+        const uint64_t bl = std::min<uint64_t>(end > pos ? end - pos : 0, batch_max(c));
         const uint64_t rend = bl ? pos + bl : end;  // resolve horizon of this batch
         size_t np = 0;
         while (c->pend_head + np < c->pending.size() && c->pending[c->pend_head + np] < rend) ++np;
-        uint32_t nnew = 0;
+        uint64_t nnew = 0;
+        c->too_dense = false;
         const uint8_t* dsrc = nullptr;
         const uint8_t* hsrc = nullptr;
         if (bl && bl <= kFusedMaxBytes && np + 2 <= kSmallResolveMax) {
@@ -671,9 +688,14 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
                 continue;
             }
         }
-        if (bl && !have_cands) {
+        if (bl && !have_cands && !c->too_dense) {
             int rc = scan_candidates(c, dsrc, bl, pos, &nnew);  // host sync: counts
             if (rc) return rc;
+        }
+        if (c->too_dense) {  // more than kMaxBatchCand candidates: redo a quarter as long
+            if (bl <= (1ull << 20)) return fail(c, PBS_ERR_NOMEM);
+            c->batch_limit = std::max<uint64_t>(1ull << 20, bl / 4);
+            continue;
         }
         const uint64_t m = (uint64_t)np + nnew;
         if (m > 0xFFFFFFF0ull) return fail(c, PBS_ERR_NOMEM);
@@ -692,8 +714,8 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
         uint8_t* tail = reinterpret_cast<uint8_t*>(c->h_small + 24);
         if (tl && device)
             HIP_TRY(c, hipMemcpyAsync(tail, dsrc + bl - tl, tl, hipMemcpyDeviceToHost, c->stream));
-        int rc = small ? run_resolve_small(c, c->d_cand.as<uint64_t>(), (uint32_t)np, nnew, rend,
-                                           out, cap, &n)
+        int rc = small ? run_resolve_small(c, c->d_cand.as<uint64_t>(), (uint32_t)np,
+                                           (uint32_t)nnew, rend, out, cap, &n)
                        : run_resolve(c, (uint32_t)m, rend, out, cap, &n);
         if (rc) return rc;
         if (bl) {
@@ -865,7 +887,7 @@ size_t pbs_chunker_scan(pbs_chunker* c, const uint8_t* data, size_t len) {
         c->timing = pbs_timing{};
         uint64_t pos = c->scanned_end;
         while (pos < end) {
-            const uint64_t bl = std::min<uint64_t>(end - pos, batch_max(c->prm));
+            const uint64_t bl = std::min<uint64_t>(end - pos, batch_max(c));
             const uint8_t* hsrc = data + (pos - c->consumed);
             if (bl <= kFusedMaxBytes) {
                 bool overflow = false;
@@ -883,8 +905,17 @@ size_t pbs_chunker_scan(pbs_chunker* c, const uint8_t* data, size_t len) {
                 fail(c, PBS_ERR_HIP);
                 return SIZE_MAX;
             }
+            c->too_dense = false;
             if (scan_host_bytes(c, c->d_in.as<uint8_t>(), hsrc, pos, bl) != PBS_OK)
                 return SIZE_MAX;
+            if (c->too_dense) {  // redo a quarter as long
+                if (bl <= (1ull << 20)) {
+                    fail(c, PBS_ERR_NOMEM);
+                    return SIZE_MAX;
+                }
+                c->batch_limit = std::max<uint64_t>(1ull << 20, bl / 4);
+                continue;
+            }
             pos += bl;
         }
     }
@@ -938,11 +969,13 @@ int pbs_chunker_candidates_device(pbs_chunker* c, const uint8_t* dev, size_t len
     std::memcpy(saved, c->carry, saved_len);
     std::memcpy(c->carry, pre, pre_len);
     c->carry_len = (uint32_t)pre_len;
-    uint32_t n = 0;
+    uint64_t n = 0;
+    c->too_dense = false;
     int rc = scan_candidates(c, dev, len, base, &n);
     std::memcpy(c->carry, saved, saved_len);
     c->carry_len = saved_len;
     if (rc) return rc;
+    if (c->too_dense) return fail(c, PBS_ERR_NOMEM);  // split the range further
     *n_out = n;
     if (n > cap) return fail(c, PBS_ERR_CAPACITY);
     rc = sort_candidates(c, n, out_dev, base + len);
@@ -994,12 +1027,13 @@ int pbs_candidates_host(const uint8_t* data, size_t len, size_t avg, uint64_t* o
     pbs_chunker* c = pbs_chunker_new(avg, &err);
     if (!c) return err;
     int rc = PBS_OK;
-    uint32_t n = 0;
+    uint64_t n = 0;
     if (len) {
         if (c->d_in.ensure(len) != hipSuccess ||
             hipMemcpyAsync(c->d_in.p, data, len, hipMemcpyHostToDevice, c->stream) != hipSuccess)
             rc = PBS_ERR_HIP;
         if (!rc) rc = scan_candidates(c, c->d_in.as<uint8_t>(), len, 0, &n);
+        if (!rc && c->too_dense) rc = PBS_ERR_NOMEM;
         if (!rc && n > cap) rc = PBS_ERR_CAPACITY;
         if (!rc && n) {
             if (c->d_C.ensure((size_t)n * 8) != hipSuccess) rc = PBS_ERR_HIP;
@@ -1026,6 +1060,11 @@ int pbs_generate_device(uint8_t* dev, size_t len, int kind, uint64_t seed, uint6
     if (hipStreamSynchronize(s) != hipSuccess) return PBS_ERR_HIP;
     return PBS_OK;
 }
+
+#ifndef PBS_BUILD_ID
+#define PBS_BUILD_ID "unknown"
+#endif
+const char* pbs_build_id(void) { return PBS_BUILD_ID; }
 
 int pbs_table_copy(uint32_t* out256) {
     if (!out256) return PBS_ERR_INVALID;

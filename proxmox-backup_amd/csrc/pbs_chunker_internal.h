@@ -33,15 +33,15 @@ int scan_main_plan(uint64_t len, int cu, uint64_t* ntiles, bool* dyn, uint64_t* 
 uint64_t scan_main_covered(uint64_t ntiles, uint64_t t_big, int seg);
 hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
-                            uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream,
+                            unsigned long long* nsusp, uint64_t cap, int grid, hipStream_t stream,
                             uint32_t* tile_ctr = nullptr, bool dynamic = false,
                             uint64_t t_big = ~0ull);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
-                             uint32_t pre_len, const uint64_t* susp, const uint32_t* nsusp,
-                             uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head,
-                             uint32_t mask, uint32_t minimum, uint64_t base, uint64_t* cand,
-                             uint32_t* ncand, uint32_t cand_cap, uint64_t max_items,
-                             hipStream_t stream);
+                             uint32_t pre_len, const uint64_t* susp,
+                             const unsigned long long* nsusp, uint64_t susp_cap, uint64_t ext_first,
+                             uint64_t ext_count, int head, uint32_t mask, uint32_t minimum,
+                             uint64_t base, uint64_t* cand, unsigned long long* ncand,
+                             uint64_t cand_cap, uint64_t max_items, hipStream_t stream);
 hipError_t sort_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
                     int end_bit, hipStream_t stream);
 hipError_t exclusive_sum_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
@@ -61,8 +61,8 @@ hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C
                                 uint64_t* out, uint64_t out_cap, uint64_t* out_host,
                                 uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
                                 uint64_t* res, uint64_t* res_host, hipStream_t stream,
-                                const uint32_t* counts = nullptr, uint32_t susp_cap = 0,
-                                uint32_t cand_cap = 0, uint32_t* counts_host = nullptr,
+                                const unsigned long long* counts = nullptr, uint64_t susp_cap = 0,
+                                uint64_t cand_cap = 0, uint64_t* counts_host = nullptr,
                                 const uint8_t* tail_src = nullptr, uint8_t* tail_host = nullptr,
                                 uint32_t tail_len = 0);
 // Small-input path (scan_blocks_kernel + resolve_small_kernel<1|2>, two launches, no
@@ -86,12 +86,12 @@ struct FusedScanArgs {
     // FUSED = 0 with counts != nullptr (speculative single-sync path): nnew is read from
     // counts[1] (scan_exact's candidate counter); counts[0] > susp_cap, counts[1] >
     // cand_cap or too many keys -> res_host[12] = 1 and nothing else is written
-    const uint32_t* counts;
-    uint32_t susp_cap;
+    const unsigned long long* counts;  // [0] suspects, [1] candidates (64-bit counters)
+    uint64_t susp_cap;
     // speculative path, written before the stand-down test (saves two D2H copies): the
     // two counters to counts_host, the tail_len <= 63 bytes at tail_src (the warm-up
     // history of the next call) to tail_host; both mapped host memory, may be null
-    uint32_t* counts_host;
+    uint64_t* counts_host;
     const uint8_t* tail_src;
     uint8_t* tail_host;
     uint32_t tail_len;
@@ -103,6 +103,8 @@ hipError_t launch_scan_resolve_small(const FusedScanArgs& fa, int resolve, uint6
                                      uint64_t* out_host, uint64_t host_cap, uint64_t* keep_host,
                                      uint64_t keep_cap, uint64_t* res, uint64_t* res_host,
                                      hipStream_t stream);
+// pbs_blob.hip: free the blob-CRC chunk counter kept for `st` (call before destroying it)
+void release_stream_counter(hipStream_t st);
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,
                       int kind, hipStream_t stream);
 

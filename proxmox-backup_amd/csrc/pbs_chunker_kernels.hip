@@ -181,18 +181,19 @@ constexpr int kExactWaves = 16;
 constexpr uint32_t kExactLds = 2048;  // candidates buffered per workgroup
 __global__ __launch_bounds__(kExactWaves * 64) void scan_exact_kernel(
     const uint8_t* __restrict__ data, uint64_t len, const uint8_t* __restrict__ pre,
-    uint32_t pre_len, const uint64_t* __restrict__ susp, const uint32_t* __restrict__ nsusp,
-    uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head, uint32_t mask,
-    uint32_t minimum, uint64_t base, uint64_t* __restrict__ cand, uint32_t* __restrict__ ncand,
-    uint32_t cand_cap) {
+    uint32_t pre_len, const uint64_t* __restrict__ susp,
+    const unsigned long long* __restrict__ nsusp, uint64_t susp_cap, uint64_t ext_first,
+    uint64_t ext_count, int head, uint32_t mask, uint32_t minimum, uint64_t base,
+    uint64_t* __restrict__ cand, unsigned long long* __restrict__ ncand, uint64_t cand_cap) {
     __shared__ uint32_t tab[256];
     __shared__ uint64_t lbuf[kExactLds];
-    __shared__ uint32_t lcnt, gbase;
+    __shared__ uint32_t lcnt;
+    __shared__ uint64_t gbase;
     for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = kBuzhashTable[i];
     if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t ns0 = nsusp ? *nsusp : 0u;
+    const uint64_t ns0 = nsusp ? *nsusp : 0ull;
     const uint64_t ns = ns0 < susp_cap ? ns0 : susp_cap;
     const uint64_t total = ns + (uint64_t)(head ? 1 : 0) + ext_count;
     const uint64_t stride = (uint64_t)gridDim.x * kExactWaves;
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(kExactWaves * 64) void scan_exact_kernel(
                     // goes straight to the output with its own atomic
                     const uint32_t idx = atomicAdd(&lcnt, c);
                     const uint32_t inl = idx >= kExactLds ? 0u : (c < kExactLds - idx ? c : kExactLds - idx);
-                    const uint32_t gidx = c > inl ? atomicAdd(ncand, c - inl) : 0u;
+                    const uint64_t gidx = c > inl ? atomicAdd(ncand, (unsigned long long)(c - inl)) : 0ull;
                     uint32_t k = 0;
                     while (m) {
                         const int bit = __builtin_ctz(m);
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(kExactWaves * 64) void scan_exact_kernel(
     }
     __syncthreads();
     const uint32_t nl = lcnt < kExactLds ? lcnt : kExactLds;
-    if (threadIdx.x == 0) gbase = nl ? atomicAdd(ncand, nl) : 0u;
+    if (threadIdx.x == 0) gbase = nl ? atomicAdd(ncand, (unsigned long long)nl) : 0ull;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
         if (gbase + i < cand_cap) cand[gbase + i] = lbuf[i];
@@ -493,14 +494,14 @@ __global__ __launch_bounds__(kSmallThreads) void resolve_small_kernel(
     const uint32_t tid = threadIdx.x, T = kSmallThreads;
     if constexpr (FUSED == 0) {
         if (fa.counts) {  // speculative: the candidate count is only known on the device
-            const uint32_t ns = fa.counts[0], nc = fa.counts[1];
+            const uint64_t ns = fa.counts[0], nc = fa.counts[1];
             if (fa.counts_host && tid < 2) fa.counts_host[tid] = tid ? nc : ns;
             if (fa.tail_host && tid < fa.tail_len) fa.tail_host[tid] = fa.tail_src[tid];
             const bool fits = ns <= fa.susp_cap && nc <= fa.cand_cap &&
                               (uint64_t)np + nc + 2 <= kSmallResolveMax;
             if (tid == 0) res_host[12] = fits ? 0u : 1u;
             if (!fits) return;  // uniform
-            nnew = nc;
+            nnew = (uint32_t)nc;
         }
     }
     uint32_t m = np + nnew;
@@ -973,7 +974,7 @@ uint64_t scan_main_covered(uint64_t ntiles, uint64_t t_big, int seg) {
 
 hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
-                            uint32_t* nsusp, uint32_t cap, int grid, hipStream_t stream,
+                            unsigned long long* nsusp, uint64_t cap, int grid, hipStream_t stream,
                             uint32_t* tile_ctr, bool dynamic, uint64_t t_big) {
     if (ntiles == 0) return hipSuccess;
     (void)hipGetLastError();  // launch errors below must not be confused with stale ones
@@ -1004,11 +1005,11 @@ hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
 }
 
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
-                             uint32_t pre_len, const uint64_t* susp, const uint32_t* nsusp,
-                             uint32_t susp_cap, uint64_t ext_first, uint64_t ext_count, int head,
-                             uint32_t mask, uint32_t minimum, uint64_t base, uint64_t* cand,
-                             uint32_t* ncand, uint32_t cand_cap, uint64_t max_items,
-                             hipStream_t stream) {
+                             uint32_t pre_len, const uint64_t* susp,
+                             const unsigned long long* nsusp, uint64_t susp_cap, uint64_t ext_first,
+                             uint64_t ext_count, int head, uint32_t mask, uint32_t minimum,
+                             uint64_t base, uint64_t* cand, unsigned long long* ncand,
+                             uint64_t cand_cap, uint64_t max_items, hipStream_t stream) {
     (void)hipGetLastError();
     // one item per wave; at most 2 workgroups per CU (one flush atomic each)
     uint64_t blocks = (max_items + kExactWaves - 1) / kExactWaves;
@@ -1065,8 +1066,8 @@ hipError_t launch_resolve_small(const uint64_t* newc, uint32_t nnew, uint64_t* C
                                 uint64_t* out, uint64_t out_cap, uint64_t* out_host,
                                 uint64_t host_cap, uint64_t* keep_host, uint64_t keep_cap,
                                 uint64_t* res, uint64_t* res_host, hipStream_t stream,
-                                const uint32_t* counts, uint32_t susp_cap, uint32_t cand_cap,
-                                uint32_t* counts_host, const uint8_t* tail_src, uint8_t* tail_host,
+                                const unsigned long long* counts, uint64_t susp_cap, uint64_t cand_cap,
+                                uint64_t* counts_host, const uint8_t* tail_src, uint8_t* tail_host,
                                 uint32_t tail_len) {
     if ((uint64_t)np + (counts ? 0 : nnew) + 2 > kSmallResolveMax) return hipErrorInvalidValue;
     (void)hipGetLastError();

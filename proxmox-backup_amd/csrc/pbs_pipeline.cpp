@@ -29,6 +29,7 @@
 
 #include "pbs_blob.h"
 #include "pbs_chunker.h"
+#include "pbs_chunker_internal.h"
 #include "pbs_digest.h"
 
 namespace {
@@ -233,6 +234,9 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     if (s_copy) (void)hipStreamDestroy(s_copy);
     if (s_scan) (void)hipStreamDestroy(s_scan);
     for (auto& s : s_dig)
-        if (s) (void)hipStreamDestroy(s);
+        if (s) {
+            pbs::release_stream_counter(s);
+            (void)hipStreamDestroy(s);
+        }
     return rc;
 }

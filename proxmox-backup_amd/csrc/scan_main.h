@@ -70,7 +70,7 @@ template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int
           int DYN = 0>
 __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
-    uint32_t thr, uint64_t* __restrict__ susp, uint32_t* __restrict__ nsusp, uint32_t cap,
+    uint32_t thr, uint64_t* __restrict__ susp, unsigned long long* __restrict__ nsusp, uint64_t cap,
     uint32_t* __restrict__ tile_ctr = nullptr, uint64_t t_big = ~0ull) {
     static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
     constexpr int SEG2 = SEG / 4;  // DYN: segment length of the small tiles (t >= t_big)
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
                 const uint64_t pos =
                     toff + (uint64_t)lane * seg_cur + (uint64_t)(it - 1) * kIter;
                 if (pos != 0) {
-                    const uint32_t idx = atomicAdd(nsusp, 1u);
+                    const uint64_t idx = atomicAdd(nsusp, 1ull);
                     if (idx < cap) susp[idx] = pos;
                 }
             }

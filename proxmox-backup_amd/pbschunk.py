@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "pbs_chunker_stream_offset",
     "pbs_chunker_chunk_start", "pbs_chunker_reset", "pbs_chunker_set_stream",
     "pbs_chunker_last_error", "pbs_strerror", "pbs_chunker_last_timing",
-    "pbs_candidates_host", "pbs_generate_device", "pbs_device_count", "pbs_table_copy",
+    "pbs_candidates_host", "pbs_generate_device", "pbs_device_count", "pbs_table_copy", "pbs_build_id",
     "pbs_chunker_candidates_device", "pbs_chunker_resolve_device",
     # include/pbs_digest.h (chunk digests, dynamic index)
     "pbs_digest_chunks_device", "pbs_digest_chunks_async", "pbs_sha256", "pbs_didx_size",
@@ -128,6 +128,7 @@ def lib():
         "pbs_generate_device": ([p, sz, i, u64, u64, p], i),
         "pbs_device_count": ([], i),
         "pbs_table_copy": ([p], i),
+        "pbs_build_id": ([], ctypes.c_char_p),
         "pbs_chunker_candidates_device": ([p, p, sz, p, sz, u64, p, sz, ctypes.POINTER(sz)], i),
         "pbs_chunker_resolve_device": ([p, p, sz, u64, i, p, sz, ctypes.POINTER(sz)], i),
         "pbs_digest_chunks_device": ([p, sz, u64, p, sz, p, sz, p, p], i),
@@ -164,6 +165,11 @@ def table() -> np.ndarray:
     t = np.empty(256, dtype=np.uint32)
     lib().pbs_table_copy(t.ctypes.data)
     return t
+
+
+def build_id() -> str:
+    """Digest of the sources the loaded library was built from (pbs_build_id)."""
+    return lib().pbs_build_id().decode()
 
 
 def max_cuts(length: int) -> int:

@@ -100,7 +100,16 @@ def chunk_sharded(ch, dev_ptr: int, length: int, base: int, total: int, tail: "t
     """Cut list of the whole ``total``-byte stream, computed from this rank's range
     [base, base + length) (device bytes at ``dev_ptr``) and the other ranks'.
     ``tail`` = this range's last min(length, 63) bytes as a tensor on the collective's
-    device (the halo the right neighbour needs)."""
+    device (the halo the right neighbour needs).
+
+    The handle is put on torch's current stream of ``device``: the gathered candidate
+    list is written there (all_gather + cat), and the handle's own stream is
+    non-blocking (include/pbs_chunker.h), so resolving on it could read the list before
+    it is complete."""
+    import torch
+
+    if getattr(device, "type", None) == "cuda":
+        ch.set_stream(torch.cuda.current_stream(device).cuda_stream)
     pre = exchange_halo(tail, dist, rank, world)
     if len(pre) != min(base, HALO):
         raise ValueError(f"rank {rank}: halo of {len(pre)} bytes for base {base}")

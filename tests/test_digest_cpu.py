@@ -69,3 +69,23 @@ def test_dynamic_index_writer_file(pbschunk, oracle, tmp_path):
         w.add_chunk(1, bytes(32))
     with pytest.raises(RuntimeError):
         w.close()
+
+
+def _blob_writer_vectors():
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "blob_writer_digests.json")) as f:
+        return json.load(f)
+
+
+def test_reference_digest_vectors_pin_the_oracle(pbschunk):
+    """The reference's own golden digests (tests/blob_writer.rs:11-32): hashlib (the
+    oracle's SHA-256) and the library's host SHA-256 both reproduce TEST_DIGEST_PLAIN and
+    TEST_DIGEST_ENC (keyed with the PBKDF2-derived id_key, crypt_config.rs:42-51)."""
+    v = _blob_writer_vectors()
+    data = bytes(i % 255 for i in range(100_000))
+    key = hashlib.pbkdf2_hmac("sha256", bytes([1] * 32), b"_id_key", 10, 32)
+    assert key.hex() == v["id_key"]
+    assert hashlib.sha256(data).hexdigest() == v["digest_plain"]
+    assert hashlib.sha256(data + key).hexdigest() == v["digest_enc"]
+    assert pbschunk.sha256(data).hex() == v["digest_plain"]
+    assert pbschunk.sha256(data + key).hex() == v["digest_enc"]

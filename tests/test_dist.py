@@ -54,3 +54,46 @@ def test_single_rank_aggregation():
     sys.path.insert(0, root)
     import bench
     assert bench.aggregate(1.5, 42, None, None) == (1.5, 42.0)
+
+
+def _run_bench(args, env=None, timeout=300):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=e,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_launcher_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts 2 rank processes itself (gloo / CPU
+    oracle stand-in here): one JSON line from rank 0 with n_gpus 2, value = all ranks'
+    bytes / the slowest rank's time, per-rank seeds seed + rank."""
+    rc, out, err = _run_bench(["--gpus", "2", "--cpu-standin", "--size-gib", "0.01",
+                               "--steps", "2", "--warmup", "1"])
+    assert rc == 0, err[-2000:]
+    assert out["n_gpus"] == 2 and out["stand_in"] is True
+    recs = sorted(out["per_rank"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in recs] == [0, 1]
+    assert recs[1]["seed"] == recs[0]["seed"] + 1
+    mx = max(r["elapsed_s"] for r in recs)
+    tot = sum(r["bytes"] for r in recs)
+    assert out["value"] == pytest.approx(tot * 2 / (1 << 30) / mx, rel=1e-3)
+    assert out["ms_per_step"] == pytest.approx(mx / 2 * 1e3, rel=1e-3)
+
+
+def test_bench_refuses_missing_gpus():
+    """--gpus 2 on a box with fewer GPUs (here none) fails loudly instead of running 1."""
+    rc, out, err = _run_bench(["--gpus", "2", "--steps", "1"], timeout=120)
+    assert rc == 2 and out is None and "GPU" in err
+
+
+def test_bench_refuses_world_mismatch():
+    rc, out, err = _run_bench(["--gpus", "4", "--cpu-standin", "--steps", "1"],
+                              env={"WORLD_SIZE": "2", "RANK": "0"}, timeout=120)
+    assert rc == 2 and "disagrees" in err

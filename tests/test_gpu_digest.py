@@ -216,3 +216,35 @@ def test_upload_stream_host(gpu, oracle, prev):
     assert out["didx"] == img and out["csum"] == csum
     new = [(int(bounds[i]), int(bounds[i + 1] - bounds[i])) for i in range(ref_known.size) if not ref_known[i]]
     assert [(s, l) for s, l, _ in out["new_chunks"]] == new
+
+
+def test_reference_digest_vectors(gpu, torch_dev):
+    """The reference-held golden digests (tests/blob_writer.rs:11-32, fixture
+    tests/golden/blob_writer_digests.json): TEST_DATA = 100 000 bytes i % 255 digested on
+    the GPU gives TEST_DIGEST_PLAIN, and with the id_key of CryptConfig::new([1; 32])
+    (PBKDF2-HMAC-SHA256, "_id_key", 10 rounds; crypt_config.rs:42-51, 79-84)
+    TEST_DIGEST_ENC -- also as one chunk among others at every start alignment."""
+    import hashlib
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "blob_writer_digests.json")) as f:
+        v = json.load(f)
+    test_data = (np.arange(100_000) % 255).astype(np.uint8)
+    key = hashlib.pbkdf2_hmac("sha256", bytes([1] * 32), b"_id_key", 10, 32)
+    for pad in range(4):
+        t, ptr = _dev(torch_dev, test_data, pad)
+        bounds = np.array([0, test_data.size], dtype=np.uint64)
+        assert bytes(gpu.digest_chunks_device(ptr, test_data.size, bounds)[0]).hex() == v["digest_plain"]
+        assert bytes(gpu.digest_chunks_device(ptr, test_data.size, bounds, key=key)[0]).hex() == v["digest_enc"]
+        del t
+    # inside a stream, between other chunks (absolute offsets with a base)
+    head = gen_np.gen_random(777, 5)
+    tail = gen_np.gen_random(4096 + 9, 6)
+    stream = np.concatenate([head, test_data, tail])
+    t, ptr = _dev(torch_dev, stream, 3)
+    base = 1 << 33
+    bounds = np.array([0, head.size, head.size + test_data.size, stream.size], dtype=np.uint64) + np.uint64(base)
+    for k, want in ((None, v["digest_plain"]), (key, v["digest_enc"])):
+        dig = gpu.digest_chunks_device(ptr, stream.size, bounds, base=base, key=k)
+        assert bytes(dig[1]).hex() == want

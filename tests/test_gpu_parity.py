@@ -349,10 +349,12 @@ def _oracle_two_phase_parallel(oracle, data: np.ndarray, avg: int, threads: int 
 @pytest.mark.slow
 @pytest.mark.parametrize("gib,kind,avg,dyn", [(8, 1, 4 * MiB, None), (6, 2, 256 * KiB, None),
                                              (3, 1, 64 * KiB, None), (64, 2, 4 * MiB, None),
+                                             (64, 2, 256 * KiB, None),
                                              (6, 2, 4 * MiB, "1"), (3, 1, 64 * KiB, "1"),
                                              (1.5, 2, 1 * MiB, "1")],
                          ids=["config2-8GiB-random-4M", "6GiB-vm-256K", "3GiB-random-64K",
-                              "config3-64GiB-vm-4M", "6GiB-vm-4M-dynamic", "3GiB-random-64K-dynamic",
+                              "config3-64GiB-vm-4M", "config5-64GiB-vm-256K",
+                              "6GiB-vm-4M-dynamic", "3GiB-random-64K-dynamic",
                               "1.5GiB+ragged-vm-1M-dynamic"])
 def test_full_size_in_hbm(gpu, oracle, monkeypatch, gib, kind, avg, dyn):
     """BASELINE config 2 (8 GiB random already in HBM, 4 MiB average), the headline
@@ -379,3 +381,39 @@ def test_full_size_in_hbm(gpu, oracle, monkeypatch, gib, kind, avg, dyn):
     # spot-check against the streaming oracle on the first 256 MiB
     head = oracle.chunk_feed(avg, host[:256 * MiB])
     assert np.array_equal(got[:head.size], head)
+
+
+# ---------------------------------------------------------------- dense periodic input
+
+def _passing_pattern(oracle, period: int, avg: int) -> np.ndarray:
+    """Random bytes of length `period` whose periodic continuation has a window hash that
+    passes the cut test at some phase (then every period-th byte is a candidate)."""
+    mask = 2 * avg - 1
+    for seed in range(1, 1 << 20):
+        pat = gen_np.gen_random(period, seed)
+        buf = np.tile(pat, 64 // period + 3)
+        if any((oracle.window_hash(buf, 63 + k) & mask) >= mask - 2 for k in range(period)):
+            return pat
+    raise AssertionError("no passing pattern")
+
+
+def test_periodic_dense_candidates(gpu, oracle):
+    """A period-7 stream whose window hash passes the test makes every 7th byte a
+    candidate: 153 M candidates in 1 GiB, more than one batch may hold (the scan redoes
+    it as shorter batches; 64-bit candidate counters), at a 4 KiB average whose chunks
+    are ~1 KiB.  The cut list equals the oracle's."""
+    import torch
+    pat = _passing_pattern(oracle, 7, 4096)
+    n = (1 << 30) + 13
+    host = np.tile(pat, n // 7 + 1)[:n]
+    dev = torch.from_numpy(host).to("cuda")
+    torch.cuda.synchronize()
+    with gpu.Chunker(4096) as c:
+        got = c.find_cuts_device(dev.data_ptr(), n, is_final=True)
+        t = c.last_timing()
+    del dev
+    ref = oracle.chunk_feed(4096, host)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    assert t["candidates"] > (1 << 27) // 4  # dense: the batches were shrunk
+    assert np.array_equal(got, ref)
