@@ -120,7 +120,9 @@ struct pbs_chunker {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     DevBuf d_table, d_pre, d_counters, d_susp, d_cand, d_C, d_sort_tmp, d_nxt, d_jtmp, d_nf, d_on,
-        d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in, d_stage, d_hits;
+        d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in, d_stage, d_hits, d_rec;
+    uint32_t rec_epoch = 0;  // fused pass: tile-record epoch of the last launch (16 bits)
+    bool fused = true;       // PBS_FUSED=0: multi-launch path for every batch (A/B)
     uint64_t susp_cap = 0, cand_cap = 0;
     uint64_t batch_limit = 0;  // bytes per batch (0 = batch_max); shrunk when a batch is too dense
     bool too_dense = false;    // the last scan found more than kMaxBatchCand candidates
@@ -630,6 +632,135 @@ int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     return PBS_OK;
 }
 
+// Averages served by the fused pass: at >= 128 KiB a tile (1-2 MiB) of random data holds
+// ~12-24 candidates, far below the 64 flagged blocks one tile's exact step takes.
+constexpr uint64_t kFusedMinAvg = 128 * 1024;
+
+bool use_fused(const pbs_chunker* c, uint64_t bl) {
+    return c->fused && c->prm.hash_cuts && c->prm.avg >= kFusedMinAvg && bl > kFusedMaxBytes &&
+           c->cu >= 2;
+}
+
+// One batch [pos, pos + bl) of device bytes `dsrc` (hsrc: the same bytes on the host, or
+// null) in ONE launch: scan_fused_kernel scans, evaluates the flagged blocks exactly and
+// resolves the cuts while it runs (scan_fused.h); one host sync.  *done = false (and
+// nothing changed) when the kernel stood down on dense input: the caller takes the
+// multi-launch path.
+int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos,
+               uint64_t bl, size_t np, uint64_t rend, uint64_t* out, size_t cap, size_t* n,
+               bool* done) {
+    const Params& p = c->prm;
+    *done = false;
+    uint64_t ntiles = 0, t_big = 0;
+    bool dyn = false;
+    const int seg = scan_main_plan(bl, c->cu, &ntiles, &dyn, &t_big);
+    const uint64_t covered = scan_main_covered(ntiles, t_big, seg);
+    const uint64_t ntail = ((bl - covered + kBlockBytes - 1) / kBlockBytes + kTailBlocks - 1) / kTailBlocks;
+    const uint64_t items = ntiles + ntail;
+    if (items == 0) return PBS_OK;
+    // tile records: a fresh allocation (or an epoch wrap) is zeroed; epochs never 0
+    const void* old_rec = c->d_rec.p;
+    const size_t old_cap = c->d_rec.cap;
+    HIP_TRY(c, c->d_rec.ensure(items * 8));
+    if (c->d_rec.p != old_rec || c->d_rec.cap != old_cap || ((c->rec_epoch + 1) & 0xFFFFu) == 0) {
+        HIP_TRY(c, hipMemsetAsync(c->d_rec.p, 0, c->d_rec.cap, c->stream));
+        c->rec_epoch = 0;
+    }
+    c->rec_epoch = (c->rec_epoch + 1) & 0xFFFFu;
+    const uint64_t expected = bl / p.avg * 3 / 2 + 1;
+    const uint64_t cand_cap = std::min<uint64_t>(std::min<uint64_t>(bl + 1, expected * 2 + 8192), kMaxBatchCand);
+    HIP_TRY(c, c->d_cand.ensure(cand_cap * 8));
+    HIP_TRY(c, c->d_counters.ensure(24));
+    HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 24, c->stream));
+    HIP_TRY(c, c->d_pre.ensure(64));
+    if (c->carry_len)
+        HIP_TRY(c, hipMemcpyAsync(c->d_pre.p, c->carry, c->carry_len, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, c->d_C.ensure(std::max<size_t>(np, 1) * 8));
+    if (np)
+        HIP_TRY(c, hipMemcpyAsync(c->d_C.p, c->pending.data() + c->pend_head, np * 8,
+                                  hipMemcpyHostToDevice, c->stream));
+    const uint64_t span = rend - c->chunk_start;
+    const uint64_t out_cap = span / p.min_eff + 3;  // every chunk before the open one >= min
+    HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
+    int rc = ensure_small_host_bufs(c);
+    if (rc) return rc;
+    uint64_t *cuts_dev = nullptr, *keep_dev = nullptr, *small_dev = nullptr;
+    if ((rc = mapped(c, c->h_cuts, &cuts_dev)) || (rc = mapped(c, c->h_keep, &keep_dev)) ||
+        (rc = mapped(c, c->h_small, &small_dev)))
+        return rc;
+    const uint64_t tl = std::min<uint64_t>(bl, kWindow - 1);
+    unsigned long long* ctr = c->d_counters.as<unsigned long long>();
+    FusedPassArgs a{};
+    a.data = dsrc;
+    a.len = bl;
+    a.ntiles = ntiles;
+    a.t_big = t_big;
+    a.table_rot = c->d_table.as<uint32_t>();
+    a.thr = p.thr;
+    a.tile_ctr = reinterpret_cast<uint32_t*>(ctr + 2);
+    a.pre = c->d_pre.as<uint8_t>();
+    a.pre_len = c->carry_len;
+    a.covered = covered;
+    a.ntail = ntail;
+    a.base = pos;
+    a.rec = c->d_rec.as<unsigned long long>();
+    a.epoch = c->rec_epoch;
+    a.cand = c->d_cand.as<uint64_t>();
+    a.ncand = ctr + 1;
+    a.cand_cap = cand_cap;
+    a.nflag = ctr;
+    a.min_eff = p.min_eff;
+    a.max_eff = p.max_eff;
+    a.max_shift = (uint32_t)__builtin_ctzll(p.max_eff);
+    a.end = rend;
+    a.s0 = c->chunk_start;
+    a.pend = c->d_C.as<uint64_t>();
+    a.npend = (uint32_t)np;
+    a.cuts = c->d_cuts.as<uint64_t>();
+    a.cuts_cap = out_cap;
+    a.cuts_host = cuts_dev;
+    a.host_cap = kHostCuts;
+    a.keep_host = keep_dev;
+    a.keep_cap = (uint32_t)kHostKeep;
+    a.res_host = small_dev + 8;
+    a.tail_src = dsrc + bl - tl;
+    a.tail_host = reinterpret_cast<uint8_t*>(small_dev + 24);
+    a.tail_len = (uint32_t)tl;
+    a.timeout_ticks = 100000000ull * 20;  // 20 s of wall_clock64 (100 MHz)
+    c->h_small[8 + 3] = ~0ull;
+    HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+    HIP_TRY(c, launch_scan_fused(a, seg, dyn, c->cu, c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const uint64_t status = c->h_small[8 + 3];
+    if (status == 1) return PBS_OK;  // stood down: dense input
+    if (status != 0) return fail(c, PBS_ERR_HIP);
+    const uint64_t ncut = c->h_small[8], s_open = c->h_small[9], nkeep = c->h_small[10];
+    if (*n + ncut > cap || ncut > out_cap || nkeep > kHostKeep) return fail(c, PBS_ERR_CAPACITY);
+    if (ncut <= kHostCuts) {
+        std::memcpy(out + *n, c->h_cuts, ncut * 8);
+    } else {
+        HIP_TRY(c, hipMemcpy(out + *n, c->d_cuts.p, ncut * 8, hipMemcpyDeviceToHost));
+    }
+    *n += ncut;
+    std::vector<uint64_t> keep(c->h_keep, c->h_keep + nkeep);
+    c->chunk_start = s_open;
+    c->pending.swap(keep);
+    c->pend_head = 0;
+    float ms = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    c->timing.scan_ms += ms;
+    c->timing.bytes += bl;
+    c->timing.suspects += c->h_small[13];
+    c->timing.candidates += c->h_small[12];
+    c->timing.cuts += ncut;
+    update_carry(c, hsrc ? hsrc + bl - tl : reinterpret_cast<uint8_t*>(c->h_small + 24), tl);
+    c->scanned_end = pos + bl;
+    *done = true;
+    return PBS_OK;
+}
+
 int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final, uint64_t* out,
                    size_t cap, size_t* n_out, bool device) {
     if (!c) return PBS_ERR_INVALID;
@@ -672,6 +803,15 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
                 HIP_TRY(c, c->d_in.ensure(bl));
                 HIP_TRY(c, hipMemcpyAsync(c->d_in.p, hsrc, bl, hipMemcpyHostToDevice, c->stream));
                 dsrc = c->d_in.as<uint8_t>();
+            }
+        }
+        if (bl && use_fused(c, bl)) {
+            bool done = false;
+            int rc = fused_pass(c, dsrc, hsrc, pos, bl, np, rend, out, cap, &n, &done);
+            if (rc) return rc;
+            if (done) {
+                pos += bl;
+                continue;
             }
         }
         bool have_cands = false;
@@ -742,7 +882,7 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
 void destroy(pbs_chunker* c) {
     DevBuf* bufs[] = {&c->d_table, &c->d_pre, &c->d_counters, &c->d_susp, &c->d_cand, &c->d_C,
                       &c->d_sort_tmp, &c->d_nxt, &c->d_jtmp, &c->d_nf, &c->d_on, &c->d_cnt,
-                      &c->d_off, &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in};
+                      &c->d_off, &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in, &c->d_rec};
     for (DevBuf* b : bufs) b->release();
     c->d_stage.release();
     c->d_hits.release();
@@ -809,6 +949,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     }
     c->prm = prm;
     if (const char* e = std::getenv("PBS_DEBUG_PHASES")) c->debug_phases = e[0] == '1';
+    if (const char* e = std::getenv("PBS_FUSED")) c->fused = e[0] != '0';
     bool ok = hipGetDevice(&c->device) == hipSuccess;
     hipDeviceProp_t prop;
     if (ok && hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)

@@ -36,6 +36,51 @@ hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             unsigned long long* nsusp, uint64_t cap, int grid, hipStream_t stream,
                             uint32_t* tile_ctr = nullptr, bool dynamic = false,
                             uint64_t t_big = ~0ull);
+// One launch for a whole batch: scan + exact positions + resolve (scan_fused.h).  `seg`
+// and `dyn` from scan_main_plan; grid = one workgroup per CU.
+struct FusedPassArgs {
+    // phase A
+    const uint8_t* data;   // batch bytes [0, len) (device)
+    uint64_t len;
+    uint64_t ntiles, t_big;
+    const uint32_t* table_rot;  // T' (256 words)
+    uint32_t thr;
+    uint32_t* tile_ctr;         // zeroed device counter (dynamic tile order)
+    const uint8_t* pre;         // the pre_len <= 63 stream bytes before data[0] (device, 64 B)
+    uint32_t pre_len;
+    uint64_t covered;           // bytes covered by the tiles
+    uint64_t ntail;             // tail items (kTailBlocks blocks each) after the tiles
+    uint64_t base;              // absolute stream offset of data[0]
+    // tile records and candidates
+    unsigned long long* rec;    // ntiles + ntail records {epoch:16 | count:16 | index:32}
+    uint32_t epoch;             // != 0, differs from every record left by earlier launches
+    uint64_t* cand;             // candidate list (absolute positions; per tile contiguous)
+    unsigned long long* ncand;  // zeroed counter
+    uint64_t cand_cap;          // <= 2^32
+    unsigned long long* nflag;  // zeroed counter: flagged blocks (statistics)
+    // phase B
+    uint64_t min_eff, max_eff;  // max_eff a power of two
+    uint32_t max_shift;         // log2(max_eff)
+    uint64_t end;               // bytes known: base + len
+    uint64_t s0;                // open chunk start
+    const uint64_t* pend;       // pending candidates of the open chunk (sorted, device)
+    uint32_t npend;
+    uint64_t* cuts;             // device cut list (cuts_cap entries)
+    uint64_t cuts_cap;
+    uint64_t* cuts_host;        // mapped host copy while ncut <= host_cap
+    uint64_t host_cap;
+    uint64_t* keep_host;        // mapped: candidates of the open chunk
+    uint32_t keep_cap;
+    uint64_t* res_host;         // mapped: [0] cuts [1] open chunk start [2] kept [3] status
+                                // [4] candidates [5] flagged blocks
+    const uint8_t* tail_src;    // the batch's last tail_len <= 63 bytes (device) -> tail_host
+    uint8_t* tail_host;
+    uint32_t tail_len;
+    uint64_t timeout_ticks;     // resolver wait limit (wall_clock64 ticks, 100 MHz)
+};
+
+constexpr int kTailBlocks = 64;  // blocks per tail item of the fused pass
+hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid, hipStream_t stream);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
                              uint32_t pre_len, const uint64_t* susp,
                              const unsigned long long* nsusp, uint64_t susp_cap, uint64_t ext_first,

@@ -1,0 +1,409 @@
+// scan_fused_kernel: the whole chunking pass of a batch in ONE launch (DESIGN.md section 2,
+// "Fused pass") -- phase A (the scan_main_kernel loop), the exact candidate positions of the
+// flagged 128-byte blocks, and phase B, the min/max rule of chunker.rs:172-183, resolved
+// while the scan runs.
+//
+//   scanner waves   every wave but one runs scan_main's tile loop.  A flagged block is a
+//                   bit in the wave's LDS bitmap (no global atomic).  At the end of a tile
+//                   (ring registers dead, the next tile's first DMA in flight) the wave
+//                   evaluates its flagged blocks exactly (exact_block.h, one block per wave
+//                   step, windows re-read from HBM), appends the tile's candidates -- already
+//                   in stream order: lanes own ascending segments, bits ascending blocks -- to
+//                   the candidate list with ONE atomic, and publishes the tile record
+//                   {epoch, count, list index} (write-through stores, drained, then the
+//                   record: the hand-off of MI355X_MICROARCH.md "Inter-workgroup
+//                   visibility").  After the tiles, the bytes past the last tile ("tail
+//                   items", 64 blocks each) are evaluated the same way.
+//   resolver wave   wave 0 of workgroup 0 takes no tiles: it reads the tile records in
+//                   stream order, 64 at a time, and runs the reference's cut rule
+//                   sequentially over the candidates as they complete (pending candidates of
+//                   the open chunk first).  Cuts go to the device list and to mapped host
+//                   memory; at the end it writes the open chunk's start, its candidates and
+//                   the batch's last 63 bytes to the host.  It finishes a few microseconds
+//                   after the last tile, so the pass costs one launch and one host sync.
+//
+// Stand-down: a tile with more than 64 flagged blocks, a full candidate list or more than
+// kFusedKeep open-chunk candidates (dense input) sets status 1 -- the host then runs the
+// batch through the multi-launch path (scan_main + scan_exact + resolve), which has no
+// such limits.  A resolver that waits longer than timeout_ticks sets status 2 (error).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "exact_block.h"
+#include "pbs_chunker_internal.h"  // FusedPassArgs
+#include "scan_main.h"
+
+namespace pbs {
+
+constexpr int kFusedKeep = 1024;    // open-chunk candidates the resolver keeps in LDS
+constexpr uint32_t kRecOverflow = 0xFFFFu;
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+}
+
+__device__ __forceinline__ void store_wt(uint64_t* p, uint64_t v) {  // write-through (sc1)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Evaluate the blocks lane j names (B_j relative to data, j < nb <= 64) exactly, append
+// their candidates to the list in lane order and publish record `item`.  `over`: more than
+// 64 flagged blocks (the record says overflow).  Wave-uniform control flow.
+__device__ __forceinline__ void fused_publish(const FusedPassArgs& a, const uint32_t* tab,
+                                              uint64_t item, int64_t myB, int nb, bool over,
+                                              int lane) {
+    uint4 mh = make_uint4(0, 0, 0, 0);
+    if (nb > 0 && !over) {
+        int64_t B = (int64_t)readlane64((uint64_t)myB, 0);
+        uint32_t wv = exact_load(a.data, a.len, a.pre, a.pre_len, B, lane);
+        for (int j = 0; j < nb; ++j) {  // the window of block j+1 loads while j is hashed
+            int64_t Bn = 0;
+            uint32_t wvn = 0;
+            if (j + 1 < nb) {
+                Bn = (int64_t)readlane64((uint64_t)myB, j + 1);
+                wvn = exact_load(a.data, a.len, a.pre, a.pre_len, Bn, lane);
+            }
+            const uint4 h = exact_hits<true>(wv, a.len, a.pre_len, B, tab, a.thr, 0u, lane);
+            if (lane == j) mh = h;
+            B = Bn;
+            wv = wvn;
+        }
+    }
+    const uint32_t cnt = __builtin_popcount(mh.x) + __builtin_popcount(mh.y) +
+                         __builtin_popcount(mh.z) + __builtin_popcount(mh.w);
+    uint32_t incl = cnt;  // inclusive prefix over lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+    uint64_t idx = 0;
+    bool ovf = over || total >= kRecOverflow;
+    if (!ovf && total) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(a.ncand, (unsigned long long)total);
+        idx = readlane64(b, 0);
+        if (idx + total > a.cand_cap) {
+            ovf = true;
+        } else {
+            uint64_t o = idx + (incl - cnt);
+            const uint64_t p0 = a.base + (uint64_t)myB;
+            const uint32_t w4[4] = {mh.x, mh.y, mh.z, mh.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t m = w4[q];
+                while (m) {
+                    const int bit = __builtin_ctz(m);
+                    m &= m - 1;
+                    store_wt(a.cand + o, p0 + (uint64_t)(q * 32 + bit));
+                    ++o;
+                }
+            }
+            // the candidates are written through to memory before the record says so
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    if (lane == 0) {
+        const uint64_t r = ((uint64_t)a.epoch << 48) |
+                           ((uint64_t)(ovf ? kRecOverflow : total) << 32) | (idx & 0xFFFFFFFFull);
+        __hip_atomic_store(a.rec + item, (unsigned long long)r, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Phase B over the tile records, one wave (see the file comment).  `keep` = LDS scratch
+// of kFusedKeep entries.
+__device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane) {
+    const uint64_t total = a.ntiles + a.ntail;
+    uint64_t s = a.s0, ncut = 0;
+    uint32_t nkeep = 0, status = 0;
+    const uint64_t t_start = wall_clock64();
+
+    auto emit = [&](uint64_t x) {
+        if (lane == 0) {
+            if (ncut < a.cuts_cap) a.cuts[ncut] = x;
+            if (ncut < a.host_cap) a.cuts_host[ncut] = x;
+        }
+        ++ncut;
+    };
+    auto forced = [&](uint64_t k) {  // k forced (max-size) cuts from s
+        for (uint64_t j = (uint64_t)lane; j < k; j += 64) {
+            const uint64_t x = s + (j + 1) * a.max_eff;
+            if (ncut + j < a.cuts_cap) a.cuts[ncut + j] = x;
+            if (ncut + j < a.host_cap) a.cuts_host[ncut + j] = x;
+        }
+        ncut += k;
+        s += k * a.max_eff;
+        nkeep = 0;
+    };
+    // chunker.rs:172-183 for the next candidate c (ascending, c >= s): forced cuts while
+    // the chunk would exceed max before c; then c cuts iff the chunk is >= min long at c
+    auto process = [&](uint64_t c) {
+        const uint64_t hi = s + a.max_eff - 1;
+        if (c > hi) forced((c - hi + a.max_eff - 1) >> a.max_shift);
+        if (c >= s + a.min_eff - 1) {
+            emit(c + 1);
+            s = c + 1;
+            nkeep = 0;
+        } else {
+            if (lane == 0 && nkeep < kFusedKeep) keep[nkeep] = c;
+            ++nkeep;
+        }
+    };
+
+    for (uint32_t i = 0; i < a.npend; i += 64) {
+        const uint64_t v = i + lane < a.npend ? a.pend[i + lane] : 0;
+        const uint32_t m = a.npend - i < 64 ? a.npend - i : 64;
+        for (uint32_t k = 0; k < m; ++k) process(readlane64(v, (int)k));
+    }
+    for (uint64_t t0 = 0; t0 < total && status == 0; t0 += 64) {
+        const uint32_t n = total - t0 < 64 ? (uint32_t)(total - t0) : 64u;
+        uint64_t rv = 0;
+        bool done = (uint32_t)lane >= n;
+        for (;;) {
+            if (!done) {
+                rv = __hip_atomic_load(a.rec + t0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                done = (uint32_t)(rv >> 48) == a.epoch;
+            }
+            if (__all(done)) break;
+            if (wall_clock64() - t_start > a.timeout_ticks) {
+                status = 2;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        if (status) break;
+        const uint32_t cnt = (uint32_t)(rv >> 32) & 0xFFFFu;
+        if (__any((uint32_t)lane < n && cnt == kRecOverflow)) {
+            status = 1;
+            break;
+        }
+        unsigned long long mask = __ballot((uint32_t)lane < n && cnt != 0);
+        while (mask) {
+            const int j = __ffsll(mask) - 1;
+            mask &= mask - 1;
+            const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)cnt, j);
+            const uint64_t ij = readlane64(rv & 0xFFFFFFFFull, j);
+            for (uint32_t q = 0; q < cj; q += 64) {
+                const uint64_t cv = q + lane < cj ? __hip_atomic_load(a.cand + ij + q + lane,
+                                                                      __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                                  : 0;
+                const uint32_t m = cj - q < 64 ? cj - q : 64;
+                for (uint32_t k = 0; k < m; ++k) process(readlane64(cv, (int)k));
+            }
+        }
+    }
+    if (status == 0) {
+        if (s + a.max_eff <= a.end) forced((a.end - s) >> a.max_shift);  // no candidate left
+        if (nkeep > kFusedKeep) status = 1;
+    }
+    if (status == 0 && nkeep <= a.keep_cap)
+        for (uint32_t i = lane; i < nkeep; i += 64) a.keep_host[i] = keep[i];
+    if ((uint32_t)lane < a.tail_len) a.tail_host[lane] = a.tail_src[lane];
+    if (lane == 0) {
+        a.res_host[0] = ncut;
+        a.res_host[1] = s;
+        a.res_host[2] = nkeep;
+        a.res_host[4] = __hip_atomic_load(a.ncand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.res_host[5] = __hip_atomic_load(a.nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.res_host[3] = status;
+    }
+}
+
+// SEG: segment bytes per lane (16/32 KiB: the fused pass serves batches of >= 1 MiB);
+// DYN: tile order as scan_main_kernel.  8 waves per workgroup, one workgroup per CU.
+template <int SEG, int DYN>
+__global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassArgs a) {
+    static_assert(SEG % 4096 == 0, "bitmap words per lane");
+    constexpr int SEG2 = SEG / 4;
+    constexpr int NW = kWavesPerWG;
+    constexpr int NBW = SEG / kIter / 32;  // bitmap words per lane (one bit per block)
+    __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4];
+    __shared__ uint32_t s_bm[NW * 64 * NBW];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < kTableDwords; i += NW * 64) s_lds[i] = a.table_rot[i >> 6];
+    for (int i = tid; i < NW * 64 * NBW; i += NW * 64) s_bm[i] = 0;
+    __syncthreads();
+    uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
+    if (blockIdx.x == 0 && wave == 0) {
+        fused_resolver(a, reinterpret_cast<uint64_t*>(stage), lane);
+        return;
+    }
+    uint32_t* bm = s_bm + wave * 64 * NBW + lane * NBW;
+
+    const uint32_t lanebase = (uint32_t)lane * 4u;
+    uint32_t voff[8], voff2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t l = 8u * j + ((uint32_t)lane >> 3);
+        const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
+        voff[j] = l * (uint32_t)SEG + k * 16u;
+        voff2[j] = l * (uint32_t)SEG2 + k * 16u;
+    }
+    const uint32_t rd_base = (uint32_t)lane * 128u;
+    const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
+    constexpr int NIT = SEG / kIter + 1;
+    const uint64_t nw = (uint64_t)gridDim.x * NW - 1;  // scanner waves (the resolver takes none)
+    uint64_t tile = (uint64_t)blockIdx.x * NW + wave - 1;
+    const uint64_t ntiles = a.ntiles, t_big = a.t_big;
+    const uint8_t* data = a.data;
+
+    auto tile_off = [&](uint64_t t) -> uint64_t {
+        if (DYN != 0 && t >= t_big) return t_big * (64ull * SEG) + (t - t_big) * (64ull * SEG2);
+        return t * (64ull * SEG);
+    };
+    auto issue = [&](uint64_t t, int it) {  // scan_main_kernel's LDS-DMA of one iteration
+        const bool sm = DYN != 0 && t >= t_big;
+        const uint8_t* tb = data + tile_off(t);
+        const bool first = (t == 0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(first ? tb : tb - kIter), 0, (int)(64u * (sm ? SEG2 : SEG) + kIter), 0x00020000);
+        const bool warm0 = first && it == 0;
+        const uint32_t soff = warm0 ? 0u : (uint32_t)it * kIter - (first ? (uint32_t)kIter : 0u);
+        if (sm) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, voff2[j], soff, 0, 2);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t vo = warm0 ? (voff[j] >= (uint32_t)kIter ? voff[j] - kIter : 0u) : voff[j];
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, vo, soff, 0, 2);
+            }
+        }
+    };
+    // the wave's flagged blocks of tile t (bitmap, lane order = stream order) -> publish
+    auto tile_end = [&](uint64_t t, uint64_t toff, uint32_t seg_cur) {
+        uint32_t w[NBW];
+#pragma unroll
+        for (int q = 0; q < NBW; ++q) {
+            w[q] = bm[q];
+            bm[q] = 0;
+        }
+        if (t == 0 && lane == 0) w[0] |= 1u;  // the stream's first block: carry bytes
+        int nb = 0;
+        bool over = false;
+        int64_t myB = 0;
+        for (;;) {
+            bool has = false;
+#pragma unroll
+            for (int q = 0; q < NBW; ++q) has |= w[q] != 0u;
+            const unsigned long long m = __ballot(has);
+            if (!m) break;
+            if (nb == 64) {
+                over = true;
+                break;
+            }
+            const int L = __ffsll(m) - 1;
+            int bitpos = 0;
+            bool found = false;
+#pragma unroll
+            for (int q = 0; q < NBW; ++q) {
+                if (!found && w[q]) {
+                    bitpos = q * 32 + __builtin_ctz(w[q]);
+                    found = true;
+                }
+            }
+            bitpos = __shfl(bitpos, L, 64);
+            if (lane == L) {
+#pragma unroll
+                for (int q = 0; q < NBW; ++q)
+                    if (q == (bitpos >> 5)) w[q] &= w[q] - 1;
+            }
+            if (lane == nb) myB = (int64_t)(toff + (uint64_t)L * seg_cur + (uint64_t)bitpos * kIter);
+            ++nb;
+        }
+        if (nb && lane == 0) atomicAdd(a.nflag, (unsigned long long)nb);
+        fused_publish(a, s_lds, t, myB, nb, over, lane);
+    };
+
+    if (tile < ntiles) {
+        uint32_t ring[128];
+#pragma unroll
+        for (int r = 0; r < 128; ++r) ring[r] = 0;
+        uint32_t h = 0;
+        uint32_t dyn_v = 0;
+        auto next_tile = [&]() -> uint64_t {
+            if constexpr (DYN != 0)
+                return nw + (uint64_t)__builtin_amdgcn_readfirstlane(dyn_v);
+            else
+                return tile + nw;
+        };
+        issue(tile, 0);
+        for (;;) {
+            if constexpr (DYN != 0) {
+                if (lane == 0) dyn_v = atomicAdd(a.tile_ctr, 1u);
+            }
+            const bool small = DYN != 0 && tile >= t_big;
+            const int nit_cur = small ? SEG2 / kIter + 1 : NIT;
+            const uint64_t toff = tile_off(tile);
+            const uint32_t seg_cur = small ? (uint32_t)SEG2 : (uint32_t)SEG;
+            for (int it = 0; it < nit_cur; ++it) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                uint32_t d[32];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint4 v = *(const uint4*)(stage + rd_base + (((uint32_t)k ^ rsw) << 4));
+                    d[4 * k] = v.x;
+                    d[4 * k + 1] = v.y;
+                    d[4 * k + 2] = v.z;
+                    d[4 * k + 3] = v.w;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                {
+                    uint64_t nt = tile;
+                    int nit = it + 1;
+                    if (nit == nit_cur) {
+                        nt = next_tile();
+                        nit = 0;
+                    }
+                    if (nt < ntiles) issue(nt, nit);
+                }
+                if (it == 0) {
+                    h = 0;
+#pragma unroll
+                    for (int r = 64; r < 128; ++r) ring[r] = 0;
+                }
+                const uint32_t acc = roll128_asm_g4(d, ring, h, lanebase);
+                if (it == 0) {
+                    if (tile == 0 && lane == 0) {  // no bytes before the stream: no warm-up
+                        h = 0;
+#pragma unroll
+                        for (int r = 64; r < 128; ++r) ring[r] = 0;
+                    }
+                } else if (acc >= a.thr) {
+                    const uint32_t bit = (uint32_t)(it - 1);
+                    atomicOr(&bm[bit >> 5], 1u << (bit & 31u));
+                }
+            }
+            tile_end(tile, toff, seg_cur);
+            tile = next_tile();
+            if (tile >= ntiles) break;
+        }
+    }
+    // the bytes past the last tile: items of kTailBlocks consecutive blocks
+    const uint64_t nblk = (a.len + kIter - 1) / kIter;
+    while (tile < ntiles + a.ntail) {
+        const uint64_t b0 = a.covered / kIter + (tile - ntiles) * kTailBlocks;
+        const int nb = (int)(nblk - b0 < (uint64_t)kTailBlocks ? nblk - b0 : (uint64_t)kTailBlocks);
+        fused_publish(a, s_lds, tile, (int64_t)((b0 + (uint64_t)lane) * kIter), nb, false, lane);
+        if constexpr (DYN != 0) {
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(a.tile_ctr, 1u);
+            tile = nw + (uint64_t)__builtin_amdgcn_readfirstlane(v);
+        } else {
+            tile += nw;
+        }
+    }
+}
+
+}  // namespace pbs

@@ -417,3 +417,55 @@ def test_periodic_dense_candidates(gpu, oracle):
         ref = np.append(ref, np.uint64(n))
     assert t["candidates"] > (1 << 27) // 4  # dense: the batches were shrunk
     assert np.array_equal(got, ref)
+
+
+# ---------------------------------------------------------------- fused pass (scan_fused.h)
+
+FUSED_CASES = [
+    # (name, maker, avg, pieces): batches > 1 MiB at avg >= 128 KiB take the one-launch
+    # pass; pieces carry the open chunk's candidates and the 63-byte history across calls
+    ("vm_40M+77_128K", lambda: gen_np.gen_vmimage(40 * MiB + 77, 0x5EED0003, 700 * MiB), 128 * KiB, 1),
+    ("random_33M_256K_x5", lambda: gen_np.gen_random(33 * MiB + 5, 41), 256 * KiB, 5),
+    ("holes_48M_1M_x3", lambda: _holes(48 * MiB + 3, 42, 3 * MiB), 1 * MiB, 3),
+    ("zebra_8x3M_4M", lambda: _zebra(8, 3 * MiB, 512 * KiB, 43), 4 * MiB, 2),
+    ("counter_24M_128K", lambda: gen_np.gen_counter(24 * MiB), 128 * KiB, 1),
+    ("zeros_70M_4M_x2", lambda: np.zeros(70 * MiB + 1, np.uint8), 4 * MiB, 2),
+]
+
+
+@pytest.mark.parametrize("name,mk,avg,pieces", FUSED_CASES, ids=[c[0] for c in FUSED_CASES])
+def test_fused_pass(gpu, oracle, monkeypatch, name, mk, avg, pieces):
+    """The one-launch pass (scan + exact + resolve in scan_fused_kernel) against the oracle
+    and against the multi-launch path (PBS_FUSED=0), whole and split into pieces."""
+    data = mk()
+    n = data.size
+    ref = oracle.chunk_feed(avg, data)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    bounds = np.linspace(0, n, pieces + 1).astype(np.int64)
+    bounds[1:-1] += 4093  # unaligned piece starts
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PBS_FUSED", fused)
+        got = []
+        with gpu.Chunker(avg) as c:
+            for a, b in zip(bounds[:-1], bounds[1:]):
+                got.append(c.find_cuts(data[a:b], is_final=b == n))
+        got = np.concatenate(got)
+        assert np.array_equal(got, ref), (name, fused, got.size, ref.size)
+
+
+def test_fused_pass_stands_down_on_dense_input(gpu, oracle):
+    """Every 7th byte a candidate at a 256 KiB average: a tile holds far more than 64
+    flagged blocks, the fused kernel stands down and the multi-launch path chunks the
+    batch -- same cuts as the oracle."""
+    pat = _passing_pattern(oracle, 7, 256 * KiB)
+    n = 24 * MiB + 3
+    rnd = gen_np.gen_random(n, 44)
+    host = rnd.copy()
+    host[8 * MiB:16 * MiB] = np.tile(pat, (8 * MiB) // 7 + 1)[:8 * MiB]
+    with gpu.Chunker(256 * KiB) as c:
+        got = c.find_cuts(host, is_final=True)
+    ref = oracle.chunk_feed(256 * KiB, host)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    assert np.array_equal(got, ref)
