@@ -1,8 +1,13 @@
 // Port of examples/test_chunk_speed2.rs onto the C++ host mirror: ChunkStream with the
 // default average (4 MiB) over a file read in pieces (tokio FramedRead + BytesCodec,
 // 8 KiB reads), printing every chunk and the summary lines (:44-60).  Without a file
-// argument the input is 1 GiB of the seeded random stream (examples/common.hpp).
+// argument the input is 1 GiB of the seeded random stream (examples/common.hpp),
+// generated before the clock starts (the reference reads random-test.dat, i.e. from the
+// page cache): each read is a memcpy of the next piece.
+// min_scan = 0 is the unchanged caller of chunk_stream.rs:40-77 (one Chunker::scan per
+// read); the default gathers 4 MiB per scan (pbs::ChunkStream::set_min_scan).
 // usage: test_chunk_speed2 [random-test.dat | -] [bytes = 1 GiB] [piece = 8192] [avg = 4 MiB]
+//                          [min_scan = 4 MiB] [quiet = 0]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -17,12 +22,19 @@ int main(int argc, char** argv) {
     const uint64_t total = argc > 2 ? std::strtoull(argv[2], nullptr, 0) : (1ull << 30);
     const size_t piece = argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 8192;
     const size_t avg = argc > 4 ? std::strtoull(argv[4], nullptr, 0) : 4096 * 1024;
+    const size_t min_scan = argc > 5 ? std::strtoull(argv[5], nullptr, 0) : (4u << 20);
+    const bool quiet = argc > 6 && std::atoi(argv[6]) != 0;
     std::FILE* f = path ? std::fopen(path, "rb") : nullptr;
     if (path && !f) {
         std::printf("error cannot open %s\n", path);
         return 1;
     }
     uint64_t off = 0;
+    std::vector<uint8_t> input;
+    if (!f) {
+        input.resize(total);
+        random_bytes(0x5EED0001ull, 0, input.data(), total);
+    }
     try {
         pbs::ChunkStream stream([&](std::vector<uint8_t>& out) {
             out.resize(piece);
@@ -31,12 +43,13 @@ int main(int argc, char** argv) {
                 n = std::fread(out.data(), 1, piece, f);
             } else if (off < total) {
                 n = (size_t)std::min<uint64_t>(piece, total - off);
-                random_bytes(0x5EED0001ull, off, out.data(), n);
+                std::memcpy(out.data(), input.data() + off, n);
             }
             off += n;
             out.resize(n);
             return n > 0;
         }, avg);
+        stream.set_min_scan(min_scan);
         const auto start = std::chrono::steady_clock::now();
         uint64_t repeat = 0, stream_len = 0;
         while (auto chunk = stream.next()) {
@@ -46,7 +59,7 @@ int main(int argc, char** argv) {
             }
             ++repeat;
             stream_len += chunk->size();
-            std::printf("Got chunk %zu\n", chunk->size());
+            if (!quiet) std::printf("Got chunk %zu\n", chunk->size());
         }
         const double us = std::chrono::duration<double, std::micro>(
                               std::chrono::steady_clock::now() - start).count();

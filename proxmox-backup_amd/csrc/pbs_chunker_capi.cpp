@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <new>
 #include <vector>
 
@@ -104,6 +105,20 @@ inline uint32_t rotl32(uint32_t x, uint32_t r) {
 
 }  // namespace
 
+// Host side of the scan server (scan_server.h): mailbox + request slot in fine-grained
+// pinned host memory, the kernel on its own stream.
+struct ScanServer {
+    ServerMailbox* mb = nullptr;  // host view (mapped)
+    ServerMailbox* mb_dev = nullptr;
+    uint8_t* slot = nullptr;
+    uint8_t* slot_dev = nullptr;
+    hipStream_t stream = nullptr;
+    uint64_t seq = 0;
+    bool running = false;
+    bool enabled = true;  // PBS_SCAN_SERVER=0: every scan() takes the batch path (A/B)
+    bool broken = false;  // a request timed out: never used again by this handle
+};
+
 struct pbs_chunker {
     Params prm;
     // stream state (absolute offsets)
@@ -137,6 +152,7 @@ struct pbs_chunker {
     pbs_timing timing{};
     int last_error = 0;
     bool debug_phases = false;  // PBS_DEBUG_PHASES=1: small-resolve phase times to stderr
+    ScanServer srv;
 };
 
 namespace {
@@ -543,6 +559,87 @@ int fused_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64
     return PBS_OK;
 }
 
+constexpr uint64_t kServerIdleTicks = 100000000ull / 1000 * 5;  // 5 ms (wall_clock64: 100 MHz)
+constexpr double kServerTimeoutS = 10.0;
+
+// Stop the scan server (quit flag, then its stream drained).  Called before any other
+// device work of the handle: a hipFree elsewhere would otherwise wait for its idle exit.
+void server_stop(pbs_chunker* c) {
+    ScanServer& sv = c->srv;
+    if (!sv.running) return;
+    __atomic_store_n(&sv.mb->quit, 1u, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(sv.stream);
+    __atomic_store_n(&sv.mb->quit, 0u, __ATOMIC_RELEASE);
+    sv.running = false;
+}
+
+int server_launch(pbs_chunker* c, uint64_t last) {
+    ScanServer& sv = c->srv;
+    __atomic_store_n(&sv.mb->exited, ~0ull, __ATOMIC_RELEASE);
+    HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.slot_dev, c->prm.mask, c->prm.minimum, last,
+                                  kServerIdleTicks, sv.stream));
+    sv.running = true;
+    return PBS_OK;
+}
+
+// scan() of host bytes [pos, pos + bl) through the scan server: their candidates are
+// appended to the pending list.  *served = false (nothing changed) when the server is off
+// or the bytes hold more than kServerCand candidates: the caller takes the batch path.
+int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, bool* served) {
+    ScanServer& sv = c->srv;
+    *served = false;
+    if (!sv.enabled || sv.broken || bl == 0 || bl > kServerMaxBytes || !c->prm.hash_cuts) return PBS_OK;
+    if (!sv.mb) {
+        const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+        HIP_TRY(c, hipHostMalloc((void**)&sv.mb, sizeof(ServerMailbox), fl));
+        std::memset(sv.mb, 0, sizeof(ServerMailbox));
+        HIP_TRY(c, hipHostMalloc((void**)&sv.slot, kServerMaxBytes, fl));
+        HIP_TRY(c, hipHostGetDevicePointer((void**)&sv.mb_dev, sv.mb, 0));
+        HIP_TRY(c, hipHostGetDevicePointer((void**)&sv.slot_dev, sv.slot, 0));
+        HIP_TRY(c, hipStreamCreateWithFlags(&sv.stream, hipStreamNonBlocking));
+    }
+    std::memcpy(sv.slot, hsrc, bl);
+    sv.mb->base = pos;
+    sv.mb->len = (uint32_t)bl;
+    sv.mb->pre_len = c->carry_len;
+    std::memcpy(sv.mb->pre, c->carry, c->carry_len);
+    const uint64_t seq = ++sv.seq;
+    if (!sv.running) {
+        int rc = server_launch(c, seq - 1);
+        if (rc) return rc;
+    }
+    __atomic_store_n(&sv.mb->req_seq, seq, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        if (__atomic_load_n(&sv.mb->ack_seq, __ATOMIC_ACQUIRE) == seq) break;
+        if (__atomic_load_n(&sv.mb->exited, __ATOMIC_ACQUIRE) == seq - 1) {
+            // it went idle just before this request: relaunch, the request is still there
+            HIP_TRY(c, hipStreamSynchronize(sv.stream));
+            int rc = server_launch(c, seq - 1);
+            if (rc) return rc;
+            continue;
+        }
+        if ((spin & 1023) == 1023 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kServerTimeoutS) {
+            sv.broken = true;
+            server_stop(c);
+            return fail(c, PBS_ERR_HIP);
+        }
+        __builtin_ia32_pause();
+    }
+    if (sv.mb->status != 0) return PBS_OK;  // too many candidates: batch path
+    const uint64_t k = sv.mb->ncand;
+    const size_t old = c->pending.size();
+    c->pending.resize(old + k);
+    std::memcpy(c->pending.data() + old, sv.mb->cand, k * 8);
+    c->timing.bytes += bl;
+    c->timing.candidates += k;
+    update_carry(c, hsrc, bl);
+    c->scanned_end = pos + bl;
+    *served = true;
+    return PBS_OK;
+}
+
 void reset_stream(pbs_chunker* c) {
     c->consumed = c->chunk_start = c->scanned_end = 0;
     c->carry_len = 0;
@@ -734,6 +831,11 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const uint64_t status = c->h_small[8 + 3];
+    if (c->debug_phases)
+        std::fprintf(stderr, "fused pass %llu B: status %llu, resolver last record ready %.1f us, "
+                     "done %.1f us, waited %.1f us (after its start)\n",
+                     (unsigned long long)bl, (unsigned long long)status, c->h_small[14] / 100.0,
+                     c->h_small[15] / 100.0, c->h_small[16] / 100.0);
     if (status == 1) return PBS_OK;  // stood down: dense input
     if (status != 0) return fail(c, PBS_ERR_HIP);
     const uint64_t ncut = c->h_small[8], s_open = c->h_small[9], nkeep = c->h_small[10];
@@ -768,6 +870,7 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
     *n_out = 0;
     if (cap < pbs_chunker_cuts_bound(c, len)) return fail(c, PBS_ERR_CAPACITY);
     HIP_TRY(c, hipSetDevice(c->device));
+    server_stop(c);
     c->timing = pbs_timing{};
     HIP_TRY(c, hipEventRecord(c->ev[5], c->stream));
     const uint64_t end = c->consumed + len;
@@ -880,6 +983,10 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
 }
 
 void destroy(pbs_chunker* c) {
+    server_stop(c);
+    if (c->srv.stream) (void)hipStreamDestroy(c->srv.stream);
+    if (c->srv.mb) (void)hipHostFree(c->srv.mb);
+    if (c->srv.slot) (void)hipHostFree(c->srv.slot);
     DevBuf* bufs[] = {&c->d_table, &c->d_pre, &c->d_counters, &c->d_susp, &c->d_cand, &c->d_C,
                       &c->d_sort_tmp, &c->d_nxt, &c->d_jtmp, &c->d_nf, &c->d_on, &c->d_cnt,
                       &c->d_off, &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in, &c->d_rec};
@@ -950,6 +1057,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     c->prm = prm;
     if (const char* e = std::getenv("PBS_DEBUG_PHASES")) c->debug_phases = e[0] == '1';
     if (const char* e = std::getenv("PBS_FUSED")) c->fused = e[0] != '0';
+    if (const char* e = std::getenv("PBS_SCAN_SERVER")) c->srv.enabled = e[0] != '0';
     bool ok = hipGetDevice(&c->device) == hipSuccess;
     hipDeviceProp_t prop;
     if (ok && hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -1026,10 +1134,29 @@ size_t pbs_chunker_scan(pbs_chunker* c, const uint8_t* data, size_t len) {
     const uint64_t end = c->consumed + len;
     if (end > c->scanned_end) {
         c->timing = pbs_timing{};
+        // No cut can fall before chunk_start + min_eff - 1, and no window of a later position
+        // reaches back before that minus 63: those bytes only update the 63-byte history
+        // (exact for every later chunk too, whose starts are later)
+        const uint64_t lo = c->chunk_start + c->prm.min_eff - 1;
+        const uint64_t skip_to = std::min<uint64_t>(end, lo >= kWindow - 1 ? lo - (kWindow - 1) : 0);
+        if (c->prm.hash_cuts && skip_to > c->scanned_end) {
+            update_carry(c, data + (c->scanned_end - c->consumed), skip_to - c->scanned_end);
+            c->timing.bytes += skip_to - c->scanned_end;
+            c->scanned_end = skip_to;
+        }
         uint64_t pos = c->scanned_end;
         while (pos < end) {
             const uint64_t bl = std::min<uint64_t>(end - pos, batch_max(c));
             const uint8_t* hsrc = data + (pos - c->consumed);
+            if (bl <= kServerMaxBytes) {
+                bool served = false;
+                if (server_scan(c, hsrc, pos, bl, &served) != PBS_OK) return SIZE_MAX;
+                if (served) {
+                    pos += bl;
+                    continue;
+                }
+            }
+            server_stop(c);  // the batch paths below do other device work on the handle
             if (bl <= kFusedMaxBytes) {
                 bool overflow = false;
                 size_t dummy = 0;
@@ -1103,6 +1230,7 @@ int pbs_chunker_candidates_device(pbs_chunker* c, const uint8_t* dev, size_t len
         return fail(c, PBS_ERR_INVALID);
     *n_out = 0;
     HIP_TRY(c, hipSetDevice(c->device));
+    server_stop(c);
     c->timing = pbs_timing{};
     // the handle's carry is the warm-up history of scan_candidates: swap the halo in
     uint8_t saved[64];
@@ -1133,6 +1261,7 @@ int pbs_chunker_resolve_device(pbs_chunker* c, const uint64_t* cand_dev, size_t 
     if (n > 0xFFFFFFF0ull) return fail(c, PBS_ERR_NOMEM);
     if (cap < pbs_chunker_cuts_bound(c, end)) return fail(c, PBS_ERR_CAPACITY);
     HIP_TRY(c, hipSetDevice(c->device));
+    server_stop(c);
     reset_stream(c);
     // keep the phase-A fields of a preceding candidates_device call
     c->timing.resolve_ms = c->timing.total_ms = 0;

@@ -148,6 +148,33 @@ hipError_t launch_scan_resolve_small(const FusedScanArgs& fa, int resolve, uint6
                                      uint64_t* out_host, uint64_t host_cap, uint64_t* keep_host,
                                      uint64_t keep_cap, uint64_t* res, uint64_t* res_host,
                                      hipStream_t stream);
+// ---- scan server (scan_server.h): the low-latency path of pbs_chunker_scan ----------
+// A persistent one-workgroup kernel polls a mailbox in fine-grained (coherent) pinned host
+// memory; the host writes a request (the new bytes go to a pinned slot) and spins on the
+// acknowledgement, so one scan() call costs one PCIe round trip instead of a copy, two
+// launches and a stream sync.
+constexpr uint32_t kServerMaxBytes = 1u << 20;  // request slot (bigger calls: batch path)
+constexpr uint32_t kServerCand = 16384;         // candidates one request may return
+struct alignas(64) ServerMailbox {
+    // host -> device
+    uint64_t req_seq;   // request number, stored last (release)
+    uint64_t base;      // absolute stream offset of the slot's first byte
+    uint32_t len;       // bytes in the slot
+    uint32_t pre_len;   // bytes in pre (the stream bytes just before `base`, <= 63)
+    uint32_t quit;      // 1: exit now
+    uint32_t pad0;
+    uint8_t pre[64];
+    // device -> host
+    alignas(64) uint64_t ack_seq;  // = req_seq once served (release)
+    uint64_t exited;               // last served request when the kernel exited; ~0 while up
+    uint64_t ncand;                // candidates in cand[] (ascending, absolute)
+    uint64_t status;               // 0 ok, 1 more than kServerCand candidates (nothing usable)
+    uint64_t cand[kServerCand];
+};
+hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, uint32_t mask,
+                              uint32_t minimum, uint64_t last_seq, uint64_t idle_ticks,
+                              hipStream_t stream);
+
 // pbs_blob.hip: free the blob-CRC chunk counter kept for `st` (call before destroying it)
 void release_stream_counter(hipStream_t st);
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,

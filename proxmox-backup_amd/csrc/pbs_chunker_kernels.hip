@@ -31,6 +31,7 @@
 #include "exact_block.h"  // exact candidate positions of one 128-byte block (one wave)
 #include "scan_main.h"  // scan_main_kernel (phase A main pass)
 #include "scan_fused.h"  // scan_fused_kernel (phase A + exact + resolve in one launch)
+#include "scan_server.h"  // scan_server_kernel (the low-latency scan() path)
 
 namespace pbs {
 
@@ -901,22 +902,30 @@ hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid
     if (a.ntiles + a.ntail == 0 || grid < 1) return hipErrorInvalidValue;
     (void)hipGetLastError();
     const dim3 gd(grid), bd(kWavesPerWG * 64);
-#define PBS_FUSED_CASE(S)                                                                   \
-    case S:                                                                                 \
-        if (dyn)                                                                            \
-            hipLaunchKernelGGL((scan_fused_kernel<S, 1>), gd, bd, 0, stream, a);            \
-        else                                                                                \
-            hipLaunchKernelGGL((scan_fused_kernel<S, 0>), gd, bd, 0, stream, a);            \
-        break;
-    switch (seg) {
-        PBS_FUSED_CASE(32768)
-        PBS_FUSED_CASE(16384)
-        PBS_FUSED_CASE(8192)
-        PBS_FUSED_CASE(4096)
-        default:
-            return hipErrorInvalidValue;
-    }
-#undef PBS_FUSED_CASE
+    // the dynamic tile order only ever uses 16 / 8 KiB segments (scan_main_plan)
+    if (dyn && seg == 16384)
+        hipLaunchKernelGGL((scan_fused_kernel<16384, 1>), gd, bd, 0, stream, a);
+    else if (dyn && seg == 8192)
+        hipLaunchKernelGGL((scan_fused_kernel<8192, 1>), gd, bd, 0, stream, a);
+    else if (!dyn && seg == 32768)
+        hipLaunchKernelGGL((scan_fused_kernel<32768, 0>), gd, bd, 0, stream, a);
+    else if (!dyn && seg == 16384)
+        hipLaunchKernelGGL((scan_fused_kernel<16384, 0>), gd, bd, 0, stream, a);
+    else if (!dyn && seg == 8192)
+        hipLaunchKernelGGL((scan_fused_kernel<8192, 0>), gd, bd, 0, stream, a);
+    else if (!dyn && seg == 4096)
+        hipLaunchKernelGGL((scan_fused_kernel<4096, 0>), gd, bd, 0, stream, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, uint32_t mask,
+                              uint32_t minimum, uint64_t last_seq, uint64_t idle_ticks,
+                              hipStream_t stream) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(scan_server_kernel, dim3(1), dim3(kSrvThreads), 0, stream, mb_dev, slot_dev,
+                       mask, minimum, last_seq, idle_ticks);
     return hipGetLastError();
 }
 

@@ -115,20 +115,18 @@ __device__ __forceinline__ void fused_publish(const FusedPassArgs& a, const uint
 }
 
 // Phase B over the tile records, one wave (see the file comment).  `keep` = LDS scratch
-// of kFusedKeep entries.
+// of kFusedKeep entries.  Per batch of 64 records: the next batch's records are already
+// in flight, the batch's candidates (<= 64 per step) load in one round trip, and the cut
+// rule runs on the candidate vector with one ballot per cut (candidates below the
+// minimum are skipped together).
 __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane) {
     const uint64_t total = a.ntiles + a.ntail;
     uint64_t s = a.s0, ncut = 0;
     uint32_t nkeep = 0, status = 0;
     const uint64_t t_start = wall_clock64();
+    uint64_t t_wait = 0, t_ready = t_start;
+    const unsigned long long below = (1ull << lane) - 1;
 
-    auto emit = [&](uint64_t x) {
-        if (lane == 0) {
-            if (ncut < a.cuts_cap) a.cuts[ncut] = x;
-            if (ncut < a.host_cap) a.cuts_host[ncut] = x;
-        }
-        ++ncut;
-    };
     auto forced = [&](uint64_t k) {  // k forced (max-size) cuts from s
         for (uint64_t j = (uint64_t)lane; j < k; j += 64) {
             const uint64_t x = s + (j + 1) * a.max_eff;
@@ -137,79 +135,127 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
         }
         ncut += k;
         s += k * a.max_eff;
-        nkeep = 0;
     };
-    // chunker.rs:172-183 for the next candidate c (ascending, c >= s): forced cuts while
-    // the chunk would exceed max before c; then c cuts iff the chunk is >= min long at c
-    auto process = [&](uint64_t c) {
-        const uint64_t hi = s + a.max_eff - 1;
-        if (c > hi) forced((c - hi + a.max_eff - 1) >> a.max_shift);
-        if (c >= s + a.min_eff - 1) {
-            emit(c + 1);
-            s = c + 1;
-            nkeep = 0;
-        } else {
-            if (lane == 0 && nkeep < kFusedKeep) keep[nkeep] = c;
-            ++nkeep;
+    // chunker.rs:172-183 over ascending candidates c (lanes in `vm`, all >= s): the next
+    // cut is the first candidate >= s + min - 1 if it is <= s + max - 1, else forced cuts
+    // until it is; candidates left over are the open chunk's (kept, in order)
+    auto process_vec = [&](uint64_t c, unsigned long long vm) {
+        unsigned long long rem = vm;
+        bool reset = false;
+        while (rem) {
+            const unsigned long long m = __ballot(c >= s + a.min_eff - 1) & rem;
+            if (!m) break;
+            const int k = __ffsll(m) - 1;
+            const uint64_t ck = readlane64(c, k);
+            const uint64_t hi = s + a.max_eff - 1;
+            reset = true;
+            if (ck > hi) {  // the lanes before k stay below every later minimum
+                forced((ck - hi + a.max_eff - 1) >> a.max_shift);
+                continue;
+            }
+            if (lane == 0) {
+                if (ncut < a.cuts_cap) a.cuts[ncut] = ck + 1;
+                if (ncut < a.host_cap) a.cuts_host[ncut] = ck + 1;
+            }
+            ++ncut;
+            s = ck + 1;
+            rem &= ~((2ull << k) - 1);
         }
+        if (reset) nkeep = 0;
+        const unsigned long long km = __ballot(c >= s) & rem;
+        if ((km >> lane) & 1ull) {
+            const uint32_t pos = nkeep + (uint32_t)__popcll(km & below);
+            if (pos < kFusedKeep) keep[pos] = c;
+        }
+        nkeep += (uint32_t)__popcll(km);
     };
 
     for (uint32_t i = 0; i < a.npend; i += 64) {
-        const uint64_t v = i + lane < a.npend ? a.pend[i + lane] : 0;
-        const uint32_t m = a.npend - i < 64 ? a.npend - i : 64;
-        for (uint32_t k = 0; k < m; ++k) process(readlane64(v, (int)k));
+        const bool v = i + lane < a.npend;
+        process_vec(v ? a.pend[i + lane] : ~0ull, __ballot(v));
     }
-    for (uint64_t t0 = 0; t0 < total && status == 0; t0 += 64) {
+    auto load_rec = [&](uint64_t t0) -> uint64_t {
+        return t0 + lane < total ? __hip_atomic_load(a.rec + t0 + lane, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0ull;
+    };
+    uint64_t rv = load_rec(0);
+    for (uint64_t t0 = 0; t0 < total; t0 += 64) {
         const uint32_t n = total - t0 < 64 ? (uint32_t)(total - t0) : 64u;
-        uint64_t rv = 0;
-        bool done = (uint32_t)lane >= n;
-        for (;;) {
-            if (!done) {
-                rv = __hip_atomic_load(a.rec + t0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                done = (uint32_t)(rv >> 48) == a.epoch;
+        bool done = (uint32_t)lane >= n || (uint32_t)(rv >> 48) == a.epoch;
+        if (!__all(done)) {
+            const uint64_t w0 = wall_clock64();
+            for (;;) {
+                __builtin_amdgcn_s_sleep(2);
+                if (!done) {
+                    rv = load_rec(t0);
+                    done = (uint32_t)(rv >> 48) == a.epoch;
+                }
+                if (__all(done)) break;
+                if (wall_clock64() - t_start > a.timeout_ticks) {
+                    status = 2;
+                    break;
+                }
             }
-            if (__all(done)) break;
-            if (wall_clock64() - t_start > a.timeout_ticks) {
-                status = 2;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(4);
+            t_ready = wall_clock64();
+            t_wait += t_ready - w0;
+            if (status) break;
         }
-        if (status) break;
-        const uint32_t cnt = (uint32_t)(rv >> 32) & 0xFFFFu;
-        if (__any((uint32_t)lane < n && cnt == kRecOverflow)) {
+        const uint32_t cnt = (uint32_t)lane < n ? (uint32_t)(rv >> 32) & 0xFFFFu : 0u;
+        const uint64_t idx = rv & 0xFFFFFFFFull;
+        if (__any(cnt == kRecOverflow)) {
             status = 1;
             break;
         }
-        unsigned long long mask = __ballot((uint32_t)lane < n && cnt != 0);
-        while (mask) {
-            const int j = __ffsll(mask) - 1;
-            mask &= mask - 1;
-            const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)cnt, j);
-            const uint64_t ij = readlane64(rv & 0xFFFFFFFFull, j);
-            for (uint32_t q = 0; q < cj; q += 64) {
-                const uint64_t cv = q + lane < cj ? __hip_atomic_load(a.cand + ij + q + lane,
-                                                                      __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                                  : 0;
-                const uint32_t m = cj - q < 64 ? cj - q : 64;
-                for (uint32_t k = 0; k < m; ++k) process(readlane64(cv, (int)k));
+        rv = load_rec(t0 + 64);  // the next batch's records, in flight meanwhile
+        const unsigned long long nz = __ballot(cnt != 0);
+        if (!nz) continue;
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
+        for (uint32_t k0 = 0; k0 < T; k0 += 64) {
+            const uint32_t k = k0 + (uint32_t)lane;
+            int j = 63;  // the record holding candidate k: the first lane whose prefix exceeds k
+            for (unsigned long long mm = nz; mm; mm &= mm - 1) {
+                const int i = __ffsll(mm) - 1;
+                if ((uint32_t)__builtin_amdgcn_readlane((int)incl, i) > k) {
+                    j = i;
+                    break;
+                }
             }
+            const uint32_t ej = (uint32_t)__shfl((int)(incl - cnt), j, 64);
+            const uint64_t ij = (uint64_t)(uint32_t)__shfl((int)(uint32_t)idx, j, 64);
+            const bool v = k < T;
+            const uint64_t c = v ? __hip_atomic_load(a.cand + ij + (k - ej), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                 : ~0ull;
+            process_vec(c, __ballot(v));
         }
     }
     if (status == 0) {
-        if (s + a.max_eff <= a.end) forced((a.end - s) >> a.max_shift);  // no candidate left
+        if (s + a.max_eff <= a.end) {  // no candidate left: forced cuts up to the end
+            forced((a.end - s) >> a.max_shift);
+            nkeep = 0;
+        }
         if (nkeep > kFusedKeep) status = 1;
     }
     if (status == 0 && nkeep <= a.keep_cap)
         for (uint32_t i = lane; i < nkeep; i += 64) a.keep_host[i] = keep[i];
     if ((uint32_t)lane < a.tail_len) a.tail_host[lane] = a.tail_src[lane];
     if (lane == 0) {
+        const uint64_t t_end = wall_clock64();
         a.res_host[0] = ncut;
         a.res_host[1] = s;
         a.res_host[2] = nkeep;
         a.res_host[4] = __hip_atomic_load(a.ncand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         a.res_host[5] = __hip_atomic_load(a.nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.res_host[6] = t_ready - t_start;  // diagnostics (100 MHz ticks): last record ready,
+        a.res_host[7] = t_end - t_start;    // resolver done, time spent waiting for records
+        a.res_host[8] = t_wait;
         a.res_host[3] = status;
     }
 }

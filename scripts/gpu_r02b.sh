@@ -1,0 +1,11 @@
+#!/bin/bash
+# fused pass: parity first (short tests, then full-size), then the bench line
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp; O=gpurun_out/r02b; mkdir -p $O
+step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
+step fused 300 python -u -m pytest tests/test_gpu_parity.py -k "fused or golden or split or device or small" -x -v --timeout 120 --timeout-method thread || exit 1
+step parity 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread || exit 1
+step bench64 300 python bench.py --cpu-baseline 0 || exit 1
+step bench64_unfused 300 env PBS_FUSED=0 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 || exit 1
+step c5 300 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 --avg 262144 || exit 1
+echo done
