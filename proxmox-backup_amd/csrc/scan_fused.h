@@ -114,52 +114,137 @@ __device__ __forceinline__ void fused_publish(const FusedPassArgs& a, const uint
     }
 }
 
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {  // divergent source lane
+    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src, 64) |
+           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64) << 32);
+}
+
+// first lane in [from, 64) whose candidate is >= x (64 if none); lanes hold ascending c
+// (~0 past the valid ones).  All 64 lanes take part (the shuffles read every lane).
+__device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, uint64_t x) {
+    int lo = from, hi = 64;
+#pragma unroll
+    for (int it = 0; it < 7; ++it) {
+        const int mid = (lo + hi) >> 1;
+        const uint64_t v = shfl64(c, mid < 64 ? mid : 63);
+        const bool go_right = lo < hi && v < x;
+        const bool go_left = lo < hi && !(v < x);
+        lo = go_right ? mid + 1 : lo;
+        hi = go_left ? mid : hi;
+    }
+    return lo;
+}
+
 // Phase B over the tile records, one wave (see the file comment).  `keep` = LDS scratch
 // of kFusedKeep entries.  Per batch of 64 records: the next batch's records are already
-// in flight, the batch's candidates (<= 64 per step) load in one round trip, and the cut
-// rule runs on the candidate vector with one ballot per cut (candidates below the
-// minimum are skipped together).
+// in flight and the batch's candidates (<= 64 per step) load in one round trip.  The cut
+// rule runs on a candidate VECTOR at once: every lane finds, for a cut at its own
+// candidate, the next cut inside the vector (lane binary search, with the forced cuts in
+// between in closed form); the chain from the vector's first cut is traced by pointer
+// jumping (6 rounds), and the cuts are written with one prefix sum.
 __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane) {
+    // every field in a register: the struct lives in kernarg memory behind a generic
+    // reference and would be re-read after each store
     const uint64_t total = a.ntiles + a.ntail;
+    const uint64_t min1 = a.min_eff - 1, max_eff = a.max_eff, max1 = a.max_eff - 1;
+    const uint32_t sh = a.max_shift, epoch = a.epoch;
+    uint64_t* const cuts = a.cuts;
+    uint64_t* const cuts_host = a.cuts_host;
+    const uint64_t cuts_cap = a.cuts_cap, host_cap = a.host_cap;
+    const unsigned long long* const rec = a.rec;
+    const uint64_t* const cand = a.cand;
+    const uint64_t timeout = a.timeout_ticks, end = a.end;
     uint64_t s = a.s0, ncut = 0;
     uint32_t nkeep = 0, status = 0;
     const uint64_t t_start = wall_clock64();
     uint64_t t_wait = 0, t_ready = t_start;
     const unsigned long long below = (1ull << lane) - 1;
 
-    auto forced = [&](uint64_t k) {  // k forced (max-size) cuts from s
-        for (uint64_t j = (uint64_t)lane; j < k; j += 64) {
-            const uint64_t x = s + (j + 1) * a.max_eff;
-            if (ncut + j < a.cuts_cap) a.cuts[ncut + j] = x;
-            if (ncut + j < a.host_cap) a.cuts_host[ncut + j] = x;
-        }
-        ncut += k;
-        s += k * a.max_eff;
+    auto put = [&](uint64_t i, uint64_t x) {
+        if (i < cuts_cap) cuts[i] = x;
+        if (i < host_cap) cuts_host[i] = x;
     };
-    // chunker.rs:172-183 over ascending candidates c (lanes in `vm`, all >= s): the next
-    // cut is the first candidate >= s + min - 1 if it is <= s + max - 1, else forced cuts
-    // until it is; candidates left over are the open chunk's (kept, in order)
+    auto forced = [&](uint64_t k) {  // k forced (max-size) cuts from s, lane-parallel
+        for (uint64_t j = (uint64_t)lane; j < k; j += 64) put(ncut + j, s + (j + 1) * max_eff);
+        ncut += k;
+        s += k * max_eff;
+    };
+    // chunker.rs:172-183 over the ascending candidates of the lanes in vm (~0 elsewhere),
+    // all >= s.  Cuts, forced cuts and the new state s; the candidates left over belong to
+    // the open chunk (kept in order)
     auto process_vec = [&](uint64_t c, unsigned long long vm) {
-        unsigned long long rem = vm;
         bool reset = false;
-        while (rem) {
-            const unsigned long long m = __ballot(c >= s + a.min_eff - 1) & rem;
+        int e = -1;
+        for (;;) {  // the vector's first cut (uniform)
+            const unsigned long long m = __ballot(c >= s + min1) & vm;
             if (!m) break;
             const int k = __ffsll(m) - 1;
             const uint64_t ck = readlane64(c, k);
-            const uint64_t hi = s + a.max_eff - 1;
-            reset = true;
-            if (ck > hi) {  // the lanes before k stay below every later minimum
-                forced((ck - hi + a.max_eff - 1) >> a.max_shift);
+            if (ck > s + max1) {  // the candidates before k stay below every later minimum
+                forced((ck - (s + max1) + max_eff - 1) >> sh);
+                reset = true;
                 continue;
             }
-            if (lane == 0) {
-                if (ncut < a.cuts_cap) a.cuts[ncut] = ck + 1;
-                if (ncut < a.host_cap) a.cuts_host[ncut] = ck + 1;
+            e = k;
+            break;
+        }
+        unsigned long long rem = vm;
+        if (e >= 0) {
+            reset = true;
+            // successor of a cut at this lane's candidate, inside the vector; nf = forced
+            // cuts after it; a lane whose chain leaves the vector points at itself and
+            // carries its exit state
+            uint64_t sk = c + 1;
+            uint32_t nf = 0;
+            int nx = lane, from = lane + 1;
+            bool active = ((vm >> lane) & 1ull) != 0;
+            while (__any(active)) {
+                const int j = lanes_lower_bound(c, from, sk + min1);
+                const uint64_t cj = shfl64(c, j < 64 ? j : 63);
+                if (active) {
+                    if (j >= 64) {
+                        active = false;
+                    } else if (cj <= sk + max1) {
+                        nx = j;
+                        active = false;
+                    } else {
+                        const uint64_t K = (cj - (sk + max1) + max_eff - 1) >> sh;
+                        nf += (uint32_t)K;
+                        sk += K * max_eff;
+                        from = j;
+                    }
+                }
             }
-            ++ncut;
-            s = ck + 1;
-            rem &= ~((2ull << k) - 1);
+            // pointer jumping: J[t] = the 2^t-th successor; lane k is on the chain from e
+            // iff the greedy descent from e over the jumps lands on k (successors ascend)
+            int J[6];
+            J[0] = nx;
+#pragma unroll
+            for (int t = 1; t < 6; ++t) J[t] = __shfl(J[t - 1], J[t - 1], 64);
+            int x = e, xl = e;
+#pragma unroll
+            for (int t = 5; t >= 0; --t) {
+                const int y = __shfl(J[t], x, 64);
+                x = y <= lane ? y : x;
+                xl = __builtin_amdgcn_readlane(J[t], xl);
+            }
+            const bool on = lane >= e && x == lane;  // xl: the chain's last node (uniform)
+            const uint32_t cnt = on ? 1u + nf : 0u;
+            uint32_t incl = cnt;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += y;
+            }
+            const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
+            if (on) {
+                uint64_t o = ncut + (incl - cnt);
+                put(o, c + 1);
+                for (uint32_t i = 1; i <= nf; ++i) put(o + i, c + 1 + (uint64_t)i * max_eff);
+            }
+            ncut += tot;
+            s = readlane64(sk, xl);
+            rem = xl >= 63 ? 0ull : vm & ~((2ull << xl) - 1);
         }
         if (reset) nkeep = 0;
         const unsigned long long km = __ballot(c >= s) & rem;
@@ -175,24 +260,24 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
         process_vec(v ? a.pend[i + lane] : ~0ull, __ballot(v));
     }
     auto load_rec = [&](uint64_t t0) -> uint64_t {
-        return t0 + lane < total ? __hip_atomic_load(a.rec + t0 + lane, __ATOMIC_RELAXED,
+        return t0 + lane < total ? __hip_atomic_load(rec + t0 + lane, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT)
                                  : 0ull;
     };
     uint64_t rv = load_rec(0);
     for (uint64_t t0 = 0; t0 < total; t0 += 64) {
         const uint32_t n = total - t0 < 64 ? (uint32_t)(total - t0) : 64u;
-        bool done = (uint32_t)lane >= n || (uint32_t)(rv >> 48) == a.epoch;
+        bool done = (uint32_t)lane >= n || (uint32_t)(rv >> 48) == epoch;
         if (!__all(done)) {
             const uint64_t w0 = wall_clock64();
             for (;;) {
                 __builtin_amdgcn_s_sleep(2);
                 if (!done) {
                     rv = load_rec(t0);
-                    done = (uint32_t)(rv >> 48) == a.epoch;
+                    done = (uint32_t)(rv >> 48) == epoch;
                 }
                 if (__all(done)) break;
-                if (wall_clock64() - t_start > a.timeout_ticks) {
+                if (wall_clock64() - t_start > timeout) {
                     status = 2;
                     break;
                 }
@@ -202,14 +287,13 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
             if (status) break;
         }
         const uint32_t cnt = (uint32_t)lane < n ? (uint32_t)(rv >> 32) & 0xFFFFu : 0u;
-        const uint64_t idx = rv & 0xFFFFFFFFull;
+        const uint32_t idx = (uint32_t)rv;
         if (__any(cnt == kRecOverflow)) {
             status = 1;
             break;
         }
         rv = load_rec(t0 + 64);  // the next batch's records, in flight meanwhile
-        const unsigned long long nz = __ballot(cnt != 0);
-        if (!nz) continue;
+        if (!__any(cnt != 0)) continue;
         uint32_t incl = cnt;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -218,27 +302,31 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
         }
         const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
         for (uint32_t k0 = 0; k0 < T; k0 += 64) {
+            // candidate k0 + lane lives in the record of the first lane whose prefix exceeds it
             const uint32_t k = k0 + (uint32_t)lane;
-            int j = 63;  // the record holding candidate k: the first lane whose prefix exceeds k
-            for (unsigned long long mm = nz; mm; mm &= mm - 1) {
-                const int i = __ffsll(mm) - 1;
-                if ((uint32_t)__builtin_amdgcn_readlane((int)incl, i) > k) {
-                    j = i;
-                    break;
-                }
+            int lo = 0, hi = 64;
+#pragma unroll
+            for (int it = 0; it < 7; ++it) {
+                const int mid = (lo + hi) >> 1;
+                const uint32_t v = (uint32_t)__shfl((int)incl, mid < 64 ? mid : 63, 64);
+                const bool right = lo < hi && v <= k;
+                const bool left = lo < hi && !(v <= k);
+                lo = right ? mid + 1 : lo;
+                hi = left ? mid : hi;
             }
+            const int j = lo < 64 ? lo : 63;
             const uint32_t ej = (uint32_t)__shfl((int)(incl - cnt), j, 64);
-            const uint64_t ij = (uint64_t)(uint32_t)__shfl((int)(uint32_t)idx, j, 64);
+            const uint32_t ij = (uint32_t)__shfl((int)idx, j, 64);
             const bool v = k < T;
-            const uint64_t c = v ? __hip_atomic_load(a.cand + ij + (k - ej), __ATOMIC_RELAXED,
+            const uint64_t c = v ? __hip_atomic_load(cand + (uint64_t)ij + (k - ej), __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT)
                                  : ~0ull;
             process_vec(c, __ballot(v));
         }
     }
     if (status == 0) {
-        if (s + a.max_eff <= a.end) {  // no candidate left: forced cuts up to the end
-            forced((a.end - s) >> a.max_shift);
+        if (s + max_eff <= end) {  // no candidate left: forced cuts up to the end
+            forced((end - s) >> sh);
             nkeep = 0;
         }
         if (nkeep > kFusedKeep) status = 1;

@@ -430,6 +430,10 @@ FUSED_CASES = [
     ("zebra_8x3M_4M", lambda: _zebra(8, 3 * MiB, 512 * KiB, 43), 4 * MiB, 2),
     ("counter_24M_128K", lambda: gen_np.gen_counter(24 * MiB), 128 * KiB, 1),
     ("zeros_70M_4M_x2", lambda: np.zeros(70 * MiB + 1, np.uint8), 4 * MiB, 2),
+    # forced-cut runs between candidate runs, candidates packed near the 64-block limit
+    ("zebra_64x(600K+200K)_128K", lambda: _zebra(64, 600 * KiB, 200 * KiB, 45), 128 * KiB, 3),
+    ("vm_300M_128K", lambda: gen_np.gen_vmimage(300 * MiB, 0x5EED0003, 3 * GiB), 128 * KiB, 1),
+    ("random_200M_256K_x7", lambda: gen_np.gen_random(200 * MiB + 9, 46), 256 * KiB, 7),
 ]
 
 
