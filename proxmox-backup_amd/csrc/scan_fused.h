@@ -119,10 +119,10 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {  // divergent 
            ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64) << 32);
 }
 
-// first lane in [from, 64) whose candidate is >= x (64 if none); lanes hold ascending c
-// (~0 past the valid ones).  All 64 lanes take part (the shuffles read every lane).
-__device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, uint64_t x) {
-    int lo = from, hi = 64;
+// first lane in [from, nv) whose candidate is >= x (nv if none); lanes [0, nv) hold
+// ascending candidates.  All 64 lanes take part (the shuffles read every lane).
+__device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, uint64_t x) {
+    int lo = from < nv ? from : nv, hi = nv;
 #pragma unroll
     for (int it = 0; it < 7; ++it) {
         const int mid = (lo + hi) >> 1;
@@ -197,12 +197,13 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
             uint64_t sk = c + 1;
             uint32_t nf = 0;
             int nx = lane, from = lane + 1;
-            bool active = ((vm >> lane) & 1ull) != 0;
-            while (__any(active)) {
-                const int j = lanes_lower_bound(c, from, sk + min1);
+            const int nv = __popcll(vm);  // the valid lanes are a prefix
+            bool active = lane < nv;
+            for (int guard = 0; guard < 64 && __any(active); ++guard) {  // each round moves j on
+                const int j = lanes_lower_bound(c, from, nv, sk + min1);
                 const uint64_t cj = shfl64(c, j < 64 ? j : 63);
                 if (active) {
-                    if (j >= 64) {
+                    if (j >= nv) {
                         active = false;
                     } else if (cj <= sk + max1) {
                         nx = j;

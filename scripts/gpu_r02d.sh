@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp; O=gpurun_out/r02d; mkdir -p $O
 step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
-step fused 300 python -u -m pytest tests/test_gpu_parity.py -k "fused or golden or split or device or small or scan or chunker1 or chunk_stream or speed_loop or invalid" -x -v --timeout 120 --timeout-method thread || exit 1
+step fused 300 python -u -m pytest tests/test_gpu_parity.py -k "fused or golden or split or device or small or scan or chunker1 or chunk_stream or speed_loop or invalid" -x -v --timeout 60 --timeout-method thread || exit 1
 step ex_8k_unchanged 120 examples/test_chunk_speed2 - 1073741824 8192 4194304 0 1 || exit 1
 step ex_256k_unchanged 120 examples/test_chunk_speed2 - 1073741824 262144 4194304 0 1 || exit 1
 step ex_8k_gather 120 examples/test_chunk_speed2 - 1073741824 8192 4194304 4194304 1 || exit 1
