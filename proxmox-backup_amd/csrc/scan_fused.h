@@ -36,7 +36,9 @@
 
 namespace pbs {
 
-constexpr int kFusedKeep = 1024;    // open-chunk candidates the resolver keeps in LDS
+constexpr int kFusedKeep = 512;     // open-chunk candidates the resolver keeps in LDS
+constexpr int kStageCand = 512;     // candidates of one resolver step staged in LDS
+constexpr int kResolveBatch = 256;  // tile records per resolver step (4 per lane)
 constexpr uint32_t kRecOverflow = 0xFFFFu;
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
@@ -120,11 +122,15 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {  // divergent 
 }
 
 // first lane in [from, nv) whose candidate is >= x (nv if none); lanes [0, nv) hold
-// ascending candidates.  All 64 lanes take part (the shuffles read every lane).
+// ascending candidates.  `from` itself is probed first (a chunk usually ends at the next
+// candidate); the rest is a binary search that runs only as long as some lane needs it.
+// All 64 lanes take part (the shuffles read every lane).
 __device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, uint64_t x) {
     int lo = from < nv ? from : nv, hi = nv;
-#pragma unroll
-    for (int it = 0; it < 7; ++it) {
+    const uint64_t v0 = shfl64(c, lo < 64 ? lo : 63);
+    if (lo < hi && v0 >= x) hi = lo;
+    else if (lo < hi) ++lo;
+    while (__any(lo < hi)) {
         const int mid = (lo + hi) >> 1;
         const uint64_t v = shfl64(c, mid < 64 ? mid : 63);
         const bool go_right = lo < hi && v < x;
@@ -136,8 +142,9 @@ __device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, u
 }
 
 // Phase B over the tile records, one wave (see the file comment).  `keep` = LDS scratch
-// of kFusedKeep entries.  Per batch of 64 records: the next batch's records are already
-// in flight and the batch's candidates (<= 64 per step) load in one round trip.  The cut
+// of kFusedKeep + kStageCand entries.  Per step of 256 records: the next step's records
+// are already in flight and the step's candidates load (8 per lane in flight) into LDS in
+// stream order.  The cut
 // rule runs on a candidate VECTOR at once: every lane finds, for a cut at its own
 // candidate, the next cut inside the vector (lane binary search, with the forced cuts in
 // between in closed form); the chain from the vector's first cut is traced by pointer
@@ -260,22 +267,35 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
         const bool v = i + lane < a.npend;
         process_vec(v ? a.pend[i + lane] : ~0ull, __ballot(v));
     }
-    auto load_rec = [&](uint64_t t0) -> uint64_t {
-        return t0 + lane < total ? __hip_atomic_load(rec + t0 + lane, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)
-                                 : 0ull;
+    // records t0 + 4*lane + q (q < 4): 256 per step, the next step's already in flight
+    uint64_t rv[4];
+    auto load_rec = [&](uint64_t t0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t t = t0 + 4 * (uint64_t)lane + q;
+            rv[q] = t < total ? __hip_atomic_load(rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : ((uint64_t)epoch << 48);
+        }
     };
-    uint64_t rv = load_rec(0);
-    for (uint64_t t0 = 0; t0 < total; t0 += 64) {
-        const uint32_t n = total - t0 < 64 ? (uint32_t)(total - t0) : 64u;
-        bool done = (uint32_t)lane >= n || (uint32_t)(rv >> 48) == epoch;
+    uint64_t* const stc = keep + kFusedKeep;  // candidates of one step, in stream order
+    load_rec(0);
+    for (uint64_t t0 = 0; t0 < total; t0 += kResolveBatch) {
+        bool done = true;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) done = done && (uint32_t)(rv[q] >> 48) == epoch;
         if (!__all(done)) {
             const uint64_t w0 = wall_clock64();
             for (;;) {
                 __builtin_amdgcn_s_sleep(2);
                 if (!done) {
-                    rv = load_rec(t0);
-                    done = (uint32_t)(rv >> 48) == epoch;
+                    done = true;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint64_t t = t0 + 4 * (uint64_t)lane + q;
+                        if ((uint32_t)(rv[q] >> 48) != epoch && t < total)
+                            rv[q] = __hip_atomic_load(rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        done = done && (uint32_t)(rv[q] >> 48) == epoch;
+                    }
                 }
                 if (__all(done)) break;
                 if (wall_clock64() - t_start > timeout) {
@@ -287,42 +307,54 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
             t_wait += t_ready - w0;
             if (status) break;
         }
-        const uint32_t cnt = (uint32_t)lane < n ? (uint32_t)(rv >> 32) & 0xFFFFu : 0u;
-        const uint32_t idx = (uint32_t)rv;
-        if (__any(cnt == kRecOverflow)) {
+        uint32_t cq[4], iq[4];
+        bool ovf = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            cq[q] = (uint32_t)(rv[q] >> 32) & 0xFFFFu;
+            iq[q] = (uint32_t)rv[q];
+            ovf = ovf || cq[q] == kRecOverflow;
+        }
+        if (__any(ovf)) {
             status = 1;
             break;
         }
-        rv = load_rec(t0 + 64);  // the next batch's records, in flight meanwhile
-        if (!__any(cnt != 0)) continue;
-        uint32_t incl = cnt;
+        load_rec(t0 + kResolveBatch);  // the next step's records, in flight meanwhile
+        const uint32_t p1 = cq[0], p2 = p1 + cq[1], p3 = p2 + cq[2], sum = p3 + cq[3];
+        if (!__any(sum != 0)) continue;
+        uint32_t incl = sum;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t y = __shfl_up(incl, d, 64);
             if (lane >= d) incl += y;
         }
+        const uint32_t base = incl - sum;
         const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
-        for (uint32_t k0 = 0; k0 < T; k0 += 64) {
-            // candidate k0 + lane lives in the record of the first lane whose prefix exceeds it
-            const uint32_t k = k0 + (uint32_t)lane;
-            int lo = 0, hi = 64;
+        for (uint32_t k0 = 0; k0 < T; k0 += kStageCand) {
+            // each lane stages its own records' candidates with step index in
+            // [k0, k0 + kStageCand), 8 loads in flight at a time
+            for (uint32_t i0 = 0; __any(i0 < sum); i0 += 8) {
+                uint64_t v[8];
+                uint32_t at[8];
 #pragma unroll
-            for (int it = 0; it < 7; ++it) {
-                const int mid = (lo + hi) >> 1;
-                const uint32_t v = (uint32_t)__shfl((int)incl, mid < 64 ? mid : 63, 64);
-                const bool right = lo < hi && v <= k;
-                const bool left = lo < hi && !(v <= k);
-                lo = right ? mid + 1 : lo;
-                hi = left ? mid : hi;
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t i = i0 + (uint32_t)u, kk = base + i;
+                    const bool ok = i < sum && kk >= k0 && kk < k0 + kStageCand;
+                    const uint32_t q = (i >= p1 ? 1u : 0u) + (i >= p2 ? 1u : 0u) + (i >= p3 ? 1u : 0u);
+                    const uint32_t ix = q == 0 ? iq[0] + i : q == 1 ? iq[1] + (i - p1)
+                                      : q == 2 ? iq[2] + (i - p2) : iq[3] + (i - p3);
+                    v[u] = ok ? __hip_atomic_load(cand + ix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                    at[u] = ok ? kk - k0 : ~0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (at[u] != ~0u) stc[at[u]] = v[u];
             }
-            const int j = lo < 64 ? lo : 63;
-            const uint32_t ej = (uint32_t)__shfl((int)(incl - cnt), j, 64);
-            const uint32_t ij = (uint32_t)__shfl((int)idx, j, 64);
-            const bool v = k < T;
-            const uint64_t c = v ? __hip_atomic_load(cand + (uint64_t)ij + (k - ej), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)
-                                 : ~0ull;
-            process_vec(c, __ballot(v));
+            const uint32_t nh = T - k0 < (uint32_t)kStageCand ? T - k0 : (uint32_t)kStageCand;
+            for (uint32_t v0 = 0; v0 < nh; v0 += 64) {
+                const bool v = v0 + lane < nh;
+                process_vec(v ? stc[v0 + lane] : ~0ull, __ballot(v));
+            }
         }
     }
     if (status == 0) {
