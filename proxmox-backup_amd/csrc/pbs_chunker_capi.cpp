@@ -567,9 +567,9 @@ constexpr double kServerTimeoutS = 10.0;
 void server_stop(pbs_chunker* c) {
     ScanServer& sv = c->srv;
     if (!sv.running) return;
-    __atomic_store_n(&sv.mb->quit, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(&sv.mb->req_len, kServerQuit, __ATOMIC_RELEASE);
     (void)hipStreamSynchronize(sv.stream);
-    __atomic_store_n(&sv.mb->quit, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&sv.mb->req_len, 0u, __ATOMIC_RELEASE);
     sv.running = false;
 }
 
@@ -593,29 +593,29 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
         HIP_TRY(c, hipHostMalloc((void**)&sv.mb, sizeof(ServerMailbox), fl));
         std::memset(sv.mb, 0, sizeof(ServerMailbox));
-        HIP_TRY(c, hipHostMalloc((void**)&sv.slot, kServerMaxBytes, fl));
+        HIP_TRY(c, hipHostMalloc((void**)&sv.slot, kServerHist + kServerMaxBytes, fl));
         HIP_TRY(c, hipHostGetDevicePointer((void**)&sv.mb_dev, sv.mb, 0));
         HIP_TRY(c, hipHostGetDevicePointer((void**)&sv.slot_dev, sv.slot, 0));
         HIP_TRY(c, hipStreamCreateWithFlags(&sv.stream, hipStreamNonBlocking));
     }
-    std::memcpy(sv.slot, hsrc, bl);
-    sv.mb->base = pos;
-    sv.mb->len = (uint32_t)bl;
-    sv.mb->pre_len = c->carry_len;
-    std::memcpy(sv.mb->pre, c->carry, c->carry_len);
-    const uint64_t seq = ++sv.seq;
+    // slot: the history right-aligned in its first kServerHist bytes, then the data
+    std::memcpy(sv.slot + kServerHist - c->carry_len, c->carry, c->carry_len);
+    std::memcpy(sv.slot + kServerHist, hsrc, bl);
+    sv.mb->req_base = pos;
+    sv.mb->req_len = (uint32_t)bl;
+    const uint32_t seq = (uint32_t)++sv.seq;
     if (!sv.running) {
-        int rc = server_launch(c, seq - 1);
+        int rc = server_launch(c, (uint32_t)(seq - 1));
         if (rc) return rc;
     }
     __atomic_store_n(&sv.mb->req_seq, seq, __ATOMIC_RELEASE);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
         if (__atomic_load_n(&sv.mb->ack_seq, __ATOMIC_ACQUIRE) == seq) break;
-        if (__atomic_load_n(&sv.mb->exited, __ATOMIC_ACQUIRE) == seq - 1) {
+        if (__atomic_load_n(&sv.mb->exited, __ATOMIC_ACQUIRE) == (uint32_t)(seq - 1)) {
             // it went idle just before this request: relaunch, the request is still there
             HIP_TRY(c, hipStreamSynchronize(sv.stream));
-            int rc = server_launch(c, seq - 1);
+            int rc = server_launch(c, (uint32_t)(seq - 1));
             if (rc) return rc;
             continue;
         }

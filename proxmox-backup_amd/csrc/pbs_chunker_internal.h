@@ -155,15 +155,17 @@ hipError_t launch_scan_resolve_small(const FusedScanArgs& fa, int resolve, uint6
 // launches and a stream sync.
 constexpr uint32_t kServerMaxBytes = 1u << 20;  // request slot (bigger calls: batch path)
 constexpr uint32_t kServerCand = 16384;         // candidates one request may return
+constexpr uint32_t kServerHist = 64;            // slot bytes before the data: the history
+constexpr uint32_t kServerQuit = 1u << 31;      // req_len flag
 struct alignas(64) ServerMailbox {
-    // host -> device
-    uint64_t req_seq;   // request number, stored last (release)
-    uint64_t base;      // absolute stream offset of the slot's first byte
-    uint32_t len;       // bytes in the slot
-    uint32_t pre_len;   // bytes in pre (the stream bytes just before `base`, <= 63)
-    uint32_t quit;      // 1: exit now
-    uint32_t pad0;
-    uint8_t pre[64];
+    // host -> device: ONE 16-byte record the kernel polls with one load (the host stores
+    // len and base before seq, all in one cache line, so a record with the new seq has them)
+    uint32_t req_seq;   // request number, stored last (release)
+    uint32_t req_len;   // data bytes in the slot (after its kServerHist history bytes);
+                        // kServerQuit set: exit now
+    uint64_t req_base;  // absolute stream offset of the data; history = the min(63, base)
+                        // stream bytes before it, right-aligned in the slot's first 64 bytes
+    uint32_t pad0[12];
     // device -> host
     alignas(64) uint64_t ack_seq;  // = req_seq once served (release)
     uint64_t exited;               // last served request when the kernel exited; ~0 while up
