@@ -137,6 +137,10 @@ struct pbs_chunker {
     DevBuf d_table, d_pre, d_counters, d_susp, d_cand, d_C, d_sort_tmp, d_nxt, d_jtmp, d_nf, d_on,
         d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in, d_stage, d_hits, d_rec;
     uint32_t rec_epoch = 0;  // fused pass: tile-record epoch of the last launch (16 bits)
+    // fused pass returns on the resolver's status word, before its kernel has retired:
+    // its scan time (ev[0] -> ev[1]) and the call's total (ev[5] -> ev[4]) are read from
+    // the events when last_timing asks for them
+    bool timing_pending = false;
     bool fused = true;       // PBS_FUSED=0: multi-launch path for every batch (A/B)
     uint64_t susp_cap = 0, cand_cap = 0;
     uint64_t batch_limit = 0;  // bytes per batch (0 = batch_max); shrunk when a batch is too dense
@@ -824,13 +828,28 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     a.tail_host = reinterpret_cast<uint8_t*>(small_dev + 24);
     a.tail_len = (uint32_t)tl;
     a.timeout_ticks = 100000000ull * 20;  // 20 s of wall_clock64 (100 MHz)
-    c->h_small[8 + 3] = ~0ull;
+    volatile uint64_t* status_word = c->h_small + 8 + 3;
+    *status_word = ~0ull;
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, launch_scan_fused(a, seg, dyn, c->cu, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    const uint64_t status = c->h_small[8 + 3];
+    // the resolver stores its status word last (system-scope release) once every tile is
+    // resolved: spin on it rather than wait for the kernel to retire; the event tells when
+    // the kernel ended without one (launch failure)
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(status_word, __ATOMIC_ACQUIRE) != ~0ull) break;
+        if ((spin & 255) == 0) {
+            const hipError_t q = hipEventQuery(c->ev[1]);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(status_word, __ATOMIC_ACQUIRE) != ~0ull) break;
+                return fail(c, PBS_ERR_HIP);
+            }
+            if (q != hipErrorNotReady) return fail(c, PBS_ERR_HIP);
+        }
+        __builtin_ia32_pause();
+    }
+    const uint64_t status = *status_word;
     if (c->debug_phases)
         std::fprintf(stderr, "fused pass %llu B: status %llu, resolver last record ready %.1f us, "
                      "done %.1f us, waited %.1f us (after its start)\n",
@@ -850,9 +869,7 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     c->chunk_start = s_open;
     c->pending.swap(keep);
     c->pend_head = 0;
-    float ms = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-    c->timing.scan_ms += ms;
+    c->timing_pending = true;  // scan_ms: last_timing reads ev[0] -> ev[1]
     c->timing.bytes += bl;
     c->timing.suspects += c->h_small[13];
     c->timing.candidates += c->h_small[12];
@@ -872,6 +889,7 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
     HIP_TRY(c, hipSetDevice(c->device));
     server_stop(c);
     c->timing = pbs_timing{};
+    c->timing_pending = false;
     HIP_TRY(c, hipEventRecord(c->ev[5], c->stream));
     const uint64_t end = c->consumed + len;
     uint64_t pos = std::max(c->consumed, c->scanned_end);
@@ -975,9 +993,11 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
         }
         reset_stream(c);
     }
-    float ms = 0;  // ev[4] = end of the last resolve (every path records it), synchronized
-    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[5], c->ev[4]));
-    c->timing.total_ms = ms;
+    if (!c->timing_pending) {
+        float ms = 0;  // ev[4] = end of the last resolve (every path records it), synchronized
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[5], c->ev[4]));
+        c->timing.total_ms = ms;
+    }
     *n_out = n;
     return PBS_OK;
 }
@@ -1117,6 +1137,17 @@ uint64_t pbs_chunker_chunk_start(const pbs_chunker* c) { return c ? c->chunk_sta
 
 int pbs_chunker_last_timing(const pbs_chunker* c, pbs_timing* t) {
     if (!c || !t) return PBS_ERR_INVALID;
+    if (c->timing_pending) {  // a fused pass returned before its kernel retired
+        pbs_chunker* m = const_cast<pbs_chunker*>(c);
+        float scan = 0, total = 0;
+        if (hipEventSynchronize(c->ev[4]) != hipSuccess ||
+            hipEventElapsedTime(&scan, c->ev[0], c->ev[1]) != hipSuccess ||
+            hipEventElapsedTime(&total, c->ev[5], c->ev[4]) != hipSuccess)
+            return fail(m, PBS_ERR_HIP);
+        m->timing.scan_ms += scan;
+        m->timing.total_ms = total;
+        m->timing_pending = false;
+    }
     *t = c->timing;
     return PBS_OK;
 }

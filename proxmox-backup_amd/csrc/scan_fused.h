@@ -377,7 +377,10 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
         a.res_host[6] = t_ready - t_start;  // diagnostics (100 MHz ticks): last record ready,
         a.res_host[7] = t_end - t_start;    // resolver done, time spent waiting for records
         a.res_host[8] = t_wait;
-        a.res_host[3] = status;
+        // last, after every other result (and the cuts) is in host memory: the host
+        // returns as soon as it sees this word
+        __hip_atomic_store(a.res_host + 3, (uint64_t)status, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
