@@ -116,39 +116,10 @@ __device__ __forceinline__ void fused_publish(const FusedPassArgs& a, const uint
     }
 }
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {  // divergent source lane
-    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src, 64) |
-           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64) << 32);
-}
-
-// first lane in [from, nv) whose candidate is >= x (nv if none); lanes [0, nv) hold
-// ascending candidates.  `from` itself is probed first (a chunk usually ends at the next
-// candidate); the rest is a binary search that runs only as long as some lane needs it.
-// All 64 lanes take part (the shuffles read every lane).
-__device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, uint64_t x) {
-    int lo = from < nv ? from : nv, hi = nv;
-    const uint64_t v0 = shfl64(c, lo < 64 ? lo : 63);
-    if (lo < hi && v0 >= x) hi = lo;
-    else if (lo < hi) ++lo;
-    while (__any(lo < hi)) {
-        const int mid = (lo + hi) >> 1;
-        const uint64_t v = shfl64(c, mid < 64 ? mid : 63);
-        const bool go_right = lo < hi && v < x;
-        const bool go_left = lo < hi && !(v < x);
-        lo = go_right ? mid + 1 : lo;
-        hi = go_left ? mid : hi;
-    }
-    return lo;
-}
-
 // Phase B over the tile records, one wave (see the file comment).  `keep` = LDS scratch
 // of kFusedKeep + kStageCand entries.  Per step of 256 records: the next step's records
 // are already in flight and the step's candidates load (8 per lane in flight) into LDS in
-// stream order.  The cut
-// rule runs on a candidate VECTOR at once: every lane finds, for a cut at its own
-// candidate, the next cut inside the vector (lane binary search, with the forced cuts in
-// between in closed form); the chain from the vector's first cut is traced by pointer
-// jumping (6 rounds), and the cuts are written with one prefix sum.
+// stream order; the cut rule then walks each 64-candidate vector (process_vec).
 __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane) {
     // every field in a register: the struct lives in kernarg memory behind a generic
     // reference and would be re-read after each store
@@ -177,83 +148,37 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
         s += k * max_eff;
     };
     // chunker.rs:172-183 over the ascending candidates of the lanes in vm (~0 elsewhere),
-    // all >= s.  Cuts, forced cuts and the new state s; the candidates left over belong to
-    // the open chunk (kept in order)
+    // all >= s: the next cut is the first candidate >= s + min - 1 -- one ballot skips
+    // every candidate below it -- if it is <= s + max - 1, else forced cuts until it is.
+    // The cuts of the vector are collected as a lane mask and written with one vector
+    // store; the candidates left over belong to the open chunk (kept, in order).
     auto process_vec = [&](uint64_t c, unsigned long long vm) {
         bool reset = false;
-        int e = -1;
-        for (;;) {  // the vector's first cut (uniform)
-            const unsigned long long m = __ballot(c >= s + min1) & vm;
+        unsigned long long chain = 0, rem = vm;
+        auto flush = [&]() {
+            if (chain) {
+                if ((chain >> lane) & 1ull) put(ncut + (uint64_t)__popcll(chain & below), c + 1);
+                ncut += (uint64_t)__popcll(chain);
+                chain = 0;
+            }
+        };
+        for (;;) {
+            const unsigned long long m = __ballot(c >= s + min1) & rem;
             if (!m) break;
             const int k = __ffsll(m) - 1;
             const uint64_t ck = readlane64(c, k);
+            reset = true;
             if (ck > s + max1) {  // the candidates before k stay below every later minimum
+                flush();
                 forced((ck - (s + max1) + max_eff - 1) >> sh);
-                reset = true;
+                rem &= ~((1ull << k) - 1);
                 continue;
             }
-            e = k;
-            break;
+            chain |= 1ull << k;
+            s = ck + 1;
+            rem = k == 63 ? 0ull : rem & ~((2ull << k) - 1);
         }
-        unsigned long long rem = vm;
-        if (e >= 0) {
-            reset = true;
-            // successor of a cut at this lane's candidate, inside the vector; nf = forced
-            // cuts after it; a lane whose chain leaves the vector points at itself and
-            // carries its exit state
-            uint64_t sk = c + 1;
-            uint32_t nf = 0;
-            int nx = lane, from = lane + 1;
-            const int nv = __popcll(vm);  // the valid lanes are a prefix
-            bool active = lane < nv;
-            for (int guard = 0; guard < 64 && __any(active); ++guard) {  // each round moves j on
-                const int j = lanes_lower_bound(c, from, nv, sk + min1);
-                const uint64_t cj = shfl64(c, j < 64 ? j : 63);
-                if (active) {
-                    if (j >= nv) {
-                        active = false;
-                    } else if (cj <= sk + max1) {
-                        nx = j;
-                        active = false;
-                    } else {
-                        const uint64_t K = (cj - (sk + max1) + max_eff - 1) >> sh;
-                        nf += (uint32_t)K;
-                        sk += K * max_eff;
-                        from = j;
-                    }
-                }
-            }
-            // pointer jumping: J[t] = the 2^t-th successor; lane k is on the chain from e
-            // iff the greedy descent from e over the jumps lands on k (successors ascend)
-            int J[6];
-            J[0] = nx;
-#pragma unroll
-            for (int t = 1; t < 6; ++t) J[t] = __shfl(J[t - 1], J[t - 1], 64);
-            int x = e, xl = e;
-#pragma unroll
-            for (int t = 5; t >= 0; --t) {
-                const int y = __shfl(J[t], x, 64);
-                x = y <= lane ? y : x;
-                xl = __builtin_amdgcn_readlane(J[t], xl);
-            }
-            const bool on = lane >= e && x == lane;  // xl: the chain's last node (uniform)
-            const uint32_t cnt = on ? 1u + nf : 0u;
-            uint32_t incl = cnt;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += y;
-            }
-            const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
-            if (on) {
-                uint64_t o = ncut + (incl - cnt);
-                put(o, c + 1);
-                for (uint32_t i = 1; i <= nf; ++i) put(o + i, c + 1 + (uint64_t)i * max_eff);
-            }
-            ncut += tot;
-            s = readlane64(sk, xl);
-            rem = xl >= 63 ? 0ull : vm & ~((2ull << xl) - 1);
-        }
+        flush();
         if (reset) nkeep = 0;
         const unsigned long long km = __ballot(c >= s) & rem;
         if ((km >> lane) & 1ull) {
