@@ -135,7 +135,7 @@ struct pbs_chunker {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     DevBuf d_table, d_pre, d_counters, d_susp, d_cand, d_C, d_sort_tmp, d_nxt, d_jtmp, d_nf, d_on,
-        d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in, d_stage, d_hits, d_rec;
+        d_cnt, d_off, d_scan_tmp, d_cuts, d_res, d_in, d_stage, d_hits, d_rec, d_scratch;
     uint32_t rec_epoch = 0;  // fused pass: tile-record epoch of the last launch (16 bits)
     // fused pass returns on the resolver's status word, before its kernel has retired:
     // its scan time (ev[0] -> ev[1]) and the call's total (ev[5] -> ev[4]) are read from
@@ -759,10 +759,11 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     const uint64_t ntail = ((bl - covered + kBlockBytes - 1) / kBlockBytes + kTailBlocks - 1) / kTailBlocks;
     const uint64_t items = ntiles + ntail;
     if (items == 0) return PBS_OK;
-    // tile records: a fresh allocation (or an epoch wrap) is zeroed; epochs never 0
+    const uint64_t nsteps = (items + kResolveBatch - 1) / kResolveBatch;
+    // tile + step records: a fresh allocation (or an epoch wrap) is zeroed; epochs never 0
     const void* old_rec = c->d_rec.p;
     const size_t old_cap = c->d_rec.cap;
-    HIP_TRY(c, c->d_rec.ensure(items * 8));
+    HIP_TRY(c, c->d_rec.ensure((items + nsteps) * 8));
     if (c->d_rec.p != old_rec || c->d_rec.cap != old_cap || ((c->rec_epoch + 1) & 0xFFFFu) == 0) {
         HIP_TRY(c, hipMemsetAsync(c->d_rec.p, 0, c->d_rec.cap, c->stream));
         c->rec_epoch = 0;
@@ -771,8 +772,10 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     const uint64_t expected = bl / p.avg * 3 / 2 + 1;
     const uint64_t cand_cap = std::min<uint64_t>(std::min<uint64_t>(bl + 1, expected * 2 + 8192), kMaxBatchCand);
     HIP_TRY(c, c->d_cand.ensure(cand_cap * 8));
-    HIP_TRY(c, c->d_counters.ensure(24));
-    HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 24, c->stream));
+    HIP_TRY(c, c->d_scratch.ensure(cand_cap * 21));  // c, sk (u64), nf (u32), nx (u8)
+    // counters: [0] flagged blocks, [1] candidates, [2] tile counter (u32), [3] scratch
+    HIP_TRY(c, c->d_counters.ensure(32));
+    HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 32, c->stream));
     HIP_TRY(c, c->d_pre.ensure(64));
     if (c->carry_len)
         HIP_TRY(c, hipMemcpyAsync(c->d_pre.p, c->carry, c->carry_len, hipMemcpyHostToDevice, c->stream));
@@ -780,9 +783,6 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     if (np)
         HIP_TRY(c, hipMemcpyAsync(c->d_C.p, c->pending.data() + c->pend_head, np * 8,
                                   hipMemcpyHostToDevice, c->stream));
-    const uint64_t span = rend - c->chunk_start;
-    const uint64_t out_cap = span / p.min_eff + 3;  // every chunk before the open one >= min
-    HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
     int rc = ensure_small_host_bufs(c);
     if (rc) return rc;
     uint64_t *cuts_dev = nullptr, *keep_dev = nullptr, *small_dev = nullptr;
@@ -817,10 +817,14 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     a.s0 = c->chunk_start;
     a.pend = c->d_C.as<uint64_t>();
     a.npend = (uint32_t)np;
-    a.cuts = c->d_cuts.as<uint64_t>();
-    a.cuts_cap = out_cap;
     a.cuts_host = cuts_dev;
     a.host_cap = kHostCuts;
+    uint8_t* scr = c->d_scratch.as<uint8_t>();
+    a.sc_c = reinterpret_cast<uint64_t*>(scr);
+    a.sc_sk = reinterpret_cast<uint64_t*>(scr + cand_cap * 8);
+    a.sc_nf = reinterpret_cast<uint32_t*>(scr + cand_cap * 16);
+    a.sc_nx = scr + cand_cap * 20;
+    a.sc_ctr = ctr + 3;
     a.keep_host = keep_dev;
     a.keep_cap = (uint32_t)kHostKeep;
     a.res_host = small_dev + 8;
@@ -858,12 +862,8 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     if (status == 1) return PBS_OK;  // stood down: dense input
     if (status != 0) return fail(c, PBS_ERR_HIP);
     const uint64_t ncut = c->h_small[8], s_open = c->h_small[9], nkeep = c->h_small[10];
-    if (*n + ncut > cap || ncut > out_cap || nkeep > kHostKeep) return fail(c, PBS_ERR_CAPACITY);
-    if (ncut <= kHostCuts) {
-        std::memcpy(out + *n, c->h_cuts, ncut * 8);
-    } else {
-        HIP_TRY(c, hipMemcpy(out + *n, c->d_cuts.p, ncut * 8, hipMemcpyDeviceToHost));
-    }
+    if (*n + ncut > cap || ncut > kHostCuts || nkeep > kHostKeep) return fail(c, PBS_ERR_CAPACITY);
+    std::memcpy(out + *n, c->h_cuts, ncut * 8);
     *n += ncut;
     std::vector<uint64_t> keep(c->h_keep, c->h_keep + nkeep);
     c->chunk_start = s_open;
@@ -1009,7 +1009,8 @@ void destroy(pbs_chunker* c) {
     if (c->srv.slot) (void)hipHostFree(c->srv.slot);
     DevBuf* bufs[] = {&c->d_table, &c->d_pre, &c->d_counters, &c->d_susp, &c->d_cand, &c->d_C,
                       &c->d_sort_tmp, &c->d_nxt, &c->d_jtmp, &c->d_nf, &c->d_on, &c->d_cnt,
-                      &c->d_off, &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in, &c->d_rec};
+                      &c->d_off, &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in, &c->d_rec,
+                      &c->d_scratch};
     for (DevBuf* b : bufs) b->release();
     c->d_stage.release();
     c->d_hits.release();

@@ -52,7 +52,8 @@ struct FusedPassArgs {
     uint64_t ntail;             // tail items (kTailBlocks blocks each) after the tiles
     uint64_t base;              // absolute stream offset of data[0]
     // tile records and candidates
-    unsigned long long* rec;    // ntiles + ntail records {epoch:16 | count:16 | index:32}
+    unsigned long long* rec;    // ntiles + ntail records {epoch:16 | count:16 | index:32},
+                                // then one record per resolver step (kResolveBatch tiles)
     uint32_t epoch;             // != 0, differs from every record left by earlier launches
     uint64_t* cand;             // candidate list (absolute positions; per tile contiguous)
     unsigned long long* ncand;  // zeroed counter
@@ -65,10 +66,15 @@ struct FusedPassArgs {
     uint64_t s0;                // open chunk start
     const uint64_t* pend;       // pending candidates of the open chunk (sorted, device)
     uint32_t npend;
-    uint64_t* cuts;             // device cut list (cuts_cap entries)
-    uint64_t cuts_cap;
-    uint64_t* cuts_host;        // mapped host copy while ncut <= host_cap
+    uint64_t* cuts_host;        // mapped host memory: the cut list (host_cap entries)
     uint64_t host_cap;
+    // resolver scratch (cand_cap entries each): a step's candidates in stream order with
+    // their in-vector successor, forced cuts and exit state (scan_fused.h fused_helper)
+    uint64_t* sc_c;
+    uint64_t* sc_sk;
+    uint32_t* sc_nf;
+    uint8_t* sc_nx;
+    unsigned long long* sc_ctr;  // zeroed counter (scratch entries handed out)
     uint64_t* keep_host;        // mapped: candidates of the open chunk
     uint32_t keep_cap;
     uint64_t* res_host;         // mapped: [0] cuts [1] open chunk start [2] kept [3] status
@@ -79,7 +85,8 @@ struct FusedPassArgs {
     uint64_t timeout_ticks;     // resolver wait limit (wall_clock64 ticks, 100 MHz)
 };
 
-constexpr int kTailBlocks = 64;  // blocks per tail item of the fused pass
+constexpr int kTailBlocks = 64;     // blocks per tail item of the fused pass
+constexpr int kResolveBatch = 256;  // tile records per resolver step (4 per lane)
 hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid, hipStream_t stream);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
                              uint32_t pre_len, const uint64_t* susp,

@@ -38,7 +38,7 @@ namespace pbs {
 
 constexpr int kFusedKeep = 512;     // open-chunk candidates the resolver keeps in LDS
 constexpr int kStageCand = 512;     // candidates of one resolver step staged in LDS
-constexpr int kResolveBatch = 256;  // tile records per resolver step (4 per lane)
+constexpr int kFusedHelpers = 2;    // resolver helper waves (workgroup 0, waves 1..2)
 constexpr uint32_t kRecOverflow = 0xFFFFu;
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
@@ -116,121 +116,82 @@ __device__ __forceinline__ void fused_publish(const FusedPassArgs& a, const uint
     }
 }
 
-// Phase B over the tile records, one wave (see the file comment).  `keep` = LDS scratch
-// of kFusedKeep + kStageCand entries.  Per step of 256 records: the next step's records
-// are already in flight and the step's candidates load (8 per lane in flight) into LDS in
-// stream order; the cut rule then walks each 64-candidate vector (process_vec).
-__device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane) {
-    // every field in a register: the struct lives in kernarg memory behind a generic
-    // reference and would be re-read after each store
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {  // divergent source lane
+    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src, 64) |
+           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64) << 32);
+}
+
+// first lane in [from, nv) whose candidate is >= x (nv if none); lanes [0, nv) hold
+// ascending candidates.  `from` itself is probed first (a chunk usually ends at the next
+// candidate); the rest is a binary search that runs only as long as some lane needs it.
+// All 64 lanes take part (the shuffles read every lane).
+__device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, uint64_t x) {
+    int lo = from < nv ? from : nv, hi = nv;
+    const uint64_t v0 = shfl64(c, lo < 64 ? lo : 63);
+    if (lo < hi && v0 >= x) hi = lo;
+    else if (lo < hi) ++lo;
+    while (__any(lo < hi)) {
+        const int mid = (lo + hi) >> 1;
+        const uint64_t v = shfl64(c, mid < 64 ? mid : 63);
+        const bool go_right = lo < hi && v < x;
+        const bool go_left = lo < hi && !(v < x);
+        lo = go_right ? mid + 1 : lo;
+        hi = go_left ? mid : hi;
+    }
+    return lo;
+}
+
+// Phase B (chunker.rs:172-183) is split over three waves of workgroup 0:
+//
+//   helpers (2)  take the record steps (kResolveBatch records) round-robin: wait for the
+//                step's tiles, gather its candidates in stream order and, for every 64-
+//                candidate vector, compute per candidate the next cut inside the vector if
+//                a cut were taken there (nx: lane, or itself when the chain leaves the
+//                vector), the forced cuts in between (nf) and the state after them (sk) --
+//                lane-parallel, independent of everything before the vector.  The step's
+//                {c, nx, nf, sk} go to a scratch area, then the step record is published.
+//   main (1)     takes the steps in order and walks the chain: the vector's first cut from
+//                the incoming state (one ballot; forced cuts in closed form), then nx from
+//                cut to cut (a few scalar instructions per cut), the cuts written with one
+//                vector store, the candidates past the chain's last cut kept for the open
+//                chunk.  Pending candidates of earlier calls come first (walked directly).
+//
+// One wave's serial walk costs ~35 instructions per cut at the 4-cycle issue cadence of a
+// wave; with the successors precomputed it is ~6, so the main wave keeps up with 256 KiB
+// averages (190 k cuts in a 64 GiB pass) and finishes a few microseconds after the last tile.
+struct FusedStep {  // one resolver step, in scratch (stream order)
+    uint64_t* c;
+    uint64_t* sk;
+    uint32_t* nf;
+    uint8_t* nx;
+};
+
+__device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int nh, int lane) {
     const uint64_t total = a.ntiles + a.ntail;
+    const uint64_t nsteps = (total + kResolveBatch - 1) / kResolveBatch;
     const uint64_t min1 = a.min_eff - 1, max_eff = a.max_eff, max1 = a.max_eff - 1;
     const uint32_t sh = a.max_shift, epoch = a.epoch;
-    uint64_t* const cuts = a.cuts;
-    uint64_t* const cuts_host = a.cuts_host;
-    const uint64_t cuts_cap = a.cuts_cap, host_cap = a.host_cap;
     const unsigned long long* const rec = a.rec;
     const uint64_t* const cand = a.cand;
-    const uint64_t timeout = a.timeout_ticks, end = a.end;
-    uint64_t s = a.s0, ncut = 0;
-    uint32_t nkeep = 0, status = 0;
+    unsigned long long* const sinfo = a.rec + total;  // step records after the tile records
+    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_nf, a.sc_nx};
     const uint64_t t_start = wall_clock64();
-    uint64_t t_wait = 0, t_ready = t_start;
-    const unsigned long long below = (1ull << lane) - 1;
-
-    auto put = [&](uint64_t i, uint64_t x) {
-        if (i < cuts_cap) cuts[i] = x;
-        if (i < host_cap) cuts_host[i] = x;
-    };
-    auto forced = [&](uint64_t k) {  // k forced (max-size) cuts from s, lane-parallel
-        for (uint64_t j = (uint64_t)lane; j < k; j += 64) put(ncut + j, s + (j + 1) * max_eff);
-        ncut += k;
-        s += k * max_eff;
-    };
-    // chunker.rs:172-183 over the ascending candidates of the lanes in vm (~0 elsewhere),
-    // all >= s: the next cut is the first candidate >= s + min - 1 -- one ballot skips
-    // every candidate below it -- if it is <= s + max - 1, else forced cuts until it is.
-    // The cuts of the vector are collected as a lane mask and written with one vector
-    // store; the candidates left over belong to the open chunk (kept, in order).
-    auto process_vec = [&](uint64_t c, unsigned long long vm) {
-        bool reset = false;
-        unsigned long long chain = 0, rem = vm;
-        auto flush = [&]() {
-            if (chain) {
-                if ((chain >> lane) & 1ull) put(ncut + (uint64_t)__popcll(chain & below), c + 1);
-                ncut += (uint64_t)__popcll(chain);
-                chain = 0;
-            }
-        };
-        for (;;) {
-            const unsigned long long m = __ballot(c >= s + min1) & rem;
-            if (!m) break;
-            const int k = __ffsll(m) - 1;
-            const uint64_t ck = readlane64(c, k);
-            reset = true;
-            if (ck > s + max1) {  // the candidates before k stay below every later minimum
-                flush();
-                forced((ck - (s + max1) + max_eff - 1) >> sh);
-                rem &= ~((1ull << k) - 1);
-                continue;
-            }
-            chain |= 1ull << k;
-            s = ck + 1;
-            rem = k == 63 ? 0ull : rem & ~((2ull << k) - 1);
-        }
-        flush();
-        if (reset) nkeep = 0;
-        const unsigned long long km = __ballot(c >= s) & rem;
-        if ((km >> lane) & 1ull) {
-            const uint32_t pos = nkeep + (uint32_t)__popcll(km & below);
-            if (pos < kFusedKeep) keep[pos] = c;
-        }
-        nkeep += (uint32_t)__popcll(km);
-    };
-
-    for (uint32_t i = 0; i < a.npend; i += 64) {
-        const bool v = i + lane < a.npend;
-        process_vec(v ? a.pend[i + lane] : ~0ull, __ballot(v));
-    }
-    // records t0 + 4*lane + q (q < 4): 256 per step, the next step's already in flight
-    uint64_t rv[4];
-    auto load_rec = [&](uint64_t t0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint64_t t = t0 + 4 * (uint64_t)lane + q;
-            rv[q] = t < total ? __hip_atomic_load(rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : ((uint64_t)epoch << 48);
-        }
-    };
-    uint64_t* const stc = keep + kFusedKeep;  // candidates of one step, in stream order
-    load_rec(0);
-    for (uint64_t t0 = 0; t0 < total; t0 += kResolveBatch) {
+    for (uint64_t st = (uint64_t)h; st < nsteps; st += (uint64_t)nh) {
+        const uint64_t t0 = st * kResolveBatch;
+        uint64_t rv[4];
         bool done = true;
+        for (;;) {
+            done = true;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) done = done && (uint32_t)(rv[q] >> 48) == epoch;
-        if (!__all(done)) {
-            const uint64_t w0 = wall_clock64();
-            for (;;) {
-                __builtin_amdgcn_s_sleep(2);
-                if (!done) {
-                    done = true;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint64_t t = t0 + 4 * (uint64_t)lane + q;
-                        if ((uint32_t)(rv[q] >> 48) != epoch && t < total)
-                            rv[q] = __hip_atomic_load(rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        done = done && (uint32_t)(rv[q] >> 48) == epoch;
-                    }
-                }
-                if (__all(done)) break;
-                if (wall_clock64() - t_start > timeout) {
-                    status = 2;
-                    break;
-                }
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t t = t0 + 4 * (uint64_t)lane + q;
+                rv[q] = t < total ? __hip_atomic_load(rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : ((uint64_t)epoch << 48);
+                done = done && (uint32_t)(rv[q] >> 48) == epoch;
             }
-            t_ready = wall_clock64();
-            t_wait += t_ready - w0;
-            if (status) break;
+            if (__all(done)) break;
+            if (wall_clock64() - t_start > a.timeout_ticks) return;  // the main wave times out too
+            __builtin_amdgcn_s_sleep(2);
         }
         uint32_t cq[4], iq[4];
         bool ovf = false;
@@ -240,13 +201,7 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
             iq[q] = (uint32_t)rv[q];
             ovf = ovf || cq[q] == kRecOverflow;
         }
-        if (__any(ovf)) {
-            status = 1;
-            break;
-        }
-        load_rec(t0 + kResolveBatch);  // the next step's records, in flight meanwhile
         const uint32_t p1 = cq[0], p2 = p1 + cq[1], p3 = p2 + cq[2], sum = p3 + cq[3];
-        if (!__any(sum != 0)) continue;
         uint32_t incl = sum;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -255,31 +210,222 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
         }
         const uint32_t base = incl - sum;
         const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
-        for (uint32_t k0 = 0; k0 < T; k0 += kStageCand) {
-            // each lane stages its own records' candidates with step index in
-            // [k0, k0 + kStageCand), 8 loads in flight at a time
-            for (uint32_t i0 = 0; __any(i0 < sum); i0 += 8) {
-                uint64_t v[8];
-                uint32_t at[8];
+        uint64_t o = 0;
+        if (!__any(ovf) && T) {
+            unsigned long long b = 0;
+            if (lane == 0) b = atomicAdd(a.sc_ctr, (unsigned long long)T);
+            o = readlane64(b, 0);
+            ovf = o + T > a.cand_cap || T >= (1u << 20);
+        }
+        if (!__any(ovf)) {
+            for (uint32_t k0 = 0; k0 < T; k0 += kStageCand) {
+                // stage this chunk's candidates in stream order, 8 loads in flight per lane
+                for (uint32_t i0 = 0; __any(i0 < sum); i0 += 8) {
+                    uint64_t v[8];
+                    uint32_t at[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t i = i0 + (uint32_t)u, kk = base + i;
-                    const bool ok = i < sum && kk >= k0 && kk < k0 + kStageCand;
-                    const uint32_t q = (i >= p1 ? 1u : 0u) + (i >= p2 ? 1u : 0u) + (i >= p3 ? 1u : 0u);
-                    const uint32_t ix = q == 0 ? iq[0] + i : q == 1 ? iq[1] + (i - p1)
-                                      : q == 2 ? iq[2] + (i - p2) : iq[3] + (i - p3);
-                    v[u] = ok ? __hip_atomic_load(cand + ix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-                    at[u] = ok ? kk - k0 : ~0u;
+                    for (int u = 0; u < 8; ++u) {
+                        const uint32_t i = i0 + (uint32_t)u, kk = base + i;
+                        const bool ok = i < sum && kk >= k0 && kk < k0 + kStageCand;
+                        const uint32_t q = (i >= p1 ? 1u : 0u) + (i >= p2 ? 1u : 0u) + (i >= p3 ? 1u : 0u);
+                        const uint32_t ix = q == 0 ? iq[0] + i : q == 1 ? iq[1] + (i - p1)
+                                          : q == 2 ? iq[2] + (i - p2) : iq[3] + (i - p3);
+                        v[u] = ok ? __hip_atomic_load(cand + ix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                        at[u] = ok ? kk - k0 : ~0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (at[u] != ~0u) stc[at[u]] = v[u];
                 }
+                const uint32_t nhere = T - k0 < (uint32_t)kStageCand ? T - k0 : (uint32_t)kStageCand;
+                for (uint32_t v0 = 0; v0 < nhere; v0 += 64) {
+                    const int nv = (int)(nhere - v0 < 64 ? nhere - v0 : 64);
+                    const uint64_t c = lane < nv ? stc[v0 + lane] : ~0ull;
+                    // successor of a cut at this lane's candidate, inside the vector
+                    uint64_t sk = c + 1;
+                    uint32_t nf = 0;
+                    int nx = lane, from = lane + 1;
+                    bool active = lane < nv;
+                    for (int guard = 0; guard < 64 && __any(active); ++guard) {  // j moves on each round
+                        const int j = lanes_lower_bound(c, from, nv, sk + min1);
+                        const uint64_t cj = shfl64(c, j < 64 ? j : 63);
+                        if (active) {
+                            if (j >= nv) {
+                                active = false;
+                            } else if (cj <= sk + max1) {
+                                nx = j;
+                                active = false;
+                            } else {
+                                const uint64_t K = (cj - (sk + max1) + max_eff - 1) >> sh;
+                                nf += (uint32_t)K;
+                                sk += K * max_eff;
+                                from = j;
+                            }
+                        }
+                    }
+                    if (lane < nv) {
+                        const uint64_t w = o + k0 + v0 + (uint64_t)lane;
+                        sc.c[w] = c;
+                        sc.sk[w] = sk;
+                        sc.nf[w] = nf;
+                        sc.nx[w] = (uint8_t)nx;
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        }
+        if (lane == 0) {
+            const uint64_t r = ((uint64_t)epoch << 48) | (__any(ovf) ? (1ull << 47) : 0ull) |
+                               ((uint64_t)(T & 0xFFFFFu) << 27) | (o & 0x7FFFFFFull);
+            __hip_atomic_store(sinfo + st, (unsigned long long)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+__device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
+    // every field in a register: the struct lives in kernarg memory behind a generic
+    // reference and would be re-read after each store
+    const uint64_t total = a.ntiles + a.ntail;
+    const uint64_t nsteps = (total + kResolveBatch - 1) / kResolveBatch;
+    const uint64_t min1 = a.min_eff - 1, max_eff = a.max_eff, max1 = a.max_eff - 1;
+    const uint32_t sh = a.max_shift, epoch = a.epoch;
+    uint64_t* const cuts_host = a.cuts_host;
+    const uint64_t host_cap = a.host_cap;
+    const unsigned long long* const sinfo = a.rec + total;
+    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_nf, a.sc_nx};
+    const uint64_t timeout = a.timeout_ticks, end = a.end;
+    uint64_t s = a.s0, ncut = 0;
+    uint32_t nkeep = 0, status = 0;
+    const uint64_t t_start = wall_clock64();
+    uint64_t t_wait = 0, t_ready = t_start;
+    const unsigned long long below = (1ull << lane) - 1;
+
+    // cuts go straight to mapped host memory; a list longer than host_cap stands down
+    auto put = [&](uint64_t i, uint64_t x) {
+        if (i < host_cap) cuts_host[i] = x;
+    };
+    auto forced = [&](uint64_t k) {  // k forced (max-size) cuts from s, lane-parallel
+        for (uint64_t j = (uint64_t)lane; j < k; j += 64) put(ncut + j, s + (j + 1) * max_eff);
+        ncut += k;
+        s += k * max_eff;
+    };
+    // the vector's first cut from state s: ballot over the candidates >= s + min - 1;
+    // forced cuts while that candidate lies past s + max - 1.  Returns its lane or -1;
+    // `rem` loses the lanes that can no longer cut.
+    auto entry = [&](uint64_t c, unsigned long long& rem, bool& reset) -> int {
+        for (;;) {
+            const unsigned long long m = __ballot(c >= s + min1) & rem;
+            if (!m) return -1;
+            const int k = __ffsll(m) - 1;
+            const uint64_t ck = readlane64(c, k);
+            reset = true;
+            if (ck > s + max1) {  // the candidates before k stay below every later minimum
+                forced((ck - (s + max1) + max_eff - 1) >> sh);
+                rem &= ~((1ull << k) - 1);
+                continue;
+            }
+            return k;
+        }
+    };
+    auto keep_rest = [&](uint64_t c, unsigned long long rem, bool reset) {
+        if (reset) nkeep = 0;
+        const unsigned long long km = __ballot(c >= s) & rem;
+        if ((km >> lane) & 1ull) {
+            const uint32_t pos = nkeep + (uint32_t)__popcll(km & below);
+            if (pos < kFusedKeep) keep[pos] = c;
+        }
+        nkeep += (uint32_t)__popcll(km);
+    };
+    // emit the chain `mask` (lanes, ascending), each cut followed by its nf forced cuts
+    auto emit_chain = [&](uint64_t c, unsigned long long mask, uint32_t nf) {
+        const bool on = (mask >> lane) & 1ull;
+        const uint32_t cnt = on ? 1u + nf : 0u;
+        uint64_t off;
+        uint32_t tot;
+        if (__any(on && nf != 0)) {
+            uint32_t incl = cnt;
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (at[u] != ~0u) stc[at[u]] = v[u];
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += y;
             }
-            const uint32_t nh = T - k0 < (uint32_t)kStageCand ? T - k0 : (uint32_t)kStageCand;
-            for (uint32_t v0 = 0; v0 < nh; v0 += 64) {
-                const bool v = v0 + lane < nh;
-                process_vec(v ? stc[v0 + lane] : ~0ull, __ballot(v));
+            off = incl - cnt;
+            tot = (uint32_t)__shfl((int)incl, 63, 64);
+        } else {
+            off = (uint64_t)__popcll(mask & below);
+            tot = (uint32_t)__popcll(mask);
+        }
+        if (on) {
+            const uint64_t o = ncut + off;
+            put(o, c + 1);
+            for (uint32_t i = 1; i <= nf; ++i) put(o + i, c + 1 + (uint64_t)i * max_eff);
+        }
+        ncut += tot;
+    };
+
+    // pending candidates of the open chunk (earlier calls): walked cut by cut
+    for (uint32_t i = 0; i < a.npend; i += 64) {
+        const bool v = i + lane < a.npend;
+        const uint64_t c = v ? a.pend[i + lane] : ~0ull;
+        unsigned long long rem = __ballot(v);
+        bool reset = false;
+        for (;;) {
+            const int k = entry(c, rem, reset);
+            if (k < 0) break;
+            emit_chain(c, 1ull << k, 0u);
+            s = readlane64(c, k) + 1;
+            rem = k == 63 ? 0ull : rem & ~((2ull << k) - 1);
+        }
+        keep_rest(c, rem, reset);
+    }
+    for (uint64_t st = 0; st < nsteps && status == 0; ++st) {
+        uint64_t r = __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(r >> 48) != epoch) {
+            const uint64_t w0 = wall_clock64();
+            while ((uint32_t)(r >> 48) != epoch) {
+                if (wall_clock64() - t_start > timeout) {
+                    status = 2;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+                r = __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            t_ready = wall_clock64();
+            t_wait += t_ready - w0;
+            if (status) break;
+        }
+        if ((r >> 47) & 1ull) {
+            status = 1;
+            break;
+        }
+        const uint32_t T = (uint32_t)(r >> 27) & 0xFFFFFu;
+        const uint64_t o = r & 0x7FFFFFFull;
+        for (uint32_t v0 = 0; v0 < T; v0 += 64) {
+            const bool v = v0 + lane < T;
+            const uint64_t w = o + v0 + (uint64_t)lane;
+            const uint64_t c = v ? __hip_atomic_load(sc.c + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0ull;
+            const uint64_t sk = v ? __hip_atomic_load(sc.sk + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+            const uint32_t nf = v ? __hip_atomic_load(sc.nf + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            const uint32_t nx = v ? (uint32_t)__hip_atomic_load(sc.nx + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : (uint32_t)lane;
+            unsigned long long rem = __ballot(v);
+            bool reset = false;
+            const int e = entry(c, rem, reset);
+            if (e >= 0) {
+                unsigned long long mask = 0;
+                int x = e;
+                for (int guard = 0; guard < 64; ++guard) {  // nx ascends: <= 64 steps
+                    mask |= 1ull << x;
+                    const int n = __builtin_amdgcn_readlane((int)nx, x);
+                    if (n == x) break;
+                    x = n;
+                }
+                emit_chain(c, mask, nf);
+                s = readlane64(sk, x);
+                rem = x == 63 ? 0ull : rem & ~((2ull << x) - 1);
+            }
+            keep_rest(c, rem, reset);
         }
     }
     if (status == 0) {
@@ -287,7 +433,7 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
             forced((end - s) >> sh);
             nkeep = 0;
         }
-        if (nkeep > kFusedKeep) status = 1;
+        if (nkeep > kFusedKeep || ncut > host_cap) status = 1;
     }
     if (status == 0 && nkeep <= a.keep_cap)
         for (uint32_t i = lane; i < nkeep; i += 64) a.keep_host[i] = keep[i];
@@ -299,8 +445,8 @@ __device__ void fused_resolver(const FusedPassArgs& a, uint64_t* keep, int lane)
         a.res_host[2] = nkeep;
         a.res_host[4] = __hip_atomic_load(a.ncand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         a.res_host[5] = __hip_atomic_load(a.nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a.res_host[6] = t_ready - t_start;  // diagnostics (100 MHz ticks): last record ready,
-        a.res_host[7] = t_end - t_start;    // resolver done, time spent waiting for records
+        a.res_host[6] = t_ready - t_start;  // diagnostics (100 MHz ticks): last step ready,
+        a.res_host[7] = t_end - t_start;    // resolver done, time spent waiting for steps
         a.res_host[8] = t_wait;
         // last, after every other result (and the cuts) is in host memory: the host
         // returns as soon as it sees this word
@@ -328,7 +474,11 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     __syncthreads();
     uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
     if (blockIdx.x == 0 && wave == 0) {
-        fused_resolver(a, reinterpret_cast<uint64_t*>(stage), lane);
+        fused_main(a, reinterpret_cast<uint64_t*>(stage), lane);
+        return;
+    }
+    if (blockIdx.x == 0 && wave <= kFusedHelpers) {
+        fused_helper(a, reinterpret_cast<uint64_t*>(stage), wave - 1, kFusedHelpers, lane);
         return;
     }
     uint32_t* bm = s_bm + wave * 64 * NBW + lane * NBW;
@@ -345,8 +495,9 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     const uint32_t rd_base = (uint32_t)lane * 128u;
     const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
     constexpr int NIT = SEG / kIter + 1;
-    const uint64_t nw = (uint64_t)gridDim.x * NW - 1;  // scanner waves (the resolver takes none)
-    uint64_t tile = (uint64_t)blockIdx.x * NW + wave - 1;
+    // scanner waves: all but workgroup 0's resolver waves
+    const uint64_t nw = (uint64_t)gridDim.x * NW - (1 + kFusedHelpers);
+    uint64_t tile = (uint64_t)blockIdx.x * NW + wave - (1 + kFusedHelpers);
     const uint64_t ntiles = a.ntiles, t_big = a.t_big;
     const uint8_t* data = a.data;
 
