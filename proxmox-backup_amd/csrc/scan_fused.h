@@ -275,8 +275,9 @@ __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int n
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         }
+        const bool any_ovf = __any(ovf);  // (a ballot inside `lane == 0` would see lane 0 only)
         if (lane == 0) {
-            const uint64_t r = ((uint64_t)epoch << 48) | (__any(ovf) ? (1ull << 47) : 0ull) |
+            const uint64_t r = ((uint64_t)epoch << 48) | (any_ovf ? (1ull << 47) : 0ull) |
                                ((uint64_t)(T & 0xFFFFFu) << 27) | (o & 0x7FFFFFFull);
             __hip_atomic_store(sinfo + st, (unsigned long long)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
