@@ -380,8 +380,29 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         }
         keep_rest(c, rem, reset);
     }
+    // the next step's record and the next vector's data are in flight while the current
+    // vector is walked
+    auto load_info = [&](uint64_t st) -> uint64_t {
+        return st < nsteps ? __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    };
+    struct Vec {
+        uint64_t c, sk;
+        uint32_t nf, nx;
+    };
+    auto load_vec = [&](uint64_t o, uint32_t T, uint32_t v0) -> Vec {
+        const bool v = v0 + lane < T;
+        const uint64_t w = o + v0 + (uint64_t)lane;
+        Vec x;
+        x.c = v ? __hip_atomic_load(sc.c + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0ull;
+        x.sk = v ? __hip_atomic_load(sc.sk + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        x.nf = v ? __hip_atomic_load(sc.nf + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        x.nx = v ? (uint32_t)__hip_atomic_load(sc.nx + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : (uint32_t)lane;
+        return x;
+    };
+    uint64_t r_next = load_info(0);
     for (uint64_t st = 0; st < nsteps && status == 0; ++st) {
-        uint64_t r = __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t r = r_next;
         if ((uint32_t)(r >> 48) != epoch) {
             const uint64_t w0 = wall_clock64();
             while ((uint32_t)(r >> 48) != epoch) {
@@ -390,27 +411,24 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
-                r = __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                r = load_info(st);
             }
             t_ready = wall_clock64();
             t_wait += t_ready - w0;
             if (status) break;
         }
+        r_next = load_info(st + 1);
         if ((r >> 47) & 1ull) {
             status = 1;
             break;
         }
         const uint32_t T = (uint32_t)(r >> 27) & 0xFFFFFu;
         const uint64_t o = r & 0x7FFFFFFull;
+        Vec cur = T ? load_vec(o, T, 0) : Vec{~0ull, 0ull, 0u, 0u};
         for (uint32_t v0 = 0; v0 < T; v0 += 64) {
-            const bool v = v0 + lane < T;
-            const uint64_t w = o + v0 + (uint64_t)lane;
-            const uint64_t c = v ? __hip_atomic_load(sc.c + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0ull;
-            const uint64_t sk = v ? __hip_atomic_load(sc.sk + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-            const uint32_t nf = v ? __hip_atomic_load(sc.nf + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            const uint32_t nx = v ? (uint32_t)__hip_atomic_load(sc.nx + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  : (uint32_t)lane;
-            unsigned long long rem = __ballot(v);
+            const Vec nxt = v0 + 64 < T ? load_vec(o, T, v0 + 64) : cur;
+            const uint64_t c = cur.c;
+            unsigned long long rem = __ballot(v0 + lane < T);
             bool reset = false;
             const int e = entry(c, rem, reset);
             if (e >= 0) {
@@ -418,15 +436,16 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
                 int x = e;
                 for (int guard = 0; guard < 64; ++guard) {  // nx ascends: <= 64 steps
                     mask |= 1ull << x;
-                    const int n = __builtin_amdgcn_readlane((int)nx, x);
+                    const int n = __builtin_amdgcn_readlane((int)cur.nx, x);
                     if (n == x) break;
                     x = n;
                 }
-                emit_chain(c, mask, nf);
-                s = readlane64(sk, x);
+                emit_chain(c, mask, cur.nf);
+                s = readlane64(cur.sk, x);
                 rem = x == 63 ? 0ull : rem & ~((2ull << x) - 1);
             }
             keep_rest(c, rem, reset);
+            cur = nxt;
         }
     }
     if (status == 0) {

@@ -9,6 +9,7 @@ step ex_256k_unchanged 120 examples/test_chunk_speed2 - 1073741824 262144 419430
 step ex_8k_gather 120 examples/test_chunk_speed2 - 1073741824 8192 4194304 4194304 1 || exit 1
 step ex_8k_unchanged_noserver 120 env PBS_SCAN_SERVER=0 examples/test_chunk_speed2 - 268435456 8192 4194304 0 1 || exit 1
 step bench64 300 env PBS_DEBUG_PHASES=1 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 || exit 1
+step bench64b 300 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 || exit 1
 step c5 300 env PBS_DEBUG_PHASES=1 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 --avg 262144 --steps 3 || exit 1
 step bench64_1M 300 env PBS_DEBUG_PHASES=1 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 --avg 1048576 --steps 3 || exit 1
 echo done
