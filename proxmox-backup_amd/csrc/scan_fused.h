@@ -424,20 +424,28 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         }
         const uint32_t T = (uint32_t)(r >> 27) & 0xFFFFFu;
         const uint64_t o = r & 0x7FFFFFFull;
+        // three vectors in flight: the one walked and the next two
         Vec cur = T ? load_vec(o, T, 0) : Vec{~0ull, 0ull, 0u, 0u};
+        Vec n1 = 64 < T ? load_vec(o, T, 64) : cur;
         for (uint32_t v0 = 0; v0 < T; v0 += 64) {
-            const Vec nxt = v0 + 64 < T ? load_vec(o, T, v0 + 64) : cur;
+            const Vec n2 = v0 + 128 < T ? load_vec(o, T, v0 + 128) : n1;
             const uint64_t c = cur.c;
             unsigned long long rem = __ballot(v0 + lane < T);
             bool reset = false;
             const int e = entry(c, rem, reset);
             if (e >= 0) {
+                // the chain from e: runs of consecutive lanes (nx = lane + 1, the usual case)
+                // are taken whole, one bit scan each; a run's last lane jumps by nx
+                const unsigned long long step1 = __ballot((int)cur.nx == lane + 1);
                 unsigned long long mask = 0;
                 int x = e;
-                for (int guard = 0; guard < 64; ++guard) {  // nx ascends: <= 64 steps
-                    mask |= 1ull << x;
-                    const int n = __builtin_amdgcn_readlane((int)cur.nx, x);
-                    if (n == x) break;
+                for (int guard = 0; guard < 64; ++guard) {
+                    const unsigned long long brk = ~step1 & (~0ull << x);  // first lane >= x not stepping by 1
+                    const int f = brk ? __ffsll(brk) - 1 : 63;
+                    mask |= (f == 63 ? ~0ull : ((2ull << f) - 1)) & (~0ull << x);
+                    const int n = __builtin_amdgcn_readlane((int)cur.nx, f);
+                    x = f;
+                    if (n == f) break;
                     x = n;
                 }
                 emit_chain(c, mask, cur.nf);
@@ -445,7 +453,8 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
                 rem = x == 63 ? 0ull : rem & ~((2ull << x) - 1);
             }
             keep_rest(c, rem, reset);
-            cur = nxt;
+            cur = n1;
+            n1 = n2;
         }
     }
     if (status == 0) {

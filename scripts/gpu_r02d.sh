@@ -12,4 +12,6 @@ step bench64 300 env PBS_DEBUG_PHASES=1 python bench.py --cpu-baseline 0 --host-
 step bench64b 300 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 || exit 1
 step c5 300 env PBS_DEBUG_PHASES=1 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 --avg 262144 --steps 3 || exit 1
 step bench64_1M 300 env PBS_DEBUG_PHASES=1 python bench.py --cpu-baseline 0 --host-inclusive-gib 0 --avg 1048576 --steps 3 || exit 1
+
+step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r02d/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-inclusive-gib 0 || exit 1
 echo done
