@@ -272,14 +272,15 @@ __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int n
                     }
                 }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            // helper and main share a CU (workgroup 0): workgroup scope is the hand-off,
+            // so the main wave reads the step from L1/L2, not HBM
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         }
         const bool any_ovf = __any(ovf);  // (a ballot inside `lane == 0` would see lane 0 only)
         if (lane == 0) {
             const uint64_t r = ((uint64_t)epoch << 48) | (any_ovf ? (1ull << 47) : 0ull) |
                                ((uint64_t)(T & 0xFFFFFu) << 27) | (o & 0x7FFFFFFull);
-            __hip_atomic_store(sinfo + st, (unsigned long long)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sinfo + st, (unsigned long long)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
 }
@@ -383,7 +384,7 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
     // the next step's record and the next vector's data are in flight while the current
     // vector is walked
     auto load_info = [&](uint64_t st) -> uint64_t {
-        return st < nsteps ? __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        return st < nsteps ? __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
     };
     struct Vec {
         uint64_t c, sk;
@@ -393,11 +394,10 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         const bool v = v0 + lane < T;
         const uint64_t w = o + v0 + (uint64_t)lane;
         Vec x;
-        x.c = v ? __hip_atomic_load(sc.c + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0ull;
-        x.sk = v ? __hip_atomic_load(sc.sk + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        x.nf = v ? __hip_atomic_load(sc.nf + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-        x.nx = v ? (uint32_t)__hip_atomic_load(sc.nx + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                 : (uint32_t)lane;
+        x.c = v ? sc.c[w] : ~0ull;
+        x.sk = v ? sc.sk[w] : 0ull;
+        x.nf = v ? sc.nf[w] : 0u;
+        x.nx = v ? (uint32_t)sc.nx[w] : (uint32_t)lane;
         return x;
     };
     uint64_t r_next = load_info(0);
@@ -417,6 +417,7 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
             t_wait += t_ready - w0;
             if (status) break;
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the step's scratch is visible
         r_next = load_info(st + 1);
         if ((r >> 47) & 1ull) {
             status = 1;
