@@ -772,7 +772,7 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     const uint64_t expected = bl / p.avg * 3 / 2 + 1;
     const uint64_t cand_cap = std::min<uint64_t>(std::min<uint64_t>(bl + 1, expected * 2 + 8192), kMaxBatchCand);
     HIP_TRY(c, c->d_cand.ensure(cand_cap * 8));
-    HIP_TRY(c, c->d_scratch.ensure(cand_cap * 21));  // c, sk (u64), nf (u32), nx (u8)
+    HIP_TRY(c, c->d_scratch.ensure(cand_cap * 29));  // c, sk, pm (u64), nf (u32), xl (u8)
     // counters: [0] flagged blocks, [1] candidates, [2] tile counter (u32), [3] scratch
     HIP_TRY(c, c->d_counters.ensure(32));
     HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 32, c->stream));
@@ -822,8 +822,9 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     uint8_t* scr = c->d_scratch.as<uint8_t>();
     a.sc_c = reinterpret_cast<uint64_t*>(scr);
     a.sc_sk = reinterpret_cast<uint64_t*>(scr + cand_cap * 8);
-    a.sc_nf = reinterpret_cast<uint32_t*>(scr + cand_cap * 16);
-    a.sc_nx = scr + cand_cap * 20;
+    a.sc_pm = reinterpret_cast<uint64_t*>(scr + cand_cap * 16);
+    a.sc_nf = reinterpret_cast<uint32_t*>(scr + cand_cap * 24);
+    a.sc_xl = scr + cand_cap * 28;
     a.sc_ctr = ctr + 3;
     a.keep_host = keep_dev;
     a.keep_cap = (uint32_t)kHostKeep;
@@ -833,7 +834,10 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     a.tail_len = (uint32_t)tl;
     a.timeout_ticks = 100000000ull * 20;  // 20 s of wall_clock64 (100 MHz)
     volatile uint64_t* status_word = c->h_small + 8 + 3;
+    volatile uint64_t* progress = c->h_small + 8 + 9;  // cuts in h_cuts so far (every 8 steps)
     *status_word = ~0ull;
+    *progress = 0;
+    uint64_t copied = 0;  // the host copies them while it waits
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, launch_scan_fused(a, seg, dyn, c->cu, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
@@ -843,6 +847,11 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     // the kernel ended without one (launch failure)
     for (uint32_t spin = 1;; ++spin) {
         if (__atomic_load_n(status_word, __ATOMIC_ACQUIRE) != ~0ull) break;
+        const uint64_t pr = std::min<uint64_t>(__atomic_load_n(progress, __ATOMIC_ACQUIRE), cap - *n);
+        if (pr > copied) {
+            std::memcpy(out + *n + copied, c->h_cuts + copied, (pr - copied) * 8);
+            copied = pr;
+        }
         if ((spin & 255) == 0) {
             const hipError_t q = hipEventQuery(c->ev[1]);
             if (q == hipSuccess) {
@@ -863,7 +872,7 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     if (status != 0) return fail(c, PBS_ERR_HIP);
     const uint64_t ncut = c->h_small[8], s_open = c->h_small[9], nkeep = c->h_small[10];
     if (*n + ncut > cap || ncut > kHostCuts || nkeep > kHostKeep) return fail(c, PBS_ERR_CAPACITY);
-    std::memcpy(out + *n, c->h_cuts, ncut * 8);
+    if (ncut > copied) std::memcpy(out + *n + copied, c->h_cuts + copied, (ncut - copied) * 8);
     *n += ncut;
     std::vector<uint64_t> keep(c->h_keep, c->h_keep + nkeep);
     c->chunk_start = s_open;

@@ -72,8 +72,9 @@ struct FusedPassArgs {
     // their in-vector successor, forced cuts and exit state (scan_fused.h fused_helper)
     uint64_t* sc_c;
     uint64_t* sc_sk;
+    uint64_t* sc_pm;
     uint32_t* sc_nf;
-    uint8_t* sc_nx;
+    uint8_t* sc_xl;
     unsigned long long* sc_ctr;  // zeroed counter (scratch entries handed out)
     uint64_t* keep_host;        // mapped: candidates of the open chunk
     uint32_t keep_cap;

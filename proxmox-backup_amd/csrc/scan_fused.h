@@ -160,10 +160,11 @@ __device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, u
 // wave; with the successors precomputed it is ~6, so the main wave keeps up with 256 KiB
 // averages (190 k cuts in a 64 GiB pass) and finishes a few microseconds after the last tile.
 struct FusedStep {  // one resolver step, in scratch (stream order)
-    uint64_t* c;
-    uint64_t* sk;
-    uint32_t* nf;
-    uint8_t* nx;
+    uint64_t* c;   // candidate
+    uint64_t* sk;  // state after a cut here and its forced cuts, if the chain leaves here
+    uint64_t* pm;  // lanes on the chain from here to where it leaves the vector
+    uint32_t* nf;  // forced cuts after a cut here
+    uint8_t* xl;   // the lane where the chain from here leaves the vector
 };
 
 __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int nh, int lane) {
@@ -174,7 +175,7 @@ __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int n
     const unsigned long long* const rec = a.rec;
     const uint64_t* const cand = a.cand;
     unsigned long long* const sinfo = a.rec + total;  // step records after the tile records
-    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_nf, a.sc_nx};
+    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_pm, a.sc_nf, a.sc_xl};
     const uint64_t t_start = wall_clock64();
     for (uint64_t st = (uint64_t)h; st < nsteps; st += (uint64_t)nh) {
         const uint64_t t0 = st * kResolveBatch;
@@ -263,12 +264,30 @@ __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int n
                             }
                         }
                     }
+                    // the chain from every lane (nx ascends): path masks and exit lanes by
+                    // one backward pass over the lanes
+                    uint64_t pm = 0;
+                    int xl = lane;
+                    for (int k = nv - 1; k >= 0; --k) {
+                        const int n = __builtin_amdgcn_readlane(nx, k);
+                        uint64_t p = 1ull << k;
+                        int x = k;
+                        if (n != k) {
+                            p |= readlane64(pm, n);
+                            x = __builtin_amdgcn_readlane(xl, n);
+                        }
+                        if (lane == k) {
+                            pm = p;
+                            xl = x;
+                        }
+                    }
                     if (lane < nv) {
                         const uint64_t w = o + k0 + v0 + (uint64_t)lane;
                         sc.c[w] = c;
                         sc.sk[w] = sk;
+                        sc.pm[w] = pm;
                         sc.nf[w] = nf;
-                        sc.nx[w] = (uint8_t)nx;
+                        sc.xl[w] = (uint8_t)xl;
                     }
                 }
             }
@@ -295,7 +314,7 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
     uint64_t* const cuts_host = a.cuts_host;
     const uint64_t host_cap = a.host_cap;
     const unsigned long long* const sinfo = a.rec + total;
-    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_nf, a.sc_nx};
+    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_pm, a.sc_nf, a.sc_xl};
     const uint64_t timeout = a.timeout_ticks, end = a.end;
     uint64_t s = a.s0, ncut = 0;
     uint32_t nkeep = 0, status = 0;
@@ -387,8 +406,8 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         return st < nsteps ? __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
     };
     struct Vec {
-        uint64_t c, sk;
-        uint32_t nf, nx;
+        uint64_t c, sk, pm;
+        uint32_t nf, xl;
     };
     auto load_vec = [&](uint64_t o, uint32_t T, uint32_t v0) -> Vec {
         const bool v = v0 + lane < T;
@@ -396,8 +415,9 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         Vec x;
         x.c = v ? sc.c[w] : ~0ull;
         x.sk = v ? sc.sk[w] : 0ull;
+        x.pm = v ? sc.pm[w] : 0ull;
         x.nf = v ? sc.nf[w] : 0u;
-        x.nx = v ? (uint32_t)sc.nx[w] : (uint32_t)lane;
+        x.xl = v ? (uint32_t)sc.xl[w] : (uint32_t)lane;
         return x;
     };
     uint64_t r_next = load_info(0);
@@ -426,7 +446,7 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         const uint32_t T = (uint32_t)(r >> 27) & 0xFFFFFu;
         const uint64_t o = r & 0x7FFFFFFull;
         // three vectors in flight: the one walked and the next two
-        Vec cur = T ? load_vec(o, T, 0) : Vec{~0ull, 0ull, 0u, 0u};
+        Vec cur = T ? load_vec(o, T, 0) : Vec{~0ull, 0ull, 0ull, 0u, 0u};
         Vec n1 = 64 < T ? load_vec(o, T, 64) : cur;
         for (uint32_t v0 = 0; v0 < T; v0 += 64) {
             const Vec n2 = v0 + 128 < T ? load_vec(o, T, v0 + 128) : n1;
@@ -434,21 +454,9 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
             unsigned long long rem = __ballot(v0 + lane < T);
             bool reset = false;
             const int e = entry(c, rem, reset);
-            if (e >= 0) {
-                // the chain from e: runs of consecutive lanes (nx = lane + 1, the usual case)
-                // are taken whole, one bit scan each; a run's last lane jumps by nx
-                const unsigned long long step1 = __ballot((int)cur.nx == lane + 1);
-                unsigned long long mask = 0;
-                int x = e;
-                for (int guard = 0; guard < 64; ++guard) {
-                    const unsigned long long brk = ~step1 & (~0ull << x);  // first lane >= x not stepping by 1
-                    const int f = brk ? __ffsll(brk) - 1 : 63;
-                    mask |= (f == 63 ? ~0ull : ((2ull << f) - 1)) & (~0ull << x);
-                    const int n = __builtin_amdgcn_readlane((int)cur.nx, f);
-                    x = f;
-                    if (n == f) break;
-                    x = n;
-                }
+            if (e >= 0) {  // the chain from e, precomputed by the helper
+                const unsigned long long mask = readlane64(cur.pm, e);
+                const int x = __builtin_amdgcn_readlane((int)cur.xl, e);
                 emit_chain(c, mask, cur.nf);
                 s = readlane64(cur.sk, x);
                 rem = x == 63 ? 0ull : rem & ~((2ull << x) - 1);
@@ -456,6 +464,11 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
             keep_rest(c, rem, reset);
             cur = n1;
             n1 = n2;
+        }
+        if ((st & 7) == 7 && lane == 0) {  // progress: the host copies the cuts written so far
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __hip_atomic_store(a.res_host + 9, ncut < host_cap ? ncut : host_cap, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     if (status == 0) {

@@ -234,11 +234,19 @@ class Chunker:
         """Output capacity find_cuts needs for ``length`` bytes at this average."""
         return int(lib().pbs_chunker_cuts_bound(self._h, length))
 
+    def _out(self, cap: int) -> np.ndarray:
+        # one output array per handle, grown as needed: a fresh multi-MiB array per call
+        # would page-fault on every first touch
+        buf = getattr(self, "_outbuf", None)
+        if buf is None or buf.size < cap:
+            buf = self._outbuf = np.empty(cap, dtype=np.uint64)
+        return buf
+
     def find_cuts(self, data, is_final: bool = False) -> np.ndarray:
         """Chunk END offsets (absolute) of every cut decided inside ``data``."""
         a = _as_u8(data)
         cap = self.cuts_bound(a.size)
-        out = np.empty(cap, dtype=np.uint64)
+        out = self._out(cap)
         n = ctypes.c_size_t(0)
         rc = lib().pbs_chunker_find_cuts(self._h, _ptr(a), a.size, int(bool(is_final)),
                                         out.ctypes.data, cap, ctypes.byref(n))
@@ -248,7 +256,7 @@ class Chunker:
     def find_cuts_device(self, dev_ptr: int, length: int, is_final: bool = False) -> np.ndarray:
         """Same over a device (HBM) buffer, e.g. ``tensor.data_ptr()``."""
         cap = self.cuts_bound(length)
-        out = np.empty(cap, dtype=np.uint64)
+        out = self._out(cap)
         n = ctypes.c_size_t(0)
         rc = lib().pbs_chunker_find_cuts_device(self._h, ctypes.c_void_p(dev_ptr), length,
                                                int(bool(is_final)), out.ctypes.data, cap,
