@@ -264,22 +264,14 @@ __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int n
                             }
                         }
                     }
-                    // the chain from every lane (nx ascends): path masks and exit lanes by
-                    // one backward pass over the lanes
-                    uint64_t pm = 0;
-                    int xl = lane;
-                    for (int k = nv - 1; k >= 0; --k) {
-                        const int n = __builtin_amdgcn_readlane(nx, k);
-                        uint64_t p = 1ull << k;
-                        int x = k;
-                        if (n != k) {
-                            p |= readlane64(pm, n);
-                            x = __builtin_amdgcn_readlane(xl, n);
-                        }
-                        if (lane == k) {
-                            pm = p;
-                            xl = x;
-                        }
+                    // the chain from every lane: path masks and exit lanes by pointer
+                    // doubling (6 rounds: pm covers 2^t nodes, J = the 2^t-th successor)
+                    uint64_t pm = (1ull << lane) | (1ull << nx);
+                    int xl = nx;
+#pragma unroll
+                    for (int t = 0; t < 6; ++t) {
+                        pm |= shfl64(pm, xl);
+                        xl = __shfl(xl, xl, 64);
                     }
                     if (lane < nv) {
                         const uint64_t w = o + k0 + v0 + (uint64_t)lane;
