@@ -528,11 +528,12 @@ def main():
             return ch.find_cuts_device(ptr, size, is_final=True)
         work_bytes = size
 
-    scan_ms, last = [], {}
+    scan_ms, last, fused = [], {}, []
 
     def after(cuts):
         t = ch.last_timing()
         scan_ms.append(t["scan_ms"])
+        fused.append(t["fused"] == t["bytes"] and t["bytes"] > 0)
         last.update(t, ncuts=int(cuts.size))
 
     elapsed, cuts = timed_steps(step, args, dist, torch.cuda.synchronize, after)
@@ -592,7 +593,8 @@ def main():
          "candidates_per_stream": int(last.get("candidates", 0))})
     out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                       "traffic_note": traffic_note, "kernel": "scan_main_kernel",
+                       "traffic_note": traffic_note,
+                       "kernel": "scan_fused_kernel" if fused and all(fused) else "scan_main_kernel",
                        "avg_launch_ms": round(avg_scan_s * 1e3, 4)}
     out["build_id"] = pbschunk.build_id()
     if world > 1:

@@ -106,7 +106,7 @@ const char *pbs_strerror(int code);
 
 /* Timing of the last find_cuts / scan device pass (HIP events on the handle's stream). */
 typedef struct {
-    float scan_ms;      /* main candidate kernel (scan_main_kernel) */
+    float scan_ms;      /* main candidate kernel (scan_fused_kernel / scan_main_kernel) */
     float exact_ms;     /* exact block re-evaluation + candidate sort */
     float resolve_ms;   /* min/max resolve over the candidate list */
     float total_ms;     /* first kernel start .. cut list on the host */
@@ -114,6 +114,7 @@ typedef struct {
     uint64_t suspects;  /* 128-byte blocks flagged by the main kernel */
     uint64_t candidates;
     uint64_t cuts;
+    uint64_t fused;     /* bytes chunked by the one-launch pass (scan_fused_kernel) */
 } pbs_timing;
 int pbs_chunker_last_timing(const pbs_chunker *c, pbs_timing *t);
 

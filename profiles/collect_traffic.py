@@ -26,7 +26,8 @@ ap.add_argument("pmc_dir")
 ap.add_argument("--size-gib", type=float, default=64.0)
 ap.add_argument("--avg", type=int, default=4 * 1024 * 1024)
 ap.add_argument("--workload", default="vmimage")
-ap.add_argument("--kernel", default="scan_main_kernel", help="kernel-name substring (e.g. crc32_chunks_kernel)")
+ap.add_argument("--kernel", default="scan_fused_kernel",
+                help="kernel-name substring (scan_fused_kernel, scan_main_kernel, crc32_chunks_kernel)")
 ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "traffic_latest.json"))
 a = ap.parse_args()
 

@@ -880,6 +880,7 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     c->pend_head = 0;
     c->timing_pending = true;  // scan_ms: last_timing reads ev[0] -> ev[1]
     c->timing.bytes += bl;
+    c->timing.fused += bl;
     c->timing.suspects += c->h_small[13];
     c->timing.candidates += c->h_small[12];
     c->timing.cuts += ncut;
