@@ -11,7 +11,9 @@
 //   3. resolve            min/max chunk-size rule -> cut list (pointer doubling):
 //                         up to kSmallResolveMax candidates one workgroup sorts and
 //                         resolves in LDS and writes the cuts into mapped pinned memory;
-//                         above that a hipcub radix sort + the multi-kernel resolve
+//                         above that the in-house radix sort (pbs_sort.hip) + the
+//                         multi-kernel resolve; batches >= 1 MiB at averages >= 128 KiB
+//                         take the one-launch pass instead (scan_fused.h)
 // Steps 1-3 run on the handle's HIP stream with ONE host sync per batch (spec_batch:
 // the one-workgroup resolve reads the candidate count on the device and stands down
 // when it does not fit; the host then takes the two-sync path); only the counts, the

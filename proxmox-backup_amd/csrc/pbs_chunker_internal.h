@@ -95,10 +95,18 @@ hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* p
                              uint64_t ext_count, int head, uint32_t mask, uint32_t minimum,
                              uint64_t base, uint64_t* cand, unsigned long long* ncand,
                              uint64_t cand_cap, uint64_t max_items, hipStream_t stream);
+// pbs_sort.hip (in-house; hipCUB-style two-call protocol: tmp == nullptr asks for the
+// temporary bytes).  radix_sort: stable LSD sort of u64 keys over [begin_bit, end_bit),
+// values (u32) carried when vin != nullptr.
+hipError_t radix_sort(void* tmp, size_t* tmp_bytes, const uint64_t* kin, uint64_t* kout,
+                      const uint32_t* vin, uint32_t* vout, uint64_t n, int begin_bit, int end_bit,
+                      hipStream_t stream);
 hipError_t sort_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
                     int end_bit, hipStream_t stream);
 hipError_t exclusive_sum_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
                              uint32_t n, hipStream_t stream);
+hipError_t inclusive_max_u32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint32_t* out,
+                             uint64_t n, hipStream_t stream);
 hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p, uint32_t* nxt,
                           uint32_t* jtmp, uint64_t* nforced, uint32_t* on, uint64_t* cnt,
                           uint64_t* off, void* scan_tmp, size_t scan_tmp_bytes, uint64_t* out,

@@ -21,7 +21,6 @@
 // address), one ds_read_b32 (replicated table), 1.5 hash ops (v_bitop3_b32 3-input XOR,
 // a v_alignbit_b32 rotate every second byte) and half a v_max3_u32.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
 #include <cstdlib>
@@ -944,16 +943,6 @@ hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* p
                        pre, pre_len, susp, nsusp, susp_cap, ext_first, ext_count, head, mask,
                        minimum, base, cand, ncand, cand_cap);
     return hipGetLastError();
-}
-
-hipError_t sort_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
-                    int end_bit, hipStream_t stream) {
-    return hipcub::DeviceRadixSort::SortKeys(tmp, *tmp_bytes, in, out, (int)n, 0, end_bit, stream);
-}
-
-hipError_t exclusive_sum_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
-                             uint32_t n, hipStream_t stream) {
-    return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, stream);
 }
 
 hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p, uint32_t* nxt,

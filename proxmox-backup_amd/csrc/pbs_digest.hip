@@ -16,7 +16,6 @@
 // its longest chunk, and the host orders the chunks by length (longest first) so the
 // 64 lanes finish together.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
 #include <algorithm>
@@ -26,6 +25,7 @@
 #include <vector>
 
 #include "pbs_chunker.h"
+#include "pbs_chunker_internal.h"
 #include "pbs_digest.h"
 
 namespace pbs {
@@ -504,8 +504,8 @@ extern "C" int pbs_known_chunks_device(const uint8_t* digests_dev, size_t n, con
         rc = PBS_ERR_NOMEM;
         goto done;
     }
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, key, skey, idx, sidx, (int)n, 0, 64, st) != hipSuccess ||
-        hipcub::DeviceScan::InclusiveScan(nullptr, tb_scan, head, rstart, hipcub::Max(), (int)n, st) != hipSuccess ||
+    if (radix_sort(nullptr, &tb_sort, key, skey, idx, sidx, n, 0, 64, st) != hipSuccess ||
+        inclusive_max_u32(nullptr, &tb_scan, head, rstart, n, st) != hipSuccess ||
         hipMalloc(&tmp, std::max(tb_sort, tb_scan)) != hipSuccess) {
         rc = PBS_ERR_NOMEM;
         goto done;
@@ -514,12 +514,12 @@ extern "C" int pbs_known_chunks_device(const uint8_t* digests_dev, size_t n, con
     hipLaunchKernelGGL(digest_prefix_kernel, dim3(grid), dim3(256), 0, st, digests_dev, (uint64_t)n, key, idx);
     tb_sort = std::max(tb_sort, tb_scan);
     tb_scan = tb_sort;
-    if (hipcub::DeviceRadixSort::SortPairs(tmp, tb_sort, key, skey, idx, sidx, (int)n, 0, 64, st) != hipSuccess) {
+    if (radix_sort(tmp, &tb_sort, key, skey, idx, sidx, n, 0, 64, st) != hipSuccess) {
         rc = PBS_ERR_HIP;
         goto done;
     }
     hipLaunchKernelGGL(run_head_kernel, dim3(grid), dim3(256), 0, st, skey, (uint64_t)n, head);
-    if (hipcub::DeviceScan::InclusiveScan(tmp, tb_scan, head, rstart, hipcub::Max(), (int)n, st) != hipSuccess ||
+    if (inclusive_max_u32(tmp, &tb_scan, head, rstart, n, st) != hipSuccess ||
         hipMemsetAsync(cnt, 0, 4, st) != hipSuccess) {
         rc = PBS_ERR_HIP;
         goto done;
