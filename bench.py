@@ -61,6 +61,9 @@ def parse():
                          "launcher and aggregation without a GPU)")
     ap.add_argument("--host-inclusive-gib", type=float, default=4.0,
                     help="also time the host-buffer path (H2D + kernels + D2H) on this many GiB; 0 = skip")
+    ap.add_argument("--secondary-random", type=int, default=1,
+                    help="after the headline, regenerate the same buffer as random data and "
+                         "time the pass over it too (a secondary line: no zero extents)")
     ap.add_argument("--digest", type=int, default=0,
                     help="also time the per-chunk SHA-256 stage (SURVEY 8(f)) over the stream's "
                          "chunks (GPU), with hashlib on the host cores beside it")
@@ -196,6 +199,42 @@ def cpu_config1(args):
     return out
 
 
+def secondary_random(args, ch, buf, stream, steps: int = 3):
+    """The same-size stream of random bytes (GEN_RANDOM, seed 0x5EED0002) through the same
+    handle: every window hashes uniformly, so no zero extents shortcut anything; timed
+    like the headline (synchronize around each pass) plus the kernel's HIP-event time."""
+    import numpy as np
+    import torch
+
+    import pbschunk
+
+    size = buf.numel()
+    pbschunk.generate_device(buf.data_ptr(), size, GEN["random"], SEEDS["random"], 0, stream.cuda_stream)
+    torch.cuda.synchronize()
+    ch.find_cuts_device(buf.data_ptr(), size, is_final=True)  # warm-up
+    torch.cuda.synchronize()
+    wall, scan, fused, n = [], [], [], 0
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        cuts = ch.find_cuts_device(buf.data_ptr(), size, is_final=True)
+        torch.cuda.synchronize()
+        wall.append(time.perf_counter() - t0)
+        t = ch.last_timing()
+        scan.append(t["scan_ms"])
+        fused.append(t["fused"] == t["bytes"])
+        n = int(cuts.size)
+    ms = float(np.mean(wall)) * 1e3
+    sk = float(np.mean(scan))
+    achieved = size / (sk / 1e3) / 1e9
+    return {"workload": f"random-{args.size_gib:g}GiB-avg{args.avg}", "seed": hex(SEEDS["random"]),
+            "value": round(size / (1 << 30) / (ms / 1e3), 3), "unit": "GiB/s", "steps": steps,
+            "ms_per_step": round(ms, 3), "chunks": n,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "kernel": "scan_fused_kernel" if all(fused) else "scan_main_kernel",
+                         "avg_launch_ms": round(sk, 4)}}
+
+
 def digest_stage(args, buf, cuts, stream, reps: int = 3):
     """Per-chunk SHA-256 of the whole device-resident stream (one lane per chunk, longest
     chunks first), timed with HIP events on the launch stream; hashlib (OpenSSL) on the
@@ -228,6 +267,37 @@ def digest_stage(args, buf, cuts, stream, reps: int = 3):
         torch.cuda.synchronize()
         ms.append(ev[0].elapsed_time(ev[1]))
     t = min(ms) / 1e3
+    # where the GPU-only time goes: each chunk-length class launched alone (HIP events)
+    classes = []
+    edges = [0, 1 << 20, 2 << 20, 4 << 20, 8 << 20, 12 << 20, 16 << 20, max(int(lens.max()) + 1, (16 << 20) + 1)]
+    for lo, hi in zip(edges[:-1], edges[1:]):
+        sel = order[(lens[order] >= lo) & (lens[order] < hi)]
+        if sel.size == 0:
+            continue
+        oc = torch.from_numpy(sel.astype(np.int32)).to(buf.device)
+        ev[0].record(stream)
+        pbschunk.digest_chunks_async(buf.data_ptr(), size, bd.data_ptr(), oc.data_ptr(), int(sel.size),
+                                     out.data_ptr(), hip_stream=stream.cuda_stream)
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        classes.append({"lo_mib": lo / (1 << 20), "hi_mib": hi / (1 << 20), "chunks": int(sel.size),
+                        "gib": round(float(lens[sel].sum()) / (1 << 30), 3),
+                        "ms": round(ev[0].elapsed_time(ev[1]), 3)})
+    # hybrid: the longest chunks on the host cores (SHA extensions), zero chunks once per
+    # length, the rest on the GPU; wall clock of the synchronous call, digests on the host
+    threads = cpu_threads(args)
+    ref = out.view(n, 32).cpu().numpy()
+    hyb = []
+    for _ in range(reps):
+        dg, tm = pbschunk.digest_chunks_hybrid(buf.data_ptr(), size, bounds, threads=threads,
+                                               hip_stream=stream.cuda_stream)
+        hyb.append(tm)
+    if not np.array_equal(dg, ref):
+        raise RuntimeError("hybrid digests differ from the GPU-only digests")
+    hb = min(hyb, key=lambda x: x["total_ms"])
+    hybrid = {"ms": round(hb["total_ms"], 3), "GiB/s": round(size / (1 << 30) / (hb["total_ms"] / 1e3), 3),
+              "sha_ni": pbschunk.sha256_host_uses_ni(),
+              **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in hb.items()}}
     # known-chunk test of the same digests (backup_writer.rs:677-697; no previous index:
     # repeats inside the stream, e.g. the zero chunks, are the known ones)
     flags = torch.empty(n, dtype=torch.uint8, device=buf.device)
@@ -240,7 +310,6 @@ def digest_stage(args, buf, cuts, stream, reps: int = 3):
     take = max(1, min(n, take))
     host = buf[: int(bounds[take])].cpu().numpy()
     mv = memoryview(host)
-    threads = cpu_threads(args)
     parts = [list(range(k, take, threads)) for k in range(threads)]
 
     def work(ix):
@@ -253,8 +322,12 @@ def digest_stage(args, buf, cuts, stream, reps: int = 3):
     [x.join() for x in ths]
     cpu_gib_s = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
     crc = crc_stage(args, buf, bd, od, n, bounds, take, threads, stream, reps)
+    best = min(t, hb["total_ms"] / 1e3)
     return {"metric": "GiB/s SHA-256 digested (per chunk, device-resident)",
-            "value": round(size / (1 << 30) / t, 3), "ms": round(t * 1e3, 3), "chunks": n,
+            "value": round(size / (1 << 30) / best, 3), "ms": round(best * 1e3, 3), "chunks": n,
+            "gpu_only": {"ms": round(t * 1e3, 3), "GiB/s": round(size / (1 << 30) / t, 3),
+                         "classes": classes},
+            "hybrid": hybrid,
             "max_chunk": int(lens.max()), "bound": "valu (one lane per chunk; serial per chunk)",
             "known_chunks": nknown, "known_ms": round(known_ms, 3),
             "cpu_baseline": {"value": round(cpu_gib_s, 3), "unit": "GiB/s", "cores": threads,
@@ -355,6 +428,9 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
             "value": round(n / (1 << 30) / wall, 3), "bytes": n, "piece": piece,
             "chunks": int(ends.size), "timing_ms": {k: round(v, 2) for k, v in t.items()
                                                      if k.endswith("_ms")},
+            "host_share": {"chunks": t["host_chunks"], "gib": round(t["host_bytes"] / (1 << 30), 3),
+                           "threads": t["host_threads"],
+                           "min_len": int(str(os.environ.get("PBS_PIPE_HOST_MIN", 8 << 20)), 0)},
             "cpu_baseline": {"value": round(cpu, 3), "unit": "GiB/s", "cores": nth,
                              "kind": "port (oracle chunker) + hashlib + zlib.crc32",
                              "sample": f"{nth} x 256 MiB slices: chunk_feed then sha256 + crc32 per chunk"}}
@@ -605,6 +681,8 @@ def main():
         out["digest"] = digest_stage(args, buf, cuts, stream)
     if args.pipeline_gib > 0 and args.mode == "streams" and world == 1:
         out["pipeline"] = pipeline_stage(args, buf)
+    if args.secondary_random and args.mode == "streams" and world == 1 and args.workload != "random":
+        out["secondary_random"] = secondary_random(args, ch, buf, stream)
     if args.cpu_baseline and world == 1:
         del buf
         out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)

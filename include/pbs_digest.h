@@ -51,6 +51,45 @@ int pbs_digest_chunks_async(const uint8_t *dev_data, size_t data_len, uint64_t b
                             const uint8_t *key, size_t key_len, uint8_t *digests_dev,
                             void *hip_stream);
 
+/* Hybrid per-chunk SHA-256: same digests as pbs_digest_chunks_device, with the work
+ * split between the GPU and host threads.  A GPU lane walks one chunk's serial chain
+ * (~35 MB/s), so the longest chunks set the GPU's makespan; a host core with the SHA
+ * extensions walks one ~40x faster.  The longest chunks go to host threads until the
+ * host's estimated time (their bytes / (threads x host_mb_s), at most 14 GB/s when
+ * they are copied from HBM) meets the GPU's (the longest remaining chunk / gpu_mb_s);
+ * long chunks (>= 1 MiB) that are all zero bytes are hashed once per distinct length.
+ * `dev_data` (device) holds stream bytes [base, base + data_len); `host_data` (NULL or a
+ * host copy of the same bytes) lets the host threads read the bytes directly instead of
+ * copying their chunks from HBM.  `bounds` (host, n + 1), `digests` (host, 32 n) as in
+ * pbs_digest_chunks_device.  `opts` may be NULL (defaults).  Synchronous. */
+typedef struct {
+    int host_threads;      /* 0: min(hardware threads, 16); < 0: GPU only */
+    uint64_t host_min_len; /* 0: cost model; else chunks at least this long go to the host */
+    double host_mb_s;      /* per-thread host SHA-256 rate for the model (0: 1400) */
+    double gpu_mb_s;       /* one GPU lane's chain rate for the model (0: 35) */
+} pbs_digest_hybrid_opts;
+typedef struct {
+    double total_ms; /* call entry .. digests in `digests` */
+    double zero_ms;  /* plan: sort + zero test of the long chunks (one sync) */
+    double gpu_ms;   /* the GPU share's kernel, HIP events */
+    double host_ms;  /* the host share, all threads joined */
+    uint64_t gpu_chunks, host_chunks, host_bytes, zero_chunks, zero_lengths;
+    uint64_t threshold; /* shortest chunk given to the host (0: none) */
+    int threads;
+} pbs_digest_hybrid_timing;
+int pbs_digest_chunks_hybrid(const uint8_t *dev_data, const uint8_t *host_data, size_t data_len,
+                             uint64_t base, const uint64_t *bounds, size_t n, const uint8_t *key,
+                             size_t key_len, uint8_t *digests, const pbs_digest_hybrid_opts *opts,
+                             pbs_digest_hybrid_timing *timing, void *hip_stream);
+
+/* SHA-256(chunk || key) of every chunk of a host buffer on `threads` host threads (0:
+ * hardware threads), SHA extensions when the CPU has them (pbs_sha256_host_uses_ni).
+ * Same arguments as pbs_digest_chunks_device with host memory. */
+int pbs_digest_chunks_host(const uint8_t *host_data, size_t data_len, uint64_t base,
+                           const uint64_t *bounds, size_t n, const uint8_t *key, size_t key_len,
+                           uint8_t *digests, int threads);
+int pbs_sha256_host_uses_ni(void);
+
 /* Known-chunk test of the upload stream (pbs-client/src/backup_writer.rs:677-697):
  * chunk i is "known" -- uploaded as a reference, not as data -- iff its digest is in the
  * previous backup's index (`known_chunks`, filled from the downloaded index,
@@ -72,13 +111,19 @@ int pbs_known_chunks_device(const uint8_t *digests_dev, size_t n, const uint8_t 
  * in chunk order, and with `crcs` != NULL each chunk's CRC-32 (the uncompressed blob's
  * DataBlob::compute_crc, include/pbs_blob.h; computed right after each digest launch on
  * the same stream); cap >= pbs_chunker_cuts_bound for the average.  Needs `len` bytes of
- * device memory.  Synchronous. */
+ * device memory.  Chunks of at least PBS_PIPE_HOST_MIN bytes (environment, default
+ * 8 MiB; 0 = none) are digested on PBS_PIPE_HOST_THREADS host threads (default
+ * min(hardware threads, 16) - 2) straight from `host`, the rest on the GPU.
+ * Synchronous. */
 typedef struct {
     double total_ms; /* first copy issued .. digests on the host */
     double h2d_ms;   /* copy thread: all pieces issued and landed */
     double chunk_ms; /* main thread inside the chunker calls */
     double drain_ms; /* last piece chunked .. digests on the host */
     uint64_t bytes, chunks, pieces;
+    uint64_t host_chunks, host_bytes; /* digests computed on the host threads */
+    double host_done_ms;              /* host threads joined (ms after the first copy) */
+    int host_threads;
 } pbs_pipeline_timing;
 int pbs_pipeline_host(size_t avg, const uint8_t *host, size_t len, size_t piece,
                       const uint8_t *key, size_t key_len, int digest_cus, uint64_t *ends,

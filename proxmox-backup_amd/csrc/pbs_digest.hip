@@ -19,14 +19,19 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include "pbs_chunker.h"
 #include "pbs_chunker_internal.h"
 #include "pbs_digest.h"
+#include "sha_host.h"
 
 namespace pbs {
 namespace {
@@ -88,6 +93,11 @@ __device__ __forceinline__ void compress(uint32_t (&st)[8], uint32_t (&w)[16]) {
     st[7] += h;
 }
 
+// 68 readable bytes in global memory: the window a producer lane loads when it has no
+// block two ahead (a select between two global pointers keeps the loads global; a
+// constant-memory dummy made them flat loads, which also count on the LDS counter)
+__device__ uint32_t g_dummy_window[17];
+
 struct DigestKey {
     uint32_t len;
     uint8_t bytes[PBS_DIGEST_MAX_KEY];
@@ -98,6 +108,16 @@ __device__ __forceinline__ void load_window(const uint32_t* __restrict__ pa, boo
 #pragma unroll
     for (int q = 0; q < 16; ++q) d[q] = __builtin_nontemporal_load(pa + q);
     d[16] = tail_dw ? __builtin_nontemporal_load(pa + 16) : 0u;
+}
+
+// Branch-free form: dword 16 is read from pa + 16 when the chunk start is misaligned
+// (it then holds a byte of the block) and from pa + 15 otherwise (inside the window;
+// the perms of an aligned block never select it).
+__device__ __forceinline__ void load_window_nb(const uint32_t* __restrict__ pa, uint32_t dw16,
+                                               uint32_t (&d)[17]) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[q] = __builtin_nontemporal_load(pa + q);
+    d[16] = __builtin_nontemporal_load(pa + dw16);
 }
 
 // Lane k hashes chunk order[k] (identity if order == nullptr): [bounds[i], bounds[i+1])
@@ -184,7 +204,7 @@ __device__ uint64_t g_sha_probe[5];
 __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint32_t* __restrict__ order, uint64_t n, DigestKey key, uint8_t* __restrict__ digests) {
-    __shared__ uint4 sw[2][16][64];  // [buffer][t / 4][lane]: W[t] + K[t] for 4 t (b128 per lane)
+    __shared__ uint4 sw[3][16][64];  // [slot][t / 4][lane]: W[t] + K[t] for 4 t (b128 per lane)
     __shared__ uint32_t s_blocks;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t k = (uint64_t)blockIdx.x * 64 + lane;
@@ -211,48 +231,58 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
     const uint64_t bits = (len + kl) * 8ull;
     const uint8_t* tp = p + (nfull << 6);
 
-    // wave 1: message block b -> W + K into buffer b & 1.  The data window of block b
-    // was loaded during the previous block's period (`pre`); the loads of block b + 1
-    // are issued here, before the schedule, so HBM latency hides behind a block period.
-    uint32_t pre[17];
-    if (wave == 1 && nfull) load_window(pa, r != 0, pre);
-    auto produce = [&](uint32_t b) {
+    // wave 1: message block b -> W + K into slot b % 3.  Its 68-byte data window sits in
+    // register window R[b % 3], loaded two blocks earlier: produce(b) issues the loads of
+    // block b + 2 into the window block b - 1 has freed, so HBM latency hides behind two
+    // block periods.  (A single `pre` window copied out before its reload made the
+    // compiler wait for the new loads right after issuing them: the phi copy at the loop
+    // latch needs their data.)
+    uint32_t R0[17], R1[17], R2[17];
+    const uint32_t dw16 = r ? 16u : 15u;
+    if (wave == 1) {
+        if (nfull) load_window_nb(pa, dw16, R0);
+        if (nfull > 1) load_window_nb(pa + 16, dw16, R1);
+    }
+    auto produce = [&](uint32_t b, uint32_t slot, uint32_t (&cur)[17], uint32_t (&nx2)[17]) {
+        // straight-line perms then loads (no branch between them, so nothing can sink the
+        // perms below the loads and make their wait cover the new loads); a lane without a
+        // window two blocks ahead loads the 68-byte dummy instead
         uint32_t w[16];
-        if ((uint64_t)b < nfull) {
-            uint32_t d[17];
 #pragma unroll
-            for (int q = 0; q < 17; ++q) d[q] = pre[q];
-            if ((uint64_t)b + 1 < nfull) load_window(pa + 16 * ((uint64_t)b + 1), r != 0, pre);
+        for (int q = 0; q < 16; ++q) w[q] = __builtin_amdgcn_perm(cur[q + 1], cur[q], sel);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t* src = (uint64_t)b + 2 < nfull ? pa + 16 * ((uint64_t)b + 2) : g_dummy_window;
+        load_window_nb(src, dw16, nx2);
+        if ((uint64_t)b >= nfull) {
+            if ((uint64_t)b < total) {
+                const uint32_t blk = (uint32_t)(b - nfull);
 #pragma unroll
-            for (int q = 0; q < 16; ++q) w[q] = __builtin_amdgcn_perm(d[q + 1], d[q], sel);
-        } else if ((uint64_t)b < total) {
-            const uint32_t blk = (uint32_t)(b - nfull);
+                for (int q = 0; q < 16; ++q) {
+                    uint32_t v = 0;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t t = blk * 64 + 4 * q + j;
-                    uint32_t byte;
-                    if (t < rem)
-                        byte = tp[t];
-                    else if (t < rem + kl)
-                        byte = key.bytes[t - rem];
-                    else if (t == rem + kl)
-                        byte = 0x80u;
-                    else if (t >= nb * 64 - 8)
-                        byte = (uint32_t)(bits >> (8 * (nb * 64 - 1 - t))) & 0xffu;
-                    else
-                        byte = 0;
-                    v = (v << 8) | byte;
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t t = blk * 64 + 4 * q + j;
+                        uint32_t byte;
+                        if (t < rem)
+                            byte = tp[t];
+                        else if (t < rem + kl)
+                            byte = key.bytes[t - rem];
+                        else if (t == rem + kl)
+                            byte = 0x80u;
+                        else if (t >= nb * 64 - 8)
+                            byte = (uint32_t)(bits >> (8 * (nb * 64 - 1 - t))) & 0xffu;
+                        else
+                            byte = 0;
+                        v = (v << 8) | byte;
+                    }
+                    w[q] = v;
                 }
-                w[q] = v;
-            }
-        } else {
+            } else {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) w[q] = 0;
+                for (int q = 0; q < 16; ++q) w[q] = 0;
+            }
         }
-        uint4 (*out)[64] = sw[b & 1];
+        uint4 (*out)[64] = sw[slot];
         uint32_t o[4];
 #pragma unroll
         for (int t = 0; t < 64; ++t) {
@@ -273,25 +303,47 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
 
     uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                       0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    if (wave == 1 && nblocks) produce(0);
+    // Three slots, the producer two blocks ahead (its data loads two blocks ahead too).
+    // The loop is unrolled by three so that slot and register window are constants in
+    // each step: rotating them through one loop body put register copies between the
+    // loads and their use, and the compiler then waited for the loads at once.
+    if (wave == 1) {
+        if (nblocks) produce(0, 0, R0, R2);
+        if (nblocks > 1) produce(1, 1, R1, R0);
+    }
     __syncthreads();
 #ifdef PBS_SHA_PROBE  // scripts/microbench/mb_sha.hip: cycles of each wave's work vs the barrier
     uint64_t pr_work = 0, pr_wait = 0;
 #endif
-    for (uint32_t b = 0; b < nblocks; ++b) {
+    // block b: the rounds wave hashes slot b % 3, the producer fills slot (b + 2) % 3
+    // The rounds wave holds W + K in kwv[16]: groups 12..15 of block b are read at the top
+    // of block b (needed from round 48), and group q < 12 of block b + 1 (complete since
+    // the last barrier) right after round 4q + 3 consumed group q of block b, so no LDS
+    // read latency lands on the chain and the barrier finds no read in flight.
+    uint4 kwv[16];
+    if (wave == 0) {
+#pragma unroll
+        for (int q = 0; q < 12; ++q) kwv[q] = sw[0][q][lane];
+    }
+    auto step = [&](uint32_t b, const uint4 (*in)[64], const uint4 (*nx)[64], uint32_t pslot,
+                    uint32_t (&cur)[17], uint32_t (&nx2)[17]) {
 #ifdef PBS_SHA_PROBE
         const uint64_t c0 = clock64();
 #endif
         if (wave == 1) {
-            if (b + 1 < nblocks) produce(b + 1);
+            if (b + 2 < nblocks) produce(b + 2, pslot, cur, nx2);
         } else if ((uint64_t)b < total) {
-            const uint4 (*in)[64] = sw[b & 1];
             uint32_t a = st[0], bb = st[1], c = st[2], d = st[3], ee = st[4], f = st[5], g = st[6], h = st[7];
-            uint4 kw4 = in[0][lane];
+#pragma unroll
+            for (int q = 12; q < 16; ++q) kwv[q] = in[q][lane];
 #pragma unroll
             for (int t = 0; t < 64; ++t) {
+                const uint4 kw4 = kwv[t >> 2];
                 const uint32_t kw = (t & 3) == 0 ? kw4.x : (t & 3) == 1 ? kw4.y : (t & 3) == 2 ? kw4.z : kw4.w;
-                if ((t & 3) == 3 && t < 63) kw4 = in[(t >> 2) + 1][lane];
+                if ((t & 3) == 3 && t < 48) {
+                    kwv[t >> 2] = nx[t >> 2][lane];
+                    __builtin_amdgcn_sched_barrier(0);  // keep the read here (hoisted, it needs copies)
+                }
                 const uint32_t S1 = xor3(rotr(ee, 6), rotr(ee, 11), rotr(ee, 25));
                 const uint32_t ch = __builtin_amdgcn_bitop3_b32(ee, f, g, 0xCA);
                 const uint32_t t1 = h + S1 + ch + kw;
@@ -323,6 +375,11 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
 #else
         __syncthreads();
 #endif
+    };
+    for (uint32_t b = 0; b < nblocks; b += 3) {
+        step(b, sw[0], sw[1], 2, R2, R1);
+        if (b + 1 < nblocks) step(b + 1, sw[1], sw[2], 0, R0, R2);
+        if (b + 2 < nblocks) step(b + 2, sw[2], sw[0], 1, R1, R0);
     }
 #ifdef PBS_SHA_PROBE
     if (blockIdx.x == 0 && lane == 0) {
@@ -410,6 +467,46 @@ __global__ void known_kernel(const uint8_t* __restrict__ dig, uint64_t n,
     const bool kn = rep || in_known;
     is_known[i] = kn ? 1 : 0;
     if (kn) atomicAdd(count, 1u);
+}
+
+
+// Zero test of the hybrid digest's long chunks: flags[k] = 1 iff chunk order[k] is all
+// zero bytes.  One workgroup per chunk, 256 lanes x 16 bytes = 4 KiB rows; a group of 16
+// rows ends with a workgroup OR, so a chunk with data stops after its first 64 KiB and
+// only all-zero chunks are read whole.
+__global__ __launch_bounds__(256) void zero_flags_kernel(const uint8_t* __restrict__ data, uint64_t base,
+                                                         const uint64_t* __restrict__ bounds,
+                                                         const uint32_t* __restrict__ order, uint64_t m,
+                                                         uint8_t* __restrict__ flags) {
+    const uint64_t k = blockIdx.x;
+    if (k >= m) return;
+    const uint64_t i = order[k];
+    const uint8_t* p = data + (bounds[i] - base);
+    const uint8_t* e = data + (bounds[i + 1] - base);
+    const uint8_t* a0 = reinterpret_cast<const uint8_t*>(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    const uint8_t* a1 = reinterpret_cast<const uint8_t*>((uintptr_t)e & ~(uintptr_t)15);
+    int nz = 0;
+    if (a0 >= a1) {  // under 32 bytes: bytewise
+        for (const uint8_t* q = p + threadIdx.x; q < e; q += 256) nz |= *q;
+    } else {
+        if (threadIdx.x < (unsigned)(a0 - p)) nz |= p[threadIdx.x];
+        if (threadIdx.x < (unsigned)(e - a1)) nz |= a1[threadIdx.x];
+        const uint4* w = reinterpret_cast<const uint4*>(a0);
+        const uint64_t nw = (uint64_t)(a1 - a0) / 16;
+        for (uint64_t r = 0; r < nw; r += 256 * 16) {
+#pragma unroll 4
+            for (int j = 0; j < 16; ++j) {
+                const uint64_t x = r + (uint64_t)j * 256 + threadIdx.x;
+                if (x < nw) {
+                    const uint4 v = w[x];
+                    nz |= (int)((v.x | v.y | v.z | v.w) != 0);
+                }
+            }
+            if (__syncthreads_or(nz)) break;
+        }
+    }
+    nz = __syncthreads_or(nz);
+    if (threadIdx.x == 0) flags[k] = nz ? 0 : 1;
 }
 
 }  // namespace
@@ -542,5 +639,277 @@ extern "C" int pbs_known_chunks_device(const uint8_t* digests_dev, size_t n, con
 done:
     for (void* q : {(void*)key, (void*)skey, (void*)idx, (void*)sidx, (void*)head, (void*)rstart, (void*)cnt, tmp})
         if (q) (void)hipFree(q);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------------------
+// Hybrid digest: the longest chunks on host threads (SHA extensions, pbs_sha_host.cpp),
+// the rest on the GPU, all-zero long chunks hashed once per distinct length.
+namespace {
+
+using HClock = std::chrono::steady_clock;
+double hms(HClock::time_point a, HClock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+}
+
+constexpr size_t kSlice = 4u << 20;         // D2H slice of a host-hashed chunk
+constexpr uint64_t kZeroMin = 1u << 20;      // chunks tested for all-zero content
+
+// Per-thread pinned double buffers and copy streams for the host share, kept for the
+// process (pinning 8 MiB per thread on every call would cost more than it hides).
+struct HostStage {
+    std::mutex mu;
+    int dev = -1;
+    std::vector<uint8_t*> buf;  // 2 * kSlice each
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> ev;  // 2 per thread
+    bool grow(int dv, int t) {
+        if (dev != dv) {
+            release();
+            dev = dv;
+        }
+        while ((int)buf.size() < t) {
+            uint8_t* b = nullptr;
+            hipStream_t s = nullptr;
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (hipHostMalloc(&b, 2 * kSlice, hipHostMallocDefault) != hipSuccess) return false;
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) {
+                (void)hipHostFree(b);
+                return false;
+            }
+            buf.push_back(b);
+            st.push_back(s);
+            ev.push_back(e0);
+            ev.push_back(e1);
+        }
+        return true;
+    }
+    void release() {
+        for (auto b : buf) (void)hipHostFree(b);
+        for (auto s : st) (void)hipStreamDestroy(s);
+        for (auto e : ev) (void)hipEventDestroy(e);
+        buf.clear();
+        st.clear();
+        ev.clear();
+    }
+};
+HostStage& host_stage() {
+    static HostStage* hs = new HostStage;  // never destroyed: HIP may be torn down first at exit
+    return *hs;
+}
+
+// SHA-256 of one device-resident chunk on this host thread: 4 MiB slices copied into the
+// thread's pinned double buffer one slice ahead of the hashing.
+bool hash_from_device(const uint8_t* src, uint64_t len, const uint8_t* key, size_t key_len, uint8_t* out,
+                      uint8_t* buf, hipStream_t st, hipEvent_t* ev) {
+    pbs::HostSha h;
+    pbs::sha256_host_init(h);
+    const uint64_t ns = len ? (len + kSlice - 1) / kSlice : 0;
+    if (ns && (hipMemcpyAsync(buf, src, std::min<uint64_t>(len, kSlice), hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipEventRecord(ev[0], st) != hipSuccess))
+        return false;
+    for (uint64_t j = 0; j < ns; ++j) {
+        const uint64_t off = j * kSlice, n = std::min<uint64_t>(len - off, kSlice);
+        uint8_t* cur = buf + (j & 1) * kSlice;
+        if (j + 1 < ns) {
+            const uint64_t n2 = std::min<uint64_t>(len - off - kSlice, kSlice);
+            if (hipMemcpyAsync(buf + ((j + 1) & 1) * kSlice, src + off + kSlice, n2, hipMemcpyDeviceToHost, st) !=
+                    hipSuccess ||
+                hipEventRecord(ev[(j + 1) & 1], st) != hipSuccess)
+                return false;
+        }
+        if (hipEventSynchronize(ev[j & 1]) != hipSuccess) return false;
+        if (j + 1 < ns) {
+            pbs::sha256_host_blocks(h, cur, n);
+        } else {
+            pbs::sha256_host_blocks(h, cur, n / 64 * 64);
+            pbs::sha256_host_final(h, cur + n / 64 * 64, n % 64, key, key_len, out);
+        }
+    }
+    if (!ns) pbs::sha256_host_final(h, nullptr, 0, key, key_len, out);
+    return true;
+}
+
+}  // namespace
+
+extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* host_data, size_t data_len,
+                                        uint64_t base, const uint64_t* bounds, size_t n, const uint8_t* key,
+                                        size_t key_len, uint8_t* digests, const pbs_digest_hybrid_opts* opts,
+                                        pbs_digest_hybrid_timing* timing, void* hip_stream) {
+    const HClock::time_point t0 = HClock::now();
+    if (timing) std::memset(timing, 0, sizeof(*timing));
+    if (n == 0) return PBS_OK;
+    if (!bounds || !digests || (data_len && !dev_data) || key_len > PBS_DIGEST_MAX_KEY || (key_len && !key) ||
+        n > 0xFFFFFFFFull)
+        return PBS_ERR_INVALID;
+    for (size_t i = 0; i < n; ++i)
+        if (bounds[i] > bounds[i + 1] || bounds[i] < base || bounds[i + 1] - base > data_len)
+            return PBS_ERR_INVALID;
+    pbs_digest_hybrid_opts o{};
+    if (opts) o = *opts;
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int threads = o.host_threads < 0 ? 0 : o.host_threads == 0 ? std::min(hw, 16) : o.host_threads;
+    const double host_rate = (o.host_mb_s > 0 ? o.host_mb_s : 1400.0) * 1e6;  // bytes/s per thread
+    const double gpu_rate = (o.gpu_mb_s > 0 ? o.gpu_mb_s : 35.0) * 1e6;        // bytes/s per chain
+    // from HBM the host share moves through 4 MiB pinned slices: ~14 GB/s measured over
+    // 16 threads on the MI355X box (profiles/r02/digest), below the threads' SHA rate
+    const double agg = std::min(threads * host_rate, host_data ? 1e12 : 14e9);
+    hipStream_t st = (hipStream_t)hip_stream;
+    auto clen = [&](uint32_t i) { return bounds[i + 1] - bounds[i]; };
+
+    std::vector<uint32_t> order(n);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return clen(a) > clen(b); });
+    size_t m = 0;  // the long chunks (order prefix) get the zero test
+    if (threads > 0)
+        while (m < n && clen(order[m]) >= kZeroMin) ++m;
+
+    uint64_t* d_bounds = nullptr;
+    uint32_t* d_order = nullptr;
+    uint8_t* d_dig = nullptr;
+    uint8_t* d_flags = nullptr;
+    int rc = PBS_OK;
+    auto fail = [&](int r) {
+        if (rc == PBS_OK) rc = r;
+    };
+    if (hipMalloc(&d_bounds, (n + 1) * 8) != hipSuccess || hipMalloc(&d_order, n * 4) != hipSuccess ||
+        hipMalloc(&d_dig, n * 32) != hipSuccess || (m && hipMalloc(&d_flags, m) != hipSuccess))
+        fail(PBS_ERR_NOMEM);
+    std::vector<uint8_t> zf(m, 0);
+    if (rc == PBS_OK && (hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                         hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess))
+        fail(PBS_ERR_HIP);
+    if (rc == PBS_OK && m) {
+        hipLaunchKernelGGL(zero_flags_kernel, dim3((unsigned)m), dim3(256), 0, st, dev_data, base, d_bounds,
+                           d_order, (uint64_t)m, d_flags);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(zf.data(), d_flags, m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            fail(PBS_ERR_HIP);
+    }
+    const HClock::time_point t_zero = HClock::now();
+
+    // work list: every chunk except the repeats of an all-zero length (longest first)
+    std::vector<uint32_t> work;
+    work.reserve(n);
+    std::vector<std::pair<uint32_t, uint32_t>> dup;  // (zero chunk, its length's representative)
+    uint64_t zero_chunks = 0, zero_lengths = 0;
+    for (size_t k = 0; k < n; ++k) {
+        const uint32_t i = order[k];
+        if (k < m && zf[k]) {
+            ++zero_chunks;
+            // order is sorted by length, so one length's zero chunks are adjacent in dup
+            if (!dup.empty() && clen(dup.back().second) == clen(i)) {
+                dup.emplace_back(i, dup.back().second);
+            } else {
+                ++zero_lengths;
+                dup.emplace_back(i, i);  // i is its own length's representative
+                work.push_back(i);
+            }
+        } else {
+            work.push_back(i);
+        }
+    }
+    // split: the first h work items go to the host; minimise max(host time, GPU time)
+    size_t h = 0;
+    if (threads > 0 && rc == PBS_OK) {
+        if (o.host_min_len) {
+            while (h < work.size() && clen(work[h]) >= o.host_min_len) ++h;
+        } else {
+            double best = (double)clen(work[0]) / gpu_rate, acc = 0;
+            for (size_t k = 1; k <= work.size(); ++k) {
+                acc += (double)clen(work[k - 1]);
+                const double c = std::max(acc / agg, k < work.size() ? (double)clen(work[k]) / gpu_rate : 0.0);
+                if (c < best) {
+                    best = c;
+                    h = k;
+                }
+            }
+        }
+    }
+    const size_t g = work.size() - h;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    if (rc == PBS_OK && g) {
+        if (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess ||
+            hipMemcpyAsync(d_order, work.data() + h, g * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipEventRecord(ev[0], st) != hipSuccess)
+            fail(PBS_ERR_HIP);
+        else {
+            const int r = pbs_digest_chunks_async(dev_data, data_len, base, d_bounds, d_order, g, key, key_len,
+                                                  d_dig, hip_stream);
+            if (r != PBS_OK)
+                fail(r);
+            else if (hipEventRecord(ev[1], st) != hipSuccess)
+                fail(PBS_ERR_HIP);
+        }
+    }
+    // host share, overlapping the GPU launch
+    const HClock::time_point t_host0 = HClock::now();
+    uint64_t host_bytes = 0;
+    for (size_t k = 0; k < h; ++k) host_bytes += clen(work[k]);
+    if (rc == PBS_OK && h) {
+        if (host_data) {
+            pbs::sha256_host_items(host_data, base, bounds, work.data(), h, key, key_len, digests, threads);
+        } else {
+            HostStage& hs = host_stage();
+            std::lock_guard<std::mutex> lk(hs.mu);
+            int dv = 0;
+            const int t = (int)std::min<size_t>((size_t)threads, h);
+            if (hipGetDevice(&dv) != hipSuccess || !hs.grow(dv, t)) {
+                fail(PBS_ERR_NOMEM);
+            } else {
+                std::atomic<size_t> next{0};
+                std::atomic<bool> bad{false};
+                auto run = [&](int j) {
+                    for (size_t k; !bad && (k = next.fetch_add(1)) < h;) {
+                        const uint32_t i = work[k];
+                        if (!hash_from_device(dev_data + (bounds[i] - base), clen(i), key, key_len,
+                                              digests + 32 * (size_t)i, hs.buf[j], hs.st[j], &hs.ev[2 * j]))
+                            bad = true;
+                    }
+                };
+                std::vector<std::thread> pool;
+                for (int j = 1; j < t; ++j) pool.emplace_back(run, j);
+                run(0);
+                for (auto& th : pool) th.join();
+                if (bad) fail(PBS_ERR_HIP);
+            }
+        }
+    }
+    const HClock::time_point t_host1 = HClock::now();
+    float gpu_ms = 0;
+    std::vector<uint8_t> gd;
+    if (rc == PBS_OK && g) {
+        gd.resize(n * 32);
+        if (hipMemcpyAsync(gd.data(), d_dig, n * 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess || hipEventElapsedTime(&gpu_ms, ev[0], ev[1]) != hipSuccess)
+            fail(PBS_ERR_HIP);
+        else
+            for (size_t k = h; k < work.size(); ++k)
+                std::memcpy(digests + 32 * (size_t)work[k], gd.data() + 32 * (size_t)work[k], 32);
+    }
+    if (rc == PBS_OK)
+        for (const auto& d : dup)
+            if (d.first != d.second) std::memcpy(digests + 32 * (size_t)d.first, digests + 32 * (size_t)d.second, 32);
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    for (void* p : {(void*)d_bounds, (void*)d_order, (void*)d_dig, (void*)d_flags})
+        if (p) (void)hipFree(p);
+    if (timing) {
+        const HClock::time_point t1 = HClock::now();
+        timing->total_ms = hms(t0, t1);
+        timing->zero_ms = hms(t0, t_zero);
+        timing->gpu_ms = gpu_ms;
+        timing->host_ms = hms(t_host0, t_host1);
+        timing->gpu_chunks = g;
+        timing->host_chunks = h;
+        timing->host_bytes = host_bytes;
+        timing->zero_chunks = zero_chunks;
+        timing->zero_lengths = zero_lengths;
+        timing->threshold = h ? clen(work[h - 1]) : 0;
+        timing->threads = threads;
+    }
     return rc;
 }

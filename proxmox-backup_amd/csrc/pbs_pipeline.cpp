@@ -13,15 +13,25 @@
 // digest workgroup, and a digest launch lasts as long as its longest chunk's serial
 // hash (~0.6 s for a 16 MiB chunk), so without the split a scan launch would wait for it.
 // The chunks are digested in a few large launches (a quarter of the stream, at most
-// 16 GiB each), which overlap on the four digest streams and with the later copies.  C ABI:
-// include/pbs_digest.h.
+// 16 GiB each), which overlap on the four digest streams and with the later copies.
+//   host threads  the LONG chunks (>= PBS_PIPE_HOST_MIN, default 8 MiB) are hashed on the
+//                 host cores straight from the caller's buffer (SHA extensions,
+//                 pbs_sha_host.cpp; all-zero chunks once per length), because one GPU
+//                 lane walks a chunk's serial chain at ~30 MB/s: a 16 MiB chunk in the
+//                 last launch kept the GPU busy ~0.6 s after the last copy.  The GPU keeps
+//                 the short chunks (and every chunk's CRC).
+// C ABI: include/pbs_digest.h.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
+#include <deque>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <numeric>
 #include <thread>
@@ -31,6 +41,7 @@
 #include "pbs_chunker.h"
 #include "pbs_chunker_internal.h"
 #include "pbs_digest.h"
+#include "sha_host.h"
 
 namespace {
 
@@ -47,6 +58,11 @@ hipError_t masked_stream(hipStream_t* s, int first, int count, int ncu) {
 }
 
 constexpr int kDigestStreams = 4;
+
+uint64_t env_u64(const char* name, uint64_t dflt) {
+    const char* e = std::getenv(name);
+    return e && *e ? std::strtoull(e, nullptr, 0) : dflt;
+}
 
 }  // namespace
 
@@ -131,6 +147,60 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         });
     }
 
+    // host share: long chunks, hashed from `host` by a pool fed in stream order
+    const uint64_t host_min = env_u64("PBS_PIPE_HOST_MIN", 8ull << 20);
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int hthreads = host_min ? (int)env_u64("PBS_PIPE_HOST_THREADS", (uint64_t)std::max(1, std::min(hw, 16) - 2)) : 0;
+    std::deque<uint64_t> hq;  // chunk indices
+    std::mutex hmu;
+    std::condition_variable hcv;
+    bool hdone = false;
+    std::atomic<uint64_t> host_chunks{0}, host_bytes{0};
+    double host_done_at = 0;
+    std::vector<uint8_t> hmask;  // 1 = digest computed on the host
+    std::map<uint64_t, std::array<uint8_t, 32>> zero_dig;  // digest of an all-zero chunk per length
+    std::vector<std::thread> hpool;
+    if (ok && hthreads > 0) {
+        hmask.assign(cap, 0);
+        for (int j = 0; j < hthreads; ++j)
+            hpool.emplace_back([&] {
+                for (;;) {
+                    uint64_t i;
+                    {
+                        std::unique_lock<std::mutex> g(hmu);
+                        hcv.wait(g, [&] { return hdone || !hq.empty(); });
+                        if (hq.empty()) return;
+                        i = hq.front();
+                        hq.pop_front();
+                    }
+                    const uint64_t s0 = i ? ends[i - 1] : 0, e0 = ends[i], cl = e0 - s0;
+                    uint8_t* out = digests + 32 * i;
+                    const bool zero = pbs::all_zero(host + s0, cl);
+                    if (zero) {  // zero extents: one hash per length
+                        bool hit = false;
+                        {
+                            std::lock_guard<std::mutex> g(hmu);
+                            auto it = zero_dig.find(cl);
+                            if (it != zero_dig.end()) {
+                                std::memcpy(out, it->second.data(), 32);
+                                hit = true;
+                            }
+                        }
+                        if (hit) {
+                            host_chunks += 1;
+                            continue;
+                        }
+                    }
+                    pbs::sha256_host_one(host + s0, cl, key, key_len, out);
+                    if (zero) {
+                        std::lock_guard<std::mutex> g(hmu);
+                        std::memcpy(zero_dig[cl].data(), out, 32);
+                    }
+                    host_chunks += 1;
+                    host_bytes += e0 - s0;
+                }
+            });
+    }
     double chunk_ms = 0, last_chunk_at = 0;
     size_t n = 0, nb = 0, launches = 0, launched = 0;
     uint64_t start = 0;  // start of the first chunk not yet digested
@@ -184,15 +254,34 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
             std::stable_sort(o.begin(), o.end(), [&](uint32_t x, uint32_t y) {
                 return b[x + 1] - b[x] > b[y + 1] - b[y];
             });
+            // the longest chunks (a prefix of o) go to the host threads
+            size_t nh = 0;
+            if (hthreads > 0) {
+                while (nh < mm && b[o[nh] + 1] - b[o[nh]] >= host_min) ++nh;
+                if (nh) {
+                    {
+                        std::lock_guard<std::mutex> g(hmu);
+                        for (size_t q = 0; q < nh; ++q) {
+                            hq.push_back(launched + o[q]);
+                            hmask[launched + o[q]] = 1;
+                        }
+                    }
+                    hcv.notify_all();
+                }
+            }
             hipStream_t sd = s_dig[launches % kDigestStreams];
+            // o sorted longest first: the CRC launch takes all of it, the digest launch
+            // the suffix after the host's prefix
             if (!hip_ok(hipMemcpyAsync(d_bounds + nb, b.data(), (mm + 1) * 8, hipMemcpyHostToDevice, sd)) ||
                 !hip_ok(hipMemcpyAsync(d_order + launched, o.data(), mm * 4, hipMemcpyHostToDevice, sd)))
                 break;
-            const int dr = pbs_digest_chunks_async(d_data, len, 0, d_bounds + nb, d_order + launched, mm,
-                                                   key, key_len, d_dig + 32 * launched, sd);
-            if (dr != PBS_OK) {
-                rc = dr;
-                break;
+            if (mm > nh) {
+                const int dr = pbs_digest_chunks_async(d_data, len, 0, d_bounds + nb, d_order + launched + nh,
+                                                       mm - nh, key, key_len, d_dig + 32 * launched, sd);
+                if (dr != PBS_OK) {
+                    rc = dr;
+                    break;
+                }
             }
             if (crcs) {  // the blob CRC of the same chunks, behind the digests on that stream
                 const int cr = pbs_crc32_chunks_async(d_data, len, 0, d_bounds + nb, d_order + launched, mm,
@@ -210,11 +299,32 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         last_chunk_at = ms_since(t0);
     }
     if (copier.joinable()) copier.join();
+    {
+        std::lock_guard<std::mutex> g(hmu);
+        hdone = true;
+    }
+    hcv.notify_all();
+    std::vector<uint8_t> gdig;
     if (rc == PBS_OK && ok) {
         for (auto& s : s_dig) hip_ok(hipStreamSynchronize(s));
-        if (rc == PBS_OK && n) hip_ok(hipMemcpy(digests, d_dig, n * 32, hipMemcpyDeviceToHost));
+        if (rc == PBS_OK && n) {
+            if (hpool.empty()) {
+                hip_ok(hipMemcpy(digests, d_dig, n * 32, hipMemcpyDeviceToHost));
+            } else {  // the GPU's digests, merged around the host's
+                gdig.resize(n * 32);
+                if (hip_ok(hipMemcpy(gdig.data(), d_dig, n * 32, hipMemcpyDeviceToHost))) {
+                    for (auto& th : hpool) th.join();
+                    hpool.clear();
+                    host_done_at = ms_since(t0);
+                    for (size_t i = 0; i < n; ++i)
+                        if (!hmask[i]) std::memcpy(digests + 32 * i, gdig.data() + 32 * i, 32);
+                }
+            }
+        }
         if (rc == PBS_OK && n && crcs) hip_ok(hipMemcpy(crcs, d_crc, n * 4, hipMemcpyDeviceToHost));
     }
+    for (auto& th : hpool) th.join();  // error paths
+    if (!host_done_at && host_chunks) host_done_at = ms_since(t0);
     const double total = ms_since(t0);
     if (timing) {
         timing->total_ms = total;
@@ -224,6 +334,10 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         timing->bytes = len;
         timing->chunks = n;
         timing->pieces = npieces;
+        timing->host_chunks = host_chunks;
+        timing->host_bytes = host_bytes;
+        timing->host_done_ms = host_done_at;
+        timing->host_threads = hthreads;
     }
     *n_out = n;
     for (auto& e : ev_copied)

@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     # include/pbs_digest.h (chunk digests, dynamic index)
     "pbs_digest_chunks_device", "pbs_digest_chunks_async", "pbs_sha256", "pbs_didx_size",
     "pbs_didx_build", "pbs_known_chunks_device", "pbs_pipeline_host", "pbs_chunker_set_cu_count",
+    "pbs_digest_chunks_hybrid", "pbs_digest_chunks_host", "pbs_sha256_host_uses_ni",
     # include/pbs_blob.h (blob CRC)
     "pbs_crc32_chunks_device", "pbs_crc32_chunks_async", "pbs_crc32", "pbs_blob_encode_uncompressed",
 )
@@ -85,6 +86,29 @@ class PipelineTiming(ctypes.Structure):
         ("total_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
         ("chunk_ms", ctypes.c_double), ("drain_ms", ctypes.c_double),
         ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64), ("pieces", ctypes.c_uint64),
+        ("host_chunks", ctypes.c_uint64), ("host_bytes", ctypes.c_uint64),
+        ("host_done_ms", ctypes.c_double), ("host_threads", ctypes.c_int),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class HybridOpts(ctypes.Structure):
+    _fields_ = [
+        ("host_threads", ctypes.c_int), ("host_min_len", ctypes.c_uint64),
+        ("host_mb_s", ctypes.c_double), ("gpu_mb_s", ctypes.c_double),
+    ]
+
+
+class HybridTiming(ctypes.Structure):
+    _fields_ = [
+        ("total_ms", ctypes.c_double), ("zero_ms", ctypes.c_double),
+        ("gpu_ms", ctypes.c_double), ("host_ms", ctypes.c_double),
+        ("gpu_chunks", ctypes.c_uint64), ("host_chunks", ctypes.c_uint64),
+        ("host_bytes", ctypes.c_uint64), ("zero_chunks", ctypes.c_uint64),
+        ("zero_lengths", ctypes.c_uint64), ("threshold", ctypes.c_uint64),
+        ("threads", ctypes.c_int),
     ]
 
     def as_dict(self) -> dict:
@@ -141,6 +165,10 @@ def lib():
         "pbs_pipeline_host": ([sz, p, sz, sz, p, sz, i, p, p, p, sz, ctypes.POINTER(sz),
                                ctypes.POINTER(PipelineTiming)], i),
         "pbs_chunker_set_cu_count": ([p, i], i),
+        "pbs_digest_chunks_hybrid": ([p, p, sz, u64, p, sz, p, sz, p, ctypes.POINTER(HybridOpts),
+                                      ctypes.POINTER(HybridTiming), p], i),
+        "pbs_digest_chunks_host": ([p, sz, u64, p, sz, p, sz, p, i], i),
+        "pbs_sha256_host_uses_ni": ([], i),
         "pbs_crc32_chunks_device": ([p, sz, u64, p, sz, p, p], i),
         "pbs_crc32_chunks_async": ([p, sz, u64, p, p, sz, p, p], i),
         "pbs_crc32": ([ctypes.c_uint32, p, sz], ctypes.c_uint32),
@@ -479,6 +507,57 @@ def digest_chunks_device(dev_ptr: int, data_len: int, bounds, base: int = 0, key
     if rc != PBS_OK:
         raise ChunkerError(rc, "pbs_digest_chunks_device")
     return out
+
+
+def digest_chunks_hybrid(dev_ptr: int, data_len: int, bounds, base: int = 0, key=None,
+                         host=None, threads: int = 0, host_min_len: int = 0,
+                         host_mb_s: float = 0.0, gpu_mb_s: float = 0.0, hip_stream: int = 0):
+    """pbs_digest_chunks_hybrid: the digests of digest_chunks_device with the longest
+    chunks hashed on ``threads`` host threads (SHA extensions) and all-zero long chunks
+    once per length; ``host`` (optional numpy uint8 array, the same bytes as the device
+    range) lets the host threads read them without a copy from HBM.  Returns ((n, 32)
+    digests, timing dict)."""
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.uint64))
+    n = max(0, b.size - 1)
+    out = np.empty((n, 32), dtype=np.uint8)
+    t = HybridTiming()
+    if n == 0:
+        return out, t.as_dict()
+    kb, kl = _key_arg(key)
+    hp = None
+    if host is not None:
+        h = _as_u8(host)
+        if h.size < data_len:
+            raise ValueError("host copy shorter than data_len")
+        hp = _ptr(h)
+    o = HybridOpts(threads, host_min_len, host_mb_s, gpu_mb_s)
+    rc = lib().pbs_digest_chunks_hybrid(ctypes.c_void_p(dev_ptr), hp, data_len, base, b.ctypes.data, n,
+                                        kb, kl, out.ctypes.data, ctypes.byref(o), ctypes.byref(t),
+                                        ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_digest_chunks_hybrid")
+    return out, t.as_dict()
+
+
+def digest_chunks_host(data, bounds, base: int = 0, key=None, threads: int = 0) -> np.ndarray:
+    """SHA-256(chunk || key) of every chunk of a host buffer on host threads (the C
+    library's SHA-extension code); (n, 32) uint8 digests."""
+    a = _as_u8(data)
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.uint64))
+    n = max(0, b.size - 1)
+    out = np.empty((n, 32), dtype=np.uint8)
+    if n == 0:
+        return out
+    kb, kl = _key_arg(key)
+    rc = lib().pbs_digest_chunks_host(_ptr(a), a.size, base, b.ctypes.data, n, kb, kl, out.ctypes.data,
+                                      threads)
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_digest_chunks_host")
+    return out
+
+
+def sha256_host_uses_ni() -> bool:
+    return bool(lib().pbs_sha256_host_uses_ni())
 
 
 def digest_chunks_async(dev_ptr: int, data_len: int, bounds_dev: int, order_dev: int, n: int,

@@ -89,3 +89,58 @@ def test_reference_digest_vectors_pin_the_oracle(pbschunk):
     assert hashlib.sha256(data + key).hexdigest() == v["digest_enc"]
     assert pbschunk.sha256(data).hex() == v["digest_plain"]
     assert pbschunk.sha256(data + key).hex() == v["digest_enc"]
+
+
+def _host_digest_cases():
+    """Chunk lengths around the padding boundaries, beside a few long ones, in one buffer."""
+    rng = np.random.default_rng(11)
+    lens = list(range(0, 130)) + [191, 192, 193, 4095, 4096, 4097, (4 << 20) + 17, (1 << 20) * 9 - 3]
+    rng.shuffle(lens)
+    bounds = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = rng.integers(0, 256, int(bounds[-1]), dtype=np.uint8)
+    return data, bounds
+
+
+@pytest.mark.parametrize("klen", [0, 1, 32, 55, 56, 64])
+def test_host_chunk_digests(pbschunk, oracle, klen):
+    """pbs_digest_chunks_host (the hybrid digest's host share) against the oracle:
+    every padding boundary, keys that push the padding into a third block, 4 threads."""
+    data, bounds = _host_digest_cases()
+    key = bytes((200 + j) % 256 for j in range(klen)) if klen else None
+    got = pbschunk.digest_chunks_host(data, bounds, key=key, threads=4)
+    assert np.array_equal(got, oracle.chunk_digests(data, bounds, key or b""))
+
+
+def test_host_chunk_digests_base_and_range(pbschunk, oracle):
+    data, bounds = _host_digest_cases()
+    base = 1000
+    sub = data[base:]
+    b = bounds[bounds >= base]
+    got = pbschunk.digest_chunks_host(sub, b, base=base, threads=2)
+    assert np.array_equal(got, oracle.chunk_digests(data, b))
+    with pytest.raises(pbschunk.ChunkerError):
+        pbschunk.digest_chunks_host(sub, np.array([base - 1, base + 5], dtype=np.uint64), base=base)
+
+
+def test_host_sha_portable_block_function(tmp_path):
+    """The portable FIPS 180-4 block function (used when the CPU lacks the SHA
+    extensions) gives the same digests; run in a child with PBS_SHA_HOST_PORTABLE=1."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys, hashlib, numpy as np; sys.path[:0] = ['proxmox-backup_amd', 'tests'];"
+        "import pbschunk; assert not pbschunk.sha256_host_uses_ni();"
+        "rng = np.random.default_rng(3); lens = list(range(0, 140)) + [100000];"
+        "b = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64);"
+        "d = rng.integers(0, 256, int(b[-1]), dtype=np.uint8);"
+        "g = pbschunk.digest_chunks_host(d, b, key=b'k' * 40, threads=3);"
+        "mv = memoryview(d);"
+        "assert all(g[i].tobytes() == hashlib.sha256(mv[int(b[i]):int(b[i+1])].tobytes() + b'k' * 40).digest()"
+        " for i in range(len(lens)))"
+    )
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PBS_SHA_HOST_PORTABLE="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -167,14 +167,21 @@ def test_known_chunks(gpu, oracle, torch_dev, n, k, clash):
     assert np.array_equal(got, ref) and cnt == int(ref.sum())
 
 
-@pytest.mark.parametrize("kind,avg,piece,key", [
-    ("vmimage", 1 << 20, 8 << 20, None),          # chunks shorter than a piece
-    ("vmimage", 4 << 20, 5 << 20 | 3, b"k" * 32),  # 16 MiB chunks spanning pieces, keyed
-    ("random", 64 << 10, 1 << 20, None),           # many chunks per piece
+@pytest.mark.parametrize("kind,avg,piece,key,host_min", [
+    ("vmimage", 1 << 20, 8 << 20, None, None),          # chunks shorter than a piece
+    ("vmimage", 4 << 20, 5 << 20 | 3, b"k" * 32, None),  # 16 MiB chunks spanning pieces, keyed
+    ("random", 64 << 10, 1 << 20, None, None),           # many chunks per piece
+    ("vmimage", 4 << 20, 8 << 20, b"k" * 32, "0"),       # GPU digests only
+    ("vmimage", 1 << 20, 4 << 20, None, "1"),            # host digests only (GPU: the CRCs)
+    ("vmimage", 256 << 10, 3 << 20, b"k" * 5, "262144"),  # split at the average
 ])
-def test_pipeline_host(gpu, oracle, kind, avg, piece, key):
+def test_pipeline_host(gpu, oracle, monkeypatch, kind, avg, piece, key, host_min):
     """Overlapped copy -> chunk -> digest over a pageable host buffer (pbs_pipeline_host)
-    equals the oracle chunker + hashlib, with chunks straddling the copy pieces."""
+    equals the oracle chunker + hashlib, with chunks straddling the copy pieces, and the
+    digests split between the GPU and the host threads (PBS_PIPE_HOST_MIN) or all on one
+    side; all-zero chunks hashed once per length on the host."""
+    if host_min is not None:
+        monkeypatch.setenv("PBS_PIPE_HOST_MIN", host_min)
     n = 100 * MiB + 77
     data = gen_np.gen_vmimage(n, 0x5EED0003, 0) if kind == "vmimage" else gen_np.gen_random(n, 21)
     ends, dig, crcs, t = gpu.pipeline_host(data, avg, piece=piece, key=key, digest_cus=32, crc=True)
@@ -186,6 +193,10 @@ def test_pipeline_host(gpu, oracle, kind, avg, piece, key):
     assert np.array_equal(dig, oracle.chunk_digests(data, bounds, key or b""))
     assert np.array_equal(crcs, oracle.chunk_crcs(data, bounds))  # the blob CRCs
     assert t["chunks"] == ref.size and t["bytes"] == n
+    if host_min == "0":
+        assert t["host_chunks"] == 0
+    elif host_min == "1":
+        assert t["host_chunks"] == ref.size
     # without the CRC output: same cut list and digests
     ends2, dig2, _ = gpu.pipeline_host(data, avg, piece=piece, key=key, digest_cus=32)
     assert np.array_equal(ends2, ends) and np.array_equal(dig2, dig)
@@ -248,3 +259,63 @@ def test_reference_digest_vectors(gpu, torch_dev):
     for k, want in ((None, v["digest_plain"]), (key, v["digest_enc"])):
         dig = gpu.digest_chunks_device(ptr, stream.size, bounds, base=base, key=k)
         assert bytes(dig[1]).hex() == want
+
+
+def _hybrid_case():
+    """Chunks of 0..3 MiB random data, a few long ones (9 MiB - 3, 4 MiB + 17 bytes: more
+    than one 4 MiB D2H slice, not 64-byte multiples), all-zero chunks of two lengths
+    (3 x 2 MiB, 2 x (1 MiB + 5)) beside a non-zero 2 MiB chunk, a zero chunk under the
+    1 MiB zero-test floor and empty chunks."""
+    rng = np.random.default_rng(21)
+    segs = [("r", int(x)) for x in rng.integers(0, 3 * MiB, 24)]
+    segs += [("r", 9 * MiB - 3), ("r", 4 * MiB + 17), ("r", 2 * MiB), ("r", 0), ("r", 0)]
+    segs += [("z", 2 * MiB)] * 3 + [("z", MiB + 5)] * 2 + [("z", MiB - 1)]
+    order = rng.permutation(len(segs))
+    parts = []
+    for k, i in enumerate(order):
+        kind, n = segs[i]
+        parts.append(np.zeros(n, np.uint8) if kind == "z" else gen_np.gen_random(n, 1000 + k))
+    data = np.concatenate(parts)
+    bounds = np.concatenate([[0], np.cumsum([p.size for p in parts])]).astype(np.uint64)
+    return data, bounds
+
+
+@pytest.mark.parametrize("mode", ["auto", "host_from_hbm", "host_from_copy", "gpu_only", "one_thread"])
+@pytest.mark.parametrize("key", [None, bytes(range(32))])
+def test_hybrid_digest(gpu, oracle, torch_dev, mode, key):
+    """pbs_digest_chunks_hybrid against the oracle: the host share reading from HBM
+    (pinned 4 MiB slices) or from a host copy, the GPU share, and the all-zero long
+    chunks hashed once per length and copied to the rest."""
+    data, bounds = _hybrid_case()
+    t, ptr = _dev(torch_dev, data, 3)
+    kw = {"auto": dict(threads=4),
+          "host_from_hbm": dict(threads=4, host_min_len=1),
+          "host_from_copy": dict(threads=4, host_min_len=1, host=data),
+          "gpu_only": dict(threads=-1),
+          "one_thread": dict(threads=1, host_min_len=MiB)}[mode]
+    got, tm = gpu.digest_chunks_hybrid(ptr, data.size, bounds, key=key, **kw)
+    assert np.array_equal(got, oracle.chunk_digests(data, bounds, key or b""))
+    n = bounds.size - 1
+    if mode == "gpu_only":
+        assert tm["host_chunks"] == 0 and tm["gpu_chunks"] == n and tm["zero_chunks"] == 0
+    else:
+        assert tm["zero_chunks"] == 5 and tm["zero_lengths"] == 2
+        assert tm["host_chunks"] + tm["gpu_chunks"] == n - 3
+    if mode.startswith("host_from"):
+        assert tm["gpu_chunks"] == 2  # the empty chunks (length 0 < host_min_len)
+
+
+def test_hybrid_digest_vm_stream(gpu, oracle, torch_dev):
+    """Chunker -> hybrid digest on a 512 MiB VM-image stream at 4 MiB (forced 16 MiB
+    chunks of the zero extents, long data chunks) with the default cost model."""
+    n = 512 * MiB + 77
+    data = gen_np.gen_vmimage(n, 0x5EED0009, 0)
+    t, ptr = _dev(torch_dev, data)
+    with gpu.Chunker(4 * MiB) as c:
+        ends = c.find_cuts_device(ptr, n, is_final=True)
+    if ends.size == 0 or int(ends[-1]) != n:
+        ends = np.append(ends, np.uint64(n))
+    bounds = np.concatenate([[0], ends]).astype(np.uint64)
+    got, tm = gpu.digest_chunks_hybrid(ptr, n, bounds, threads=8)
+    assert np.array_equal(got, oracle.chunk_digests(data, bounds))
+    assert tm["host_chunks"] > 0 and tm["gpu_chunks"] > 0
