@@ -14,13 +14,14 @@
 //                   record: the hand-off of MI355X_MICROARCH.md "Inter-workgroup
 //                   visibility").  After the tiles, the bytes past the last tile ("tail
 //                   items", 64 blocks each) are evaluated the same way.
-//   resolver wave   wave 0 of workgroup 0 takes no tiles: it reads the tile records in
-//                   stream order, 64 at a time, and runs the reference's cut rule
-//                   sequentially over the candidates as they complete (pending candidates of
-//                   the open chunk first).  Cuts go to the device list and to mapped host
-//                   memory; at the end it writes the open chunk's start, its candidates and
-//                   the batch's last 63 bytes to the host.  It finishes a few microseconds
-//                   after the last tile, so the pass costs one launch and one host sync.
+//   resolver waves  waves 0..2 of workgroup 0 take no tiles: two helpers turn the tile
+//                   records, in stream order and 256 records per step, into per-candidate
+//                   chain data (below); the main wave walks the cut chain over them, with
+//                   the pending candidates of the open chunk first.  Cuts go to mapped host
+//                   memory (the host copies them out while the pass runs); at the end the
+//                   main wave writes the open chunk's start, its candidates and the batch's
+//                   last 63 bytes to the host.  It finishes a few microseconds after the
+//                   last tile, so the pass costs one launch and one host sync.
 //
 // Stand-down: a tile with more than 64 flagged blocks, a full candidate list or more than
 // kFusedKeep open-chunk candidates (dense input) sets status 1 -- the host then runs the
@@ -145,20 +146,24 @@ __device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, u
 //
 //   helpers (2)  take the record steps (kResolveBatch records) round-robin: wait for the
 //                step's tiles, gather its candidates in stream order and, for every 64-
-//                candidate vector, compute per candidate the next cut inside the vector if
-//                a cut were taken there (nx: lane, or itself when the chain leaves the
-//                vector), the forced cuts in between (nf) and the state after them (sk) --
-//                lane-parallel, independent of everything before the vector.  The step's
-//                {c, nx, nf, sk} go to a scratch area, then the step record is published.
-//   main (1)     takes the steps in order and walks the chain: the vector's first cut from
-//                the incoming state (one ballot; forced cuts in closed form), then nx from
-//                cut to cut (a few scalar instructions per cut), the cuts written with one
-//                vector store, the candidates past the chain's last cut kept for the open
-//                chunk.  Pending candidates of earlier calls come first (walked directly).
+//                candidate vector, compute per candidate lane-parallel (independent of
+//                everything before the vector): the next cut inside the vector if a cut
+//                were taken there (or "leaves the vector"), the forced cuts in between (nf)
+//                and the state after them (sk); then by pointer doubling (6 rounds of
+//                shuffles) the chain mask pm = the lanes cut on the chain from this lane
+//                until it leaves the vector, and xl = the lane where it leaves.  The step's
+//                {c, sk, pm, nf, xl} go to a scratch area, then the step record is
+//                published (workgroup scope: helpers and main share the CU).
+//   main (1)     takes the steps in order: per vector, the first cut from the incoming
+//                state (one ballot; forced cuts in closed form), then the whole chain from
+//                pm / xl of that lane in O(1) -- the cuts (and each cut's nf forced cuts)
+//                written with vector stores, the candidates past the chain kept for the
+//                open chunk.  Pending candidates of earlier calls come first (walked cut by
+//                cut).
 //
-// One wave's serial walk costs ~35 instructions per cut at the 4-cycle issue cadence of a
-// wave; with the successors precomputed it is ~6, so the main wave keeps up with 256 KiB
-// averages (190 k cuts in a 64 GiB pass) and finishes a few microseconds after the last tile.
+// One wave's serial walk cost ~35 instructions per cut at the ~4-cycle issue cadence of a
+// wave; with the chain masks it is a few instructions per 64 candidates, so the main wave
+// keeps up with 128 KiB averages and finishes a few microseconds after the last tile.
 struct FusedStep {  // one resolver step, in scratch (stream order)
     uint64_t* c;   // candidate
     uint64_t* sk;  // state after a cut here and its forced cuts, if the chain leaves here
