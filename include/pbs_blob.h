@@ -51,6 +51,38 @@ uint32_t pbs_crc32(uint32_t crc, const uint8_t *data, size_t len);
 size_t pbs_blob_encode_uncompressed(const uint8_t *data, size_t len, uint32_t crc, uint8_t *out,
                                     size_t cap);
 
+/* DataBlob images of every chunk on the GPU (`DataBlob::encode(data, None, compress)`,
+ * data_blob.rs:87-176, unencrypted path).  compress != 0: each chunk is compressed into a
+ * zstd frame (independent 128 KiB blocks: RLE, compressed with raw literals and the
+ * predefined FSE tables, or raw; decodable by any zstd decoder, the reference's
+ * `zstd::stream::decode_all` :214 included -- but not byte-identical to libzstd level 1,
+ * which is what the reference writes: "parity unpinned"); the blob
+ * is {COMPRESSED_BLOB_MAGIC_1_0, CRC, frame} when the frame is shorter than the chunk
+ * (:153), else {UNCOMPRESSED_BLOB_MAGIC_1_0, CRC, chunk}.  compress == 0: every blob
+ * uncompressed.  CRC = crc32fast over the payload (compute_crc, :70-75).
+ * `dev_data` (device) holds stream bytes [base, base + data_len); `bounds` (host, n + 1
+ * ascending absolute offsets; every chunk <= 128 MiB, MAX_BLOB_SIZE :13/:92).  The blobs
+ * are written back to back into `blobs_dev` (device, blobs_cap >= pbs_blob_stream_bound);
+ * blob i is [blob_offsets[i], blob_offsets[i+1]) (host, n + 1); `crcs` (host, n) and
+ * `compressed` (host, n: 1 = zstd) may be NULL.  Needs ~ (bytes of the chunks) of device
+ * scratch, kept for the process.  Synchronous.  C ABI of include/pbs_chunker.h's codes. */
+typedef struct {
+    double total_ms;    /* call entry .. outputs on the host */
+    double compress_ms; /* block compression + frame sizes + offset scans (HIP events) */
+    double assemble_ms; /* blocks / chunk bytes into the blob images */
+    double crc_ms;      /* payload CRCs + headers */
+    uint64_t bytes_in, bytes_out, blocks, compressed_chunks;
+} pbs_blob_encode_timing;
+int pbs_blob_encode_chunks_device(const uint8_t *dev_data, size_t data_len, uint64_t base,
+                                  const uint64_t *bounds, size_t n, int compress, uint8_t *blobs_dev,
+                                  size_t blobs_cap, uint64_t *blob_offsets, uint32_t *crcs,
+                                  uint8_t *compressed, pbs_blob_encode_timing *timing,
+                                  void *hip_stream);
+/* 12 n + (bounds[n] - bounds[0]): the largest blob stream of n chunks. */
+size_t pbs_blob_stream_bound(const uint64_t *bounds, size_t n);
+/* Largest zstd frame this encoder writes for `len` bytes (header + raw blocks). */
+size_t pbs_zstd_frame_bound(size_t len);
+
 #ifdef __cplusplus
 }
 #endif

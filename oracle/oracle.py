@@ -213,3 +213,82 @@ def blob_uncompressed(chunk: bytes) -> bytes:
     import zlib
 
     return UNCOMPRESSED_BLOB_MAGIC + struct.pack("<I", zlib.crc32(chunk)) + bytes(chunk)
+
+
+# ---- zstd-1 blobs (data_blob.rs:139-176): parity of the compressed bytes is UNPINNED ----
+# The reference's compressor is libzstd level 1 (zstd crate 0.12 -> libzstd 1.5.x), not in
+# this image.  What is checked: (1) the GPU's frames equal the host twin's
+# (oracle/zstd_twin.cpp, the same parse written as loops); (2) the image's libzstd.so.1
+# (1.4.8, through ctypes) decodes every frame back to the chunk; (3) the blob rules below.
+COMPRESSED_BLOB_MAGIC = bytes([49, 185, 88, 66, 111, 182, 163, 127])  # file_formats.rs:12
+_twin = None
+_zstd = None
+
+
+def _twin_lib():
+    global _twin
+    if _twin is None:
+        path = os.path.join(_HERE, "build", "libzstd_twin.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.zstd_twin_bound.restype = ctypes.c_uint64
+        L.zstd_twin_bound.argtypes = [ctypes.c_uint64]
+        L.zstd_twin_frame.restype = ctypes.c_uint64
+        L.zstd_twin_frame.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        _twin = L
+    return _twin
+
+
+def zstd_twin_frame(chunk) -> bytes:
+    """The frame the GPU encoder must write for `chunk` (host twin)."""
+    a = np.ascontiguousarray(np.frombuffer(bytes(chunk), dtype=np.uint8))
+    L = _twin_lib()
+    out = np.empty(int(L.zstd_twin_bound(a.size)) + 16, dtype=np.uint8)
+    n = L.zstd_twin_frame(a.ctypes.data if a.size else None, a.size, out.ctypes.data)
+    return out[:n].tobytes()
+
+
+def libzstd():
+    """The image's libzstd.so.1 (decoder of record for the frames; also the CPU
+    baseline's level-1 compressor)."""
+    global _zstd
+    if _zstd is None:
+        L = ctypes.CDLL("libzstd.so.1")
+        sz, p = ctypes.c_size_t, ctypes.c_void_p
+        L.ZSTD_decompress.restype = sz
+        L.ZSTD_decompress.argtypes = [p, sz, p, sz]
+        L.ZSTD_compress.restype = sz
+        L.ZSTD_compress.argtypes = [p, sz, p, sz, ctypes.c_int]
+        L.ZSTD_compressBound.restype = sz
+        L.ZSTD_compressBound.argtypes = [sz]
+        L.ZSTD_isError.restype = ctypes.c_uint
+        L.ZSTD_isError.argtypes = [sz]
+        L.ZSTD_getErrorName.restype = ctypes.c_char_p
+        L.ZSTD_getErrorName.argtypes = [sz]
+        L.ZSTD_versionNumber.restype = ctypes.c_uint
+        _zstd = L
+    return _zstd
+
+
+def zstd_decompress(frame: bytes, size: int) -> bytes:
+    L = libzstd()
+    src = np.frombuffer(bytes(frame), dtype=np.uint8)
+    dst = np.empty(max(size, 1), dtype=np.uint8)
+    r = L.ZSTD_decompress(dst.ctypes.data, dst.size, src.ctypes.data, src.size)
+    if L.ZSTD_isError(r):
+        raise ValueError(L.ZSTD_getErrorName(r).decode())
+    return dst[:r].tobytes()
+
+
+def blob_compressed(chunk: bytes) -> bytes:
+    """DataBlob::encode(chunk, None, true) with the twin's frame in place of libzstd's:
+    the compressed blob only if the frame is shorter than the chunk (:153), else the
+    uncompressed one; CRC over the payload."""
+    import struct
+    import zlib
+
+    frame = zstd_twin_frame(chunk)
+    if len(frame) < len(chunk):
+        return COMPRESSED_BLOB_MAGIC + struct.pack("<I", zlib.crc32(frame)) + frame
+    return blob_uncompressed(chunk)

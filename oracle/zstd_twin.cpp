@@ -1,0 +1,134 @@
+// TEST INFRASTRUCTURE ONLY (imported by tests/ and nothing in the product path).
+//
+// Host twin of the GPU zstd block encoder (proxmox-backup_amd/csrc/pbs_zstd.hip): the
+// same round-parallel greedy parse written as plain loops, through the same frame
+// writer primitives (csrc/zstd_enc.h), so the GPU's frames can be compared byte for byte
+// while libzstd (the image's libzstd.so.1, 1.4.8) checks that every frame decodes to the
+// chunk.  The reference's own compressor is libzstd level 1 (data_blob.rs:99, :151),
+// whose bytes cannot be reproduced here: parity of the compressed bytes is UNPINNED;
+// what is pinned is decode(frame) == chunk and the blob rules of data_blob.rs:139-176.
+//
+// Parse (per 128 KiB block, positions in rounds of kRound):
+//   1. every position p of the round with 4 bytes left looks up h = hash(p) in a table
+//      holding, per hash, 1 + the last position of an EARLIER round with that hash;
+//   2. then the round's positions are inserted (largest position wins);
+//   3. a candidate c matches if 4 bytes agree; its length is the common prefix, capped at
+//      kCap while matching (the parse extends a chosen capped match to its true end);
+//   4. greedy: from the current position, the first matching position starts a sequence
+//      {literals since the last match, length, offset p - c}; parsing resumes after it.
+#include <stdint.h>
+
+#include <cstring>
+#include <vector>
+
+#include "zstd_enc.h"
+
+namespace {
+
+using namespace pbs::zstd;
+
+constexpr uint32_t kRound = 256, kHashLog = 13, kCap = 32;
+
+inline uint32_t rd32(const uint8_t* p) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;
+}
+inline uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
+
+struct Tables {
+    FseCTable ll, ml, of;
+    Tables() {
+        build_ctable(ll, kLLNorm, 36, kLLLog);
+        build_ctable(ml, kMLNorm, 53, kMLLog);
+        build_ctable(of, kOFNorm, 29, kOFLog);
+    }
+};
+const Tables& tables() {
+    static Tables t;
+    return t;
+}
+
+// One block of n <= 128 KiB bytes at src; writes header + body at out, returns its size.
+size_t block(const uint8_t* src, uint32_t n, bool last, uint8_t* out) {
+    bool rle = n > 0;
+    for (uint32_t i = 1; i < n && rle; ++i) rle = src[i] == src[0];
+    if (rle) {
+        write_block_header(out, last, 1, n);
+        out[3] = src[0];
+        return 4;
+    }
+    std::vector<uint32_t> table(1u << kHashLog, 0), cand(kRound), mlen(kRound);
+    std::vector<Seq> seqs;
+    std::vector<uint8_t> lits;
+    uint32_t cur = 0, lit_start = 0;
+    for (uint32_t r0 = 0; r0 < n; r0 += kRound) {
+        const uint32_t r1 = r0 + kRound < n ? r0 + kRound : n;
+        for (uint32_t p = r0; p < r1; ++p) cand[p - r0] = p + 4 <= n ? table[hash4(rd32(src + p))] : 0;
+        for (uint32_t p = r0; p < r1 && p + 4 <= n; ++p) {
+            uint32_t& t = table[hash4(rd32(src + p))];
+            if (p + 1 > t) t = p + 1;
+        }
+        for (uint32_t p = r0; p < r1; ++p) {
+            uint32_t L = 0;
+            if (cand[p - r0]) {
+                const uint32_t c = cand[p - r0] - 1, lim = n - p < kCap ? n - p : kCap;
+                while (L < lim && src[c + L] == src[p + L]) ++L;
+            }
+            mlen[p - r0] = L >= 4 ? L : 0;
+        }
+        for (uint32_t p = r0 < cur ? cur : r0; p < r1; ++p) {
+            if (!mlen[p - r0]) continue;
+            const uint32_t c = cand[p - r0] - 1;
+            uint32_t L = mlen[p - r0];
+            if (L == kCap)
+                while (p + L < n && src[c + L] == src[p + L]) ++L;
+            seqs.push_back({p - lit_start, L, p - c});
+            lits.insert(lits.end(), src + lit_start, src + p);
+            cur = p + L;
+            lit_start = cur;
+            p = cur - 1;
+        }
+    }
+    lits.insert(lits.end(), src + lit_start, src + n);
+    std::vector<uint8_t> body(3 + (size_t)n + 64);
+    size_t o = 3;
+    o += write_raw_literals_header(body.data() + o, (uint32_t)lits.size());
+    if (!lits.empty()) std::memcpy(body.data() + o, lits.data(), lits.size());
+    o += lits.size();
+    const Tables& t = tables();
+    const size_t sq = o - 3 >= n ? SIZE_MAX
+                                 : write_sequences(body.data() + o, seqs.data(), (uint32_t)seqs.size(), t.ll,
+                                                   t.ml, t.of, body.data() + 3 + n);
+    if (sq == SIZE_MAX || o + sq - 3 >= n) {  // not shorter: raw block
+        write_block_header(out, last, 0, n);
+        std::memcpy(out + 3, src, n);
+        return 3 + (size_t)n;
+    }
+    o += sq;
+    write_block_header(body.data(), last, 2, (uint32_t)(o - 3));
+    std::memcpy(out, body.data(), o);
+    return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t zstd_twin_bound(uint64_t len) { return frame_bound(len); }
+
+// The frame of one chunk; returns its size (cap >= zstd_twin_bound(len)).
+uint64_t zstd_twin_frame(const uint8_t* src, uint64_t len, uint8_t* out) {
+    size_t o = write_frame_header(out, len);
+    if (len == 0) {
+        write_block_header(out + o, true, 0, 0);
+        return o + 3;
+    }
+    for (uint64_t b = 0; b < len; b += kBlockMax) {
+        const uint32_t n = (uint32_t)(len - b < kBlockMax ? len - b : kBlockMax);
+        o += block(src + b, n, b + n == len, out + o);
+    }
+    return o;
+}
+
+}  // extern "C"

@@ -188,7 +188,7 @@ __device__ __forceinline__ uint32_t row_step(const uint32_t* tf, uint32_t r, uin
 __global__ __launch_bounds__(kCrcThreads) void crc32_chunks_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint32_t* __restrict__ order, uint64_t n, const CrcTables* __restrict__ tab,
-    uint32_t* __restrict__ out, unsigned long long* __restrict__ next_ctr) {
+    uint32_t* __restrict__ out, unsigned long long* __restrict__ next_ctr, uint64_t skip) {
     __shared__ __attribute__((aligned(16))) uint32_t tf[16 * 256];
     __shared__ uint32_t tb[256];
     __shared__ uint32_t red[kCrcThreads / 64];
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_chunks_kernel(
             if (tid == 0) s_next = gridDim.x + atomicAdd(next_ctr, 1ull);
         }
         const uint64_t ci = order ? order[k] : k;
-        const uint64_t s = bounds[ci] - base, e = bounds[ci + 1] - base;
+        const uint64_t s = bounds[ci] - base + skip, e = bounds[ci + 1] - base;
         if (e - s < 4) {  // shorter than the init register: serially, one lane
             if (tid == 0) {
                 uint32_t r = 0xFFFFFFFFu;
@@ -280,6 +280,29 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_chunks_kernel(
 
 using namespace pbs;
 
+// Blob images [bounds[i], bounds[i+1]) with a `skip`-byte header: the CRC of each payload
+// (pbs_zstd.hip; static chunk order, the blobs are in stream order).
+hipError_t pbs::launch_crc32_skip(const uint8_t* data, const uint64_t* bounds_dev, uint64_t n, uint64_t skip,
+                                  uint32_t* out, hipStream_t st) {
+    int dev = 0, ncu = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return hipErrorInvalidDevice;
+    const CrcTables* tab = device_tables(dev);
+    if (!tab) return hipErrorOutOfMemory;
+    const unsigned grid = (unsigned)std::min<uint64_t>(n, (uint64_t)ncu * kCrcGroupsPerCu);
+    unsigned long long* ctr = nullptr;
+    if (n > grid) {
+        ctr = stream_counter(st, dev);
+        if (!ctr) return hipErrorOutOfMemory;
+        const hipError_t e = hipMemsetAsync(ctr, 0, sizeof(unsigned long long), st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(crc32_chunks_kernel, dim3(grid), dim3(kCrcThreads), 0, st, data, (uint64_t)0, bounds_dev,
+                       (const uint32_t*)nullptr, n, tab, out, ctr, skip);
+    return hipGetLastError();
+}
+
 extern "C" int pbs_crc32_chunks_async(const uint8_t* dev_data, size_t data_len, uint64_t base,
                                       const uint64_t* bounds_dev, const uint32_t* order_dev, size_t n,
                                       uint32_t* crcs_dev, void* hip_stream) {
@@ -304,7 +327,7 @@ extern "C" int pbs_crc32_chunks_async(const uint8_t* dev_data, size_t data_len, 
         if (hipMemsetAsync(ctr, 0, sizeof(unsigned long long), st) != hipSuccess) return PBS_ERR_HIP;
     }
     hipLaunchKernelGGL(crc32_chunks_kernel, dim3(grid), dim3(kCrcThreads), 0, (hipStream_t)hip_stream,
-                       dev_data, base, bounds_dev, order_dev, (uint64_t)n, tab, crcs_dev, ctr);
+                       dev_data, base, bounds_dev, order_dev, (uint64_t)n, tab, crcs_dev, ctr, (uint64_t)0);
     return hipGetLastError() == hipSuccess ? PBS_OK : PBS_ERR_HIP;
 }
 

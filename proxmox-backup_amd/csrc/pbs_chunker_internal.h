@@ -105,6 +105,9 @@ hipError_t sort_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* 
                     int end_bit, hipStream_t stream);
 hipError_t exclusive_sum_u64(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
                              uint32_t n, hipStream_t stream);
+// pbs_blob.hip: CRC-32 of blob payloads [bounds[i] + skip, bounds[i+1]) of `data`
+hipError_t launch_crc32_skip(const uint8_t* data, const uint64_t* bounds_dev, uint64_t n, uint64_t skip,
+                             uint32_t* out, hipStream_t st);
 hipError_t inclusive_max_u32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint32_t* out,
                              uint64_t n, hipStream_t stream);
 hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p, uint32_t* nxt,

@@ -1,0 +1,477 @@
+// Compressed DataBlob images of every chunk on the GPU (second
+// half): `DataBlob::encode(data, None, compress = true)` (pbs-datastore/src/data_blob.rs:
+// 139-176) -- a zstd frame of the chunk (`zstd::stream::copy_encode(data, .., 1)`, :151)
+// behind the 12-byte header {COMPRESSED_BLOB_MAGIC_1_0, CRC} when it is shorter than the
+// chunk, else the uncompressed blob {UNCOMPRESSED_BLOB_MAGIC_1_0, CRC, bytes}; the CRC
+// (`compute_crc`, :70-75) covers everything after the header.  C ABI: include/pbs_blob.h.
+//
+// The frame (zstd_enc.h) is built from independent 128 KiB zstd blocks, one workgroup per
+// block (a 64 GiB stream is 512 k blocks, so the chip is full):
+//   1. RLE test (every byte equal: a 4-byte RLE block -- the zero pages of a VM image);
+//   2. match finding in rounds of 256 positions, one per thread: hash of the 4 bytes at
+//      p -> candidate = the last position of an earlier round with that hash (LDS table,
+//      8 K entries, `atomicMax` inserts after the lookups), common prefix capped at 32;
+//   3. greedy parse by wave 0 over the round's 256-bit match mask (one ballot per wave):
+//      from the current position the next matching position starts a sequence, a capped
+//      match is extended 64 bytes per step (ballot of mismatches);
+//   4. wave 0 lane 0 writes the FSE-coded sequences (predefined tables) while waves 1-3
+//      copy the literal runs; raw block if that is not shorter.
+// Then per chunk: frame size, compressed-or-not (the reference's "only if shorter",
+// :153), blob offsets by an exclusive scan, the blocks gathered into the blob images,
+// and the blob CRC by the CRC kernel of pbs_blob.hip (12-byte header skipped).
+//
+// The parse is the host twin's (oracle/zstd_twin.cpp) step for step, so the bytes are
+// compared exactly; libzstd decodes every frame back to the chunk (tests).  The bytes are
+// not libzstd's level 1 (parity unpinned).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "pbs_blob.h"
+#include "pbs_chunker.h"
+#include "pbs_chunker_internal.h"
+#include "zstd_enc.h"
+
+namespace pbs {
+namespace {
+
+using namespace zstd;
+
+constexpr int kZThreads = 256;
+constexpr uint32_t kZRound = 256, kZHashLog = 13, kZCap = 32;
+constexpr uint64_t kSlot = 131200;  // block header + up to 128 KiB + slack for 8-byte flushes
+constexpr uint32_t kMaxSeq = kBlockMax / 4;
+constexpr int kZGroupsPerCu = 4;
+
+// pbs-datastore/src/file_formats.rs:9, :12
+constexpr uint8_t kUncompressedMagic[8] = {66, 171, 56, 7, 190, 131, 112, 161};
+constexpr uint8_t kCompressedMagic[8] = {49, 185, 88, 66, 111, 182, 163, 127};
+
+struct ZTables {
+    FseCTable ll, ml, of;
+};
+
+__device__ __forceinline__ uint32_t rd32(const uint8_t* p) {
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+__global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
+    const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
+    const uint64_t* __restrict__ items, uint64_t nitems, const ZTables* __restrict__ zt,
+    uint8_t* __restrict__ slots, uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch,
+    uint2* __restrict__ run_scratch) {
+    __shared__ uint32_t table[1u << kZHashLog];
+    __shared__ uint32_t s_ml[kZRound], s_c[kZRound];
+    __shared__ unsigned long long s_mask[kZThreads / 64];
+    __shared__ ZTables s_zt;
+    __shared__ uint32_t s_u[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t i = tid; i < sizeof(ZTables) / 4; i += kZThreads)
+        reinterpret_cast<uint32_t*>(&s_zt)[i] = reinterpret_cast<const uint32_t*>(zt)[i];
+    Seq* const seqs = seq_scratch + (uint64_t)blockIdx.x * kMaxSeq;
+    uint2* const runs = run_scratch + (uint64_t)blockIdx.x * kMaxSeq;
+
+    for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
+        __syncthreads();  // LDS of the previous item
+        const uint64_t it = items[k];
+        const uint64_t ci = it >> 32, j = (uint32_t)it;
+        const uint64_t len = bounds[ci + 1] - bounds[ci], off = j * (uint64_t)kBlockMax;
+        const uint32_t n = (uint32_t)(len > off ? (len - off < kBlockMax ? len - off : kBlockMax) : 0);
+        const bool last = off + n == len;
+        const uint8_t* const src = data + (bounds[ci] - base) + off;
+        uint8_t* const out = slots + k * kSlot;
+        if (n == 0) {  // the empty chunk's frame: one empty raw block
+            if (tid == 0) {
+                write_block_header(out, true, 0, 0);
+                sizes[k] = 3;
+            }
+            continue;
+        }
+        const uint8_t b0 = src[0];
+        int same = 1;
+        for (uint32_t i = tid; i < n; i += kZThreads) same &= src[i] == b0;
+        if (__syncthreads_and(same)) {
+            if (tid == 0) {
+                write_block_header(out, last, 1, n);
+                out[3] = b0;
+                sizes[k] = 4;
+            }
+            continue;
+        }
+        for (uint32_t i = tid; i < (1u << kZHashLog); i += kZThreads) table[i] = 0;
+        __syncthreads();
+        uint32_t cur = 0, lit_start = 0, ns = 0, lit_out = 0;  // wave 0 (uniform)
+        for (uint32_t r0 = 0; r0 < n; r0 += kZRound) {
+            const uint32_t p = r0 + tid;
+            const bool has4 = p + 4 <= n;
+            uint32_t h = 0, c1 = 0;
+            if (has4) {
+                h = (rd32(src + p) * 2654435761u) >> (32 - kZHashLog);
+                c1 = table[h];
+            }
+            __syncthreads();  // every lookup sees the table before this round's inserts
+            if (has4) atomicMax(&table[h], p + 1);
+            uint32_t L = 0;
+            if (c1) {
+                const uint32_t c = c1 - 1, lim = n - p < kZCap ? n - p : kZCap;
+                while (L < lim && src[c + L] == src[p + L]) ++L;
+            }
+            if (L < 4) L = 0;
+            s_ml[tid] = L;
+            s_c[tid] = c1 - 1;
+            const unsigned long long m = __ballot(L != 0);
+            if (lane == 0) s_mask[wave] = m;
+            __syncthreads();
+            if (wave == 0) {  // greedy parse of the round, wave-uniform
+                uint32_t q = cur > r0 ? cur - r0 : 0;
+                while (q < kZRound) {
+                    uint32_t w = q >> 6;
+                    unsigned long long mm = s_mask[w] & (~0ull << (q & 63));
+                    while (!mm && ++w < kZThreads / 64) mm = s_mask[w];
+                    if (!mm) break;
+                    const uint32_t b = w * 64 + (uint32_t)__builtin_ctzll(mm);
+                    const uint32_t pp = r0 + b, c = s_c[b];
+                    uint32_t ml = s_ml[b];
+                    if (ml == kZCap) {  // extend a capped match, 64 bytes per step
+                        for (;;) {
+                            const uint32_t x = pp + ml + lane;
+                            const bool ok = x < n && src[c + ml + lane] == src[x];
+                            const unsigned long long bad = __ballot(!ok);
+                            if (bad) {
+                                ml += (uint32_t)__builtin_ctzll(bad);
+                                break;
+                            }
+                            ml += 64;
+                        }
+                    }
+                    if (lane == 0) {
+                        seqs[ns] = Seq{pp - lit_start, ml, pp - c};
+                        runs[ns] = make_uint2(lit_start, lit_out);
+                    }
+                    lit_out += pp - lit_start;
+                    ++ns;
+                    cur = pp + ml;
+                    lit_start = cur;
+                    q = cur - r0;
+                }
+            }
+            __syncthreads();  // s_ml / s_c / s_mask are rewritten by the next round
+        }
+        if (tid == 0) {
+            s_u[0] = ns;
+            s_u[1] = lit_out + (n - lit_start);
+            s_u[2] = lit_start;
+        }
+        __syncthreads();
+        ns = s_u[0];
+        const uint32_t nlit = s_u[1], tail_start = s_u[2];
+        const uint32_t lith = nlit < 32 ? 1 : nlit < 4096 ? 2 : 3;
+        const uint32_t seq_at = 3 + lith + nlit;
+        bool raw = seq_at - 3 >= n;
+        if (!raw) {
+            if (wave == 0) {
+                if (lane == 0) {
+                    const size_t sz = write_sequences(out + seq_at, seqs, ns, s_zt.ll, s_zt.ml, s_zt.of,
+                                                      out + 3 + n);
+                    s_u[3] = sz == SIZE_MAX ? 0xFFFFFFFFu : (uint32_t)sz;
+                }
+            } else {  // waves 1-3: the literal runs (run ns: the bytes after the last match)
+                uint8_t* const lo = out + 3 + lith;
+                for (uint32_t r = 0; r <= ns; ++r) {
+                    uint32_t from, to, cnt;
+                    if (r < ns) {
+                        const uint2 ru = runs[r];
+                        from = ru.x;
+                        to = ru.y;
+                        cnt = seqs[r].ll;
+                    } else {
+                        from = tail_start;
+                        cnt = n - tail_start;
+                        to = nlit - cnt;
+                    }
+                    for (uint32_t i = tid - 64; i < cnt; i += kZThreads - 64) lo[to + i] = src[from + i];
+                }
+            }
+            __syncthreads();
+            const uint32_t sz = s_u[3];
+            if (sz == 0xFFFFFFFFu || seq_at + sz - 3 >= n) {
+                raw = true;
+            } else if (tid == 0) {
+                write_block_header(out, last, 2, seq_at + sz - 3);
+                write_raw_literals_header(out + 3, nlit);
+                sizes[k] = seq_at + sz;
+            }
+        }
+        if (raw) {
+            for (uint32_t i = tid; i < n; i += kZThreads) out[3 + i] = src[i];
+            if (tid == 0) {
+                write_block_header(out, last, 0, n);
+                sizes[k] = 3 + (uint64_t)n;
+            }
+        }
+    }
+}
+
+// Per chunk: frame size, compressed-or-not, blob size.  fsz[n] = 0 (scan padding).
+__global__ void zstd_frame_sizes_kernel(const uint64_t* __restrict__ bounds, const uint64_t* __restrict__ first,
+                                        const uint64_t* __restrict__ sizes, uint64_t n, int compress,
+                                        uint64_t* __restrict__ bsz, uint8_t* __restrict__ comp) {
+    const uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ci > n) return;
+    if (ci == n) {
+        bsz[n] = 0;
+        return;
+    }
+    const uint64_t len = bounds[ci + 1] - bounds[ci];
+    bool c = false;
+    uint64_t fs = 0;
+    if (compress) {
+        fs = frame_header_size(len);
+        for (uint64_t k = first[ci]; k < first[ci + 1]; ++k) fs += sizes[k];
+        c = fs < len;  // data_blob.rs:153: only if shorter
+    }
+    comp[ci] = c ? 1 : 0;
+    bsz[ci] = 12 + (c ? fs : len);
+}
+
+// Per item: its part of the blob image.  Compressed chunk: the block (and, for the first
+// block, the magic and the frame header); otherwise the item's 128 KiB of chunk bytes.
+__global__ __launch_bounds__(kZThreads) void zstd_assemble_kernel(
+    const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
+    const uint64_t* __restrict__ items, uint64_t nitems, const uint64_t* __restrict__ first,
+    const uint8_t* __restrict__ slots, const uint64_t* __restrict__ sizes, const uint64_t* __restrict__ ipre,
+    const uint64_t* __restrict__ boff, const uint8_t* __restrict__ comp, uint8_t* __restrict__ blobs) {
+    for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
+        const uint64_t it = items[k];
+        const uint64_t ci = it >> 32, j = (uint32_t)it;
+        const uint64_t len = bounds[ci + 1] - bounds[ci];
+        uint8_t* const blob = blobs + boff[ci];
+        const bool c = comp[ci] != 0;
+        const uint32_t fh = frame_header_size(len);
+        if (j == 0 && threadIdx.x < 8) blob[threadIdx.x] = c ? kCompressedMagic[threadIdx.x] : kUncompressedMagic[threadIdx.x];
+        if (c) {
+            if (j == 0 && threadIdx.x == 0) write_frame_header(blob + 12, len);
+            uint8_t* const dst = blob + 12 + fh + (ipre[k] - ipre[first[ci]]);
+            const uint8_t* const sl = slots + k * kSlot;
+            const uint64_t sz = sizes[k];
+            for (uint64_t i = threadIdx.x; i < sz; i += kZThreads) dst[i] = sl[i];
+        } else {
+            const uint64_t off = j * (uint64_t)kBlockMax;
+            const uint64_t n = len > off ? (len - off < kBlockMax ? len - off : kBlockMax) : 0;
+            const uint8_t* const src = data + (bounds[ci] - base) + off;
+            uint8_t* const dst = blob + 12 + off;
+            for (uint64_t i = threadIdx.x; i < n; i += kZThreads) dst[i] = src[i];
+        }
+    }
+}
+
+__global__ void blob_crc_header_kernel(const uint64_t* __restrict__ boff, const uint32_t* __restrict__ crc,
+                                       uint64_t n, uint8_t* __restrict__ blobs) {
+    const uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ci >= n) return;
+    uint8_t* const h = blobs + boff[ci] + 8;
+    const uint32_t v = crc[ci];
+    h[0] = (uint8_t)v;
+    h[1] = (uint8_t)(v >> 8);
+    h[2] = (uint8_t)(v >> 16);
+    h[3] = (uint8_t)(v >> 24);
+}
+
+// Per-device scratch kept for the process: the block slots (~ the input size), the
+// sequence lists of the resident workgroups and the FSE tables.
+struct ZScratch {
+    std::mutex mu;
+    int dev = -1;
+    uint8_t* slots = nullptr;
+    size_t slots_cap = 0;
+    Seq* seqs = nullptr;
+    uint2* runs = nullptr;
+    size_t groups = 0;
+    ZTables* zt = nullptr;
+};
+ZScratch& zscratch() {
+    static ZScratch* z = new ZScratch;  // never destroyed (HIP may be torn down first at exit)
+    return *z;
+}
+
+template <typename T>
+bool grow(T** p, size_t* cap, size_t need) {
+    if (*cap >= need) return true;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, need * sizeof(T)) != hipSuccess) return false;
+    *cap = need;
+    return true;
+}
+
+}  // namespace
+}  // namespace pbs
+
+using namespace pbs;
+
+extern "C" size_t pbs_zstd_frame_bound(size_t len) { return (size_t)zstd::frame_bound(len); }
+
+extern "C" size_t pbs_blob_stream_bound(const uint64_t* bounds, size_t n) {
+    if (!bounds || n == 0) return 0;
+    return 12 * n + (size_t)(bounds[n] - bounds[0]);
+}
+
+extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t data_len, uint64_t base,
+                                             const uint64_t* bounds, size_t n, int compress, uint8_t* blobs_dev,
+                                             size_t blobs_cap, uint64_t* blob_offsets, uint32_t* crcs,
+                                             uint8_t* compressed, pbs_blob_encode_timing* timing,
+                                             void* hip_stream) {
+    using Clock = std::chrono::steady_clock;
+    const Clock::time_point t0 = Clock::now();
+    if (timing) std::memset(timing, 0, sizeof(*timing));
+    if (!blob_offsets) return PBS_ERR_INVALID;
+    blob_offsets[0] = 0;
+    if (n == 0) return PBS_OK;
+    if (!bounds || !blobs_dev || (data_len && !dev_data) || n >= 0xFFFFFFFFull) return PBS_ERR_INVALID;
+    for (size_t i = 0; i < n; ++i)
+        if (bounds[i] > bounds[i + 1] || bounds[i] < base || bounds[i + 1] - base > data_len)
+            return PBS_ERR_INVALID;
+    // the reference refuses blobs over MAX_BLOB_SIZE (data_blob.rs:92, 128 MiB, :13)
+    for (size_t i = 0; i < n; ++i)
+        if (bounds[i + 1] - bounds[i] > (128ull << 20)) return PBS_ERR_INVALID;
+    hipStream_t st = (hipStream_t)hip_stream;
+    int dev = 0, ncu = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return PBS_ERR_NO_DEVICE;
+
+    // items: (chunk, 128 KiB block) pairs; an empty chunk is one item
+    std::vector<uint64_t> items, first(n + 1);
+    for (size_t i = 0; i < n; ++i) {
+        first[i] = items.size();
+        const uint64_t len = bounds[i + 1] - bounds[i];
+        const uint64_t nb = len ? (len + zstd::kBlockMax - 1) / zstd::kBlockMax : 1;
+        for (uint64_t j = 0; j < nb; ++j) items.push_back((uint64_t)i << 32 | j);
+    }
+    first[n] = items.size();
+    const uint64_t ni = items.size();
+
+    uint64_t *d_bounds = nullptr, *d_items = nullptr, *d_first = nullptr, *d_sizes = nullptr, *d_ipre = nullptr,
+             *d_bsz = nullptr, *d_boff = nullptr;
+    uint8_t* d_comp = nullptr;
+    uint32_t* d_crc = nullptr;
+    void* d_tmp = nullptr;
+    hipEvent_t ev[4] = {};
+    int rc = PBS_OK;
+    auto fail = [&](int r) {
+        if (rc == PBS_OK) rc = r;
+        return false;
+    };
+    auto ok = [&](hipError_t e) { return e == hipSuccess || fail(PBS_ERR_HIP); };
+    size_t t1b = 0, t2b = 0;
+    (void)exclusive_sum_u64(nullptr, &t1b, nullptr, nullptr, (uint32_t)(n + 1), st);
+    (void)exclusive_sum_u64(nullptr, &t2b, nullptr, nullptr, (uint32_t)(ni + 1), st);
+    size_t tmpb = std::max(t1b, t2b);
+    if (hipMalloc(&d_bounds, (n + 1) * 8) != hipSuccess || hipMalloc(&d_items, ni * 8) != hipSuccess ||
+        hipMalloc(&d_first, (n + 1) * 8) != hipSuccess || hipMalloc(&d_sizes, (ni + 1) * 8) != hipSuccess ||
+        hipMalloc(&d_ipre, (ni + 1) * 8) != hipSuccess || hipMalloc(&d_bsz, (n + 1) * 8) != hipSuccess ||
+        hipMalloc(&d_boff, (n + 1) * 8) != hipSuccess || hipMalloc(&d_comp, n) != hipSuccess ||
+        hipMalloc(&d_crc, n * 4) != hipSuccess || hipMalloc(&d_tmp, std::max<size_t>(tmpb, 256)) != hipSuccess)
+        fail(PBS_ERR_NOMEM);
+    for (auto& e : ev)
+        if (rc == PBS_OK) ok(hipEventCreate(&e));
+    ZScratch& zs = zscratch();
+    std::lock_guard<std::mutex> lk(zs.mu);
+    const unsigned grid = (unsigned)std::min<uint64_t>(ni, (uint64_t)ncu * kZGroupsPerCu);
+    if (rc == PBS_OK && compress) {
+        if (zs.dev != dev) {  // first use on this device (or another device): fresh scratch
+            zs.slots = nullptr;
+            zs.slots_cap = 0;
+            zs.seqs = nullptr;
+            zs.runs = nullptr;
+            zs.groups = 0;
+            zs.zt = nullptr;
+            zs.dev = dev;
+        }
+        size_t seq_cap = zs.groups * kMaxSeq, run_cap = zs.groups * kMaxSeq;
+        if (!grow(&zs.slots, &zs.slots_cap, ni * kSlot) || !grow(&zs.seqs, &seq_cap, (size_t)grid * kMaxSeq) ||
+            !grow(&zs.runs, &run_cap, (size_t)grid * kMaxSeq)) {
+            fail(PBS_ERR_NOMEM);
+        } else {
+            zs.groups = std::max<size_t>(zs.groups, grid);
+        }
+        if (rc == PBS_OK && !zs.zt) {
+            ZTables h;
+            zstd::build_ctable(h.ll, zstd::kLLNorm, 36, zstd::kLLLog);
+            zstd::build_ctable(h.ml, zstd::kMLNorm, 53, zstd::kMLLog);
+            zstd::build_ctable(h.of, zstd::kOFNorm, 29, zstd::kOFLog);
+            if (hipMalloc(&zs.zt, sizeof(ZTables)) != hipSuccess ||
+                hipMemcpy(zs.zt, &h, sizeof(ZTables), hipMemcpyHostToDevice) != hipSuccess) {
+                zs.zt = nullptr;
+                fail(PBS_ERR_NOMEM);
+            }
+        }
+    }
+    if (rc == PBS_OK)
+        ok(hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st)) &&
+            ok(hipMemcpyAsync(d_items, items.data(), ni * 8, hipMemcpyHostToDevice, st)) &&
+            ok(hipMemcpyAsync(d_first, first.data(), (n + 1) * 8, hipMemcpyHostToDevice, st)) &&
+            ok(hipMemsetAsync(d_sizes, 0, (ni + 1) * 8, st));
+    if (rc == PBS_OK) {
+        (void)hipGetLastError();
+        ok(hipEventRecord(ev[0], st));
+        if (compress)
+            hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds,
+                               d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.runs);
+        hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
+                           d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
+        ok(hipGetLastError()) && ok(exclusive_sum_u64(d_tmp, &tmpb, d_bsz, d_boff,
+                                                      (uint32_t)(n + 1), st)) &&
+            (!compress ||
+             ok(exclusive_sum_u64(d_tmp, &tmpb, d_sizes, d_ipre, (uint32_t)(ni + 1), st))) &&
+            ok(hipEventRecord(ev[1], st)) &&
+            ok(hipMemcpyAsync(blob_offsets, d_boff, (n + 1) * 8, hipMemcpyDeviceToHost, st)) &&
+            ok(hipStreamSynchronize(st));
+    }
+    if (rc == PBS_OK && blob_offsets[n] > blobs_cap) fail(PBS_ERR_CAPACITY);
+    if (rc == PBS_OK) {
+        hipLaunchKernelGGL(zstd_assemble_kernel, dim3((unsigned)std::min<uint64_t>(ni, (uint64_t)ncu * 8)),
+                           dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items, ni, d_first, zs.slots,
+                           d_sizes, d_ipre, d_boff, d_comp, blobs_dev);
+        ok(hipGetLastError()) && ok(hipEventRecord(ev[2], st));
+    }
+    if (rc == PBS_OK) {
+        const hipError_t e = launch_crc32_skip(blobs_dev, d_boff, n, 12, d_crc, st);
+        if (e != hipSuccess) fail(e == hipErrorOutOfMemory ? PBS_ERR_NOMEM : PBS_ERR_HIP);
+    }
+    if (rc == PBS_OK) {
+        hipLaunchKernelGGL(blob_crc_header_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_boff,
+                           d_crc, (uint64_t)n, blobs_dev);
+        ok(hipGetLastError()) && ok(hipEventRecord(ev[3], st)) &&
+            (!crcs || ok(hipMemcpyAsync(crcs, d_crc, n * 4, hipMemcpyDeviceToHost, st))) &&
+            (!compressed || ok(hipMemcpyAsync(compressed, d_comp, n, hipMemcpyDeviceToHost, st))) &&
+            ok(hipStreamSynchronize(st));
+    }
+    if (rc == PBS_OK && timing) {
+        float a = 0, b = 0, c = 0;
+        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+        (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+        (void)hipEventElapsedTime(&c, ev[2], ev[3]);
+        timing->compress_ms = a;
+        timing->assemble_ms = b;
+        timing->crc_ms = c;
+        timing->bytes_in = bounds[n] - bounds[0];
+        timing->bytes_out = blob_offsets[n];
+        timing->blocks = ni;
+        if (compressed)
+            for (size_t i = 0; i < n; ++i) timing->compressed_chunks += compressed[i];
+    }
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    for (void* p : {(void*)d_bounds, (void*)d_items, (void*)d_first, (void*)d_sizes, (void*)d_ipre, (void*)d_bsz,
+                    (void*)d_boff, (void*)d_comp, (void*)d_crc, d_tmp})
+        if (p) (void)hipFree(p);
+    if (timing) timing->total_ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+    return rc;
+}

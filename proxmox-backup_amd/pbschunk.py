@@ -55,6 +55,7 @@ EXPORTED_SYMBOLS = (
     "pbs_digest_chunks_hybrid", "pbs_digest_chunks_host", "pbs_sha256_host_uses_ni",
     # include/pbs_blob.h (blob CRC)
     "pbs_crc32_chunks_device", "pbs_crc32_chunks_async", "pbs_crc32", "pbs_blob_encode_uncompressed",
+    "pbs_blob_encode_chunks_device", "pbs_blob_stream_bound", "pbs_zstd_frame_bound",
 )
 
 
@@ -88,6 +89,18 @@ class PipelineTiming(ctypes.Structure):
         ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64), ("pieces", ctypes.c_uint64),
         ("host_chunks", ctypes.c_uint64), ("host_bytes", ctypes.c_uint64),
         ("host_done_ms", ctypes.c_double), ("host_threads", ctypes.c_int),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class BlobEncodeTiming(ctypes.Structure):
+    _fields_ = [
+        ("total_ms", ctypes.c_double), ("compress_ms", ctypes.c_double),
+        ("assemble_ms", ctypes.c_double), ("crc_ms", ctypes.c_double),
+        ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
+        ("blocks", ctypes.c_uint64), ("compressed_chunks", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -173,6 +186,10 @@ def lib():
         "pbs_crc32_chunks_async": ([p, sz, u64, p, p, sz, p, p], i),
         "pbs_crc32": ([ctypes.c_uint32, p, sz], ctypes.c_uint32),
         "pbs_blob_encode_uncompressed": ([p, sz, ctypes.c_uint32, p, sz], sz),
+        "pbs_blob_encode_chunks_device": ([p, sz, u64, p, sz, i, p, sz, p, p, p,
+                                           ctypes.POINTER(BlobEncodeTiming), p], i),
+        "pbs_blob_stream_bound": ([p, sz], sz),
+        "pbs_zstd_frame_bound": ([sz], sz),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -592,6 +609,31 @@ def crc32_chunks_device(dev_ptr: int, data_len: int, bounds, base: int = 0, hip_
     if rc != PBS_OK:
         raise ChunkerError(rc, "pbs_crc32_chunks_device")
     return out
+
+
+def blob_encode_chunks_device(dev_ptr: int, data_len: int, bounds, blobs_dev: int, blobs_cap: int,
+                              base: int = 0, compress: bool = True, hip_stream: int = 0):
+    """pbs_blob_encode_chunks_device: the DataBlob image of every chunk written back to
+    back at device address blobs_dev (data_blob.rs:87-176; zstd frames where shorter).
+    Returns (offsets (n + 1), crcs (n), compressed flags (n), timing dict)."""
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.uint64))
+    n = max(0, b.size - 1)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    crcs = np.empty(n, dtype=np.uint32)
+    comp = np.empty(n, dtype=np.uint8)
+    t = BlobEncodeTiming()
+    rc = lib().pbs_blob_encode_chunks_device(ctypes.c_void_p(dev_ptr), data_len, base, b.ctypes.data, n,
+                                             1 if compress else 0, ctypes.c_void_p(blobs_dev), blobs_cap,
+                                             offs.ctypes.data, crcs.ctypes.data, comp.ctypes.data,
+                                             ctypes.byref(t), ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_blob_encode_chunks_device")
+    return offs, crcs, comp, t.as_dict()
+
+
+def blob_stream_bound(bounds) -> int:
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.uint64))
+    return int(lib().pbs_blob_stream_bound(b.ctypes.data, max(0, b.size - 1)))
 
 
 def crc32_chunks_async(dev_ptr: int, data_len: int, bounds_dev: int, order_dev: int, n: int, crcs_dev: int,

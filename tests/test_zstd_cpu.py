@@ -1,0 +1,73 @@
+"""CPU checks of the zstd-1 blob stage's format writer (csrc/zstd_enc.h) through its host
+twin (oracle/zstd_twin.cpp, the GPU parse written as loops): every frame decodes with the
+image's libzstd (1.4.8) back to the input, across block boundaries, RLE, raw and
+compressed blocks, and the blob rules of data_blob.rs:139-176.
+
+Parity of the compressed BYTES with the reference is unpinned: the reference writes
+libzstd 1.5.x level-1 frames (data_blob.rs:151), which no encoder here reproduces; the
+reference only ever decodes them with `zstd::stream::decode_all` (:214), so a frame that
+decodes to the chunk is a valid drop-in."""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import gen_np
+
+KiB, MiB = 1024, 1024 * 1024
+
+
+def _inputs():
+    rng = np.random.default_rng(5)
+    text = np.frombuffer(b"proxmox backup chunk store " * 5000, dtype=np.uint8)
+    yield "empty", np.zeros(0, np.uint8)
+    for n in (1, 2, 3, 4, 5, 31, 32, 33, 63, 64, 255, 256, 257, 4095, 4096, 65791, 65792):
+        yield f"random_{n}", rng.integers(0, 256, n, dtype=np.uint8)
+    yield "text", text
+    yield "zeros_128K", np.zeros(128 * KiB, np.uint8)
+    yield "zeros_128K+1", np.zeros(128 * KiB + 1, np.uint8)
+    yield "ff_300K", np.full(300 * KiB, 0xFF, np.uint8)
+    yield "text_256K+5", np.resize(text, 256 * KiB + 5)
+    yield "random_300K", gen_np.gen_random(300 * KiB, 9)
+    yield "counter_1M", gen_np.gen_counter(MiB)
+    yield "vm_4M", gen_np.gen_vmimage(4 * MiB, 0x5EED0003, 0)
+    # periodic data whose matches run across block boundaries and to the block end
+    yield "period7_400K", np.resize(np.arange(7, dtype=np.uint8), 400 * KiB)
+    # random pages with short repeats (many sequences per block)
+    base = rng.integers(0, 256, 64, dtype=np.uint8)
+    yield "short_repeats_512K", np.concatenate([np.concatenate([base[:rng.integers(4, 60)],
+                                                                rng.integers(0, 256, 9, dtype=np.uint8)])
+                                                for _ in range(12000)])[: 512 * KiB]
+
+
+@pytest.mark.parametrize("name,data", list(_inputs()), ids=[n for n, _ in _inputs()])
+def test_twin_frames_decode_with_libzstd(oracle, name, data):
+    f = oracle.zstd_twin_frame(data.tobytes())
+    assert f[:4] == b"\x28\xb5\x2f\xfd"
+    assert oracle.zstd_decompress(f, data.size) == data.tobytes()
+    assert len(f) <= 13 + data.size + 3 * max(1, -(-data.size // (128 * KiB)))  # frame bound
+
+
+def test_blob_rules(oracle):
+    """data_blob.rs:139-176: compressed blob only if the frame is shorter; CRC over the
+    payload (compute_crc :70-75); header magic per file_formats.rs:9/:12."""
+    zeros = bytes(200 * KiB)
+    b = oracle.blob_compressed(zeros)
+    assert b[:8] == oracle.COMPRESSED_BLOB_MAGIC
+    assert struct.unpack("<I", b[8:12])[0] == zlib.crc32(b[12:])
+    assert oracle.zstd_decompress(b[12:], len(zeros)) == zeros
+    rnd = gen_np.gen_random(100 * KiB, 3).tobytes()  # incompressible: stays uncompressed
+    b = oracle.blob_compressed(rnd)
+    assert b == oracle.blob_uncompressed(rnd)
+
+
+def test_ratio_near_libzstd_level1(oracle):
+    """Not parity, a sanity bound: on the VM-image data the frames are within 5 % of
+    libzstd level 1's size (raw literals, no repeat offsets, predefined tables)."""
+    data = gen_np.gen_vmimage(8 * MiB, 0x5EED0003, 0)
+    L = oracle.libzstd()
+    dst = np.empty(L.ZSTD_compressBound(data.size), np.uint8)
+    ref = L.ZSTD_compress(dst.ctypes.data, dst.size, data.ctypes.data, data.size, 1)
+    ours = len(oracle.zstd_twin_frame(data.tobytes()))
+    assert ours <= ref * 1.05, (ours, ref)
