@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--secondary-random", type=int, default=1,
                     help="after the headline, regenerate the same buffer as random data and "
                          "time the pass over it too (a secondary line: no zero extents)")
+    ap.add_argument("--blobs", type=int, default=0,
+                    help="also time the compressed DataBlob stage (zstd frames + CRC, SURVEY 8(f) rank 4) "
+                         "over the stream's chunks, with libzstd level 1 + zlib on the host cores beside it")
     ap.add_argument("--digest", type=int, default=0,
                     help="also time the per-chunk SHA-256 stage (SURVEY 8(f)) over the stream's "
                          "chunks (GPU), with hashlib on the host cores beside it")
@@ -233,6 +236,70 @@ def secondary_random(args, ch, buf, stream, steps: int = 3):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "kernel": "scan_fused_kernel" if all(fused) else "scan_main_kernel",
                          "avg_launch_ms": round(sk, 4)}}
+
+
+def blob_stage(args, buf, cuts, stream, reps: int = 2):
+    """SURVEY 8(f) rank 4: DataBlob::encode(chunk, None, compress = true) for every chunk of
+    the device-resident stream (pbs_blob_encode_chunks_device: zstd frames of 128 KiB
+    blocks, compressed-or-not per chunk, blob images + CRC), wall clock of the synchronous
+    call; libzstd level 1 (the image's 1.4.8) + zlib.crc32 on the host cores over a bounded
+    sample of the same chunks beside it, with both compressed sizes of that sample."""
+    import zlib
+
+    import numpy as np
+    import torch
+
+    import pbschunk
+
+    oracle = _oracle()
+    size = buf.numel()
+    bounds = np.concatenate([[0], cuts]).astype(np.uint64)
+    n = bounds.size - 1
+    cap = pbschunk.blob_stream_bound(bounds)
+    out = torch.empty(cap, dtype=torch.uint8, device=buf.device)
+    pbschunk.blob_encode_chunks_device(buf.data_ptr(), size, bounds, out.data_ptr(), cap,
+                                       hip_stream=stream.cuda_stream)  # warm-up (scratch allocation)
+    best = None
+    for _ in range(reps):
+        offs, crcs, comp, tm = pbschunk.blob_encode_chunks_device(buf.data_ptr(), size, bounds, out.data_ptr(), cap,
+                                                                  hip_stream=stream.cuda_stream)
+        if best is None or tm["total_ms"] < best["total_ms"]:
+            best = tm
+    # host reference point: libzstd level 1 + crc32 over the first chunks (~1 GiB)
+    lens = np.diff(bounds.astype(np.int64))
+    take = max(1, min(n, int(np.searchsorted(np.cumsum(lens), 1 << 30)) + 1))
+    host = buf[: int(bounds[take])].cpu().numpy()
+    L = oracle.libzstd()
+    threads = cpu_threads(args)
+    sizes = np.zeros(take, dtype=np.int64)
+
+    def work(ix):
+        dst = np.empty(L.ZSTD_compressBound(int(lens.max())), dtype=np.uint8)
+        for i in ix:
+            a, b = int(bounds[i]), int(bounds[i + 1])
+            r = L.ZSTD_compress(dst.ctypes.data, dst.size, host.ctypes.data + a, b - a, 1)
+            sizes[i] = r
+            zlib.crc32(memoryview(dst)[:r])
+
+    parts = [list(range(k, take, threads)) for k in range(threads)]
+    ths = [threading.Thread(target=work, args=(ix,)) for ix in parts]
+    t0 = time.perf_counter()
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    cpu_gib_s = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
+    ours = int(offs[take]) - 12 * take
+    return {"metric": "GiB/s chunks -> compressed DataBlob images (zstd frames + CRC, device-resident)",
+            "value": round(size / (1 << 30) / (best["total_ms"] / 1e3), 3), "ms": round(best["total_ms"], 3),
+            "kernel_ms": {k: round(best[k], 3) for k in ("compress_ms", "assemble_ms", "crc_ms")},
+            "chunks": n, "blocks": int(best["blocks"]), "compressed_chunks": int(best["compressed_chunks"]),
+            "bytes_in": int(best["bytes_in"]), "bytes_out": int(best["bytes_out"]),
+            "ratio_out_in": round(best["bytes_out"] / max(1, best["bytes_in"]), 4),
+            "sample_payload_bytes": {"ours": ours, "libzstd_level1": int(sizes.sum()),
+                                     "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"},
+            "parity": "frames decode with libzstd to the chunks (tests); bytes are not libzstd's: unpinned",
+            "cpu_baseline": {"value": round(cpu_gib_s, 3), "unit": "GiB/s", "cores": threads,
+                             "kind": f"libzstd {L.ZSTD_versionNumber()} level 1 + zlib.crc32 (ctypes)",
+                             "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"}}
 
 
 def digest_stage(args, buf, cuts, stream, reps: int = 3):
@@ -679,6 +746,8 @@ def main():
         out["host_inclusive_gib_s"] = round(host_incl, 3)
     if args.digest and args.mode == "streams":
         out["digest"] = digest_stage(args, buf, cuts, stream)
+    if args.blobs and args.mode == "streams":
+        out["blobs"] = blob_stage(args, buf, cuts, stream)
     if args.pipeline_gib > 0 and args.mode == "streams" and world == 1:
         out["pipeline"] = pipeline_stage(args, buf)
     if args.secondary_random and args.mode == "streams" and world == 1 and args.workload != "random":

@@ -8,12 +8,14 @@
 // whose bytes cannot be reproduced here: parity of the compressed bytes is UNPINNED;
 // what is pinned is decode(frame) == chunk and the blob rules of data_blob.rs:139-176.
 //
-// Parse (per 128 KiB block, positions in rounds of kRound):
+// Parse (per 64 KiB block, positions in rounds of kRound):
 //   1. every position p of the round with 4 bytes left looks up h = hash(p) in a table
 //      holding, per hash, 1 + the last position of an EARLIER round with that hash;
 //   2. then the round's positions are inserted (largest position wins);
 //   3. a candidate c matches if 4 bytes agree; its length is the common prefix, capped at
-//      kCap while matching (the parse extends a chosen capped match to its true end);
+//      kCap while matching (the parse extends a chosen capped match to its true end); when
+//      the table's candidate does not match, the run candidate p - 1 (offset 1) is tried,
+//      so a run of equal bytes is one match even inside the round it starts in;
 //   4. greedy: from the current position, the first matching position starts a sequence
 //      {literals since the last match, length, offset p - c}; parsing resumes after it.
 #include <stdint.h>
@@ -27,7 +29,7 @@ namespace {
 
 using namespace pbs::zstd;
 
-constexpr uint32_t kRound = 256, kHashLog = 13, kCap = 32;
+constexpr uint32_t kRound = 1024, kHashLog = 11, kCap = 32;
 
 inline uint32_t rd32(const uint8_t* p) {
     uint32_t v;
@@ -49,7 +51,7 @@ const Tables& tables() {
     return t;
 }
 
-// One block of n <= 128 KiB bytes at src; writes header + body at out, returns its size.
+// One block of n <= 64 KiB bytes at src; writes header + body at out, returns its size.
 size_t block(const uint8_t* src, uint32_t n, bool last, uint8_t* out) {
     bool rle = n > 0;
     for (uint32_t i = 1; i < n && rle; ++i) rle = src[i] == src[0];
@@ -70,10 +72,16 @@ size_t block(const uint8_t* src, uint32_t n, bool last, uint8_t* out) {
             if (p + 1 > t) t = p + 1;
         }
         for (uint32_t p = r0; p < r1; ++p) {
+            const uint32_t lim = n - p < kCap ? n - p : kCap;
             uint32_t L = 0;
             if (cand[p - r0]) {
-                const uint32_t c = cand[p - r0] - 1, lim = n - p < kCap ? n - p : kCap;
+                const uint32_t c = cand[p - r0] - 1;
                 while (L < lim && src[c + L] == src[p + L]) ++L;
+            }
+            if (L < 4 && p > 0) {  // else the run candidate p - 1 (offset 1)
+                L = 0;
+                while (L < lim && src[p - 1 + L] == src[p + L]) ++L;
+                cand[p - r0] = L >= 4 ? p : cand[p - r0];  // 1 + (p - 1)
             }
             mlen[p - r0] = L >= 4 ? L : 0;
         }
@@ -124,8 +132,8 @@ uint64_t zstd_twin_frame(const uint8_t* src, uint64_t len, uint8_t* out) {
         write_block_header(out + o, true, 0, 0);
         return o + 3;
     }
-    for (uint64_t b = 0; b < len; b += kBlockMax) {
-        const uint32_t n = (uint32_t)(len - b < kBlockMax ? len - b : kBlockMax);
+    for (uint64_t b = 0; b < len; b += kEncBlock) {
+        const uint32_t n = (uint32_t)(len - b < kEncBlock ? len - b : kEncBlock);
         o += block(src + b, n, b + n == len, out + o);
     }
     return o;

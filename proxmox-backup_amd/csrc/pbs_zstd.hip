@@ -5,15 +5,17 @@
 // chunk, else the uncompressed blob {UNCOMPRESSED_BLOB_MAGIC_1_0, CRC, bytes}; the CRC
 // (`compute_crc`, :70-75) covers everything after the header.  C ABI: include/pbs_blob.h.
 //
-// The frame (zstd_enc.h) is built from independent 128 KiB zstd blocks, one workgroup per
-// block (a 64 GiB stream is 512 k blocks, so the chip is full):
+// The frame (zstd_enc.h) is built from independent 64 KiB zstd blocks, one workgroup per
+// block (a 64 GiB stream is 1 M blocks), the block staged in LDS (16-byte loads of its
+// aligned span; every byte and word read after that is LDS: 2 workgroups per CU):
 //   1. RLE test (every byte equal: a 4-byte RLE block -- the zero pages of a VM image);
-//   2. match finding in rounds of 256 positions, one per thread: hash of the 4 bytes at
+//   2. match finding in rounds of 1024 positions, four per thread: hash of the 4 bytes at
 //      p -> candidate = the last position of an earlier round with that hash (LDS table,
-//      8 K entries, `atomicMax` inserts after the lookups), common prefix capped at 32;
-//   3. greedy parse by wave 0 over the round's 256-bit match mask (one ballot per wave):
+//      2 K entries, `atomicMax` inserts after the lookups), common prefix (word compares)
+//      capped at 32 -- skipped for positions inside the match the parse has chosen;
+//   3. greedy parse by wave 0 over the round's 1024-bit match mask (ballots):
 //      from the current position the next matching position starts a sequence, a capped
-//      match is extended 64 bytes per step (ballot of mismatches);
+//      match is extended 256 bytes per step (a word per lane, ballot of mismatches);
 //   4. wave 0 lane 0 writes the FSE-coded sequences (predefined tables) while waves 1-3
 //      copy the literal runs; raw block if that is not shorter.
 // Then per chunk: frame size, compressed-or-not (the reference's "only if shorter",
@@ -43,10 +45,12 @@ namespace {
 using namespace zstd;
 
 constexpr int kZThreads = 256;
-constexpr uint32_t kZRound = 256, kZHashLog = 13, kZCap = 32;
-constexpr uint64_t kSlot = 131200;  // block header + up to 128 KiB + slack for 8-byte flushes
-constexpr uint32_t kMaxSeq = kBlockMax / 4;
-constexpr int kZGroupsPerCu = 4;
+constexpr uint32_t kZRound = 1024, kZHashLog = 11, kZCap = 32;
+constexpr int kZPer = kZRound / kZThreads;  // positions per thread and round
+constexpr uint64_t kSlot = kEncBlock + 128;  // block header + up to 64 KiB + slack for 8-byte flushes
+constexpr uint32_t kMaxSeq = kEncBlock / 4;
+constexpr uint32_t kStageWords = kEncBlock / 16 + 1;  // 16-byte words covering a block at any alignment
+constexpr int kZGroupsPerCu = 2;                    // LDS: 77.5 KiB per workgroup
 
 // pbs-datastore/src/file_formats.rs:9, :12
 constexpr uint8_t kUncompressedMagic[8] = {66, 171, 56, 7, 190, 131, 112, 161};
@@ -56,8 +60,71 @@ struct ZTables {
     FseCTable ll, ml, of;
 };
 
-__device__ __forceinline__ uint32_t rd32(const uint8_t* p) {
-    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
+    return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+           ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+}
+
+// The block staged in LDS: 16-byte words of the aligned span around it; block byte i is
+// LDS byte i + r (r = the block's address & 15).
+struct Stage {
+    const uint32_t* w;  // LDS words
+    uint32_t r;
+    __device__ __forceinline__ uint32_t byte(uint32_t i) const {
+        return reinterpret_cast<const uint8_t*>(w)[i + r];
+    }
+    // little-endian 4 bytes at block position i (i + 3 inside the staged span)
+    __device__ __forceinline__ uint32_t word(uint32_t i) const {
+        const uint32_t o = i + r;
+        return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
+    }
+};
+
+// Common prefix of the block at positions c < p, at most lim bytes: word compares, the
+// first differing byte from the lowest set bit of the XOR.
+__device__ __forceinline__ uint32_t common_prefix(const Stage& s, uint32_t c, uint32_t p, uint32_t lim) {
+    uint32_t L = 0;
+    while (L + 4 <= lim) {
+        const uint32_t x = s.word(c + L) ^ s.word(p + L);
+        if (x) return L + ((uint32_t)__builtin_ctz(x) >> 3);
+        L += 4;
+    }
+    while (L < lim && s.byte(c + L) == s.byte(p + L)) ++L;
+    return L;
+}
+
+// cnt bytes of the staged block from position `from` to global dst: head bytes up to a
+// 4-aligned dst, then dword stores (one LDS word read each), then the tail; threads t of nt.
+__device__ __forceinline__ void copy_from_stage(uint8_t* dst, const Stage& S, uint32_t from, uint32_t cnt,
+                                                uint32_t t, uint32_t nt) {
+    uint32_t head = (uint32_t)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3);
+    if (head > cnt) head = cnt;
+    if (t < head) dst[t] = (uint8_t)S.byte(from + t);
+    const uint32_t nwd = (cnt - head) >> 2;
+    uint32_t* const dw = reinterpret_cast<uint32_t*>(dst + head);
+    for (uint32_t w = t; w < nwd; w += nt) dw[w] = S.word(from + head + 4 * w);
+    for (uint32_t i = head + 4 * nwd + t; i < cnt; i += nt) dst[i] = (uint8_t)S.byte(from + i);
+}
+
+// n bytes global -> global at any alignments: dword stores at 4-aligned dst, each built
+// from the two aligned source dwords around it (never a page past a source byte).
+__device__ __forceinline__ void copy_global(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t t,
+                                            uint32_t nt) {
+    uint64_t head = (4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3;
+    if (head > n) head = n;
+    if (t < head) dst[t] = src[t];
+    const uint8_t* const s2 = src + head;
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(s2) & 3);
+    const uint32_t* const sa = reinterpret_cast<const uint32_t*>(s2 - sh);
+    const uint64_t nwd = (n - head) >> 2;
+    uint32_t* const dw = reinterpret_cast<uint32_t*>(dst + head);
+    for (uint64_t w = t; w < nwd; w += nt) {
+        const uint32_t lo = sa[w];
+        dw[w] = sh ? __builtin_amdgcn_alignbyte(sa[w + 1], lo, sh) : lo;
+    }
+    for (uint64_t i = head + 4 * nwd + t; i < n; i += nt) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
@@ -65,9 +132,11 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
     const uint64_t* __restrict__ items, uint64_t nitems, const ZTables* __restrict__ zt,
     uint8_t* __restrict__ slots, uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch,
     uint2* __restrict__ run_scratch) {
+    __shared__ uint4 blk[kStageWords + 1];
     __shared__ uint32_t table[1u << kZHashLog];
-    __shared__ uint32_t s_ml[kZRound], s_c[kZRound];
-    __shared__ unsigned long long s_mask[kZThreads / 64];
+    __shared__ uint8_t s_ml[kZRound];   // match length (<= kZCap), 0: none
+    __shared__ uint16_t s_c[kZRound];   // its candidate position
+    __shared__ unsigned long long s_mask[kZRound / 64];
     __shared__ ZTables s_zt;
     __shared__ uint32_t s_u[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -80,8 +149,8 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         __syncthreads();  // LDS of the previous item
         const uint64_t it = items[k];
         const uint64_t ci = it >> 32, j = (uint32_t)it;
-        const uint64_t len = bounds[ci + 1] - bounds[ci], off = j * (uint64_t)kBlockMax;
-        const uint32_t n = (uint32_t)(len > off ? (len - off < kBlockMax ? len - off : kBlockMax) : 0);
+        const uint64_t len = bounds[ci + 1] - bounds[ci], off = j * (uint64_t)kEncBlock;
+        const uint32_t n = (uint32_t)(len > off ? (len - off < kEncBlock ? len - off : kEncBlock) : 0);
         const bool last = off + n == len;
         const uint8_t* const src = data + (bounds[ci] - base) + off;
         uint8_t* const out = slots + k * kSlot;
@@ -92,13 +161,30 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             }
             continue;
         }
-        const uint8_t b0 = src[0];
+        // stage: the aligned 16-byte words holding [src, src + n) (never past a page that
+        // holds a block byte)
+        const uintptr_t a0 = reinterpret_cast<uintptr_t>(src) & ~(uintptr_t)15;
+        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+        const uint32_t nw = (n + r + 15) >> 4;
+        for (uint32_t i = tid; i < nw; i += kZThreads) {
+            const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(a0) + i);
+            blk[i] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+        if (tid == 0) blk[nw] = make_uint4(0, 0, 0, 0);  // word reads past the end stay defined
+        __syncthreads();
+        const Stage S{reinterpret_cast<const uint32_t*>(blk), r};
+        const uint32_t b0 = S.byte(0), b4 = b0 * 0x01010101u;
         int same = 1;
-        for (uint32_t i = tid; i < n; i += kZThreads) same &= src[i] == b0;
+        for (uint32_t i = 4 * tid; i < n; i += 4 * kZThreads) {
+            if (i + 4 <= n)
+                same &= S.word(i) == b4;
+            else
+                for (uint32_t q = i; q < n; ++q) same &= S.byte(q) == b0;
+        }
         if (__syncthreads_and(same)) {
             if (tid == 0) {
                 write_block_header(out, last, 1, n);
-                out[3] = b0;
+                out[3] = (uint8_t)b0;
                 sizes[k] = 4;
             }
             continue;
@@ -106,47 +192,76 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         for (uint32_t i = tid; i < (1u << kZHashLog); i += kZThreads) table[i] = 0;
         __syncthreads();
         uint32_t cur = 0, lit_start = 0, ns = 0, lit_out = 0;  // wave 0 (uniform)
+        if (tid == 0) s_u[3] = 0;                               // cur, for the other waves
         for (uint32_t r0 = 0; r0 < n; r0 += kZRound) {
-            const uint32_t p = r0 + tid;
-            const bool has4 = p + 4 <= n;
-            uint32_t h = 0, c1 = 0;
-            if (has4) {
-                h = (rd32(src + p) * 2654435761u) >> (32 - kZHashLog);
-                c1 = table[h];
+            // position r0 + tid + 256 i: lanes read consecutive bytes
+            uint32_t h[kZPer], c1[kZPer];
+            const uint32_t covered = s_u[3];  // positions below it lie inside a chosen match
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + tid + kZThreads * i;
+                h[i] = p + 4 <= n ? (S.word(p) * 2654435761u) >> (32 - kZHashLog) : ~0u;
+                c1[i] = h[i] != ~0u && p >= covered ? table[h[i]] : 0;
             }
             __syncthreads();  // every lookup sees the table before this round's inserts
-            if (has4) atomicMax(&table[h], p + 1);
-            uint32_t L = 0;
-            if (c1) {
-                const uint32_t c = c1 - 1, lim = n - p < kZCap ? n - p : kZCap;
-                while (L < lim && src[c + L] == src[p + L]) ++L;
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i)
+                if (h[i] != ~0u) atomicMax(&table[h[i]], r0 + tid + kZThreads * i + 1);
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + tid + kZThreads * i;
+                const uint32_t lim = n - p < kZCap ? n - p : kZCap;
+                uint32_t L = 0, c = c1[i] - 1;
+                if (c1[i]) L = common_prefix(S, c, p, lim);
+                if (L < 4 && p > 0 && p >= covered && p < n) {  // the run candidate p - 1
+                    L = common_prefix(S, p - 1, p, lim);
+                    if (L >= 4) c = p - 1;
+                }
+                if (L < 4) L = 0;
+                s_ml[tid + kZThreads * i] = (uint8_t)L;
+                s_c[tid + kZThreads * i] = (uint16_t)c;
+                const unsigned long long m = __ballot(L != 0);
+                if (lane == 0) s_mask[i * (kZThreads / 64) + wave] = m;
             }
-            if (L < 4) L = 0;
-            s_ml[tid] = L;
-            s_c[tid] = c1 - 1;
-            const unsigned long long m = __ballot(L != 0);
-            if (lane == 0) s_mask[wave] = m;
             __syncthreads();
             if (wave == 0) {  // greedy parse of the round, wave-uniform
+                // the round's 16 mask words in lanes 0..15, the nonzero ones as a ballot: the
+                // next match is found in registers (a serial LDS scan of empty words cost
+                // ~16 LDS latencies per round on incompressible data)
+                const unsigned long long mword = lane < kZRound / 64 ? s_mask[lane] : 0ull;
+                const unsigned long long nzw = __ballot(mword != 0ull);
                 uint32_t q = cur > r0 ? cur - r0 : 0;
                 while (q < kZRound) {
                     uint32_t w = q >> 6;
-                    unsigned long long mm = s_mask[w] & (~0ull << (q & 63));
-                    while (!mm && ++w < kZThreads / 64) mm = s_mask[w];
-                    if (!mm) break;
+                    unsigned long long mm = readlane64(mword, (int)w) & (~0ull << (q & 63));
+                    if (!mm) {
+                        const unsigned long long nz = w + 1 < 64 ? nzw & (~0ull << (w + 1)) : 0ull;
+                        if (!nz) break;
+                        w = (uint32_t)__builtin_ctzll(nz);
+                        mm = readlane64(mword, (int)w);
+                    }
                     const uint32_t b = w * 64 + (uint32_t)__builtin_ctzll(mm);
                     const uint32_t pp = r0 + b, c = s_c[b];
                     uint32_t ml = s_ml[b];
-                    if (ml == kZCap) {  // extend a capped match, 64 bytes per step
+                    if (ml == kZCap) {  // extend a capped match: 4 bytes per lane, 256 per step
                         for (;;) {
-                            const uint32_t x = pp + ml + lane;
-                            const bool ok = x < n && src[c + ml + lane] == src[x];
-                            const unsigned long long bad = __ballot(!ok);
+                            const uint32_t x = pp + ml + 4 * lane;
+                            uint32_t mis = 4;  // first mismatching byte of my 4 (4: none)
+                            if (x + 4 <= n) {
+                                const uint32_t d = S.word(c + ml + 4 * lane) ^ S.word(x);
+                                if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
+                            } else {
+                                mis = 0;
+                                while (x + mis < n && S.byte(c + ml + 4 * lane + mis) == S.byte(x + mis)) ++mis;
+                                if (x >= n) mis = 0;
+                            }
+                            const unsigned long long bad = __ballot(mis < 4 || x + 4 > n);
                             if (bad) {
-                                ml += (uint32_t)__builtin_ctzll(bad);
+                                const int f = __builtin_ctzll(bad);
+                                ml += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
                                 break;
                             }
-                            ml += 64;
+                            ml += 256;
                         }
                     }
                     if (lane == 0) {
@@ -159,6 +274,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                     lit_start = cur;
                     q = cur - r0;
                 }
+                if (lane == 0) s_u[3] = cur;
             }
             __syncthreads();  // s_ml / s_c / s_mask are rewritten by the next round
         }
@@ -182,19 +298,19 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 }
             } else {  // waves 1-3: the literal runs (run ns: the bytes after the last match)
                 uint8_t* const lo = out + 3 + lith;
-                for (uint32_t r = 0; r <= ns; ++r) {
+                for (uint32_t q = 0; q <= ns; ++q) {
                     uint32_t from, to, cnt;
-                    if (r < ns) {
-                        const uint2 ru = runs[r];
+                    if (q < ns) {
+                        const uint2 ru = runs[q];
                         from = ru.x;
                         to = ru.y;
-                        cnt = seqs[r].ll;
+                        cnt = seqs[q].ll;
                     } else {
                         from = tail_start;
                         cnt = n - tail_start;
                         to = nlit - cnt;
                     }
-                    for (uint32_t i = tid - 64; i < cnt; i += kZThreads - 64) lo[to + i] = src[from + i];
+                    copy_from_stage(lo + to, S, from, cnt, tid - 64, kZThreads - 64);
                 }
             }
             __syncthreads();
@@ -208,7 +324,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             }
         }
         if (raw) {
-            for (uint32_t i = tid; i < n; i += kZThreads) out[3 + i] = src[i];
+            copy_from_stage(out + 3, S, 0, n, tid, kZThreads);
             if (tid == 0) {
                 write_block_header(out, last, 0, n);
                 sizes[k] = 3 + (uint64_t)n;
@@ -257,15 +373,12 @@ __global__ __launch_bounds__(kZThreads) void zstd_assemble_kernel(
         if (c) {
             if (j == 0 && threadIdx.x == 0) write_frame_header(blob + 12, len);
             uint8_t* const dst = blob + 12 + fh + (ipre[k] - ipre[first[ci]]);
-            const uint8_t* const sl = slots + k * kSlot;
-            const uint64_t sz = sizes[k];
-            for (uint64_t i = threadIdx.x; i < sz; i += kZThreads) dst[i] = sl[i];
+            copy_global(dst, slots + k * kSlot, sizes[k], threadIdx.x, kZThreads);
         } else {
-            const uint64_t off = j * (uint64_t)kBlockMax;
-            const uint64_t n = len > off ? (len - off < kBlockMax ? len - off : kBlockMax) : 0;
+            const uint64_t off = j * (uint64_t)kEncBlock;
+            const uint64_t n = len > off ? (len - off < kEncBlock ? len - off : kEncBlock) : 0;
             const uint8_t* const src = data + (bounds[ci] - base) + off;
-            uint8_t* const dst = blob + 12 + off;
-            for (uint64_t i = threadIdx.x; i < n; i += kZThreads) dst[i] = src[i];
+            copy_global(blob + 12 + off, src, n, threadIdx.x, kZThreads);
         }
     }
 }
@@ -351,7 +464,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     for (size_t i = 0; i < n; ++i) {
         first[i] = items.size();
         const uint64_t len = bounds[i + 1] - bounds[i];
-        const uint64_t nb = len ? (len + zstd::kBlockMax - 1) / zstd::kBlockMax : 1;
+        const uint64_t nb = len ? (len + zstd::kEncBlock - 1) / zstd::kEncBlock : 1;
         for (uint64_t j = 0; j < nb; ++j) items.push_back((uint64_t)i << 32 | j);
     }
     first[n] = items.size();

@@ -11,7 +11,7 @@
 // What is written:
 //   frame   magic FD2FB528, single-segment frame header with the content size (no window
 //           descriptor, no checksum, no dictionary), then the blocks;
-//   blocks  128 KiB of the chunk each (the last shorter): RLE when every byte is equal,
+//   blocks  64 KiB of the chunk each (the last shorter): RLE when every byte is equal,
 //           compressed when that is shorter than the bytes, else raw;
 //   compressed block = raw literals section + sequences with the PREDEFINED FSE tables
 //           for literal lengths, match lengths and offsets (symbol compression modes 0),
@@ -30,7 +30,8 @@ namespace pbs {
 namespace zstd {
 
 constexpr uint32_t kMagic = 0xFD2FB528u;
-constexpr uint32_t kBlockMax = 128u * 1024u;
+constexpr uint32_t kBlockMax = 128u * 1024u;  // the format's largest block
+constexpr uint32_t kEncBlock = 64u * 1024u;   // the blocks this encoder writes (LDS-resident)
 constexpr uint32_t kFrameHeaderMax = 4 + 1 + 8;  // magic, descriptor, content size
 
 // RFC 8878 3.1.1.3.2.1: literal-length and match-length codes (baseline, extra bits)
@@ -296,7 +297,7 @@ PBS_HD inline uint32_t frame_header_size(uint64_t len) {
 // Largest frame for a chunk: header + every block raw (3-byte header each; an empty
 // chunk is one empty raw block).
 PBS_HD inline uint64_t frame_bound(uint64_t len) {
-    const uint64_t nb = len ? (len + kBlockMax - 1) / kBlockMax : 1;
+    const uint64_t nb = len ? (len + kEncBlock - 1) / kEncBlock : 1;
     return frame_header_size(len) + len + 3 * nb;
 }
 

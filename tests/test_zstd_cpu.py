@@ -46,7 +46,7 @@ def test_twin_frames_decode_with_libzstd(oracle, name, data):
     f = oracle.zstd_twin_frame(data.tobytes())
     assert f[:4] == b"\x28\xb5\x2f\xfd"
     assert oracle.zstd_decompress(f, data.size) == data.tobytes()
-    assert len(f) <= 13 + data.size + 3 * max(1, -(-data.size // (128 * KiB)))  # frame bound
+    assert len(f) <= 13 + data.size + 3 * max(1, -(-data.size // (64 * KiB)))  # frame bound
 
 
 def test_blob_rules(oracle):
