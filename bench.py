@@ -525,6 +525,8 @@ def launch_ranks(args) -> int:
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if args.cpu_standin:  # gloo on the loopback device (the hostname may not resolve)
+            env.setdefault("GLOO_SOCKET_IFNAME", "lo")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
     rc, live = 0, list(procs)

@@ -21,6 +21,7 @@ def _worker(rank, world, port, q):
     sys.path.insert(0, root)
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # loopback: the hostname may not resolve
     dist.init_process_group("gloo", rank=rank, world_size=world)
     elapsed = 1.0 + rank  # rank 1 is the slow one
     nbytes = (rank + 1) * 1000

@@ -72,6 +72,7 @@ def _worker(rank, world, port, n, avg, q):
     import torch.distributed as dist
     import shard
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # loopback: the hostname may not resolve
     dist.init_process_group("gloo", rank=rank, world_size=world)
     data = _stream(n)
     base, ln = shard.shard_ranges(n, world)[rank]
