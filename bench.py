@@ -748,10 +748,10 @@ def main():
         out["host_inclusive_gib_s"] = round(host_incl, 3)
     if args.digest and args.mode == "streams":
         out["digest"] = digest_stage(args, buf, cuts, stream)
+    if args.pipeline_gib > 0 and args.mode == "streams" and world == 1:
+        out["pipeline"] = pipeline_stage(args, buf)  # before the blob stage's 64 GiB scratch
     if args.blobs and args.mode == "streams":
         out["blobs"] = blob_stage(args, buf, cuts, stream)
-    if args.pipeline_gib > 0 and args.mode == "streams" and world == 1:
-        out["pipeline"] = pipeline_stage(args, buf)
     if args.secondary_random and args.mode == "streams" and world == 1 and args.workload != "random":
         out["secondary_random"] = secondary_random(args, ch, buf, stream)
     if args.cpu_baseline and world == 1:

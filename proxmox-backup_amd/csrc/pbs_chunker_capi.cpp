@@ -143,7 +143,8 @@ struct pbs_chunker {
     // its scan time (ev[0] -> ev[1]) and the call's total (ev[5] -> ev[4]) are read from
     // the events when last_timing asks for them
     bool timing_pending = false;
-    bool fused = true;       // PBS_FUSED=0: multi-launch path for every batch (A/B)
+    bool fused = true;        // PBS_FUSED=0: multi-launch path for every batch (A/B)
+    bool fused_force = false; // PBS_FUSED=1: the fused pass for every batch it can serve (tests)
     uint64_t susp_cap = 0, cand_cap = 0;
     uint64_t batch_limit = 0;  // bytes per batch (0 = batch_max); shrunk when a batch is too dense
     bool too_dense = false;    // the last scan found more than kMaxBatchCand candidates
@@ -739,9 +740,18 @@ int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
 // ~12-24 candidates, far below the 64 flagged blocks one tile's exact step takes.
 constexpr uint64_t kFusedMinAvg = 128 * 1024;
 
+// ... and batches large enough for the dynamic tile order (>= 32 GiB on 256 CUs): with
+// the static order of smaller batches (2-4 tiles per wave) the fused pass measured slower
+// than scan_main + resolve (8 GiB random: 1.76 vs 1.36-1.41 ms kernel,
+// profiles/r02/final/c2.log); PBS_FUSED=1 forces it (its parity tests run small inputs).
 bool use_fused(const pbs_chunker* c, uint64_t bl) {
-    return c->fused && c->prm.hash_cuts && c->prm.avg >= kFusedMinAvg && bl > kFusedMaxBytes &&
-           c->cu >= 2;
+    if (!(c->fused && c->prm.hash_cuts && c->prm.avg >= kFusedMinAvg && bl > kFusedMaxBytes && c->cu >= 2))
+        return false;
+    if (c->fused_force) return true;
+    uint64_t nt = 0, tb = 0;
+    bool dyn = false;
+    (void)scan_main_plan(bl, c->cu, &nt, &dyn, &tb);
+    return dyn;
 }
 
 // One batch [pos, pos + bl) of device bytes `dsrc` (hsrc: the same bytes on the host, or
@@ -1089,7 +1099,10 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     }
     c->prm = prm;
     if (const char* e = std::getenv("PBS_DEBUG_PHASES")) c->debug_phases = e[0] == '1';
-    if (const char* e = std::getenv("PBS_FUSED")) c->fused = e[0] != '0';
+    if (const char* e = std::getenv("PBS_FUSED")) {
+        c->fused = e[0] != '0';
+        c->fused_force = e[0] == '1';
+    }
     if (const char* e = std::getenv("PBS_SCAN_SERVER")) c->srv.enabled = e[0] != '0';
     bool ok = hipGetDevice(&c->device) == hipSuccess;
     hipDeviceProp_t prop;

@@ -458,10 +458,12 @@ def test_fused_pass(gpu, oracle, monkeypatch, name, mk, avg, pieces):
         assert np.array_equal(got, ref), (name, fused, got.size, ref.size)
 
 
-def test_fused_pass_stands_down_on_dense_input(gpu, oracle):
+def test_fused_pass_stands_down_on_dense_input(gpu, oracle, monkeypatch):
     """Every 7th byte a candidate at a 256 KiB average: a tile holds far more than 64
     flagged blocks, the fused kernel stands down and the multi-launch path chunks the
-    batch -- same cuts as the oracle."""
+    batch -- same cuts as the oracle.  (PBS_FUSED=1: a 24 MiB batch would otherwise take
+    the multi-launch path directly.)"""
+    monkeypatch.setenv("PBS_FUSED", "1")
     pat = _passing_pattern(oracle, 7, 256 * KiB)
     n = 24 * MiB + 3
     rnd = gen_np.gen_random(n, 44)
