@@ -288,6 +288,8 @@ def blob_stage(args, buf, cuts, stream, reps: int = 2):
     [x.join() for x in ths]
     cpu_gib_s = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
     ours = int(offs[take]) - 12 * take
+    del out
+    pbschunk.blob_encode_release()
     return {"metric": "GiB/s chunks -> compressed DataBlob images (zstd frames + CRC, device-resident)",
             "value": round(size / (1 << 30) / (best["total_ms"] / 1e3), 3), "ms": round(best["total_ms"], 3),
             "kernel_ms": {k: round(best[k], 3) for k in ("compress_ms", "assemble_ms", "crc_ms")},

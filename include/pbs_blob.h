@@ -65,7 +65,7 @@ size_t pbs_blob_encode_uncompressed(const uint8_t *data, size_t len, uint32_t cr
  * are written back to back into `blobs_dev` (device, blobs_cap >= pbs_blob_stream_bound);
  * blob i is [blob_offsets[i], blob_offsets[i+1]) (host, n + 1); `crcs` (host, n) and
  * `compressed` (host, n: 1 = zstd) may be NULL.  Needs ~ (bytes of the chunks) of device
- * scratch, kept for the process.  Synchronous.  C ABI of include/pbs_chunker.h's codes. */
+ * scratch, kept between calls until pbs_blob_encode_release.  Synchronous.  C ABI of include/pbs_chunker.h's codes. */
 typedef struct {
     double total_ms;    /* call entry .. outputs on the host */
     double compress_ms; /* block compression + frame sizes + offset scans (HIP events) */
@@ -78,6 +78,8 @@ int pbs_blob_encode_chunks_device(const uint8_t *dev_data, size_t data_len, uint
                                   size_t blobs_cap, uint64_t *blob_offsets, uint32_t *crcs,
                                   uint8_t *compressed, pbs_blob_encode_timing *timing,
                                   void *hip_stream);
+/* Frees the device scratch pbs_blob_encode_chunks_device keeps between calls. */
+void pbs_blob_encode_release(void);
 /* 12 n + (bounds[n] - bounds[0]): the largest blob stream of n chunks. */
 size_t pbs_blob_stream_bound(const uint64_t *bounds, size_t n);
 /* Largest zstd frame this encoder writes for `len` bytes (header + raw blocks). */

@@ -82,6 +82,9 @@ int pbs_digest_chunks_hybrid(const uint8_t *dev_data, const uint8_t *host_data, 
                              size_t key_len, uint8_t *digests, const pbs_digest_hybrid_opts *opts,
                              pbs_digest_hybrid_timing *timing, void *hip_stream);
 
+/* Frees the pinned host slices the hybrid digest keeps between calls. */
+void pbs_digest_hybrid_release(void);
+
 /* SHA-256(chunk || key) of every chunk of a host buffer on `threads` host threads (0:
  * hardware threads), SHA extensions when the CPU has them (pbs_sha256_host_uses_ni).
  * Same arguments as pbs_digest_chunks_device with host memory. */

@@ -734,6 +734,14 @@ bool hash_from_device(const uint8_t* src, uint64_t len, const uint8_t* key, size
 
 }  // namespace
 
+// Frees the hybrid digest's pinned host slices and their streams.
+extern "C" void pbs_digest_hybrid_release(void) {
+    HostStage& hs = host_stage();
+    std::lock_guard<std::mutex> lk(hs.mu);
+    hs.release();
+    hs.dev = -1;
+}
+
 extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* host_data, size_t data_len,
                                         uint64_t base, const uint64_t* bounds, size_t n, const uint8_t* key,
                                         size_t key_len, uint8_t* digests, const pbs_digest_hybrid_opts* opts,

@@ -30,6 +30,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -50,7 +52,7 @@ constexpr int kZPer = kZRound / kZThreads;  // positions per thread and round
 constexpr uint64_t kSlot = kEncBlock + 128;  // block header + up to 64 KiB + slack for 8-byte flushes
 constexpr uint32_t kMaxSeq = kEncBlock / 4;
 constexpr uint32_t kStageWords = kEncBlock / 16 + 1;  // 16-byte words covering a block at any alignment
-constexpr int kZGroupsPerCu = 2;                    // LDS: 77.5 KiB per workgroup
+constexpr int kZGroupsPerCu = 2;                    // LDS: 77 KiB per workgroup
 
 // pbs-datastore/src/file_formats.rs:9, :12
 constexpr uint8_t kUncompressedMagic[8] = {66, 171, 56, 7, 190, 131, 112, 161};
@@ -127,6 +129,12 @@ __device__ __forceinline__ void copy_global(uint8_t* dst, const uint8_t* src, ui
     for (uint64_t i = head + 4 * nwd + t; i < n; i += nt) dst[i] = src[i];
 }
 
+// PBS_ZSTD_PROBE=1 (diagnostics): workgroup 0 adds wall-clock ticks (100 MHz) per phase
+// into g_zprobe: 0 stage, 1 RLE test, 2 rounds (lookups/matches), 3 parse (wave 0), 4
+// encode + literal copy, 5 raw copy, 6 items, 7 sequences.
+__device__ unsigned long long g_zprobe[8];
+
+template <bool PROBE>
 __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, const ZTables* __restrict__ zt,
@@ -145,14 +153,33 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
     Seq* const seqs = seq_scratch + (uint64_t)blockIdx.x * kMaxSeq;
     uint2* const runs = run_scratch + (uint64_t)blockIdx.x * kMaxSeq;
 
+    const bool probe = PROBE && blockIdx.x == 0 && tid == 0;
+    uint64_t tp = probe ? wall_clock64() : 0;
+    auto mark = [&](int ph) {
+        if (probe) {
+            const uint64_t t = wall_clock64();
+            g_zprobe[ph] += t - tp;
+            tp = t;
+        }
+    };
+    // the next item's metadata loads while this one is compressed
+    uint64_t it_n = blockIdx.x < nitems ? items[blockIdx.x] : 0;
+    uint64_t b0_n = blockIdx.x < nitems ? bounds[it_n >> 32] : 0, b1_n = blockIdx.x < nitems ? bounds[(it_n >> 32) + 1] : 0;
     for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
         __syncthreads();  // LDS of the previous item
-        const uint64_t it = items[k];
+        const uint64_t it = it_n, bb0 = b0_n, bb1 = b1_n;
+        if (k + gridDim.x < nitems) {
+            it_n = items[k + gridDim.x];
+            b0_n = bounds[it_n >> 32];
+            b1_n = bounds[(it_n >> 32) + 1];
+        }
+        if (probe) g_zprobe[6] += 1;
         const uint64_t ci = it >> 32, j = (uint32_t)it;
-        const uint64_t len = bounds[ci + 1] - bounds[ci], off = j * (uint64_t)kEncBlock;
+        (void)ci;
+        const uint64_t len = bb1 - bb0, off = j * (uint64_t)kEncBlock;
         const uint32_t n = (uint32_t)(len > off ? (len - off < kEncBlock ? len - off : kEncBlock) : 0);
         const bool last = off + n == len;
-        const uint8_t* const src = data + (bounds[ci] - base) + off;
+        const uint8_t* const src = data + (bb0 - base) + off;
         uint8_t* const out = slots + k * kSlot;
         if (n == 0) {  // the empty chunk's frame: one empty raw block
             if (tid == 0) {
@@ -162,26 +189,43 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             continue;
         }
         // stage: the aligned 16-byte words holding [src, src + n) (never past a page that
-        // holds a block byte)
-        const uintptr_t a0 = reinterpret_cast<uintptr_t>(src) & ~(uintptr_t)15;
+        // holds a block byte); all of a thread's loads in flight before the LDS stores
         const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
+        const uint8_t* const a0 = src - r;  // pointer arithmetic keeps the loads global (not flat)
         const uint32_t nw = (n + r + 15) >> 4;
-        for (uint32_t i = tid; i < nw; i += kZThreads) {
-            const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(a0) + i);
-            blk[i] = make_uint4(v.x, v.y, v.z, v.w);
+        for (uint32_t i0 = tid; i0 < nw; i0 += 5 * kZThreads) {  // 5 loads in flight per thread
+            v4u v[5];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const uint32_t i = i0 + kZThreads * q;
+                if (i < nw) v[q] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(a0) + i);
+            }
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const uint32_t i = i0 + kZThreads * q;
+                if (i < nw) blk[i] = make_uint4(v[q].x, v[q].y, v[q].z, v[q].w);
+            }
         }
         if (tid == 0) blk[nw] = make_uint4(0, 0, 0, 0);  // word reads past the end stay defined
         __syncthreads();
+        mark(0);
         const Stage S{reinterpret_cast<const uint32_t*>(blk), r};
         const uint32_t b0 = S.byte(0), b4 = b0 * 0x01010101u;
         int same = 1;
-        for (uint32_t i = 4 * tid; i < n; i += 4 * kZThreads) {
-            if (i + 4 <= n)
-                same &= S.word(i) == b4;
-            else
-                for (uint32_t q = i; q < n; ++q) same &= S.byte(q) == b0;
+        for (uint32_t q = tid; q < nw; q += kZThreads) {  // staged word q = block bytes 16q - r ..
+            if (16 * q >= r && 16 * q + 16 - r <= n) {
+                const uint4 w = blk[q];
+                same &= (w.x == b4) & (w.y == b4) & (w.z == b4) & (w.w == b4);
+            } else {
+                for (uint32_t i = 0; i < 16; ++i) {
+                    const int64_t pos = (int64_t)(16 * q + i) - (int64_t)r;
+                    if (pos >= 0 && pos < (int64_t)n) same &= S.byte((uint32_t)pos) == b0;
+                }
+            }
         }
-        if (__syncthreads_and(same)) {
+        const int rle = __syncthreads_and(same);
+        mark(1);
+        if (rle) {
             if (tid == 0) {
                 write_block_header(out, last, 1, n);
                 out[3] = (uint8_t)b0;
@@ -197,33 +241,57 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             // position r0 + tid + 256 i: lanes read consecutive bytes
             uint32_t h[kZPer], c1[kZPer];
             const uint32_t covered = s_u[3];  // positions below it lie inside a chosen match
+            // branch-free: every LDS read below is issued unconditionally at a clamped
+            // address and its value selected afterwards, so the reads of the 4 positions
+            // overlap (conditional reads became one basic block and one wait each)
+            const uint32_t plim = n >= 4 ? n - 4 : 0;
+            uint32_t wp[kZPer], wm[kZPer];
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
                 const uint32_t p = r0 + tid + kZThreads * i;
-                h[i] = p + 4 <= n ? (S.word(p) * 2654435761u) >> (32 - kZHashLog) : ~0u;
-                c1[i] = h[i] != ~0u && p >= covered ? table[h[i]] : 0;
+                const uint32_t pc = p < plim ? p : plim;
+                wp[i] = S.word(pc);
+                wm[i] = S.word(pc ? pc - 1 : 0);  // p - 1: the run candidate (lane 0 needs it)
             }
-            __syncthreads();  // every lookup sees the table before this round's inserts
-#pragma unroll
-            for (int i = 0; i < kZPer; ++i)
-                if (h[i] != ~0u) atomicMax(&table[h[i]], r0 + tid + kZThreads * i + 1);
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
                 const uint32_t p = r0 + tid + kZThreads * i;
-                const uint32_t lim = n - p < kZCap ? n - p : kZCap;
-                uint32_t L = 0, c = c1[i] - 1;
-                if (c1[i]) L = common_prefix(S, c, p, lim);
-                if (L < 4 && p > 0 && p >= covered && p < n) {  // the run candidate p - 1
-                    L = common_prefix(S, p - 1, p, lim);
-                    if (L >= 4) c = p - 1;
+                h[i] = (wp[i] * 2654435761u) >> (32 - kZHashLog);
+                const uint32_t t = table[h[i]];
+                // an AND, not a select: a select let the compiler sink the read into a branch
+                c1[i] = t & (0u - (uint32_t)(p + 4 <= n && p >= covered));
+            }
+            uint32_t wc[kZPer], wr[kZPer];
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                wc[i] = S.word(c1[i] ? c1[i] - 1 : 0);
+                const uint32_t up = (uint32_t)__shfl_up((int)wp[i], 1, 64);
+                wr[i] = lane ? up : wm[i];
+            }
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + tid + kZThreads * i;
+                const bool live = p + 4 <= n && p >= covered;
+                const bool mt = live && c1[i] && wc[i] == wp[i];
+                const bool mr = live && !mt && p > 0 && wr[i] == wp[i];
+                uint32_t L = 0, c = mr ? p - 1 : c1[i] - 1;
+                if (mt || mr) {  // rare: a match, extended to the cap
+                    const uint32_t lim = n - p < kZCap ? n - p : kZCap;
+                    L = 4 + common_prefix(S, c + 4, p + 4, lim - 4);
                 }
-                if (L < 4) L = 0;
                 s_ml[tid + kZThreads * i] = (uint8_t)L;
                 s_c[tid + kZThreads * i] = (uint16_t)c;
                 const unsigned long long m = __ballot(L != 0);
                 if (lane == 0) s_mask[i * (kZThreads / 64) + wave] = m;
             }
-            __syncthreads();
+            __syncthreads();  // every lookup done (and the masks ready) before the inserts
+            mark(2);
+            // the round's inserts, while wave 0 parses (the next round's lookups see them)
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {  // positions without 4 bytes insert 0: no effect
+                const uint32_t p = r0 + tid + kZThreads * i;
+                atomicMax(&table[h[i]], p + 4 <= n ? p + 1 : 0u);
+            }
             if (wave == 0) {  // greedy parse of the round, wave-uniform
                 // the round's 16 mask words in lanes 0..15, the nonzero ones as a ballot: the
                 // next match is found in registers (a serial LDS scan of empty words cost
@@ -276,7 +344,8 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 }
                 if (lane == 0) s_u[3] = cur;
             }
-            __syncthreads();  // s_ml / s_c / s_mask are rewritten by the next round
+            __syncthreads();  // inserts done, s_ml / s_c / s_mask free for the next round
+            mark(3);
         }
         if (tid == 0) {
             s_u[0] = ns;
@@ -285,14 +354,30 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         }
         __syncthreads();
         ns = s_u[0];
+        if (probe) g_zprobe[7] += ns;
         const uint32_t nlit = s_u[1], tail_start = s_u[2];
+        // the sequences and literal runs into LDS (the hash table's space is free now): the
+        // serial encoder and the run copies then read LDS, not the global list one latency
+        // at a time
+        constexpr uint32_t kLdsSeq = sizeof(table) / (sizeof(Seq) + sizeof(uint2));
+        uint2* const lrun = reinterpret_cast<uint2*>(table);
+        Seq* const lseq = reinterpret_cast<Seq*>(lrun + kLdsSeq);
+        const bool in_lds = ns <= kLdsSeq;
+        if (in_lds)
+            for (uint32_t q = tid; q < ns; q += kZThreads) {
+                lseq[q] = seqs[q];
+                lrun[q] = runs[q];
+            }
+        __syncthreads();
+        const Seq* const sq = in_lds ? lseq : seqs;
+        const uint2* const rq = in_lds ? lrun : runs;
         const uint32_t lith = nlit < 32 ? 1 : nlit < 4096 ? 2 : 3;
         const uint32_t seq_at = 3 + lith + nlit;
         bool raw = seq_at - 3 >= n;
         if (!raw) {
             if (wave == 0) {
                 if (lane == 0) {
-                    const size_t sz = write_sequences(out + seq_at, seqs, ns, s_zt.ll, s_zt.ml, s_zt.of,
+                    const size_t sz = write_sequences(out + seq_at, sq, ns, s_zt.ll, s_zt.ml, s_zt.of,
                                                       out + 3 + n);
                     s_u[3] = sz == SIZE_MAX ? 0xFFFFFFFFu : (uint32_t)sz;
                 }
@@ -301,10 +386,10 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 for (uint32_t q = 0; q <= ns; ++q) {
                     uint32_t from, to, cnt;
                     if (q < ns) {
-                        const uint2 ru = runs[q];
+                        const uint2 ru = rq[q];
                         from = ru.x;
                         to = ru.y;
-                        cnt = seqs[q].ll;
+                        cnt = sq[q].ll;
                     } else {
                         from = tail_start;
                         cnt = n - tail_start;
@@ -314,6 +399,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 }
             }
             __syncthreads();
+            mark(4);
             const uint32_t sz = s_u[3];
             if (sz == 0xFFFFFFFFu || seq_at + sz - 3 >= n) {
                 raw = true;
@@ -329,6 +415,10 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 write_block_header(out, last, 0, n);
                 sizes[k] = 3 + (uint64_t)n;
             }
+        }
+        if (PROBE) {
+            __syncthreads();
+            mark(5);
         }
     }
 }
@@ -429,6 +519,21 @@ bool grow(T** p, size_t* cap, size_t need) {
 using namespace pbs;
 
 extern "C" size_t pbs_zstd_frame_bound(size_t len) { return (size_t)zstd::frame_bound(len); }
+
+// Frees the blob encoder's cached device scratch (~ the bytes of the largest call).
+extern "C" void pbs_blob_encode_release(void) {
+    ZScratch& z = zscratch();
+    std::lock_guard<std::mutex> lk(z.mu);
+    for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.runs, (void*)z.zt})
+        if (p) (void)hipFree(p);
+    z.slots = nullptr;
+    z.seqs = nullptr;
+    z.runs = nullptr;
+    z.zt = nullptr;
+    z.slots_cap = 0;
+    z.groups = 0;
+    z.dev = -1;
+}
 
 extern "C" size_t pbs_blob_stream_bound(const uint64_t* bounds, size_t n) {
     if (!bounds || n == 0) return 0;
@@ -534,9 +639,26 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     if (rc == PBS_OK) {
         (void)hipGetLastError();
         ok(hipEventRecord(ev[0], st));
-        if (compress)
-            hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds,
+        static const bool probe = [] {
+            const char* e = std::getenv("PBS_ZSTD_PROBE");
+            return e && e[0] == '1';
+        }();
+        if (compress && probe) {
+            const unsigned long long z[8] = {};
+            (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
+            hipLaunchKernelGGL(zstd_block_kernel<true>, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds,
                                d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.runs);
+            unsigned long long h[8] = {};
+            (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
+            (void)hipStreamSynchronize(st);
+            std::fprintf(stderr,
+                         "zstd probe (workgroup 0, us): stage %.1f rle %.1f rounds %.1f parse %.1f encode+lits %.1f "
+                         "raw %.1f | items %llu seqs %llu\n",
+                         h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[4] / 100.0, h[5] / 100.0, h[6], h[7]);
+        } else if (compress) {
+            hipLaunchKernelGGL(zstd_block_kernel<false>, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds,
+                               d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.runs);
+        }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
         ok(hipGetLastError()) && ok(exclusive_sum_u64(d_tmp, &tmpb, d_bsz, d_boff,

@@ -56,6 +56,7 @@ EXPORTED_SYMBOLS = (
     # include/pbs_blob.h (blob CRC)
     "pbs_crc32_chunks_device", "pbs_crc32_chunks_async", "pbs_crc32", "pbs_blob_encode_uncompressed",
     "pbs_blob_encode_chunks_device", "pbs_blob_stream_bound", "pbs_zstd_frame_bound",
+    "pbs_blob_encode_release", "pbs_digest_hybrid_release",
 )
 
 
@@ -190,6 +191,8 @@ def lib():
                                            ctypes.POINTER(BlobEncodeTiming), p], i),
         "pbs_blob_stream_bound": ([p, sz], sz),
         "pbs_zstd_frame_bound": ([sz], sz),
+        "pbs_blob_encode_release": ([], None),
+        "pbs_digest_hybrid_release": ([], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -629,6 +632,16 @@ def blob_encode_chunks_device(dev_ptr: int, data_len: int, bounds, blobs_dev: in
     if rc != PBS_OK:
         raise ChunkerError(rc, "pbs_blob_encode_chunks_device")
     return offs, crcs, comp, t.as_dict()
+
+
+def blob_encode_release() -> None:
+    """Free the blob encoder's cached device scratch."""
+    lib().pbs_blob_encode_release()
+
+
+def digest_hybrid_release() -> None:
+    """Free the hybrid digest's cached pinned host slices."""
+    lib().pbs_digest_hybrid_release()
 
 
 def blob_stream_bound(bounds) -> int:

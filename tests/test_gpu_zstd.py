@@ -113,3 +113,13 @@ def test_chunker_to_blobs_vm_stream(gpu, oracle, torch_dev, avg):
     blob, offs, crcs, comp, tm = _encode(gpu, torch_dev, data, bounds)
     _check(oracle, data, bounds, blob, offs, crcs, comp)
     assert tm["bytes_out"] < n  # the zero pages compress
+
+
+def test_blob_encode_after_release(gpu, oracle, torch_dev):
+    """pbs_blob_encode_release frees the cached scratch; the next call allocates it anew
+    and writes the same blobs."""
+    data, bounds = _mixed()
+    a = _encode(gpu, torch_dev, data, bounds)[0]
+    gpu.blob_encode_release()
+    b = _encode(gpu, torch_dev, data, bounds)[0]
+    assert a == b
