@@ -767,6 +767,16 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     uint64_t ntiles = 0, t_big = 0;
     bool dyn = false;
     const int seg = scan_main_plan(bl, c->cu, &ntiles, &dyn, &t_big);
+    if (!dyn) {
+        // static order over the cu * 8 - 3 scanner waves: a whole number of tiles per wave,
+        // the remainder as tail items every wave shares (with scan_main's tile count the
+        // first ntiles mod waves took one tile more: 8 GiB 1.84 vs 1.40 ms)
+        const uint64_t nw = (uint64_t)c->cu * kFusedWavesPerWG - kFusedResolverWaves;
+        if (ntiles >= nw && ntiles % nw) {
+            ntiles -= ntiles % nw;
+            t_big = std::min(t_big, ntiles);
+        }
+    }
     const uint64_t covered = scan_main_covered(ntiles, t_big, seg);
     const uint64_t ntail = ((bl - covered + kBlockBytes - 1) / kBlockBytes + kTailBlocks - 1) / kTailBlocks;
     const uint64_t items = ntiles + ntail;

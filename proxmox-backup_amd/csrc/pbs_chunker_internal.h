@@ -38,6 +38,11 @@ hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             uint64_t t_big = ~0ull);
 // One launch for a whole batch: scan + exact positions + resolve (scan_fused.h).  `seg`
 // and `dyn` from scan_main_plan; grid = one workgroup per CU.
+// scan_fused_kernel geometry (checked in scan_fused.h): 8 waves per workgroup, waves 0..2
+// of workgroup 0 resolve, every other wave scans tiles.
+constexpr int kFusedWavesPerWG = 8;
+constexpr int kFusedResolverWaves = 3;
+
 struct FusedPassArgs {
     // phase A
     const uint8_t* data;   // batch bytes [0, len) (device)

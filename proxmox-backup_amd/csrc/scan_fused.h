@@ -3,7 +3,8 @@
 // flagged 128-byte blocks, and phase B, the min/max rule of chunker.rs:172-183, resolved
 // while the scan runs.
 //
-//   scanner waves   every wave but one runs scan_main's tile loop.  A flagged block is a
+//   scanner waves   every wave but workgroup 0.s three resolver waves runs scan_main.s tile
+//                   loop (static order: a whole number of tiles each).  A flagged block is a
 //                   bit in the wave's LDS bitmap (no global atomic).  At the end of a tile
 //                   (ring registers dead, the next tile's first DMA in flight) the wave
 //                   evaluates its flagged blocks exactly (exact_block.h, one block per wave
@@ -41,6 +42,8 @@ constexpr int kFusedKeep = 512;     // open-chunk candidates the resolver keeps 
 constexpr int kStageCand = 512;     // candidates of one resolver step staged in LDS
 constexpr int kFusedHelpers = 2;    // resolver helper waves (workgroup 0, waves 1..2)
 constexpr uint32_t kRecOverflow = 0xFFFFu;
+static_assert(kFusedWavesPerWG == kWavesPerWG && kFusedResolverWaves == 1 + kFusedHelpers,
+              "pbs_chunker_internal.h describes this kernel's wave roles");
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
