@@ -8,16 +8,19 @@
 // whose bytes cannot be reproduced here: parity of the compressed bytes is UNPINNED;
 // what is pinned is decode(frame) == chunk and the blob rules of data_blob.rs:139-176.
 //
-// Parse (per 64 KiB block, positions in rounds of kRound):
-//   1. every position p of the round with 4 bytes left looks up h = hash(p) in a table
-//      holding, per hash, 1 + the last position of an EARLIER round with that hash;
+// Parse (per 64 KiB block, in 16 KiB sub-blocks -- one wave each on the GPU -- with their
+// own table; positions in rounds of kRound):
+//   1. every position p of the round with 4 bytes left looks up h = hash(p) in the
+//      sub-block's table, holding per hash 1 + the last position of an EARLIER round;
 //   2. then the round's positions are inserted (largest position wins);
 //   3. a candidate c matches if 4 bytes agree; its length is the common prefix, capped at
-//      kCap while matching (the parse extends a chosen capped match to its true end); when
+//      kCap while matching and at the sub-block end (the parse extends a chosen capped
+//      match to its true end inside the sub-block); when
 //      the table's candidate does not match, the run candidate p - 1 (offset 1) is tried,
 //      so a run of equal bytes is one match even inside the round it starts in;
 //   4. greedy: from the current position, the first matching position starts a sequence
-//      {literals since the last match, length, offset p - c}; parsing resumes after it.
+//      {literals since the last match, length, offset p - c}; parsing resumes after it
+//      (each sub-block starts at its first byte; literals carry over sub-block ends).
 #include <stdint.h>
 
 #include <cstring>
@@ -29,7 +32,7 @@ namespace {
 
 using namespace pbs::zstd;
 
-constexpr uint32_t kRound = 1024, kHashLog = 11, kCap = 32;
+constexpr uint32_t kRound = 256, kHashLog = 9, kCap = 32, kSub = 16384;
 
 inline uint32_t rd32(const uint8_t* p) {
     uint32_t v;
@@ -60,42 +63,47 @@ size_t block(const uint8_t* src, uint32_t n, bool last, uint8_t* out) {
         out[3] = src[0];
         return 4;
     }
-    std::vector<uint32_t> table(1u << kHashLog, 0), cand(kRound), mlen(kRound);
+    std::vector<uint32_t> table(1u << kHashLog), cand(kRound), mlen(kRound);
     std::vector<Seq> seqs;
     std::vector<uint8_t> lits;
-    uint32_t cur = 0, lit_start = 0;
-    for (uint32_t r0 = 0; r0 < n; r0 += kRound) {
-        const uint32_t r1 = r0 + kRound < n ? r0 + kRound : n;
-        for (uint32_t p = r0; p < r1; ++p) cand[p - r0] = p + 4 <= n ? table[hash4(rd32(src + p))] : 0;
-        for (uint32_t p = r0; p < r1 && p + 4 <= n; ++p) {
-            uint32_t& t = table[hash4(rd32(src + p))];
-            if (p + 1 > t) t = p + 1;
-        }
-        for (uint32_t p = r0; p < r1; ++p) {
-            const uint32_t lim = n - p < kCap ? n - p : kCap;
-            uint32_t L = 0;
-            if (cand[p - r0]) {
+    uint32_t lit_start = 0;
+    for (uint32_t s0 = 0; s0 < n; s0 += kSub) {  // sub-blocks: one wave each on the GPU
+        const uint32_t se = s0 + kSub < n ? s0 + kSub : n;
+        std::fill(table.begin(), table.end(), 0u);
+        uint32_t cur = s0;
+        for (uint32_t r0 = s0; r0 < se; r0 += kRound) {
+            const uint32_t r1 = r0 + kRound < se ? r0 + kRound : se;
+            for (uint32_t p = r0; p < r1; ++p) cand[p - r0] = p + 4 <= n ? table[hash4(rd32(src + p))] : 0;
+            for (uint32_t p = r0; p < r1 && p + 4 <= n; ++p) {
+                uint32_t& t = table[hash4(rd32(src + p))];
+                if (p + 1 > t) t = p + 1;
+            }
+            for (uint32_t p = r0; p < r1; ++p) {
+                const uint32_t lim = se - p < kCap ? se - p : kCap;
+                uint32_t L = 0;
+                if (cand[p - r0]) {
+                    const uint32_t c = cand[p - r0] - 1;
+                    while (L < lim && src[c + L] == src[p + L]) ++L;
+                }
+                if (L < 4 && p > 0) {  // else the run candidate p - 1 (offset 1)
+                    L = 0;
+                    while (L < lim && src[p - 1 + L] == src[p + L]) ++L;
+                    cand[p - r0] = L >= 4 ? p : cand[p - r0];  // 1 + (p - 1)
+                }
+                mlen[p - r0] = L >= 4 ? L : 0;
+            }
+            for (uint32_t p = r0 < cur ? cur : r0; p < r1; ++p) {
+                if (!mlen[p - r0]) continue;
                 const uint32_t c = cand[p - r0] - 1;
-                while (L < lim && src[c + L] == src[p + L]) ++L;
+                uint32_t L = mlen[p - r0];
+                if (L == kCap)
+                    while (p + L < se && src[c + L] == src[p + L]) ++L;
+                seqs.push_back({p - lit_start, L, p - c});
+                lits.insert(lits.end(), src + lit_start, src + p);
+                cur = p + L;
+                lit_start = cur;
+                p = cur - 1;
             }
-            if (L < 4 && p > 0) {  // else the run candidate p - 1 (offset 1)
-                L = 0;
-                while (L < lim && src[p - 1 + L] == src[p + L]) ++L;
-                cand[p - r0] = L >= 4 ? p : cand[p - r0];  // 1 + (p - 1)
-            }
-            mlen[p - r0] = L >= 4 ? L : 0;
-        }
-        for (uint32_t p = r0 < cur ? cur : r0; p < r1; ++p) {
-            if (!mlen[p - r0]) continue;
-            const uint32_t c = cand[p - r0] - 1;
-            uint32_t L = mlen[p - r0];
-            if (L == kCap)
-                while (p + L < n && src[c + L] == src[p + L]) ++L;
-            seqs.push_back({p - lit_start, L, p - c});
-            lits.insert(lits.end(), src + lit_start, src + p);
-            cur = p + L;
-            lit_start = cur;
-            p = cur - 1;
         }
     }
     lits.insert(lits.end(), src + lit_start, src + n);

@@ -47,8 +47,10 @@ namespace {
 using namespace zstd;
 
 constexpr int kZThreads = 256;
-constexpr uint32_t kZRound = 1024, kZHashLog = 11, kZCap = 32;
-constexpr int kZPer = kZRound / kZThreads;  // positions per thread and round
+constexpr uint32_t kZSub = 16384;                 // one wave's sub-block of a block
+constexpr uint32_t kZRound = 256, kZHashLog = 9, kZCap = 32;
+constexpr int kZPer = kZRound / 64;              // positions per lane and round
+constexpr uint32_t kSubSeq = kZSub / 4;          // sequences one sub-block can hold
 constexpr uint64_t kSlot = kEncBlock + 128;  // block header + up to 64 KiB + slack for 8-byte flushes
 constexpr uint32_t kMaxSeq = kEncBlock / 4;
 constexpr uint32_t kStageWords = kEncBlock / 16 + 1;  // 16-byte words covering a block at any alignment
@@ -64,10 +66,6 @@ struct ZTables {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
-    return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
-           ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
-}
 
 // The block staged in LDS: 16-byte words of the aligned span around it; block byte i is
 // LDS byte i + r (r = the block's address & 15).
@@ -130,8 +128,8 @@ __device__ __forceinline__ void copy_global(uint8_t* dst, const uint8_t* src, ui
 }
 
 // PBS_ZSTD_PROBE=1 (diagnostics): workgroup 0 adds wall-clock ticks (100 MHz) per phase
-// into g_zprobe: 0 stage, 1 RLE test, 2 rounds (lookups/matches), 3 parse (wave 0), 4
-// encode + literal copy, 5 raw copy, 6 items, 7 sequences.
+// into g_zprobe: 0 stage, 1 RLE test, 2 wave 0's sub-block (lookups, matches, parse), 3
+// combine (barrier included), 4 encode + literal copy, 5 raw copy, 6 items, 7 sequences.
 __device__ unsigned long long g_zprobe[8];
 
 template <bool PROBE>
@@ -139,19 +137,17 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, const ZTables* __restrict__ zt,
     uint8_t* __restrict__ slots, uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch,
-    uint2* __restrict__ run_scratch) {
+    Seq* __restrict__ seq_out_scratch) {
     __shared__ uint4 blk[kStageWords + 1];
-    __shared__ uint32_t table[1u << kZHashLog];
-    __shared__ uint8_t s_ml[kZRound];   // match length (<= kZCap), 0: none
-    __shared__ uint16_t s_c[kZRound];   // its candidate position
-    __shared__ unsigned long long s_mask[kZRound / 64];
+    __shared__ uint32_t table[kZThreads / 64][1u << kZHashLog];  // one per wave
+    __shared__ uint32_t s_wave[kZThreads / 64][3];               // per wave: sequences, matched bytes, end
     __shared__ ZTables s_zt;
     __shared__ uint32_t s_u[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (uint32_t i = tid; i < sizeof(ZTables) / 4; i += kZThreads)
         reinterpret_cast<uint32_t*>(&s_zt)[i] = reinterpret_cast<const uint32_t*>(zt)[i];
-    Seq* const seqs = seq_scratch + (uint64_t)blockIdx.x * kMaxSeq;
-    uint2* const runs = run_scratch + (uint64_t)blockIdx.x * kMaxSeq;
+    Seq* const wseq = seq_scratch + (uint64_t)blockIdx.x * kMaxSeq + (uint64_t)wave * kSubSeq;  // positions
+    Seq* const gseq = seq_out_scratch + (uint64_t)blockIdx.x * kMaxSeq;
 
     const bool probe = PROBE && blockIdx.x == 0 && tid == 0;
     uint64_t tp = probe ? wall_clock64() : 0;
@@ -233,97 +229,97 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             }
             continue;
         }
-        for (uint32_t i = tid; i < (1u << kZHashLog); i += kZThreads) table[i] = 0;
-        __syncthreads();
-        uint32_t cur = 0, lit_start = 0, ns = 0, lit_out = 0;  // wave 0 (uniform)
-        if (tid == 0) s_u[3] = 0;                               // cur, for the other waves
-        for (uint32_t r0 = 0; r0 < n; r0 += kZRound) {
-            // position r0 + tid + 256 i: lanes read consecutive bytes
-            uint32_t h[kZPer], c1[kZPer];
-            const uint32_t covered = s_u[3];  // positions below it lie inside a chosen match
-            // branch-free: every LDS read below is issued unconditionally at a clamped
-            // address and its value selected afterwards, so the reads of the 4 positions
-            // overlap (conditional reads became one basic block and one wait each)
+        // each wave parses its own 16 KiB sub-block with its own table: no workgroup
+        // barrier until the sequences are combined (a shared 1024-position round needed two
+        // per round and left the parse to one wave)
+        const uint32_t s0 = (uint32_t)wave * kZSub;
+        uint32_t ns = 0, msum = 0, cur = s0;  // wave-uniform
+        if (s0 < n) {
+            const uint32_t se = s0 + kZSub < n ? s0 + kZSub : n;
+            uint32_t* const tw = table[wave];
+#pragma unroll
+            for (int i = 0; i < (1 << kZHashLog) / 64; ++i) tw[lane + 64 * i] = 0;
             const uint32_t plim = n >= 4 ? n - 4 : 0;
-            uint32_t wp[kZPer], wm[kZPer];
+            for (uint32_t r0 = s0; r0 < se; r0 += kZRound) {
+                // branch-free lookups: every LDS read issued at a clamped address, the value
+                // selected after (conditional reads became a branch and a wait each)
+                uint32_t h[kZPer], c1[kZPer], wp[kZPer], wm[kZPer];
 #pragma unroll
-            for (int i = 0; i < kZPer; ++i) {
-                const uint32_t p = r0 + tid + kZThreads * i;
-                const uint32_t pc = p < plim ? p : plim;
-                wp[i] = S.word(pc);
-                wm[i] = S.word(pc ? pc - 1 : 0);  // p - 1: the run candidate (lane 0 needs it)
-            }
-#pragma unroll
-            for (int i = 0; i < kZPer; ++i) {
-                const uint32_t p = r0 + tid + kZThreads * i;
-                h[i] = (wp[i] * 2654435761u) >> (32 - kZHashLog);
-                const uint32_t t = table[h[i]];
-                // an AND, not a select: a select let the compiler sink the read into a branch
-                c1[i] = t & (0u - (uint32_t)(p + 4 <= n && p >= covered));
-            }
-            uint32_t wc[kZPer], wr[kZPer];
-#pragma unroll
-            for (int i = 0; i < kZPer; ++i) {
-                wc[i] = S.word(c1[i] ? c1[i] - 1 : 0);
-                const uint32_t up = (uint32_t)__shfl_up((int)wp[i], 1, 64);
-                wr[i] = lane ? up : wm[i];
-            }
-#pragma unroll
-            for (int i = 0; i < kZPer; ++i) {
-                const uint32_t p = r0 + tid + kZThreads * i;
-                const bool live = p + 4 <= n && p >= covered;
-                const bool mt = live && c1[i] && wc[i] == wp[i];
-                const bool mr = live && !mt && p > 0 && wr[i] == wp[i];
-                uint32_t L = 0, c = mr ? p - 1 : c1[i] - 1;
-                if (mt || mr) {  // rare: a match, extended to the cap
-                    const uint32_t lim = n - p < kZCap ? n - p : kZCap;
-                    L = 4 + common_prefix(S, c + 4, p + 4, lim - 4);
+                for (int i = 0; i < kZPer; ++i) {
+                    const uint32_t p = r0 + lane + 64 * i;
+                    const uint32_t pc = p < plim ? p : plim;
+                    wp[i] = S.word(pc);
+                    wm[i] = S.word(pc ? pc - 1 : 0);  // p - 1: the run candidate (lane 0)
                 }
-                s_ml[tid + kZThreads * i] = (uint8_t)L;
-                s_c[tid + kZThreads * i] = (uint16_t)c;
-                const unsigned long long m = __ballot(L != 0);
-                if (lane == 0) s_mask[i * (kZThreads / 64) + wave] = m;
-            }
-            __syncthreads();  // every lookup done (and the masks ready) before the inserts
-            mark(2);
-            // the round's inserts, while wave 0 parses (the next round's lookups see them)
 #pragma unroll
-            for (int i = 0; i < kZPer; ++i) {  // positions without 4 bytes insert 0: no effect
-                const uint32_t p = r0 + tid + kZThreads * i;
-                atomicMax(&table[h[i]], p + 4 <= n ? p + 1 : 0u);
-            }
-            if (wave == 0) {  // greedy parse of the round, wave-uniform
-                // the round's 16 mask words in lanes 0..15, the nonzero ones as a ballot: the
-                // next match is found in registers (a serial LDS scan of empty words cost
-                // ~16 LDS latencies per round on incompressible data)
-                const unsigned long long mword = lane < kZRound / 64 ? s_mask[lane] : 0ull;
-                const unsigned long long nzw = __ballot(mword != 0ull);
+                for (int i = 0; i < kZPer; ++i) {
+                    const uint32_t p = r0 + lane + 64 * i;
+                    h[i] = (wp[i] * 2654435761u) >> (32 - kZHashLog);
+                    const uint32_t t = tw[h[i]];
+                    // an AND, not a select: a select let the compiler sink the read into a branch
+                    c1[i] = t & (0u - (uint32_t)(p + 4 <= n && p < se && p >= cur));
+                }
+                uint32_t wc[kZPer], wr[kZPer];
+#pragma unroll
+                for (int i = 0; i < kZPer; ++i) {
+                    wc[i] = S.word(c1[i] ? c1[i] - 1 : 0);
+                    const uint32_t up = (uint32_t)__shfl_up((int)wp[i], 1, 64);
+                    wr[i] = lane ? up : wm[i];
+                }
+                uint32_t Lm[kZPer], Cm[kZPer];
+                unsigned long long m[kZPer];
+#pragma unroll
+                for (int i = 0; i < kZPer; ++i) {
+                    const uint32_t p = r0 + lane + 64 * i;
+                    const bool live = p + 4 <= n && p < se && p >= cur;
+                    const bool mt = live && c1[i] && wc[i] == wp[i];
+                    const bool mr = live && !mt && p > 0 && wr[i] == wp[i];
+                    uint32_t L = 0;
+                    const uint32_t c = mr ? p - 1 : c1[i] - 1;
+                    if (mt || mr) {  // rare: a match, extended to the cap (within the sub-block)
+                        const uint32_t lim = se - p < kZCap ? se - p : kZCap;
+                        L = lim >= 4 ? 4 + common_prefix(S, c + 4, p + 4, lim - 4) : 0;
+                    }
+                    Lm[i] = L;
+                    Cm[i] = c;
+                    m[i] = __ballot(L != 0);
+                }
+                // this round's inserts, after every lookup of the round (program order)
+#pragma unroll
+                for (int i = 0; i < kZPer; ++i) {
+                    const uint32_t p = r0 + lane + 64 * i;
+                    atomicMax(&tw[h[i]], p + 4 <= n && p < se ? p + 1 : 0u);
+                }
+                // greedy parse of the round from the match masks (wave-uniform)
                 uint32_t q = cur > r0 ? cur - r0 : 0;
                 while (q < kZRound) {
                     uint32_t w = q >> 6;
-                    unsigned long long mm = readlane64(mword, (int)w) & (~0ull << (q & 63));
-                    if (!mm) {
-                        const unsigned long long nz = w + 1 < 64 ? nzw & (~0ull << (w + 1)) : 0ull;
-                        if (!nz) break;
-                        w = (uint32_t)__builtin_ctzll(nz);
-                        mm = readlane64(mword, (int)w);
+                    unsigned long long mm = 0;
+                    for (; w < (uint32_t)kZPer; ++w) {
+                        mm = (w == 0 ? m[0] : w == 1 ? m[1] : w == 2 ? m[2] : m[3]) &
+                             (w == (q >> 6) ? (~0ull << (q & 63)) : ~0ull);
+                        if (mm) break;
                     }
-                    const uint32_t b = w * 64 + (uint32_t)__builtin_ctzll(mm);
-                    const uint32_t pp = r0 + b, c = s_c[b];
-                    uint32_t ml = s_ml[b];
-                    if (ml == kZCap) {  // extend a capped match: 4 bytes per lane, 256 per step
+                    if (!mm) break;
+                    const int l = __builtin_ctzll(mm);
+                    const uint32_t pp = r0 + w * 64 + (uint32_t)l;
+                    const uint32_t Lw = w == 0 ? Lm[0] : w == 1 ? Lm[1] : w == 2 ? Lm[2] : Lm[3];
+                    const uint32_t Cw = w == 0 ? Cm[0] : w == 1 ? Cm[1] : w == 2 ? Cm[2] : Cm[3];
+                    uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
+                    if (ml == kZCap) {  // extend to the sub-block end: a word per lane, 256 bytes a step
                         for (;;) {
                             const uint32_t x = pp + ml + 4 * lane;
                             uint32_t mis = 4;  // first mismatching byte of my 4 (4: none)
-                            if (x + 4 <= n) {
+                            if (x + 4 <= se) {
                                 const uint32_t d = S.word(c + ml + 4 * lane) ^ S.word(x);
                                 if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
                             } else {
                                 mis = 0;
-                                while (x + mis < n && S.byte(c + ml + 4 * lane + mis) == S.byte(x + mis)) ++mis;
-                                if (x >= n) mis = 0;
+                                while (x + mis < se && S.byte(c + ml + 4 * lane + mis) == S.byte(x + mis)) ++mis;
+                                if (x >= se) mis = 0;
                             }
-                            const unsigned long long bad = __ballot(mis < 4 || x + 4 > n);
+                            const unsigned long long bad = __ballot(mis < 4 || x + 4 > se);
                             if (bad) {
                                 const int f = __builtin_ctzll(bad);
                                 ml += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
@@ -332,45 +328,55 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                             ml += 256;
                         }
                     }
-                    if (lane == 0) {
-                        seqs[ns] = Seq{pp - lit_start, ml, pp - c};
-                        runs[ns] = make_uint2(lit_start, lit_out);
-                    }
-                    lit_out += pp - lit_start;
+                    if (lane == 0) wseq[ns] = Seq{pp, ml, pp - c};  // position form: ll comes later
                     ++ns;
+                    msum += ml;
                     cur = pp + ml;
-                    lit_start = cur;
                     q = cur - r0;
                 }
-                if (lane == 0) s_u[3] = cur;
             }
-            __syncthreads();  // inserts done, s_ml / s_c / s_mask free for the next round
-            mark(3);
         }
-        if (tid == 0) {
-            s_u[0] = ns;
-            s_u[1] = lit_out + (n - lit_start);
-            s_u[2] = lit_start;
+        if (lane == 0) {
+            s_wave[wave][0] = ns;
+            s_wave[wave][1] = msum;
+            s_wave[wave][2] = cur;
         }
+        mark(2);
         __syncthreads();
-        ns = s_u[0];
+        // combine the waves' sequences: literal length = position - end of the previous
+        // match (across sub-blocks: literals carry over), into LDS (the tables are free) or,
+        // when they do not fit, a contiguous global list
+        static_assert(kZThreads / 64 == 4, "four sub-blocks per block");
+        const uint32_t b1 = s_wave[0][0], b2 = b1 + s_wave[1][0], b3 = b2 + s_wave[2][0];
+        const uint32_t matched = s_wave[0][1] + s_wave[1][1] + s_wave[2][1] + s_wave[3][1];
+        ns = b3 + s_wave[3][0];
         if (probe) g_zprobe[7] += ns;
-        const uint32_t nlit = s_u[1], tail_start = s_u[2];
-        // the sequences and literal runs into LDS (the hash table's space is free now): the
-        // serial encoder and the run copies then read LDS, not the global list one latency
-        // at a time
-        constexpr uint32_t kLdsSeq = sizeof(table) / (sizeof(Seq) + sizeof(uint2));
-        uint2* const lrun = reinterpret_cast<uint2*>(table);
-        Seq* const lseq = reinterpret_cast<Seq*>(lrun + kLdsSeq);
-        const bool in_lds = ns <= kLdsSeq;
-        if (in_lds)
-            for (uint32_t q = tid; q < ns; q += kZThreads) {
-                lseq[q] = seqs[q];
-                lrun[q] = runs[q];
+        constexpr uint32_t kLdsSeq = sizeof(table) / sizeof(Seq);
+        Seq* const sq = ns <= kLdsSeq ? reinterpret_cast<Seq*>(&table[0][0]) : gseq;
+        const Seq* const pos0 = seq_scratch + (uint64_t)blockIdx.x * kMaxSeq;
+        auto at = [&](uint32_t q) -> Seq {  // q-th sequence (position form), selects only
+            const uint32_t w = (uint32_t)(q >= b1) + (uint32_t)(q >= b2) + (uint32_t)(q >= b3);
+            const uint32_t b = w == 0 ? 0 : w == 1 ? b1 : w == 2 ? b2 : b3;
+            return pos0[(uint64_t)w * kSubSeq + (q - b)];
+        };
+        for (uint32_t q = tid; q < ns; q += kZThreads) {
+            const Seq e = at(q);
+            uint32_t prev_end = 0;
+            if (q) {
+                const Seq f = at(q - 1);
+                prev_end = f.ll + f.ml;
+            }
+            sq[q] = Seq{e.ll - prev_end, e.ml, e.off};
+        }
+        uint32_t tail_start = 0;  // end of the last match
+        for (int w = kZThreads / 64 - 1; w >= 0; --w)
+            if (s_wave[w][0]) {
+                tail_start = s_wave[w][2];
+                break;
             }
         __syncthreads();
-        const Seq* const sq = in_lds ? lseq : seqs;
-        const uint2* const rq = in_lds ? lrun : runs;
+        mark(3);
+        const uint32_t nlit = n - matched;
         const uint32_t lith = nlit < 32 ? 1 : nlit < 4096 ? 2 : 3;
         const uint32_t seq_at = 3 + lith + nlit;
         bool raw = seq_at - 3 >= n;
@@ -381,21 +387,21 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                                                       out + 3 + n);
                     s_u[3] = sz == SIZE_MAX ? 0xFFFFFFFFu : (uint32_t)sz;
                 }
-            } else {  // waves 1-3: the literal runs (run ns: the bytes after the last match)
+            } else {  // waves 1-3: the literal runs in order (run ns: after the last match)
                 uint8_t* const lo = out + 3 + lith;
+                uint32_t from = 0, to = 0;
                 for (uint32_t q = 0; q <= ns; ++q) {
-                    uint32_t from, to, cnt;
+                    uint32_t cnt;
                     if (q < ns) {
-                        const uint2 ru = rq[q];
-                        from = ru.x;
-                        to = ru.y;
-                        cnt = sq[q].ll;
+                        const Seq e = sq[q];
+                        cnt = e.ll;
+                        copy_from_stage(lo + to, S, from, cnt, tid - 64, kZThreads - 64);
+                        from += cnt + e.ml;
                     } else {
-                        from = tail_start;
                         cnt = n - tail_start;
-                        to = nlit - cnt;
+                        copy_from_stage(lo + to, S, tail_start, cnt, tid - 64, kZThreads - 64);
                     }
-                    copy_from_stage(lo + to, S, from, cnt, tid - 64, kZThreads - 64);
+                    to += cnt;
                 }
             }
             __syncthreads();
@@ -493,7 +499,7 @@ struct ZScratch {
     uint8_t* slots = nullptr;
     size_t slots_cap = 0;
     Seq* seqs = nullptr;
-    uint2* runs = nullptr;
+    Seq* seqs_out = nullptr;  // the combined list when it does not fit in LDS
     size_t groups = 0;
     ZTables* zt = nullptr;
 };
@@ -524,11 +530,11 @@ extern "C" size_t pbs_zstd_frame_bound(size_t len) { return (size_t)zstd::frame_
 extern "C" void pbs_blob_encode_release(void) {
     ZScratch& z = zscratch();
     std::lock_guard<std::mutex> lk(z.mu);
-    for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.runs, (void*)z.zt})
+    for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.seqs_out, (void*)z.zt})
         if (p) (void)hipFree(p);
     z.slots = nullptr;
     z.seqs = nullptr;
-    z.runs = nullptr;
+    z.seqs_out = nullptr;
     z.zt = nullptr;
     z.slots_cap = 0;
     z.groups = 0;
@@ -607,14 +613,14 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
             zs.slots = nullptr;
             zs.slots_cap = 0;
             zs.seqs = nullptr;
-            zs.runs = nullptr;
+            zs.seqs_out = nullptr;
             zs.groups = 0;
             zs.zt = nullptr;
             zs.dev = dev;
         }
         size_t seq_cap = zs.groups * kMaxSeq, run_cap = zs.groups * kMaxSeq;
         if (!grow(&zs.slots, &zs.slots_cap, ni * kSlot) || !grow(&zs.seqs, &seq_cap, (size_t)grid * kMaxSeq) ||
-            !grow(&zs.runs, &run_cap, (size_t)grid * kMaxSeq)) {
+            !grow(&zs.seqs_out, &run_cap, (size_t)grid * kMaxSeq)) {
             fail(PBS_ERR_NOMEM);
         } else {
             zs.groups = std::max<size_t>(zs.groups, grid);
@@ -647,17 +653,17 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
             const unsigned long long z[8] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
             hipLaunchKernelGGL(zstd_block_kernel<true>, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds,
-                               d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.runs);
+                               d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.seqs_out);
             unsigned long long h[8] = {};
             (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
             (void)hipStreamSynchronize(st);
             std::fprintf(stderr,
-                         "zstd probe (workgroup 0, us): stage %.1f rle %.1f rounds %.1f parse %.1f encode+lits %.1f "
+                         "zstd probe (workgroup 0, us): stage %.1f rle %.1f sub-block %.1f combine %.1f encode+lits %.1f "
                          "raw %.1f | items %llu seqs %llu\n",
                          h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[4] / 100.0, h[5] / 100.0, h[6], h[7]);
         } else if (compress) {
             hipLaunchKernelGGL(zstd_block_kernel<false>, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds,
-                               d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.runs);
+                               d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.seqs_out);
         }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
