@@ -20,7 +20,10 @@
 //      so a run of equal bytes is one match even inside the round it starts in;
 //   4. greedy: from the current position, the first matching position starts a sequence
 //      {literals since the last match, length, offset p - c}; parsing resumes after it
-//      (each sub-block starts at its first byte; literals carry over sub-block ends).
+//      (each sub-block starts at its first byte; literals carry over sub-block ends);
+//   5. a round samples every step-th position: step 1 after a round with a match,
+//      doubling up to kMaxStep while rounds find none (incompressible data is crossed
+//      8x faster -- the acceleration of zstd's fast strategy, in round units).
 #include <stdint.h>
 
 #include <cstring>
@@ -32,7 +35,7 @@ namespace {
 
 using namespace pbs::zstd;
 
-constexpr uint32_t kRound = 256, kHashLog = 9, kCap = 32, kSub = 16384;
+constexpr uint32_t kRound = 256, kHashLog = 9, kCap = 32, kSub = 16384, kMaxStep = 8;
 
 inline uint32_t rd32(const uint8_t* p) {
     uint32_t v;
@@ -70,40 +73,54 @@ size_t block(const uint8_t* src, uint32_t n, bool last, uint8_t* out) {
     for (uint32_t s0 = 0; s0 < n; s0 += kSub) {  // sub-blocks: one wave each on the GPU
         const uint32_t se = s0 + kSub < n ? s0 + kSub : n;
         std::fill(table.begin(), table.end(), 0u);
-        uint32_t cur = s0;
-        for (uint32_t r0 = s0; r0 < se; r0 += kRound) {
-            const uint32_t r1 = r0 + kRound < se ? r0 + kRound : se;
-            for (uint32_t p = r0; p < r1; ++p) cand[p - r0] = p + 4 <= n ? table[hash4(rd32(src + p))] : 0;
-            for (uint32_t p = r0; p < r1 && p + 4 <= n; ++p) {
+        uint32_t cur = s0, step = 1;
+        for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
+            rn = r0 + kRound * step;  // the next round starts where this one's samples end
+            // the round's positions: r0 + j * step, j < kRound (step 1 after a match,
+            // doubling up to kMaxStep while rounds find none)
+            uint32_t pos[kRound];
+            uint32_t np = 0;
+            for (uint32_t j = 0; j < kRound && r0 + j * step < se; ++j) pos[np++] = r0 + j * step;
+            for (uint32_t k = 0; k < np; ++k) {
+                const uint32_t p = pos[k];
+                cand[k] = p + 4 <= n ? table[hash4(rd32(src + p))] : 0;
+            }
+            for (uint32_t k = 0; k < np; ++k) {
+                const uint32_t p = pos[k];
+                if (p + 4 > n) continue;
                 uint32_t& t = table[hash4(rd32(src + p))];
                 if (p + 1 > t) t = p + 1;
             }
-            for (uint32_t p = r0; p < r1; ++p) {
+            for (uint32_t k = 0; k < np; ++k) {
+                const uint32_t p = pos[k];
                 const uint32_t lim = se - p < kCap ? se - p : kCap;
                 uint32_t L = 0;
-                if (cand[p - r0]) {
-                    const uint32_t c = cand[p - r0] - 1;
+                if (cand[k]) {
+                    const uint32_t c = cand[k] - 1;
                     while (L < lim && src[c + L] == src[p + L]) ++L;
                 }
                 if (L < 4 && p > 0) {  // else the run candidate p - 1 (offset 1)
                     L = 0;
                     while (L < lim && src[p - 1 + L] == src[p + L]) ++L;
-                    cand[p - r0] = L >= 4 ? p : cand[p - r0];  // 1 + (p - 1)
+                    cand[k] = L >= 4 ? p : cand[k];  // 1 + (p - 1)
                 }
-                mlen[p - r0] = L >= 4 ? L : 0;
+                mlen[k] = L >= 4 ? L : 0;
             }
-            for (uint32_t p = r0 < cur ? cur : r0; p < r1; ++p) {
-                if (!mlen[p - r0]) continue;
-                const uint32_t c = cand[p - r0] - 1;
-                uint32_t L = mlen[p - r0];
+            bool found = false;
+            for (uint32_t k = 0; k < np; ++k) {
+                const uint32_t p = pos[k];
+                if (p < cur || !mlen[k]) continue;
+                const uint32_t c = cand[k] - 1;
+                uint32_t L = mlen[k];
                 if (L == kCap)
                     while (p + L < se && src[c + L] == src[p + L]) ++L;
                 seqs.push_back({p - lit_start, L, p - c});
                 lits.insert(lits.end(), src + lit_start, src + p);
                 cur = p + L;
                 lit_start = cur;
-                p = cur - 1;
+                found = true;
             }
+            step = found ? 1 : (step * 2 < kMaxStep ? step * 2 : kMaxStep);
         }
     }
     lits.insert(lits.end(), src + lit_start, src + n);

@@ -9,13 +9,18 @@
 // block (a 64 GiB stream is 1 M blocks), the block staged in LDS (16-byte loads of its
 // aligned span; every byte and word read after that is LDS: 2 workgroups per CU):
 //   1. RLE test (every byte equal: a 4-byte RLE block -- the zero pages of a VM image);
-//   2. match finding in rounds of 1024 positions, four per thread: hash of the 4 bytes at
-//      p -> candidate = the last position of an earlier round with that hash (LDS table,
-//      2 K entries, `atomicMax` inserts after the lookups), common prefix (word compares)
-//      capped at 32 -- skipped for positions inside the match the parse has chosen;
-//   3. greedy parse by wave 0 over the round's 1024-bit match mask (ballots):
-//      from the current position the next matching position starts a sequence, a capped
-//      match is extended 256 bytes per step (a word per lane, ballot of mismatches);
+//   2. each wave parses its own 16 KiB sub-block with its own 512-entry LDS table, in
+//      rounds of 256 sampled positions (4 per lane; every step-th byte: step 1 after a
+//      round with a match, doubling to 8 while rounds find none): hash of the 4 bytes at
+//      p -> candidate = the last sampled position of an earlier round with that hash
+//      (`ds_max` inserts after the round's lookups), else the run candidate p - 1; the
+//      4-byte compares and all LDS reads issued unconditionally; matches capped at 32
+//      and at the sub-block end; positions inside a chosen match skipped;
+//   3. the wave's greedy parse over the round's match masks (ballots, registers): from
+//      the current position the next matching position starts a sequence, a capped match
+//      is extended 256 bytes per step (a word per lane, ballot of mismatches) -- no
+//      workgroup barrier until the four waves' sequences are combined (literals carry
+//      over sub-block ends);
 //   4. wave 0 lane 0 writes the FSE-coded sequences (predefined tables) while waves 1-3
 //      copy the literal runs; raw block if that is not shorter.
 // Then per chunk: frame size, compressed-or-not (the reference's "only if shorter",
@@ -48,7 +53,7 @@ using namespace zstd;
 
 constexpr int kZThreads = 256;
 constexpr uint32_t kZSub = 16384;                 // one wave's sub-block of a block
-constexpr uint32_t kZRound = 256, kZHashLog = 9, kZCap = 32;
+constexpr uint32_t kZRound = 256, kZHashLog = 9, kZCap = 32, kZMaxStep = 8;
 constexpr int kZPer = kZRound / 64;              // positions per lane and round
 constexpr uint32_t kSubSeq = kZSub / 4;          // sequences one sub-block can hold
 constexpr uint64_t kSlot = kEncBlock + 128;  // block header + up to 64 KiB + slack for 8-byte flushes
@@ -240,20 +245,22 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
 #pragma unroll
             for (int i = 0; i < (1 << kZHashLog) / 64; ++i) tw[lane + 64 * i] = 0;
             const uint32_t plim = n >= 4 ? n - 4 : 0;
-            for (uint32_t r0 = s0; r0 < se; r0 += kZRound) {
+            uint32_t step = 1;  // positions sampled per round: 1 after a match, doubling to 8 without
+            for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
+                rn = r0 + kZRound * step;  // the next round starts where this one's samples end
                 // branch-free lookups: every LDS read issued at a clamped address, the value
                 // selected after (conditional reads became a branch and a wait each)
                 uint32_t h[kZPer], c1[kZPer], wp[kZPer], wm[kZPer];
 #pragma unroll
                 for (int i = 0; i < kZPer; ++i) {
-                    const uint32_t p = r0 + lane + 64 * i;
+                    const uint32_t p = r0 + (lane + 64 * i) * step;
                     const uint32_t pc = p < plim ? p : plim;
                     wp[i] = S.word(pc);
                     wm[i] = S.word(pc ? pc - 1 : 0);  // p - 1: the run candidate (lane 0)
                 }
 #pragma unroll
                 for (int i = 0; i < kZPer; ++i) {
-                    const uint32_t p = r0 + lane + 64 * i;
+                    const uint32_t p = r0 + (lane + 64 * i) * step;
                     h[i] = (wp[i] * 2654435761u) >> (32 - kZHashLog);
                     const uint32_t t = tw[h[i]];
                     // an AND, not a select: a select let the compiler sink the read into a branch
@@ -264,13 +271,13 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 for (int i = 0; i < kZPer; ++i) {
                     wc[i] = S.word(c1[i] ? c1[i] - 1 : 0);
                     const uint32_t up = (uint32_t)__shfl_up((int)wp[i], 1, 64);
-                    wr[i] = lane ? up : wm[i];
+                    wr[i] = lane && step == 1 ? up : wm[i];
                 }
                 uint32_t Lm[kZPer], Cm[kZPer];
                 unsigned long long m[kZPer];
 #pragma unroll
                 for (int i = 0; i < kZPer; ++i) {
-                    const uint32_t p = r0 + lane + 64 * i;
+                    const uint32_t p = r0 + (lane + 64 * i) * step;
                     const bool live = p + 4 <= n && p < se && p >= cur;
                     const bool mt = live && c1[i] && wc[i] == wp[i];
                     const bool mr = live && !mt && p > 0 && wr[i] == wp[i];
@@ -287,11 +294,13 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 // this round's inserts, after every lookup of the round (program order)
 #pragma unroll
                 for (int i = 0; i < kZPer; ++i) {
-                    const uint32_t p = r0 + lane + 64 * i;
+                    const uint32_t p = r0 + (lane + 64 * i) * step;
                     atomicMax(&tw[h[i]], p + 4 <= n && p < se ? p + 1 : 0u);
                 }
-                // greedy parse of the round from the match masks (wave-uniform)
-                uint32_t q = cur > r0 ? cur - r0 : 0;
+                // greedy parse of the round from the match masks (wave-uniform); bit q is
+                // position r0 + q * step
+                bool found = false;
+                uint32_t q = cur > r0 ? (cur - r0 + step - 1) / step : 0;
                 while (q < kZRound) {
                     uint32_t w = q >> 6;
                     unsigned long long mm = 0;
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                     }
                     if (!mm) break;
                     const int l = __builtin_ctzll(mm);
-                    const uint32_t pp = r0 + w * 64 + (uint32_t)l;
+                    const uint32_t pp = r0 + (w * 64 + (uint32_t)l) * step;
                     const uint32_t Lw = w == 0 ? Lm[0] : w == 1 ? Lm[1] : w == 2 ? Lm[2] : Lm[3];
                     const uint32_t Cw = w == 0 ? Cm[0] : w == 1 ? Cm[1] : w == 2 ? Cm[2] : Cm[3];
                     uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
@@ -332,8 +341,10 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                     ++ns;
                     msum += ml;
                     cur = pp + ml;
-                    q = cur - r0;
+                    q = (cur - r0 + step - 1) / step;
+                    found = true;
                 }
+                step = found ? 1 : (2 * step < kZMaxStep ? 2 * step : kZMaxStep);
             }
         }
         if (lane == 0) {
