@@ -15,9 +15,9 @@
 //   2. then the round's positions are inserted (largest position wins);
 //   3. a candidate c matches if 4 bytes agree; its length is the common prefix, capped at
 //      kCap while matching and at the sub-block end (the parse extends a chosen capped
-//      match to its true end inside the sub-block); when
-//      the table's candidate does not match, the run candidate p - 1 (offset 1) is tried,
-//      so a run of equal bytes is one match even inside the round it starts in;
+//      match to its true end inside the sub-block); the run candidate p - 1 (offset 1)
+//      is compared too and the longer match wins (ties: the table's), so a run of equal
+//      bytes is one match even inside the round it starts in;
 //   4. greedy: from the current position, the first matching position starts a sequence
 //      {literals since the last match, length, offset p - c}; parsing resumes after it
 //      (each sub-block starts at its first byte; literals carry over sub-block ends);
@@ -94,15 +94,16 @@ size_t block(const uint8_t* src, uint32_t n, bool last, uint8_t* out) {
             for (uint32_t k = 0; k < np; ++k) {
                 const uint32_t p = pos[k];
                 const uint32_t lim = se - p < kCap ? se - p : kCap;
-                uint32_t L = 0;
+                uint32_t L = 0, R = 0;
                 if (cand[k]) {
                     const uint32_t c = cand[k] - 1;
                     while (L < lim && src[c + L] == src[p + L]) ++L;
                 }
-                if (L < 4 && p > 0) {  // else the run candidate p - 1 (offset 1)
-                    L = 0;
-                    while (L < lim && src[p - 1 + L] == src[p + L]) ++L;
-                    cand[k] = L >= 4 ? p : cand[k];  // 1 + (p - 1)
+                if (p > 0)  // the run candidate p - 1 (offset 1); the longer one wins, ties the table's
+                    while (R < lim && src[p - 1 + R] == src[p + R]) ++R;
+                if (R >= 4 && R > (L >= 4 ? L : 0)) {
+                    L = R;
+                    cand[k] = p;  // 1 + (p - 1)
                 }
                 mlen[k] = L >= 4 ? L : 0;
             }

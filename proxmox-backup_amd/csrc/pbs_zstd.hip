@@ -13,8 +13,9 @@
 //      rounds of 256 sampled positions (4 per lane; every step-th byte: step 1 after a
 //      round with a match, doubling to 8 while rounds find none): hash of the 4 bytes at
 //      p -> candidate = the last sampled position of an earlier round with that hash
-//      (`ds_max` inserts after the round's lookups), else the run candidate p - 1; the
-//      4-byte compares and all LDS reads issued unconditionally; matches capped at 32
+//      (`ds_max` inserts after the round's lookups) or the run candidate p - 1, the
+//      longer match winning; the 4-byte compares and all LDS reads issued
+//      unconditionally; matches capped at 32
 //      and at the sub-block end; positions inside a chosen match skipped;
 //   3. the wave's greedy parse over the round's match masks (ballots, registers): from
 //      the current position the next matching position starts a sequence, a capped match
@@ -56,6 +57,7 @@ constexpr uint32_t kZSub = 16384;                 // one wave's sub-block of a b
 constexpr uint32_t kZRound = 256, kZHashLog = 9, kZCap = 32, kZMaxStep = 8;
 constexpr int kZPer = kZRound / 64;              // positions per lane and round
 constexpr uint32_t kSubSeq = kZSub / 4;          // sequences one sub-block can hold
+constexpr uint32_t kWaveLdsSeq = 64;             // of them kept in LDS (the rest in global scratch)
 constexpr uint64_t kSlot = kEncBlock + 128;  // block header + up to 64 KiB + slack for 8-byte flushes
 constexpr uint32_t kMaxSeq = kEncBlock / 4;
 constexpr uint32_t kStageWords = kEncBlock / 16 + 1;  // 16-byte words covering a block at any alignment
@@ -146,6 +148,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
     __shared__ uint4 blk[kStageWords + 1];
     __shared__ uint32_t table[kZThreads / 64][1u << kZHashLog];  // one per wave
     __shared__ uint32_t s_wave[kZThreads / 64][3];               // per wave: sequences, matched bytes, end
+    __shared__ Seq s_wseq[kZThreads / 64][kWaveLdsSeq];            // each wave's first sequences
     __shared__ ZTables s_zt;
     __shared__ uint32_t s_u[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -280,12 +283,20 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                     const uint32_t p = r0 + (lane + 64 * i) * step;
                     const bool live = p + 4 <= n && p < se && p >= cur;
                     const bool mt = live && c1[i] && wc[i] == wp[i];
-                    const bool mr = live && !mt && p > 0 && wr[i] == wp[i];
-                    uint32_t L = 0;
-                    const uint32_t c = mr ? p - 1 : c1[i] - 1;
-                    if (mt || mr) {  // rare: a match, extended to the cap (within the sub-block)
+                    const bool mr = live && p > 0 && wr[i] == wp[i];
+                    uint32_t L = 0, c = c1[i] - 1;
+                    if (mt || mr) {  // rare: matches extended to the cap (within the sub-block);
+                        // the run candidate p - 1 wins when longer (ties: the table's)
                         const uint32_t lim = se - p < kZCap ? se - p : kZCap;
-                        L = lim >= 4 ? 4 + common_prefix(S, c + 4, p + 4, lim - 4) : 0;
+                        if (lim >= 4) {
+                            const uint32_t Lt = mt ? 4 + common_prefix(S, c + 4, p + 4, lim - 4) : 0;
+                            const uint32_t Lr = mr ? 4 + common_prefix(S, p + 3, p + 4, lim - 4) : 0;
+                            L = Lt;
+                            if (Lr > Lt) {
+                                L = Lr;
+                                c = p - 1;
+                            }
+                        }
                     }
                     Lm[i] = L;
                     Cm[i] = c;
@@ -337,7 +348,12 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                             ml += 256;
                         }
                     }
-                    if (lane == 0) wseq[ns] = Seq{pp, ml, pp - c};  // position form: ll comes later
+                    if (lane == 0) {  // position form: ll comes later
+                        if (ns < kWaveLdsSeq)
+                            s_wseq[wave][ns] = Seq{pp, ml, pp - c};
+                        else
+                            wseq[ns] = Seq{pp, ml, pp - c};
+                    }
                     ++ns;
                     msum += ml;
                     cur = pp + ml;
@@ -368,7 +384,8 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         auto at = [&](uint32_t q) -> Seq {  // q-th sequence (position form), selects only
             const uint32_t w = (uint32_t)(q >= b1) + (uint32_t)(q >= b2) + (uint32_t)(q >= b3);
             const uint32_t b = w == 0 ? 0 : w == 1 ? b1 : w == 2 ? b2 : b3;
-            return pos0[(uint64_t)w * kSubSeq + (q - b)];
+            const uint32_t j = q - b;
+            return j < kWaveLdsSeq ? s_wseq[w][j] : pos0[(uint64_t)w * kSubSeq + j];
         };
         for (uint32_t q = tid; q < ns; q += kZThreads) {
             const Seq e = at(q);
