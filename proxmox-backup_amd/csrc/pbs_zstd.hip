@@ -115,23 +115,32 @@ __device__ __forceinline__ void copy_from_stage(uint8_t* dst, const Stage& S, ui
     for (uint32_t i = head + 4 * nwd + t; i < cnt; i += nt) dst[i] = (uint8_t)S.byte(from + i);
 }
 
-// n bytes global -> global at any alignments: dword stores at 4-aligned dst, each built
-// from the two aligned source dwords around it (never a page past a source byte).
+// n bytes global -> global at any alignments: 16-byte stores at 16-aligned dst, each built
+// from the five aligned source dwords around it (v_alignbyte; never a page past a source
+// byte), head and tail bytewise.
 __device__ __forceinline__ void copy_global(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t t,
                                             uint32_t nt) {
-    uint64_t head = (4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3;
+    uint64_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
     if (head > n) head = n;
     if (t < head) dst[t] = src[t];
     const uint8_t* const s2 = src + head;
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(s2) & 3);
     const uint32_t* const sa = reinterpret_cast<const uint32_t*>(s2 - sh);
-    const uint64_t nwd = (n - head) >> 2;
-    uint32_t* const dw = reinterpret_cast<uint32_t*>(dst + head);
-    for (uint64_t w = t; w < nwd; w += nt) {
-        const uint32_t lo = sa[w];
-        dw[w] = sh ? __builtin_amdgcn_alignbyte(sa[w + 1], lo, sh) : lo;
+    const uint64_t nq = (n - head) >> 4;
+    uint4* const dq = reinterpret_cast<uint4*>(dst + head);
+    for (uint64_t q = t; q < nq; q += nt) {
+        const uint32_t* const w = sa + 4 * q;
+        uint4 v;
+        if (sh) {
+            const uint32_t a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+            v = make_uint4(__builtin_amdgcn_alignbyte(b, a, sh), __builtin_amdgcn_alignbyte(c, b, sh),
+                           __builtin_amdgcn_alignbyte(d, c, sh), __builtin_amdgcn_alignbyte(e, d, sh));
+        } else {
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        dq[q] = v;
     }
-    for (uint64_t i = head + 4 * nwd + t; i < n; i += nt) dst[i] = src[i];
+    for (uint64_t i = head + 16 * nq + t; i < n; i += nt) dst[i] = src[i];
 }
 
 // PBS_ZSTD_PROBE=1 (diagnostics): workgroup 0 adds wall-clock ticks (100 MHz) per phase
