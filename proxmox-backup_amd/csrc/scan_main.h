@@ -20,6 +20,7 @@ constexpr int kWavesPerWG = 8;  // product geometry
 constexpr int kIter = 128;                       // bytes per lane per iteration
 constexpr int kStagePerWave = 64 * kIter;        // 8 KiB
 constexpr int kTableDwords = 256 * 64;           // 64 KiB
+constexpr int kSuspBuf = 128;                    // per-wave LDS list of suspect blocks (1 KiB)
 
 __device__ __forceinline__ uint32_t rotl1(uint32_t h) {
     return __builtin_amdgcn_alignbit(h, h, 31);
@@ -76,8 +77,10 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     constexpr int SEG2 = SEG / 4;  // DYN: segment length of the small tiles (t >= t_big)
     static_assert(SEG2 % kIter == 0, "small segment must be a multiple of the iteration size");
     constexpr int NW = kWavesPerWG;
-    // + 256 B per wave: landing area of the L2 "touch" DMAs (PF > 0)
-    __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4 + NW * 64];
+    // + 256 B per wave: landing area of the L2 "touch" DMAs (PF > 0); + 1 KiB per wave:
+    // the wave's suspect list
+    __shared__ __attribute__((aligned(16)))
+    uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4 + NW * 64 + NW * kSuspBuf * 2];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -93,6 +96,20 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
     uint8_t* touch_area = (uint8_t*)(s_lds + kTableDwords + NW * kStagePerWave / 4) + wave * 256;
     const uint32_t voff_touch = (uint32_t)lane * (uint32_t)SEG + 64u;
+    // Suspect blocks are collected per wave in LDS and appended to susp[] with one atomic
+    // per kSuspBuf - 63 or more: an atomic per suspect (the wave waiting for its return
+    // before the store) cost 26 % at 64 KiB averages (~1 suspect per 340 blocks).
+    uint64_t* s_susp = (uint64_t*)(s_lds + kTableDwords + NW * kStagePerWave / 4 + NW * 64) + wave * kSuspBuf;
+    uint32_t scnt = 0;  // wave-uniform
+    auto flush = [&]() {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(nsusp, (unsigned long long)scnt);
+        b = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+            __builtin_amdgcn_readfirstlane((uint32_t)b);
+        for (uint32_t i = lane; i < scnt; i += 64)
+            if (b + i < cap) susp[b + i] = s_susp[i];
+        scnt = 0;
+    };
     const uint32_t lanebase = (uint32_t)lane * 4u;
     const uint32_t lb0 = ((uint32_t)lane & 31u) * 4u, lb1 = lb0 + 128u;
     uint32_t voff[8];
@@ -247,18 +264,24 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
 #pragma unroll
                     for (int r = 64; r < 128; ++r) ring[r] = 0;
                 }
-            } else if (acc >= thr) {
+            } else {
                 const uint64_t pos =
                     toff + (uint64_t)lane * seg_cur + (uint64_t)(it - 1) * kIter;
-                if (pos != 0) {
-                    const uint64_t idx = atomicAdd(nsusp, 1ull);
-                    if (idx < cap) susp[idx] = pos;
+                const bool hit = acc >= thr && pos != 0;
+                const uint64_t m = __ballot(hit);
+                if (m) {
+                    const uint32_t pre =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (hit) s_susp[scnt + pre] = pos;
+                    scnt += (uint32_t)__popcll(m);
+                    if (scnt > (uint32_t)kSuspBuf - 64u) flush();
                 }
             }
         }
         tile = next_tile();
         if (tile >= ntiles) break;
     }
+    if (scnt) flush();
 #ifdef PBS_SCAN_PROBE  // scripts/microbench/scan_probe.py: per-wave finish time
     if (lane == 0 && blockIdx.x * NW + wave < kScanProbeMax)
         g_scan_probe[blockIdx.x * NW + wave] = wall_clock64();

@@ -216,8 +216,10 @@ PBS_HD inline size_t write_sequences(uint8_t* dst, const Seq* s, uint32_t ns, co
         b.add(q.ml - kMLBase[mlc], kMLBits[mlc]);
         b.add(ofv - (1u << ofc), ofc);
         b.flush();
+        Seq nx = ns >= 2 ? s[ns - 2] : Seq{0, 0, 0};  // one sequence ahead (hides the load)
         for (uint32_t k = ns - 1; k-- > 0;) {
-            const Seq& x = s[k];
+            const Seq x = nx;
+            if (k) nx = s[k - 1];
             const uint32_t lc = ll_code(x.ll), mc = ml_code(x.ml), ov = x.off + 3, oc = highbit(ov);
             sof.encode(b, tof, oc);
             sml.encode(b, tml, mc);
