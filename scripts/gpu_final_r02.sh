@@ -5,7 +5,7 @@
 # command, digest + blob + pipeline stages, configs 2 and 5, 64 KiB, examples.  Each GPU
 # step has its own time limit; the script stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-R="$(pwd)"; export TMPDIR=/tmp; O=gpurun_out/final_r02; mkdir -p $O
+R="$(pwd)"; export TMPDIR=/tmp; O=${OUT:-gpurun_out/final_r02}; mkdir -p $O
 step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
 step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread || exit 1
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
