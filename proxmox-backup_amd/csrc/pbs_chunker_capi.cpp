@@ -145,6 +145,10 @@ struct pbs_chunker {
     bool timing_pending = false;
     bool fused = true;        // PBS_FUSED=0: multi-launch path for every batch (A/B)
     bool fused_force = false; // PBS_FUSED=1: the fused pass for every batch it can serve (tests)
+    uint64_t fused_min_avg = 0;
+    int balance = 1;           // PBS_BALANCE=0: no priority trading between SIMD partners (A/B)
+    int scan_dyn_env = -1;         // PBS_SCAN_DYN=0/1: force the static / dynamic tile order
+    uint64_t fused_min_bytes = 0;  // smallest batch for the fused pass (PBS_FUSED_MIN_BYTES)  // smallest average served by the fused pass (PBS_FUSED_MIN_AVG: A/B)
     uint64_t susp_cap = 0, cand_cap = 0;
     uint64_t batch_limit = 0;  // bytes per batch (0 = batch_max); shrunk when a batch is too dense
     bool too_dense = false;    // the last scan found more than kMaxBatchCand candidates
@@ -236,7 +240,7 @@ int scan_launch(pbs_chunker* c, const uint8_t* d_data, uint64_t len, uint64_t ba
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, launch_scan_main(d_data, sp.ntiles, sp.seg, c->d_table.as<uint32_t>(), p.thr,
                                 c->d_susp.as<uint64_t>(), d_nsusp, c->susp_cap, c->cu, c->stream,
-                                reinterpret_cast<uint32_t*>(d_nsusp + 2), sp.dyn, sp.t_big));
+                                reinterpret_cast<uint32_t*>(d_nsusp + 2), sp.dyn, sp.t_big, c->balance != 0 && !sp.dyn));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     const uint64_t max_items = c->susp_cap + 1 + sp.ext_count;
     HIP_TRY(c, launch_scan_exact(d_data, len, c->d_pre.as<uint8_t>(), c->carry_len,
@@ -736,22 +740,74 @@ int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     return PBS_OK;
 }
 
+// Static tile order of the fused pass over `nw` scanner waves: every wave gets the same
+// work, and the tiles cover the batch up to less than one row of 64 blocks (8 KiB).  Tail
+// items (the bytes past the tiles) are evaluated block by block, which costs far more per
+// byte than the scan: with scan_main's power-of-two segments 8 GiB left 12 MiB of them
+// (+0.1 ms).  Rounds of tiles of q blocks (<= kFusedStaticSeg - 128 bytes), then one short
+// round (~q/8): the tiles of a round all end together, and the resolver gets the last
+// round's candidates only when the scan is over -- half of them at 2 rounds, a quarter-
+// second backlog at 256 KiB averages on 8 GiB.  Small batches: fewer tiles than waves (>= 4
+// KiB segments), one group.
+void fused_static_plan(uint64_t len, uint64_t nw, FusedPassArgs* a) {
+    const uint64_t rows = len / (64 * kBlockBytes);
+    const uint64_t qmax = (uint64_t)kFusedStaticSeg / kBlockBytes - 1, qmin = 32, qsmin = 8;
+    a->ntiles = a->t_long = a->t_small = a->t_small_long = 0;
+    a->seg_q = a->seg_qs = 0;
+    if (rows < qmin) return;  // all tail items
+    if (rows < qmin * nw * 9 / 8) {
+        const uint64_t nt = std::min(rows / qmin, nw);
+        a->ntiles = a->t_small = nt;
+        a->seg_q = (uint32_t)(rows / nt);
+        a->t_long = rows - (uint64_t)a->seg_q * nt;
+        return;
+    }
+    const uint64_t T = (rows + nw * qmax - 1) / (nw * qmax);  // rounds of full tiles
+    uint64_t q = std::min<uint64_t>(8 * rows / (nw * (8 * T + 1)), qmax);
+    uint64_t rem = rows - T * nw * q;
+    if (rem / nw < qsmin) {  // no short round: T rounds, the remainder spread over them
+        a->ntiles = a->t_small = T * nw;
+        a->seg_q = (uint32_t)(rows / a->ntiles);
+        a->t_long = rows - (uint64_t)a->seg_q * a->ntiles;
+        return;
+    }
+    a->seg_q = (uint32_t)q;
+    a->t_small = T * nw;
+    a->seg_qs = (uint32_t)(rem / nw);
+    a->t_small_long = rem - (uint64_t)a->seg_qs * nw;
+    a->ntiles = (T + 1) * nw;
+}
+
 // Averages served by the fused pass: at >= 128 KiB a tile (1-2 MiB) of random data holds
 // ~12-24 candidates, far below the 64 flagged blocks one tile's exact step takes.
 constexpr uint64_t kFusedMinAvg = 128 * 1024;
+constexpr uint64_t kFusedMinBytes = 0;
 
-// ... and batches large enough for the dynamic tile order (>= 32 GiB on 256 CUs): with
-// the static order of smaller batches (2-4 tiles per wave) the fused pass measured slower
-// than scan_main + resolve (8 GiB random: 1.76 vs 1.36-1.41 ms kernel,
-// profiles/r02/final/c2.log); PBS_FUSED=1 forces it (its parity tests run small inputs).
-bool use_fused(const pbs_chunker* c, uint64_t bl) {
-    if (!(c->fused && c->prm.hash_cuts && c->prm.avg >= kFusedMinAvg && bl > kFusedMaxBytes && c->cu >= 2))
-        return false;
-    if (c->fused_force) return true;
+// Tile order of the fused pass: static with SIMD balancing (the wave behind its SIMD partner
+// takes the issue priority, scan_fused.h) for averages >= kStaticMinAvg -- 64 GiB at 4 MiB:
+// 10.39-10.42 vs 10.64-10.66 ms dynamic, 8 GiB random 1.45-1.47 vs 1.49-1.52 ms -- and the
+// dynamic order of scan_main_plan below that (64 GiB at 256 KiB: 11.05-11.19 dynamic vs
+// 11.43-11.62 static, scripts/gpu_r02ak.sh / r02al.sh).  PBS_SCAN_DYN=0/1 forces one (A/B).
+constexpr uint64_t kStaticMinAvg = 1 << 20;
+bool fused_dynamic(const pbs_chunker* c, uint64_t bl) {
+    if (c->scan_dyn_env >= 0) return c->scan_dyn_env == 1;
     uint64_t nt = 0, tb = 0;
     bool dyn = false;
     (void)scan_main_plan(bl, c->cu, &nt, &dyn, &tb);
-    return dyn;
+    return dyn && c->prm.avg < kStaticMinAvg;
+}
+
+// The fused pass serves batches > 1 MiB at averages >= fused_min_avg: every such batch at
+// averages >= kStaticMinAvg (static order: faster than scan_main + resolve from 128 MiB to
+// 64 GiB, equal at 2-4 GiB, scripts/gpu_r02ak.sh), and batches in the dynamic order below
+// that.  PBS_FUSED=1 forces it for every batch it can serve (its parity tests run small
+// inputs), PBS_FUSED_MIN_BYTES raises the size threshold (A/B).
+bool use_fused(const pbs_chunker* c, uint64_t bl) {
+    if (!(c->fused && c->prm.hash_cuts && c->prm.avg >= c->fused_min_avg && bl > kFusedMaxBytes && c->cu >= 2))
+        return false;
+    if (c->fused_force) return true;
+    if (bl < c->fused_min_bytes) return false;
+    return c->prm.avg >= kStaticMinAvg || fused_dynamic(c, bl);
 }
 
 // One batch [pos, pos + bl) of device bytes `dsrc` (hsrc: the same bytes on the host, or
@@ -764,20 +820,20 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
                bool* done) {
     const Params& p = c->prm;
     *done = false;
-    uint64_t ntiles = 0, t_big = 0;
+    FusedPassArgs a{};
+    uint64_t ntiles = 0, t_big = 0, covered = 0;
     bool dyn = false;
-    const int seg = scan_main_plan(bl, c->cu, &ntiles, &dyn, &t_big);
-    if (!dyn) {
-        // static order over the cu * 8 - 3 scanner waves: a whole number of tiles per wave,
-        // the remainder as tail items every wave shares (with scan_main's tile count the
-        // first ntiles mod waves took one tile more: 8 GiB 1.84 vs 1.40 ms)
-        const uint64_t nw = (uint64_t)c->cu * kFusedWavesPerWG - kFusedResolverWaves;
-        if (ntiles >= nw && ntiles % nw) {
-            ntiles -= ntiles % nw;
-            t_big = std::min(t_big, ntiles);
-        }
+    // tile order: fused_dynamic (static with SIMD balancing at averages >= 1 MiB)
+    int seg = scan_main_plan(bl, c->cu, &ntiles, &dyn, &t_big);
+    dyn = dyn && fused_dynamic(c, bl);
+    if (dyn) {
+        covered = scan_main_covered(ntiles, t_big, seg);
+    } else {
+        fused_static_plan(bl, (uint64_t)c->cu * kFusedWavesPerWG - kFusedResolverWaves, &a);
+        ntiles = t_big = a.ntiles;
+        covered = ((a.t_small * a.seg_q + a.t_long) + (ntiles - a.t_small) * a.seg_qs + a.t_small_long) *
+                  64 * kBlockBytes;
     }
-    const uint64_t covered = scan_main_covered(ntiles, t_big, seg);
     const uint64_t ntail = ((bl - covered + kBlockBytes - 1) / kBlockBytes + kTailBlocks - 1) / kTailBlocks;
     const uint64_t items = ntiles + ntail;
     if (items == 0) return PBS_OK;
@@ -813,11 +869,11 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
         return rc;
     const uint64_t tl = std::min<uint64_t>(bl, kWindow - 1);
     unsigned long long* ctr = c->d_counters.as<unsigned long long>();
-    FusedPassArgs a{};
     a.data = dsrc;
     a.len = bl;
     a.ntiles = ntiles;
     a.t_big = t_big;
+    a.balance = (uint32_t)c->balance;
     a.table_rot = c->d_table.as<uint32_t>();
     a.thr = p.thr;
     a.tile_ctr = reinterpret_cast<uint32_t*>(ctr + 2);
@@ -1114,6 +1170,12 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
         c->fused_force = e[0] == '1';
     }
     if (const char* e = std::getenv("PBS_SCAN_SERVER")) c->srv.enabled = e[0] != '0';
+    c->fused_min_avg = kFusedMinAvg;
+    if (const char* e = std::getenv("PBS_BALANCE")) c->balance = std::atoi(e);
+    if (const char* e = std::getenv("PBS_SCAN_DYN")) c->scan_dyn_env = e[0] == '1' ? 1 : 0;
+    c->fused_min_bytes = kFusedMinBytes;
+    if (const char* e = std::getenv("PBS_FUSED_MIN_BYTES")) c->fused_min_bytes = std::strtoull(e, nullptr, 0);
+    if (const char* e = std::getenv("PBS_FUSED_MIN_AVG")) c->fused_min_avg = std::strtoull(e, nullptr, 0);
     bool ok = hipGetDevice(&c->device) == hipSuccess;
     hipDeviceProp_t prop;
     if (ok && hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)

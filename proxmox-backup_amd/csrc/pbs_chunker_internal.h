@@ -35,7 +35,7 @@ hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
                             unsigned long long* nsusp, uint64_t cap, int grid, hipStream_t stream,
                             uint32_t* tile_ctr = nullptr, bool dynamic = false,
-                            uint64_t t_big = ~0ull);
+                            uint64_t t_big = ~0ull, bool balance = false);
 // One launch for a whole batch: scan + exact positions + resolve (scan_fused.h).  `seg`
 // and `dyn` from scan_main_plan; grid = one workgroup per CU.
 // scan_fused_kernel geometry (checked in scan_fused.h): 8 waves per workgroup, waves 0..2
@@ -47,7 +47,13 @@ struct FusedPassArgs {
     // phase A
     const uint8_t* data;   // batch bytes [0, len) (device)
     uint64_t len;
-    uint64_t ntiles, t_big;
+    uint64_t ntiles, t_big;     // dynamic order: tiles, first small tile
+    // static order (fused_static_plan): tiles [0, t_small) have segments of seg_q 128-byte
+    // blocks, the first t_long of them one more; tiles [t_small, ntiles) -- the last, short
+    // round -- seg_qs blocks, the first t_small_long of them one more
+    uint32_t seg_q, seg_qs;
+    uint64_t t_long, t_small, t_small_long;
+    uint32_t balance;           // SIMD partners trade issue priority by progress (PBS_BALANCE)
     const uint32_t* table_rot;  // T' (256 words)
     uint32_t thr;
     uint32_t* tile_ctr;         // zeroed device counter (dynamic tile order)
@@ -92,6 +98,7 @@ struct FusedPassArgs {
 };
 
 constexpr int kTailBlocks = 64;     // blocks per tail item of the fused pass
+constexpr int kFusedStaticSeg = 40960;  // static-order fused pass: longest segment (bitmap size)
 constexpr int kResolveBatch = 256;  // tile records per resolver step (4 per lane)
 hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid, hipStream_t stream);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,

@@ -868,22 +868,24 @@ uint64_t scan_main_covered(uint64_t ntiles, uint64_t t_big, int seg) {
 hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
                             const uint32_t* table_rot, uint32_t thr, uint64_t* susp,
                             unsigned long long* nsusp, uint64_t cap, int grid, hipStream_t stream,
-                            uint32_t* tile_ctr, bool dynamic, uint64_t t_big) {
+                            uint32_t* tile_ctr, bool dynamic, uint64_t t_big, bool balance) {
     if (ntiles == 0) return hipSuccess;
     (void)hipGetLastError();  // launch errors below must not be confused with stale ones
     const uint64_t need = (ntiles + kWavesPerWG - 1) / kWavesPerWG;
     const int g = (uint64_t)grid < need ? grid : (int)need;
     const dim3 gd(g), bd(kWavesPerWG * 64);
     const bool dyn = tile_ctr && dynamic;  // tile_ctr: a zeroed device counter
+    const uint32_t bal = balance ? 1u : 0u;
 #define PBS_SCAN_CASE(S)                                                                          \
     case S:                                                                                       \
         if (dyn)                                                                                  \
             hipLaunchKernelGGL((scan_main_kernel<S, kModeFull, 2, 4, 0, 0, kScanFrame, 1>), gd, bd, 0, \
                                stream, data, ntiles, table_rot, thr, susp, nsusp, cap, tile_ctr,    \
-                               t_big);                                                             \
+                               t_big, bal);                                                        \
         else                                                                                      \
             hipLaunchKernelGGL((scan_main_kernel<S, kModeFull, 2, 4, 0, 0, kScanFrame, 0>), gd, bd, 0, \
-                               stream, data, ntiles, table_rot, thr, susp, nsusp, cap, nullptr);    \
+                               stream, data, ntiles, table_rot, thr, susp, nsusp, cap, nullptr,     \
+                               ~0ull, bal);                                                        \
         break;
     switch (seg) {
         PBS_SCAN_CASE(32768)
@@ -901,19 +903,16 @@ hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid
     if (a.ntiles + a.ntail == 0 || grid < 1) return hipErrorInvalidValue;
     (void)hipGetLastError();
     const dim3 gd(grid), bd(kWavesPerWG * 64);
-    // the dynamic tile order only ever uses 16 / 8 KiB segments (scan_main_plan)
+    // the dynamic tile order only ever uses 16 / 8 KiB segments (scan_main_plan); the
+    // static order has runtime segment lengths up to kFusedStaticSeg (fused_static_plan)
     if (dyn && seg == 16384)
         hipLaunchKernelGGL((scan_fused_kernel<16384, 1>), gd, bd, 0, stream, a);
     else if (dyn && seg == 8192)
         hipLaunchKernelGGL((scan_fused_kernel<8192, 1>), gd, bd, 0, stream, a);
-    else if (!dyn && seg == 32768)
-        hipLaunchKernelGGL((scan_fused_kernel<32768, 0>), gd, bd, 0, stream, a);
-    else if (!dyn && seg == 16384)
-        hipLaunchKernelGGL((scan_fused_kernel<16384, 0>), gd, bd, 0, stream, a);
-    else if (!dyn && seg == 8192)
-        hipLaunchKernelGGL((scan_fused_kernel<8192, 0>), gd, bd, 0, stream, a);
-    else if (!dyn && seg == 4096)
-        hipLaunchKernelGGL((scan_fused_kernel<4096, 0>), gd, bd, 0, stream, a);
+    else if (!dyn && a.seg_q + (a.t_long ? 1u : 0u) <= (uint32_t)kFusedStaticSeg / kBlockBytes &&
+             a.seg_qs + (a.t_small_long ? 1u : 0u) <= (uint32_t)kFusedStaticSeg / kBlockBytes &&
+             a.t_small <= a.ntiles)
+        hipLaunchKernelGGL((scan_fused_kernel<kFusedStaticSeg, 0>), gd, bd, 0, stream, a);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -1039,6 +1038,10 @@ hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t wo
 #ifdef PBS_SCAN_PROBE
 // probe build only (scripts/microbench/scan_probe.py): the per-wave finish times of the
 // last scan_main launch, wall_clock64 ticks (100 MHz)
+extern "C" int pbs_fused_probe_read(uint64_t* out) {  // 4 * 4096: start, tiles done, done, SIMD
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pbs::g_fused_probe), sizeof(pbs::g_fused_probe)) == hipSuccess
+               ? 0 : -1;
+}
 extern "C" int pbs_scan_probe_read(uint64_t* out) {  // 2 * 4096: finish, then start times
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(pbs::g_scan_probe), sizeof(pbs::g_scan_probe)) == hipSuccess
                ? 0 : -1;

@@ -41,6 +41,8 @@ namespace pbs {
 constexpr int kFusedKeep = 512;     // open-chunk candidates the resolver keeps in LDS
 constexpr int kStageCand = 512;     // candidates of one resolver step staged in LDS
 constexpr int kFusedHelpers = 2;    // resolver helper waves (workgroup 0, waves 1..2)
+constexpr int kPubDepth = 8;        // exact windows in flight per wave (fused_publish)
+
 constexpr uint32_t kRecOverflow = 0xFFFFu;
 static_assert(kFusedWavesPerWG == kWavesPerWG && kFusedResolverWaves == 1 + kFusedHelpers,
               "pbs_chunker_internal.h describes this kernel's wave roles");
@@ -62,19 +64,30 @@ __device__ __forceinline__ void fused_publish(const FusedPassArgs& a, const uint
                                               int lane) {
     uint4 mh = make_uint4(0, 0, 0, 0);
     if (nb > 0 && !over) {
-        int64_t B = (int64_t)readlane64((uint64_t)myB, 0);
-        uint32_t wv = exact_load(a.data, a.len, a.pre, a.pre_len, B, lane);
-        for (int j = 0; j < nb; ++j) {  // the window of block j+1 loads while j is hashed
-            int64_t Bn = 0;
-            uint32_t wvn = 0;
-            if (j + 1 < nb) {
-                Bn = (int64_t)readlane64((uint64_t)myB, j + 1);
-                wvn = exact_load(a.data, a.len, a.pre, a.pre_len, Bn, lane);
+        // groups of kPubDepth blocks: the windows of group g+1 load while group g is hashed
+        // (one block at a time waited a memory latency per block: a 64-block tail item,
+        // never streamed before, cost ~64 HBM round trips -- 8 GiB static order: +0.1 ms)
+        uint32_t cur[kPubDepth], nxt[kPubDepth];
+        auto load_group = [&](int g, uint32_t (&w)[kPubDepth]) {
+#pragma unroll
+            for (int k = 0; k < kPubDepth; ++k)
+                w[k] = g + k < nb ? exact_load(a.data, a.len, a.pre, a.pre_len,
+                                               (int64_t)readlane64((uint64_t)myB, g + k), lane)
+                                  : 0u;
+        };
+        load_group(0, cur);
+        for (int g = 0; g < nb; g += kPubDepth) {
+            if (g + kPubDepth < nb) load_group(g + kPubDepth, nxt);
+#pragma unroll
+            for (int k = 0; k < kPubDepth; ++k) {
+                if (g + k < nb) {
+                    const int64_t B = (int64_t)readlane64((uint64_t)myB, g + k);
+                    const uint4 h = exact_hits<true>(cur[k], a.len, a.pre_len, B, tab, a.thr, 0u, lane);
+                    if (lane == g + k) mh = h;
+                }
             }
-            const uint4 h = exact_hits<true>(wv, a.len, a.pre_len, B, tab, a.thr, 0u, lane);
-            if (lane == j) mh = h;
-            B = Bn;
-            wv = wvn;
+#pragma unroll
+            for (int k = 0; k < kPubDepth; ++k) cur[k] = nxt[k];
         }
     }
     const uint32_t cnt = __builtin_popcount(mh.x) + __builtin_popcount(mh.y) +
@@ -498,6 +511,15 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
     }
 }
 
+#ifdef PBS_SCAN_PROBE  // scripts/microbench/fused_probe.py: per-wave start / tiles done / done
+__device__ uint64_t g_fused_probe[4 * kScanProbeMax];  // start, tiles done, done, SIMD
+#define PBS_FUSED_STAMP(k)                                                               \
+    if (lane == 0 && blockIdx.x * NW + wave < kScanProbeMax)                             \
+        g_fused_probe[(k) * kScanProbeMax + blockIdx.x * NW + wave] = wall_clock64();
+#else
+#define PBS_FUSED_STAMP(k)
+#endif
+
 // SEG: segment bytes per lane (16/32 KiB: the fused pass serves batches of >= 1 MiB);
 // DYN: tile order as scan_main_kernel.  8 waves per workgroup, one workgroup per CU.
 template <int SEG, int DYN>
@@ -508,14 +530,32 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     constexpr int NBW = SEG / kIter / 32;  // bitmap words per lane (one bit per block)
     __shared__ __attribute__((aligned(16))) uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4];
     __shared__ uint32_t s_bm[NW * 64 * NBW];
+    __shared__ uint32_t s_simd[NW], s_prog[NW];  // SIMD of each wave; blocks scanned so far
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < kTableDwords; i += NW * 64) s_lds[i] = a.table_rot[i >> 6];
     for (int i = tid; i < NW * 64 * NBW; i += NW * 64) s_bm[i] = 0;
+    if (lane == 0) {
+        s_simd[wave] = (__builtin_amdgcn_s_getreg(kHwRegHwId) >> 4) & 3u;  // HW_ID.SIMD_ID
+        s_prog[wave] = 0;
+    }
     __syncthreads();
+    // SIMD partner: the other wave of this workgroup on the same SIMD (the issue arbiter
+    // favours the older one by ~30 %: probe, scripts/microbench/fused_probe.py), or none
+    int partner = wave;
+    for (int w = 0; w < NW; ++w)
+        if (w != wave && s_simd[w] == s_simd[wave]) partner = w;
+    partner = __builtin_amdgcn_readfirstlane(partner);
+    const bool balance = a.balance != 0 && partner != wave;  // equal progress of SIMD partners
+    const bool bal_sleep = a.balance == 2;
+#ifdef PBS_SCAN_PROBE
+    if (lane == 0 && blockIdx.x * NW + wave < kScanProbeMax)
+        g_fused_probe[3 * kScanProbeMax + blockIdx.x * NW + wave] = s_simd[wave] | ((uint64_t)partner << 8);
+#endif
     uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
+    PBS_FUSED_STAMP(0)
     if (blockIdx.x == 0 && wave == 0) {
         fused_main(a, reinterpret_cast<uint64_t*>(stage), lane);
         return;
@@ -527,33 +567,56 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     uint32_t* bm = s_bm + wave * 64 * NBW + lane * NBW;
 
     const uint32_t lanebase = (uint32_t)lane * 4u;
+    // LDS-DMA lane offsets of a tile with segments of `seg` bytes: instruction j stages
+    // lines of segments 8j..8j+7, chunk k of lane l's line at the XOR-swizzled slot
     uint32_t voff[8], voff2[8];
+    auto set_voff = [&](uint32_t (&v)[8], uint32_t seg) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const uint32_t l = 8u * j + ((uint32_t)lane >> 3);
-        const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
-        voff[j] = l * (uint32_t)SEG + k * 16u;
-        voff2[j] = l * (uint32_t)SEG2 + k * 16u;
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t l = 8u * j + ((uint32_t)lane >> 3);
+            const uint32_t k = ((uint32_t)lane & 7u) ^ ((l >> 1) & 7u);
+            v[j] = l * seg + k * 16u;
+        }
+    };
+    if constexpr (DYN != 0) {
+        set_voff(voff, (uint32_t)SEG);
+        set_voff(voff2, (uint32_t)SEG2);
     }
     const uint32_t rd_base = (uint32_t)lane * 128u;
     const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
-    constexpr int NIT = SEG / kIter + 1;
     // scanner waves: all but workgroup 0's resolver waves
     const uint64_t nw = (uint64_t)gridDim.x * NW - (1 + kFusedHelpers);
     uint64_t tile = (uint64_t)blockIdx.x * NW + wave - (1 + kFusedHelpers);
     const uint64_t ntiles = a.ntiles, t_big = a.t_big;
     const uint8_t* data = a.data;
 
+    // tile geometry.  DYN: SEG-byte segments, SEG2 from tile t_big on.  Static: two groups
+    // of runtime segment lengths (FusedPassArgs; the host sizes them so the tiles cover the
+    // batch up to < 8 KiB, every scanner wave gets the same work, and the last round is short)
+    auto tile_nit = [&](uint64_t t) -> uint32_t {  // blocks per segment
+        if constexpr (DYN != 0)
+            return (uint32_t)((t >= t_big ? SEG2 : SEG) / kIter);
+        else
+            return t < a.t_small ? a.seg_q + (t < a.t_long ? 1u : 0u)
+                                 : a.seg_qs + (t - a.t_small < a.t_small_long ? 1u : 0u);
+    };
     auto tile_off = [&](uint64_t t) -> uint64_t {
-        if (DYN != 0 && t >= t_big) return t_big * (64ull * SEG) + (t - t_big) * (64ull * SEG2);
-        return t * (64ull * SEG);
+        if constexpr (DYN != 0) {
+            if (t >= t_big) return t_big * (64ull * SEG) + (t - t_big) * (64ull * SEG2);
+            return t * (64ull * SEG);
+        } else {
+            if (t < a.t_small) return (t * a.seg_q + (t < a.t_long ? t : a.t_long)) * (64ull * kIter);
+            const uint64_t u = t - a.t_small;
+            return (a.t_small * a.seg_q + a.t_long + u * a.seg_qs +
+                    (u < a.t_small_long ? u : a.t_small_long)) * (64ull * kIter);
+        }
     };
     auto issue = [&](uint64_t t, int it) {  // scan_main_kernel's LDS-DMA of one iteration
         const bool sm = DYN != 0 && t >= t_big;
         const uint8_t* tb = data + tile_off(t);
         const bool first = (t == 0);
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(first ? tb : tb - kIter), 0, (int)(64u * (sm ? SEG2 : SEG) + kIter), 0x00020000);
+            (void*)(first ? tb : tb - kIter), 0, (int)(64u * tile_nit(t) * kIter + kIter), 0x00020000);
         const bool warm0 = first && it == 0;
         const uint32_t soff = warm0 ? 0u : (uint32_t)it * kIter - (first ? (uint32_t)kIter : 0u);
         if (sm) {
@@ -621,24 +684,29 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
         for (int r = 0; r < 128; ++r) ring[r] = 0;
         uint32_t h = 0;
         uint32_t dyn_v = 0;
+        uint32_t prog = 0;  // blocks scanned (wave-uniform)
         auto next_tile = [&]() -> uint64_t {
             if constexpr (DYN != 0)
                 return nw + (uint64_t)__builtin_amdgcn_readfirstlane(dyn_v);
             else
                 return tile + nw;
         };
+        if constexpr (DYN == 0) set_voff(voff, tile_nit(tile) * kIter);
         issue(tile, 0);
         for (;;) {
             if constexpr (DYN != 0) {
                 if (lane == 0) dyn_v = atomicAdd(a.tile_ctr, 1u);
             }
-            const bool small = DYN != 0 && tile >= t_big;
-            const int nit_cur = small ? SEG2 / kIter + 1 : NIT;
+            const int nit_cur = (int)tile_nit(tile) + 1;  // + the warm-up block
             const uint64_t toff = tile_off(tile);
-            const uint32_t seg_cur = small ? (uint32_t)SEG2 : (uint32_t)SEG;
+            const uint32_t seg_cur = tile_nit(tile) * kIter;
             for (int it = 0; it < nit_cur; ++it) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 uint32_t d[32];
+                if (balance) {
+                    if (lane == 0) s_prog[wave] = prog;
+                }
+                const uint32_t pprog = balance ? s_prog[partner] : 0u;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const uint4 v = *(const uint4*)(stage + rd_base + (((uint32_t)k ^ rsw) << 4));
@@ -648,12 +716,26 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
                     d[4 * k + 3] = v.w;
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (balance) {
+                    // the wave behind its SIMD partner takes the issue priority until it
+                    // has caught up, so both finish together
+                    const uint32_t pp = __builtin_amdgcn_readfirstlane(pprog);
+                    if (pp > prog)
+                        __builtin_amdgcn_s_setprio(2);
+                    else
+                        __builtin_amdgcn_s_setprio(0);
+                    if (bal_sleep && prog > pp + 2) __builtin_amdgcn_s_sleep(1);  // ahead: yield
+                    ++prog;
+                }
                 {
                     uint64_t nt = tile;
                     int nit = it + 1;
                     if (nit == nit_cur) {
                         nt = next_tile();
                         nit = 0;
+                        // static order: the next tile's segment length (this tile issues no more)
+                        if constexpr (DYN == 0)
+                            if (nt < ntiles) set_voff(voff, tile_nit(nt) * kIter);
                     }
                     if (nt < ntiles) issue(nt, nit);
                 }
@@ -679,6 +761,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
             if (tile >= ntiles) break;
         }
     }
+    PBS_FUSED_STAMP(1)
     // the bytes past the last tile: items of kTailBlocks consecutive blocks
     const uint64_t nblk = (a.len + kIter - 1) / kIter;
     while (tile < ntiles + a.ntail) {
@@ -693,6 +776,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
             tile += nw;
         }
     }
+    PBS_FUSED_STAMP(2)
 }
 
 }  // namespace pbs

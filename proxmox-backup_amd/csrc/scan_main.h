@@ -21,6 +21,8 @@ constexpr int kIter = 128;                       // bytes per lane per iteration
 constexpr int kStagePerWave = 64 * kIter;        // 8 KiB
 constexpr int kTableDwords = 256 * 64;           // 64 KiB
 constexpr int kSuspBuf = 128;                    // per-wave LDS list of suspect blocks (1 KiB)
+// s_getreg_b32 operand for HW_REG_HW_ID (id 4, offset 0, 32 bits): SIMD_ID in bits 5:4
+constexpr int kHwRegHwId = 4 | (31 << 11);
 
 __device__ __forceinline__ uint32_t rotl1(uint32_t h) {
     return __builtin_amdgcn_alignbit(h, h, 31);
@@ -72,7 +74,7 @@ template <int SEG, int MODE = kModeFull, int AUX = 2, int G = 4, int PF = 0, int
 __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     const uint8_t* __restrict__ data, uint64_t ntiles, const uint32_t* __restrict__ table_rot,
     uint32_t thr, uint64_t* __restrict__ susp, unsigned long long* __restrict__ nsusp, uint64_t cap,
-    uint32_t* __restrict__ tile_ctr = nullptr, uint64_t t_big = ~0ull) {
+    uint32_t* __restrict__ tile_ctr = nullptr, uint64_t t_big = ~0ull, uint32_t balance_on = 0) {
     static_assert(SEG % kIter == 0, "segment must be a multiple of the iteration size");
     constexpr int SEG2 = SEG / 4;  // DYN: segment length of the small tiles (t >= t_big)
     static_assert(SEG2 % kIter == 0, "small segment must be a multiple of the iteration size");
@@ -82,9 +84,15 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
     __shared__ __attribute__((aligned(16)))
     uint32_t s_lds[kTableDwords + NW * kStagePerWave / 4 + NW * 64 + NW * kSuspBuf * 2];
 
+    __shared__ uint32_t s_simd[NW], s_prog[NW];  // SIMD of each wave; blocks scanned so far
+
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (lane == 0) {
+        s_simd[wave] = (__builtin_amdgcn_s_getreg(kHwRegHwId) >> 4) & 3u;  // HW_ID.SIMD_ID
+        s_prog[wave] = 0;
+    }
     if constexpr (FR == 2) {
         for (int i = tid; i < kTableDwords; i += NW * 64)
             s_lds[i] = table_rot[((i >> 5) & 1) * 256 + (i >> 6)];
@@ -92,6 +100,16 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
         for (int i = tid; i < kTableDwords; i += NW * 64) s_lds[i] = table_rot[i >> 6];
     }
     __syncthreads();
+    // balance_on: the wave behind its SIMD partner (the other wave of this workgroup on its
+    // SIMD) takes the issue priority -- the arbiter otherwise favours the older wave by ~30 %
+    // (scripts/microbench/fused_probe.py), and in the static tile order the younger one then
+    // finishes alone
+    int partner = wave;
+    for (int w = 0; w < NW; ++w)
+        if (w != wave && s_simd[w] == s_simd[wave]) partner = w;
+    partner = __builtin_amdgcn_readfirstlane(partner);
+    const bool balance = balance_on != 0 && partner != wave;
+    uint32_t prog = 0;
 
     uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
     uint8_t* touch_area = (uint8_t*)(s_lds + kTableDwords + NW * kStagePerWave / 4) + wave * 256;
@@ -207,6 +225,10 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
             else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             uint32_t d[32];
+            if (balance) {
+                if (lane == 0) s_prog[wave] = prog;
+            }
+            const uint32_t pprog = balance ? s_prog[partner] : 0u;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const uint4 v = *(const uint4*)(stage + rd_base + (((uint32_t)k ^ rsw) << 4));
@@ -216,6 +238,13 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_main_kernel(
                 d[4 * k + 3] = v.w;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (balance) {
+                if (__builtin_amdgcn_readfirstlane(pprog) > prog)
+                    __builtin_amdgcn_s_setprio(2);
+                else
+                    __builtin_amdgcn_s_setprio(0);
+                ++prog;
+            }
             {
                 uint64_t nt = tile;
                 int nit = it + 1;

@@ -347,24 +347,36 @@ def _oracle_two_phase_parallel(oracle, data: np.ndarray, avg: int, threads: int 
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("gib,kind,avg,dyn", [(8, 1, 4 * MiB, None), (6, 2, 256 * KiB, None),
-                                             (3, 1, 64 * KiB, None), (64, 2, 4 * MiB, None),
-                                             (64, 2, 256 * KiB, None),
-                                             (6, 2, 4 * MiB, "1"), (3, 1, 64 * KiB, "1"),
-                                             (1.5, 2, 1 * MiB, "1")],
+@pytest.mark.parametrize("gib,kind,avg,dyn,fused",
+                         [(8, 1, 4 * MiB, None, None), (6, 2, 256 * KiB, None, None),
+                          (3, 1, 64 * KiB, None, None), (64, 2, 4 * MiB, None, None),
+                          (64, 2, 256 * KiB, None, None),
+                          (6, 2, 4 * MiB, "1", None), (3, 1, 64 * KiB, "1", None),
+                          (1.5, 2, 1 * MiB, "1", None),
+                          (8, 1, 4 * MiB, None, "0"), (8, 1, 4 * MiB, None, "1"),
+                          (5.5, 2, 256 * KiB, None, "1"), (16.25, 1, 1 * MiB, None, "1")],
                          ids=["config2-8GiB-random-4M", "6GiB-vm-256K", "3GiB-random-64K",
                               "config3-64GiB-vm-4M", "config5-64GiB-vm-256K",
                               "6GiB-vm-4M-dynamic", "3GiB-random-64K-dynamic",
-                              "1.5GiB+ragged-vm-1M-dynamic"])
-def test_full_size_in_hbm(gpu, oracle, monkeypatch, gib, kind, avg, dyn):
+                              "1.5GiB+ragged-vm-1M-dynamic",
+                              "config2-8GiB-random-4M-multi-launch",
+                              "config2-8GiB-random-4M-fused-static",
+                              "5.5GiB+ragged-vm-256K-fused-static",
+                              "16.25GiB+ragged-random-1M-fused-static"])
+def test_full_size_in_hbm(gpu, oracle, monkeypatch, gib, kind, avg, dyn, fused):
     """BASELINE config 2 (8 GiB random already in HBM, 4 MiB average), the headline
     config 3 (64 GiB VM image, 4 MiB: 16 KiB segments in the dynamic tile order), and
     sizes that select the other scan_main segment lengths (16 KiB, 8 KiB) in both tile
-    orders (PBS_SCAN_DYN forces the dynamic one): the full cut list is diffed against
-    the (multi-threaded two-phase) oracle."""
+    orders (PBS_SCAN_DYN forces the dynamic one), and the one-launch pass in the static
+    tile order (PBS_FUSED=1: runtime segment lengths, one block longer for the first
+    tiles, 1-3 tiles per scanner wave, an 8 KiB tail) against the multi-launch path
+    (PBS_FUSED=0): the full cut list is diffed against the (multi-threaded two-phase)
+    oracle."""
     import torch
     if dyn is not None:
         monkeypatch.setenv("PBS_SCAN_DYN", dyn)
+    if fused is not None:
+        monkeypatch.setenv("PBS_FUSED", fused)
     n = int(gib * GiB) + (12345 if gib != int(gib) else 0)  # ragged: the tail after the small tiles
     seed = 0x5EED0002 if kind == 1 else 0x5EED0003
     n8 = (n + 7) // 8 * 8  # the generator writes whole words
