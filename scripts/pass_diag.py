@@ -13,6 +13,9 @@ import torch  # noqa: E402
 
 import pbschunk  # noqa: E402
 
+if os.environ.get("DIAG_LIB"):  # another build of the library (A/B across builds)
+    pbschunk.LIB_PATH = os.path.abspath(os.environ["DIAG_LIB"])
+
 size_gib, workload, avg = float(sys.argv[1]), sys.argv[2], int(sys.argv[3])
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 30
 gen = {"random": (pbschunk.GEN_RANDOM, 0x5EED0002), "vmimage": (pbschunk.GEN_VMIMAGE, 0x5EED0003)}[workload]
