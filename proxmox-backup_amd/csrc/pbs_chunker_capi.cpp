@@ -797,17 +797,15 @@ bool fused_dynamic(const pbs_chunker* c, uint64_t bl) {
     return dyn && c->prm.avg < kStaticMinAvg;
 }
 
-// The fused pass serves batches > 1 MiB at averages >= fused_min_avg: every such batch at
-// averages >= kStaticMinAvg (static order: faster than scan_main + resolve from 128 MiB to
-// 64 GiB, equal at 2-4 GiB, scripts/gpu_r02ak.sh), and batches in the dynamic order below
-// that.  PBS_FUSED=1 forces it for every batch it can serve (its parity tests run small
-// inputs), PBS_FUSED_MIN_BYTES raises the size threshold (A/B).
+// The fused pass serves every batch > 1 MiB at averages >= fused_min_avg (static order:
+// faster than scan_main + resolve from 128 MiB to 64 GiB, equal at 2-4 GiB; 8 GiB at
+// 256 KiB 1.52-1.55 vs 1.59-1.60 ms, scripts/gpu_r02ak.sh / r02at.sh).  PBS_FUSED=1 forces it
+// for every batch it can serve (its parity tests run small inputs), PBS_FUSED=0 never,
+// PBS_FUSED_MIN_BYTES raises the size threshold (A/B).
 bool use_fused(const pbs_chunker* c, uint64_t bl) {
     if (!(c->fused && c->prm.hash_cuts && c->prm.avg >= c->fused_min_avg && bl > kFusedMaxBytes && c->cu >= 2))
         return false;
-    if (c->fused_force) return true;
-    if (bl < c->fused_min_bytes) return false;
-    return c->prm.avg >= kStaticMinAvg || fused_dynamic(c, bl);
+    return c->fused_force || bl >= c->fused_min_bytes;
 }
 
 // One batch [pos, pos + bl) of device bytes `dsrc` (hsrc: the same bytes on the host, or

@@ -41,7 +41,7 @@ hipError_t launch_scan_main(const uint8_t* data, uint64_t ntiles, int seg,
 // scan_fused_kernel geometry (checked in scan_fused.h): 8 waves per workgroup, waves 0..2
 // of workgroup 0 resolve, every other wave scans tiles.
 constexpr int kFusedWavesPerWG = 8;
-constexpr int kFusedResolverWaves = 3;
+constexpr int kFusedResolverWaves = 5;
 
 struct FusedPassArgs {
     // phase A

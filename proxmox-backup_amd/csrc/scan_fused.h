@@ -15,7 +15,7 @@
 //                   record: the hand-off of MI355X_MICROARCH.md "Inter-workgroup
 //                   visibility").  After the tiles, the bytes past the last tile ("tail
 //                   items", 64 blocks each) are evaluated the same way.
-//   resolver waves  waves 0..2 of workgroup 0 take no tiles: two helpers turn the tile
+//   resolver waves  waves 0..4 of workgroup 0 take no tiles: four helpers turn the tile
 //                   records, in stream order and 256 records per step, into per-candidate
 //                   chain data (below); the main wave walks the cut chain over them, with
 //                   the pending candidates of the open chunk first.  Cuts go to mapped host
@@ -40,7 +40,7 @@ namespace pbs {
 
 constexpr int kFusedKeep = 512;     // open-chunk candidates the resolver keeps in LDS
 constexpr int kStageCand = 512;     // candidates of one resolver step staged in LDS
-constexpr int kFusedHelpers = 2;    // resolver helper waves (workgroup 0, waves 1..2)
+constexpr int kFusedHelpers = 4;    // resolver helper waves (workgroup 0, waves 1..4)
 constexpr int kPubDepth = 8;        // exact windows in flight per wave (fused_publish)
 
 constexpr uint32_t kRecOverflow = 0xFFFFu;
@@ -158,9 +158,10 @@ __device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, u
     return lo;
 }
 
-// Phase B (chunker.rs:172-183) is split over three waves of workgroup 0:
+// Phase B (chunker.rs:172-183) is split over five waves of workgroup 0 (four helpers: with
+// two, the static tile order at 256 KiB averages waited for them -- 8 GiB 1.62 -> 1.50-1.53 ms):
 //
-//   helpers (2)  take the record steps (kResolveBatch records) round-robin: wait for the
+//   helpers (4)  take the record steps (kResolveBatch records) round-robin: wait for the
 //                step's tiles, gather its candidates in stream order and, for every 64-
 //                candidate vector, compute per candidate lane-parallel (independent of
 //                everything before the vector): the next cut inside the vector if a cut

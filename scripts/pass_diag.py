@@ -13,7 +13,7 @@ import torch  # noqa: E402
 
 import pbschunk  # noqa: E402
 
-if os.environ.get("DIAG_LIB"):  # another build of the library (A/B across builds)
+if os.environ.get("DIAG_LIB"):  # noqa: SIM102  # another build of the library (A/B across builds)
     pbschunk.LIB_PATH = os.path.abspath(os.environ["DIAG_LIB"])
 
 size_gib, workload, avg = float(sys.argv[1]), sys.argv[2], int(sys.argv[3])
