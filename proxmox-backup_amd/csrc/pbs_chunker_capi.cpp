@@ -765,7 +765,7 @@ void fused_static_plan(uint64_t len, uint64_t nw, FusedPassArgs* a) {
     const uint64_t T = (rows + nw * qmax - 1) / (nw * qmax);  // rounds of full tiles
     uint64_t q = std::min<uint64_t>(8 * rows / (nw * (8 * T + 1)), qmax);
     uint64_t rem = rows - T * nw * q;
-    if (rem / nw < qsmin) {  // no short round: T rounds, the remainder spread over them
+    if (rem / nw < qsmin || rem / nw + 1 > qmax) {  // no short round: T rounds, the remainder spread over them
         a->ntiles = a->t_small = T * nw;
         a->seg_q = (uint32_t)(rows / a->ntiles);
         a->t_long = rows - (uint64_t)a->seg_q * a->ntiles;
@@ -1462,6 +1462,25 @@ int pbs_generate_device(uint8_t* dev, size_t len, int kind, uint64_t seed, uint6
 #define PBS_BUILD_ID "unknown"
 #endif
 const char* pbs_build_id(void) { return PBS_BUILD_ID; }
+
+// Test hook (not part of the drop-in API, so not in include/): the static tile plan of the
+// fused pass for a batch of `len` bytes over `nw` scanner waves -- out = {ntiles, seg_q,
+// t_long, t_small, seg_qs, t_small_long, covered bytes}.  tests/test_capi_cpu.py checks
+// its invariants on the CPU.
+int pbs_test_fused_static_plan(uint64_t len, uint64_t nw, uint64_t* out) {
+    if (!out || nw == 0) return PBS_ERR_INVALID;
+    FusedPassArgs a{};
+    fused_static_plan(len, nw, &a);
+    out[0] = a.ntiles;
+    out[1] = a.seg_q;
+    out[2] = a.t_long;
+    out[3] = a.t_small;
+    out[4] = a.seg_qs;
+    out[5] = a.t_small_long;
+    out[6] = ((a.t_small * a.seg_q + a.t_long) + (a.ntiles - a.t_small) * a.seg_qs + a.t_small_long) *
+             64 * kBlockBytes;
+    return PBS_OK;
+}
 
 int pbs_table_copy(uint32_t* out256) {
     if (!out256) return PBS_ERR_INVALID;
