@@ -551,10 +551,6 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     partner = __builtin_amdgcn_readfirstlane(partner);
     const bool balance = a.balance != 0 && partner != wave;  // equal progress of SIMD partners
     const bool bal_sleep = a.balance == 2;
-#ifdef PBS_SCAN_PROBE
-    if (lane == 0 && blockIdx.x * NW + wave < kScanProbeMax)
-        g_fused_probe[3 * kScanProbeMax + blockIdx.x * NW + wave] = s_simd[wave] | ((uint64_t)partner << 8);
-#endif
     uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
     PBS_FUSED_STAMP(0)
     if (blockIdx.x == 0 && wave == 0) {
@@ -778,6 +774,11 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
         }
     }
     PBS_FUSED_STAMP(2)
+#ifdef PBS_SCAN_PROBE  // SIMD and partner, stored last (stored at the start, it made the probe
+                       // build of the static kernel spill: probe timings of such a build are void)
+    if (lane == 0 && blockIdx.x * NW + wave < kScanProbeMax)
+        g_fused_probe[3 * kScanProbeMax + blockIdx.x * NW + wave] = s_simd[wave] | ((uint64_t)partner << 8);
+#endif
 }
 
 }  // namespace pbs
