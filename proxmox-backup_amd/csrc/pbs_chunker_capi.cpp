@@ -747,8 +747,9 @@ int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
 // (+0.1 ms).  Rounds of tiles of q blocks (<= kFusedStaticSeg - 128 bytes), then one short
 // round (~q/8): the tiles of a round all end together, and the resolver gets the last
 // round's candidates only when the scan is over -- half of them at 2 rounds, a quarter-
-// second backlog at 256 KiB averages on 8 GiB.  Small batches: fewer tiles than waves (>= 4
-// KiB segments), one group.
+// second backlog at 256 KiB averages on 8 GiB.  From 8 rounds on, the short round is half
+// a round drawn from a counter as 8 x nw small tiles (the pool, below).  Small batches:
+// fewer tiles than waves (>= 4 KiB segments), one group.
 void fused_static_plan(uint64_t len, uint64_t nw, FusedPassArgs* a) {
     const uint64_t rows = len / (64 * kBlockBytes);
     const uint64_t qmax = (uint64_t)kFusedStaticSeg / kBlockBytes - 1, qmin = 32, qsmin = 8;
@@ -763,7 +764,15 @@ void fused_static_plan(uint64_t len, uint64_t nw, FusedPassArgs* a) {
         return;
     }
     const uint64_t T = (rows + nw * qmax - 1) / (nw * qmax);  // rounds of full tiles
-    uint64_t q = std::min<uint64_t>(8 * rows / (nw * (8 * T + 1)), qmax);
+    // the short round, in eighths of a full round, and the pool: from 8 rounds on (64 GiB:
+    // 13) a half round drawn as 8 x nw tiles -- 64 GiB VM image 10.46-10.55 -> 10.36-10.39 ms,
+    // random 11.19-11.25 -> 11.10-11.15; with 2 rounds (8 GiB) the pool's short tiles cost
+    // more than they balance (1.42 -> 1.45 ms), scripts/gpu_r02az.sh.  PBS_POOL_ROUND /
+    // PBS_POOL_DIV override (sweeps)
+    uint64_t k8 = T >= 8 ? 4 : 1, d = T >= 8 ? 8 : 0;
+    if (const char* e = std::getenv("PBS_POOL_ROUND")) k8 = std::max<uint64_t>(1, std::strtoull(e, nullptr, 0));
+    if (const char* e = std::getenv("PBS_POOL_DIV")) d = std::strtoull(e, nullptr, 0);
+    uint64_t q = std::min<uint64_t>(8 * rows / (nw * (8 * T + k8)), qmax);
     uint64_t rem = rows - T * nw * q;
     if (rem / nw < qsmin || rem / nw + 1 > qmax) {  // no short round: T rounds, the remainder spread over them
         a->ntiles = a->t_small = T * nw;
@@ -776,6 +785,15 @@ void fused_static_plan(uint64_t len, uint64_t nw, FusedPassArgs* a) {
     a->seg_qs = (uint32_t)(rem / nw);
     a->t_small_long = rem - (uint64_t)a->seg_qs * nw;
     a->ntiles = (T + 1) * nw;
+    // pool (d > 1): the short round's rows as nw * d tiles of seg_qs / d blocks that the
+    // waves draw from the counter, so the waves that run ahead (faster CUs) take more
+    if (d > 1 && rem / (nw * d) >= qsmin) {
+        const uint64_t ns = nw * d;
+        a->seg_qs = (uint32_t)(rem / ns);
+        a->t_small_long = rem - (uint64_t)a->seg_qs * ns;
+        a->ntiles = a->t_small + ns;
+        a->pool = 1;
+    }
 }
 
 // Averages served by the fused pass: at >= 128 KiB a tile (1-2 MiB) of random data holds
@@ -1465,7 +1483,7 @@ const char* pbs_build_id(void) { return PBS_BUILD_ID; }
 
 // Test hook (not part of the drop-in API, so not in include/): the static tile plan of the
 // fused pass for a batch of `len` bytes over `nw` scanner waves -- out = {ntiles, seg_q,
-// t_long, t_small, seg_qs, t_small_long, covered bytes}.  tests/test_capi_cpu.py checks
+// t_long, t_small, seg_qs, t_small_long, covered bytes, pool}.  tests/test_capi_cpu.py checks
 // its invariants on the CPU.
 int pbs_test_fused_static_plan(uint64_t len, uint64_t nw, uint64_t* out) {
     if (!out || nw == 0) return PBS_ERR_INVALID;
@@ -1479,6 +1497,7 @@ int pbs_test_fused_static_plan(uint64_t len, uint64_t nw, uint64_t* out) {
     out[5] = a.t_small_long;
     out[6] = ((a.t_small * a.seg_q + a.t_long) + (a.ntiles - a.t_small) * a.seg_qs + a.t_small_long) *
              64 * kBlockBytes;
+    out[7] = a.pool;
     return PBS_OK;
 }
 

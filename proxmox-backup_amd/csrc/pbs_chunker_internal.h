@@ -54,6 +54,7 @@ struct FusedPassArgs {
     uint32_t seg_q, seg_qs;
     uint64_t t_long, t_small, t_small_long;
     uint32_t balance;           // SIMD partners trade issue priority by progress (PBS_BALANCE)
+    uint32_t pool;              // static order: tiles [t_small, ntiles) are drawn from tile_ctr
     const uint32_t* table_rot;  // T' (256 words)
     uint32_t thr;
     uint32_t* tile_ctr;         // zeroed device counter (dynamic tile order)

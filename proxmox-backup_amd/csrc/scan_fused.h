@@ -52,6 +52,11 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
 }
 
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {  // wave-uniform value into SGPRs
+    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
 __device__ __forceinline__ void store_wt(uint64_t* p, uint64_t v) {  // write-through (sc1)
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -590,22 +595,25 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     // tile geometry.  DYN: SEG-byte segments, SEG2 from tile t_big on.  Static: two groups
     // of runtime segment lengths (FusedPassArgs; the host sizes them so the tiles cover the
     // batch up to < 8 KiB, every scanner wave gets the same work, and the last round is short)
+    // (wave-uniform copies: selecting between two fields of `a` made the compiler load the
+    // chosen one through a computed address in VGPRs, and the static kernel spill)
+    const uint32_t g_q = __builtin_amdgcn_readfirstlane(a.seg_q);
+    const uint32_t g_qs = __builtin_amdgcn_readfirstlane(a.seg_qs);
+    const uint64_t g_tl = uni64(a.t_long), g_ts = uni64(a.t_small), g_tsl = uni64(a.t_small_long);
     auto tile_nit = [&](uint64_t t) -> uint32_t {  // blocks per segment
         if constexpr (DYN != 0)
             return (uint32_t)((t >= t_big ? SEG2 : SEG) / kIter);
         else
-            return t < a.t_small ? a.seg_q + (t < a.t_long ? 1u : 0u)
-                                 : a.seg_qs + (t - a.t_small < a.t_small_long ? 1u : 0u);
+            return t < g_ts ? g_q + (t < g_tl ? 1u : 0u) : g_qs + (t - g_ts < g_tsl ? 1u : 0u);
     };
     auto tile_off = [&](uint64_t t) -> uint64_t {
         if constexpr (DYN != 0) {
             if (t >= t_big) return t_big * (64ull * SEG) + (t - t_big) * (64ull * SEG2);
             return t * (64ull * SEG);
         } else {
-            if (t < a.t_small) return (t * a.seg_q + (t < a.t_long ? t : a.t_long)) * (64ull * kIter);
-            const uint64_t u = t - a.t_small;
-            return (a.t_small * a.seg_q + a.t_long + u * a.seg_qs +
-                    (u < a.t_small_long ? u : a.t_small_long)) * (64ull * kIter);
+            if (t < g_ts) return (t * g_q + (t < g_tl ? t : g_tl)) * (64ull * kIter);
+            const uint64_t u = t - g_ts;
+            return (g_ts * g_q + g_tl + u * g_qs + (u < g_tsl ? u : g_tsl)) * (64ull * kIter);
         }
     };
     auto issue = [&](uint64_t t, int it) {  // scan_main_kernel's LDS-DMA of one iteration
@@ -675,6 +683,12 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
         fused_publish(a, s_lds, t, myB, nb, over, lane);
     };
 
+    const bool pool = DYN == 0 && __builtin_amdgcn_readfirstlane(a.pool) != 0;
+    if (pool && tile >= g_ts) {  // no static tile: the counter hands out the rest
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(a.tile_ctr, 1u);
+        tile = g_ts + (uint64_t)__builtin_amdgcn_readfirstlane(v);
+    }
     if (tile < ntiles) {
         uint32_t ring[128];
 #pragma unroll
@@ -682,16 +696,20 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
         uint32_t h = 0;
         uint32_t dyn_v = 0;
         uint32_t prog = 0;  // blocks scanned (wave-uniform)
+        // static order with a pool (a.pool): tiles [0, t_small) round-robin, then the pool's
+        // short tiles from the counter (drawn at the start of a wave's last static tile)
         auto next_tile = [&]() -> uint64_t {
             if constexpr (DYN != 0)
                 return nw + (uint64_t)__builtin_amdgcn_readfirstlane(dyn_v);
             else
-                return tile + nw;
+                return (pool && tile + nw >= g_ts)
+                           ? g_ts + (uint64_t)__builtin_amdgcn_readfirstlane(dyn_v)
+                           : tile + nw;
         };
         if constexpr (DYN == 0) set_voff(voff, tile_nit(tile) * kIter);
         issue(tile, 0);
         for (;;) {
-            if constexpr (DYN != 0) {
+            if (DYN != 0 || (pool && tile + nw >= g_ts)) {
                 if (lane == 0) dyn_v = atomicAdd(a.tile_ctr, 1u);
             }
             const int nit_cur = (int)tile_nit(tile) + 1;  // + the warm-up block
@@ -765,10 +783,10 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
         const uint64_t b0 = a.covered / kIter + (tile - ntiles) * kTailBlocks;
         const int nb = (int)(nblk - b0 < (uint64_t)kTailBlocks ? nblk - b0 : (uint64_t)kTailBlocks);
         fused_publish(a, s_lds, tile, (int64_t)((b0 + (uint64_t)lane) * kIter), nb, false, lane);
-        if constexpr (DYN != 0) {
+        if (DYN != 0 || pool) {
             uint32_t v = 0;
             if (lane == 0) v = atomicAdd(a.tile_ctr, 1u);
-            tile = nw + (uint64_t)__builtin_amdgcn_readfirstlane(v);
+            tile = (DYN != 0 ? nw : g_ts) + (uint64_t)__builtin_amdgcn_readfirstlane(v);
         } else {
             tile += nw;
         }

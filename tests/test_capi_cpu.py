@@ -129,19 +129,20 @@ def test_fused_static_plan_covers_the_batch(pbschunk, nw):
     the tiles cover the batch up to less than one row of 64 blocks (8 KiB; batches under 32
     rows are tail items only), no segment
     exceeds the kernel's bitmap (40 KiB), every wave gets the same number of full-round
-    tiles, and the short last round (if any) is one tile per wave."""
+    tiles, and the short last round (if any) is one tile per wave or, from 8 rounds on, a
+    pool of 8 small tiles per wave."""
     import ctypes
     lib = pbschunk.lib()
     f = lib.pbs_test_fused_static_plan
     f.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
-    out = (ctypes.c_uint64 * 7)()
+    out = (ctypes.c_uint64 * 8)()
     rng = np.random.default_rng(7)
     sizes = [0, 1, 8191, 8192, 32 * 8192 - 1, 32 * 8192, 1 << 20, (1 << 20) + 77, 64 * MiB + 12345,
              1 << 30, (1 << 30) + 12345, 8 << 30, int(5.5 * (1 << 30)) + 12345, 64 << 30,
              (64 << 30) + 4099, 200 << 30] + [int(x) for x in rng.integers(1, 70 << 30, 40)]
     for n in sizes:
         assert f(n, nw, out) == 0
-        nt, q, tl, ts, qs, tsl, cov = (int(x) for x in out)
+        nt, q, tl, ts, qs, tsl, cov, pool = (int(x) for x in out)
         if nt == 0:  # under 32 rows: tail items only (the fused pass serves > 1 MiB)
             assert cov == 0 and n < 32 * 64 * 128
             continue
@@ -149,7 +150,8 @@ def test_fused_static_plan_covers_the_batch(pbschunk, nw):
         assert 0 < ts <= nt and tl < max(ts, 1) and tsl <= nt - ts
         assert (q + (tl > 0)) * 128 <= 40960 and (qs + (tsl > 0)) * 128 <= 40960
         assert q >= 32 or ts == nt
-        if nt > ts:  # rounds of full tiles plus one short round
-            assert ts % nw == 0 and nt - ts == nw and 0 < qs <= q
+        if nt > ts:  # rounds of full tiles plus one short round, or a pool drawn dynamically
+            assert ts % nw == 0 and (nt - ts) % nw == 0 and 0 < qs <= q
+            assert (nt - ts == nw) == (pool == 0)
         elif nt >= nw:
             assert nt % nw == 0

@@ -487,3 +487,29 @@ def test_fused_pass_stands_down_on_dense_input(gpu, oracle, monkeypatch):
     if ref.size == 0 or int(ref[-1]) != n:
         ref = np.append(ref, np.uint64(n))
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("gib,kind,avg,div,rnd", [(1, 1, 1 * MiB, 2, 8), (2, 2, 4 * MiB, 4, 8)],
+                         ids=["1GiB+ragged-random-1M-pool2", "2GiB+ragged-vm-4M-pool4"])
+def test_fused_pass_pool(gpu, oracle, monkeypatch, gib, kind, avg, div, rnd):
+    """The static order's pool (pbs_chunker_capi.cpp fused_static_plan: the last, short
+    round drawn from a counter as small tiles; by default only from 8 rounds on, i.e. the
+    64 GiB headline stream) forced on smaller streams: full cut lists against the oracle."""
+    import torch
+    monkeypatch.setenv("PBS_FUSED", "1")
+    monkeypatch.setenv("PBS_POOL_DIV", str(div))
+    monkeypatch.setenv("PBS_POOL_ROUND", str(rnd))
+    n = int(gib * GiB) + 12345
+    seed = 0x5EED0002 if kind == 1 else 0x5EED0003
+    n8 = (n + 7) // 8 * 8
+    dev = torch.empty(n8, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n8, kind, seed, 0)
+    with gpu.Chunker(avg) as c:
+        got = c.find_cuts_device(dev.data_ptr(), n, is_final=False)
+        t = c.last_timing()
+    host = dev[:n].cpu().numpy()
+    del dev
+    cand, ref = _oracle_two_phase_parallel(oracle, host, avg)
+    assert t["fused"] == n and t["candidates"] == cand.size
+    assert np.array_equal(got, ref)
