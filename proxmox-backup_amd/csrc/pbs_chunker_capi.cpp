@@ -802,11 +802,13 @@ constexpr uint64_t kFusedMinAvg = 128 * 1024;
 constexpr uint64_t kFusedMinBytes = 0;
 
 // Tile order of the fused pass: static with SIMD balancing (the wave behind its SIMD partner
-// takes the issue priority, scan_fused.h) for averages >= kStaticMinAvg -- 64 GiB at 4 MiB:
-// 10.39-10.42 vs 10.64-10.66 ms dynamic, 8 GiB random 1.45-1.47 vs 1.49-1.52 ms -- and the
-// dynamic order of scan_main_plan below that (64 GiB at 256 KiB: 11.05-11.19 dynamic vs
-// 11.43-11.62 static, scripts/gpu_r02ak.sh / r02al.sh).  PBS_SCAN_DYN=0/1 forces one (A/B).
-constexpr uint64_t kStaticMinAvg = 1 << 20;
+// takes the issue priority, scan_fused.h) and, from 8 rounds on, the pool (fused_static_plan)
+// for averages >= kStaticMinAvg -- 64 GiB at 4 MiB: 10.31-10.39 ms vs 10.64-10.94 dynamic;
+// at 256 KiB (config 5) 10.62-10.70 vs 11.04-11.11; at 512 KiB 10.49-10.51 vs 10.89-10.95;
+// 8 GiB random 1.41-1.45 vs 1.49-1.52 -- and the dynamic order of scan_main_plan below it
+// (64 GiB at 128 KiB: 11.28 dynamic vs 11.69-11.71 static; scripts/gpu_r02ba.sh and the
+// logs under profiles/r02/balance/).  PBS_SCAN_DYN=0/1 forces one (A/B).
+constexpr uint64_t kStaticMinAvg = 256 << 10;
 bool fused_dynamic(const pbs_chunker* c, uint64_t bl) {
     if (c->scan_dyn_env >= 0) return c->scan_dyn_env == 1;
     uint64_t nt = 0, tb = 0;
