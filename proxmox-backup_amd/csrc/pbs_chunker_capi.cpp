@@ -752,7 +752,10 @@ int spec_batch(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
 // fewer tiles than waves (>= 4 KiB segments), one group.
 void fused_static_plan(uint64_t len, uint64_t nw, FusedPassArgs* a) {
     const uint64_t rows = len / (64 * kBlockBytes);
-    const uint64_t qmax = (uint64_t)kFusedStaticSeg / kBlockBytes - 1, qmin = 32, qsmin = 8;
+    uint64_t qmax = (uint64_t)kFusedStaticSeg / kBlockBytes - 1;
+    const uint64_t qmin = 32, qsmin = 8;
+    if (const char* e = std::getenv("PBS_STATIC_QMAX"))  // shorter segments, more rounds (sweeps)
+        qmax = std::min<uint64_t>(qmax, std::max<uint64_t>(qmin, std::strtoull(e, nullptr, 0)));
     a->ntiles = a->t_long = a->t_small = a->t_small_long = 0;
     a->seg_q = a->seg_qs = 0;
     if (rows < qmin) return;  // all tail items
