@@ -28,10 +28,13 @@ torch.cuda.synchronize()
 ch = pbschunk.Chunker(avg)
 ch.set_stream(st.cuda_stream)
 ref = None
+BASE_ENV = dict(os.environ)
 for w in range(20):  # clock ramp
     ch.find_cuts_device(buf.data_ptr(), size, is_final=True)
 for rnd in range(3):
     for cfg in os.environ.get("DIAG_CONFIGS", "PBS_FUSED=0;PBS_FUSED=1").split(";"):
+        os.environ.clear()  # each setting starts from the launch environment
+        os.environ.update(BASE_ENV)
         for kv in cfg.split(","):
             k, v = kv.split("=")
             os.environ[k] = v
