@@ -871,7 +871,7 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     const uint64_t expected = bl / p.avg * 3 / 2 + 1;
     const uint64_t cand_cap = std::min<uint64_t>(std::min<uint64_t>(bl + 1, expected * 2 + 8192), kMaxBatchCand);
     HIP_TRY(c, c->d_cand.ensure(cand_cap * 8));
-    HIP_TRY(c, c->d_scratch.ensure(cand_cap * 29));  // c, sk, pm (u64), nf (u32), xl (u8)
+    HIP_TRY(c, c->d_scratch.ensure(cand_cap * 32));  // c, sk, pm, nf | xl << 32 (u64 each)
     // counters: [0] flagged blocks, [1] candidates, [2] tile counter (u32), [3] scratch
     HIP_TRY(c, c->d_counters.ensure(32));
     HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 32, c->stream));
@@ -922,8 +922,7 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     a.sc_c = reinterpret_cast<uint64_t*>(scr);
     a.sc_sk = reinterpret_cast<uint64_t*>(scr + cand_cap * 8);
     a.sc_pm = reinterpret_cast<uint64_t*>(scr + cand_cap * 16);
-    a.sc_nf = reinterpret_cast<uint32_t*>(scr + cand_cap * 24);
-    a.sc_xl = scr + cand_cap * 28;
+    a.sc_nx = reinterpret_cast<uint64_t*>(scr + cand_cap * 24);
     a.sc_ctr = ctr + 3;
     a.keep_host = keep_dev;
     a.keep_cap = (uint32_t)kHostKeep;

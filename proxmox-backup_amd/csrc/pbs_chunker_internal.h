@@ -85,8 +85,7 @@ struct FusedPassArgs {
     uint64_t* sc_c;
     uint64_t* sc_sk;
     uint64_t* sc_pm;
-    uint32_t* sc_nf;
-    uint8_t* sc_xl;
+    uint64_t* sc_nx;  // nf | xl << 32
     unsigned long long* sc_ctr;  // zeroed counter (scratch entries handed out)
     uint64_t* keep_host;        // mapped: candidates of the open chunk
     uint32_t keep_cap;

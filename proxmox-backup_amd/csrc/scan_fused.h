@@ -39,6 +39,9 @@
 namespace pbs {
 
 constexpr int kFusedKeep = 512;     // open-chunk candidates the resolver keeps in LDS
+constexpr int kCutBuf = kStagePerWave / 8 - kFusedKeep;  // cuts the main wave buffers in LDS
+constexpr int kLaneProbes = 3;      // linear probes before the binary lane search
+constexpr int kMainAhead = 8;       // resolver vectors the main wave has in flight
 constexpr int kStageCand = 512;     // candidates of one resolver step staged in LDS
 constexpr int kFusedHelpers = 4;    // resolver helper waves (workgroup 0, waves 1..4)
 constexpr int kPubDepth = 8;        // exact windows in flight per wave (fused_publish)
@@ -144,14 +147,25 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {  // divergent 
 }
 
 // first lane in [from, nv) whose candidate is >= x (nv if none); lanes [0, nv) hold
-// ascending candidates.  `from` itself is probed first (a chunk usually ends at the next
-// candidate); the rest is a binary search that runs only as long as some lane needs it.
+// ascending candidates.  The next few lanes are probed first (a chunk usually ends at one
+// of the next candidates); the rest is a binary search that runs only as long as some lane needs it.
 // All 64 lanes take part (the shuffles read every lane).
 __device__ __forceinline__ int lanes_lower_bound(uint64_t c, int from, int nv, uint64_t x) {
     int lo = from < nv ? from : nv, hi = nv;
-    const uint64_t v0 = shfl64(c, lo < 64 ? lo : 63);
-    if (lo < hi && v0 >= x) hi = lo;
-    else if (lo < hi) ++lo;
+    // kLaneProbes linear probes first: with one, ~1 lane in 5 still needed the search at
+    // 64 KiB averages (the next candidate within the minimum size), so nearly every
+    // vector paid its 6 shuffle rounds
+#pragma unroll
+    for (int p = 0; p < kLaneProbes; ++p) {
+        if (!__any(lo < hi)) break;
+        const uint64_t v = shfl64(c, lo < 64 ? lo : 63);
+        if (lo < hi) {
+            if (v >= x)
+                hi = lo;
+            else
+                ++lo;
+        }
+    }
     while (__any(lo < hi)) {
         const int mid = (lo + hi) >> 1;
         const uint64_t v = shfl64(c, mid < 64 ? mid : 63);
@@ -190,8 +204,8 @@ struct FusedStep {  // one resolver step, in scratch (stream order)
     uint64_t* c;   // candidate
     uint64_t* sk;  // state after a cut here and its forced cuts, if the chain leaves here
     uint64_t* pm;  // lanes on the chain from here to where it leaves the vector
-    uint32_t* nf;  // forced cuts after a cut here
-    uint8_t* xl;   // the lane where the chain from here leaves the vector
+    uint64_t* nx;  // forced cuts after a cut here | the lane where the chain from here
+                   // leaves the vector << 32 (one load: both are read where the walk needs them)
 };
 
 __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int nh, int lane) {
@@ -202,7 +216,7 @@ __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int n
     const unsigned long long* const rec = a.rec;
     const uint64_t* const cand = a.cand;
     unsigned long long* const sinfo = a.rec + total;  // step records after the tile records
-    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_pm, a.sc_nf, a.sc_xl};
+    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_pm, a.sc_nx};
     const uint64_t t_start = wall_clock64();
     for (uint64_t st = (uint64_t)h; st < nsteps; st += (uint64_t)nh) {
         const uint64_t t0 = st * kResolveBatch;
@@ -305,8 +319,7 @@ __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int n
                         sc.c[w] = c;
                         sc.sk[w] = sk;
                         sc.pm[w] = pm;
-                        sc.nf[w] = nf;
-                        sc.xl[w] = (uint8_t)xl;
+                        sc.nx[w] = (uint64_t)nf | ((uint64_t)(uint32_t)xl << 32);
                     }
                 }
             }
@@ -333,7 +346,7 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
     uint64_t* const cuts_host = a.cuts_host;
     const uint64_t host_cap = a.host_cap;
     const unsigned long long* const sinfo = a.rec + total;
-    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_pm, a.sc_nf, a.sc_xl};
+    const FusedStep sc{a.sc_c, a.sc_sk, a.sc_pm, a.sc_nx};
     const uint64_t timeout = a.timeout_ticks, end = a.end;
     uint64_t s = a.s0, ncut = 0;
     uint32_t nkeep = 0, status = 0;
@@ -341,12 +354,36 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
     uint64_t t_wait = 0, t_ready = t_start;
     const unsigned long long below = (1ull << lane) - 1;
 
-    // cuts go straight to mapped host memory; a list longer than host_cap stands down
-    auto put = [&](uint64_t i, uint64_t x) {
-        if (i < host_cap) cuts_host[i] = x;
+    // cuts go to mapped host memory (a list longer than host_cap stands down) through an
+    // LDS buffer: cuts [fl, ncut) wait in cbuf[0, ncut - fl) and go out kCutBuf at a time.
+    // Stored one vector at a time, every wait for the next vector's loads also waited for
+    // the PCIe acknowledgement of the previous stores (vmcnt counts both): ~1 us per
+    // vector, which made the main wave the bottleneck at 64 KiB averages (17.7 ms pass).
+    uint64_t* const cbuf = keep + kFusedKeep;  // the second half of the wave's stage
+    uint64_t fl = 0;
+    auto flush = [&]() {
+        const uint64_t nb = ncut - fl;
+        for (uint64_t j = (uint64_t)lane; j < nb; j += 64)
+            if (fl + j < host_cap) cuts_host[fl + j] = cbuf[j];
+        fl = ncut;
+    };
+    // room for k more cuts: true = put them in cbuf, false = straight to host memory
+    auto reserve = [&](uint64_t k) -> bool {
+        if (ncut - fl + k <= (uint64_t)kCutBuf) return true;
+        flush();
+        if (k <= (uint64_t)kCutBuf) return true;
+        fl = ncut + k;  // a long run of forced cuts: written directly
+        return false;
+    };
+    auto put = [&](bool lds, uint64_t i, uint64_t x) {
+        if (lds)
+            cbuf[i - fl] = x;
+        else if (i < host_cap)
+            cuts_host[i] = x;
     };
     auto forced = [&](uint64_t k) {  // k forced (max-size) cuts from s, lane-parallel
-        for (uint64_t j = (uint64_t)lane; j < k; j += 64) put(ncut + j, s + (j + 1) * max_eff);
+        const bool lds = reserve(k);
+        for (uint64_t j = (uint64_t)lane; j < k; j += 64) put(lds, ncut + j, s + (j + 1) * max_eff);
         ncut += k;
         s += k * max_eff;
     };
@@ -396,10 +433,11 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
             off = (uint64_t)__popcll(mask & below);
             tot = (uint32_t)__popcll(mask);
         }
+        const bool lds = reserve(tot);
         if (on) {
             const uint64_t o = ncut + off;
-            put(o, c + 1);
-            for (uint32_t i = 1; i <= nf; ++i) put(o + i, c + 1 + (uint64_t)i * max_eff);
+            put(lds, o, c + 1);
+            for (uint32_t i = 1; i <= nf; ++i) put(lds, o + i, c + 1 + (uint64_t)i * max_eff);
         }
         ncut += tot;
     };
@@ -425,19 +463,35 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         return st < nsteps ? __hip_atomic_load(sinfo + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
     };
     struct Vec {
-        uint64_t c, sk, pm;
-        uint32_t nf, xl;
+        uint64_t c, sk, pm, nx;
     };
+    // lane i of a vector at v0 (clamped to the step's last candidate: the loads are
+    // unconditional, so the compiler can count them in vmcnt)
     auto load_vec = [&](uint64_t o, uint32_t T, uint32_t v0) -> Vec {
-        const bool v = v0 + lane < T;
-        const uint64_t w = o + v0 + (uint64_t)lane;
-        Vec x;
-        x.c = v ? sc.c[w] : ~0ull;
-        x.sk = v ? sc.sk[w] : 0ull;
-        x.pm = v ? sc.pm[w] : 0ull;
-        x.nf = v ? sc.nf[w] : 0u;
-        x.xl = v ? (uint32_t)sc.xl[w] : (uint32_t)lane;
-        return x;
+        const uint32_t i = v0 + (uint32_t)lane < T ? v0 + (uint32_t)lane : T - 1;
+        const uint64_t w = o + i;
+        return Vec{sc.c[w], sc.sk[w], sc.pm[w], sc.nx[w]};
+    };
+    // one vector: the first cut from the incoming state, then the chain the helper
+    // precomputed from that lane
+    auto walk = [&](const Vec& q, uint32_t v0, uint32_t T) {
+        const bool v = v0 + (uint32_t)lane < T;
+        const uint64_t c = v ? q.c : ~0ull;
+        unsigned long long rem = __ballot(v);
+        bool reset = false;
+        const int e = entry(c, rem, reset);
+        // read unconditionally (lane 0 when no cut): used only under the branch, the loads
+        // were sunk into it and issued one vector ahead instead of kMainAhead
+        const int ee = e < 0 ? 0 : e;
+        const unsigned long long mask = readlane64(q.pm, ee);
+        const int x = __builtin_amdgcn_readlane((int)(uint32_t)(q.nx >> 32), ee);
+        const uint64_t sx = readlane64(q.sk, x);
+        if (e >= 0) {
+            emit_chain(c, mask, (uint32_t)q.nx);
+            s = sx;
+            rem = x == 63 ? 0ull : rem & ~((2ull << x) - 1);
+        }
+        keep_rest(c, rem, reset);
     };
     uint64_t r_next = load_info(0);
     for (uint64_t st = 0; st < nsteps && status == 0; ++st) {
@@ -464,29 +518,27 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         }
         const uint32_t T = (uint32_t)(r >> 27) & 0xFFFFFu;
         const uint64_t o = r & 0x7FFFFFFull;
-        // three vectors in flight: the one walked and the next two
-        Vec cur = T ? load_vec(o, T, 0) : Vec{~0ull, 0ull, 0ull, 0u, 0u};
-        Vec n1 = 64 < T ? load_vec(o, T, 64) : cur;
-        for (uint32_t v0 = 0; v0 < T; v0 += 64) {
-            const Vec n2 = v0 + 128 < T ? load_vec(o, T, v0 + 128) : n1;
-            const uint64_t c = cur.c;
-            unsigned long long rem = __ballot(v0 + lane < T);
-            bool reset = false;
-            const int e = entry(c, rem, reset);
-            if (e >= 0) {  // the chain from e, precomputed by the helper
-                const unsigned long long mask = readlane64(cur.pm, e);
-                const int x = __builtin_amdgcn_readlane((int)cur.xl, e);
-                emit_chain(c, mask, cur.nf);
-                s = readlane64(cur.sk, x);
-                rem = x == 63 ? 0ull : rem & ~((2ull << x) - 1);
+        // kMainAhead vectors in flight, in a ring walked in place: rotating them through
+        // copies (cur = next) made every vector wait for the loads issued with it
+        if (T) {
+            Vec q[kMainAhead];
+#pragma unroll
+            for (int i = 0; i < kMainAhead; ++i) q[i] = load_vec(o, T, 64u * i);
+            for (uint32_t v0 = 0; v0 < T; v0 += 64u * kMainAhead) {
+#pragma unroll
+                for (int i = 0; i < kMainAhead; ++i) {
+                    const uint32_t vi = v0 + 64u * i;
+                    if (vi < T) {
+                        walk(q[i], vi, T);
+                        q[i] = load_vec(o, T, vi + 64u * kMainAhead);
+                    }
+                }
             }
-            keep_rest(c, rem, reset);
-            cur = n1;
-            n1 = n2;
         }
-        if ((st & 7) == 7 && lane == 0) {  // progress: the host copies the cuts written so far
+        if ((st & 7) == 7 && lane == 0) {  // progress: the host copies the cuts stored so far
+            const uint64_t done = fl < ncut ? fl : ncut;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            __hip_atomic_store(a.res_host + 9, ncut < host_cap ? ncut : host_cap, __ATOMIC_RELAXED,
+            __hip_atomic_store(a.res_host + 9, done < host_cap ? done : host_cap, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
@@ -497,6 +549,7 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         }
         if (nkeep > kFusedKeep || ncut > host_cap) status = 1;
     }
+    if (fl < ncut) flush();
     if (status == 0 && nkeep <= a.keep_cap)
         for (uint32_t i = lane; i < nkeep; i += 64) a.keep_host[i] = keep[i];
     if ((uint32_t)lane < a.tail_len) a.tail_host[lane] = a.tail_src[lane];
