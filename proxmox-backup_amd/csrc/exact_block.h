@@ -19,7 +19,7 @@ constexpr int kExactBlock = 128;  // bytes per block (= scan_main's lane iterati
 //   h(j) = rotl( P(j) ^ P(j-64), j mod 32 ),   P(j) = XOR_{i<=j} rotr( T[w_i], i mod 32 )
 // (rotl(T, j-i) = rotl(rotr(T, i), j), so the rotation of each term only depends on its
 // own index; window indices j, i).  Lane l < 48 owns window bytes [4l, 4l+4): one dword
-// load, 4 table lookups, a wave-wide prefix XOR (6 shuffles) and P(j-64) from lane l-16;
+// load, 4 table lookups, a wave-wide prefix XOR (6 DPP steps) and P(j-64) from lane l-16;
 // lanes 16..47 test positions j = 64..191, i.e. block positions 4(l-16)+k.
 // Bytes that do not exist (before the stream, after `len`) are read with clamped
 // addresses: a reportable position (q >= 0, q < len, q + pre_len >= 63) has all 64
@@ -52,6 +52,13 @@ __device__ __forceinline__ uint32_t exact_load(const uint8_t* __restrict__ data,
     return wv;
 }
 
+// v moved across lanes by the DPP control CTRL (rows/banks outside the masks, and lanes
+// whose source lies outside their row, read 0: the identity of XOR and OR)
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, BANK_MASK, false);
+}
+
 // ROT = false: `tab` is the plain table (256 words), the test (h & mask) >= minimum
 // (chunker.rs:185).  ROT = true: `tab` is the scan kernels' pre-rotated table replicated
 // 64x (T' = rotl(T, rot) at dword b*64 + lane, conflict-free for any 64 bytes) and `mask`
@@ -74,12 +81,15 @@ __device__ __forceinline__ uint4 exact_hits(uint32_t wv, uint64_t len, uint32_t 
         acc ^= lane < 48 ? t : 0u;
         u[k] = acc;
     }
-    uint32_t S = acc;  // inclusive prefix XOR over lanes
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t v = __shfl_up(S, d, 64);
-        if (lane >= d) S ^= v;
-    }
+    // inclusive prefix XOR over lanes with DPP (VALU lane moves, no LDS round trip):
+    // shifts 1, 2, 4, 8 inside each row of 16, then the row totals by row_bcast
+    uint32_t S = acc;
+    S ^= dpp_mov<0x111>(S);  // row_shr:1
+    S ^= dpp_mov<0x112>(S);  // row_shr:2
+    S ^= dpp_mov<0x114>(S);  // row_shr:4
+    S ^= dpp_mov<0x118>(S);  // row_shr:8
+    S ^= dpp_mov<0x142, 0xa>(S);  // row_bcast:15 into rows 1 and 3
+    S ^= dpp_mov<0x143, 0xc>(S);  // row_bcast:31 into rows 2 and 3
     const uint32_t E = S ^ acc;  // exclusive
     uint32_t nib = 0;
 #pragma unroll
@@ -93,10 +103,13 @@ __device__ __forceinline__ uint4 exact_hits(uint32_t wv, uint64_t len, uint32_t 
     }
     const bool tester = lane >= 16 && lane < 48;
     uint32_t v = tester ? nib << (4 * ((lane - 16) & 7)) : 0u;
-    v |= __shfl_xor(v, 1, 64);
-    v |= __shfl_xor(v, 2, 64);
-    v |= __shfl_xor(v, 4, 64);
-    uint4 hit = make_uint4(__shfl(v, 16, 64), __shfl(v, 24, 64), __shfl(v, 32, 64), __shfl(v, 40, 64));
+    v |= dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+    v |= dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+    v |= dpp_mov<0x141>(v);  // row_half_mirror: the other quad of the 8 lanes
+    uint4 hit = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)v, 16),
+                           (uint32_t)__builtin_amdgcn_readlane((int)v, 24),
+                           (uint32_t)__builtin_amdgcn_readlane((int)v, 32),
+                           (uint32_t)__builtin_amdgcn_readlane((int)v, 40));
     const bool fast = B >= 64 && B + kExactBlock <= ilen;
     if (!fast) {
         // reportable window indices [cmin, vhi): q >= 0, q + pre_len >= 63, q < len
