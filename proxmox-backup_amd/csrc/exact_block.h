@@ -59,6 +59,17 @@ __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, BANK_MASK, false);
 }
 
+// inclusive prefix sum over the 64 lanes (DPP: row shifts, then the row totals)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += dpp_mov<0x111>(v);
+    v += dpp_mov<0x112>(v);
+    v += dpp_mov<0x114>(v);
+    v += dpp_mov<0x118>(v);
+    v += dpp_mov<0x142, 0xa>(v);
+    v += dpp_mov<0x143, 0xc>(v);
+    return v;
+}
+
 // ROT = false: `tab` is the plain table (256 words), the test (h & mask) >= minimum
 // (chunker.rs:185).  ROT = true: `tab` is the scan kernels' pre-rotated table replicated
 // 64x (T' = rotl(T, rot) at dword b*64 + lane, conflict-free for any 64 bytes) and `mask`

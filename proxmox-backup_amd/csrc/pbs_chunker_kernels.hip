@@ -104,8 +104,8 @@ __global__ __launch_bounds__(kExactWaves * 64) void scan_exact_kernel(
         const uint64_t left = (total - w0 + stride - 1) / stride;
         const int cnt = left < 64 ? (int)left : 64;
         auto getB = [&](int j) -> uint64_t {
-            return (uint64_t)(uint32_t)__shfl((int)Blo, j, 64) |
-                   ((uint64_t)(uint32_t)__shfl((int)Bhi, j, 64) << 32);
+            return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Blo, j) |  // j is wave-uniform
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Bhi, j) << 32);
         };
         uint64_t B = getB(0);
         uint32_t wv = exact_load(data, len, pre, pre_len, (int64_t)B, lane);

@@ -100,13 +100,8 @@ __device__ __forceinline__ void fused_publish(const FusedPassArgs& a, const uint
     }
     const uint32_t cnt = __builtin_popcount(mh.x) + __builtin_popcount(mh.y) +
                          __builtin_popcount(mh.z) + __builtin_popcount(mh.w);
-    uint32_t incl = cnt;  // inclusive prefix over lanes
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+    const uint32_t incl = wave_incl_sum(cnt);  // inclusive prefix over lanes
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     uint64_t idx = 0;
     bool ovf = over || total >= kRecOverflow;
     if (!ovf && total) {
@@ -244,14 +239,9 @@ __device__ void fused_helper(const FusedPassArgs& a, uint64_t* stc, int h, int n
             ovf = ovf || cq[q] == kRecOverflow;
         }
         const uint32_t p1 = cq[0], p2 = p1 + cq[1], p3 = p2 + cq[2], sum = p3 + cq[3];
-        uint32_t incl = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
+        const uint32_t incl = wave_incl_sum(sum);
         const uint32_t base = incl - sum;
-        const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         uint64_t o = 0;
         if (!__any(ovf) && T) {
             unsigned long long b = 0;
@@ -421,14 +411,9 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
         uint64_t off;
         uint32_t tot;
         if (__any(on && nf != 0)) {
-            uint32_t incl = cnt;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += y;
-            }
+            const uint32_t incl = wave_incl_sum(cnt);
             off = incl - cnt;
-            tot = (uint32_t)__shfl((int)incl, 63, 64);
+            tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         } else {
             off = (uint64_t)__popcll(mask & below);
             tot = (uint32_t)__popcll(mask);
@@ -723,7 +708,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
                     found = true;
                 }
             }
-            bitpos = __shfl(bitpos, L, 64);
+            bitpos = __builtin_amdgcn_readlane(bitpos, L);  // L is wave-uniform
             if (lane == L) {
 #pragma unroll
                 for (int q = 0; q < NBW; ++q)
