@@ -516,7 +516,8 @@ def launch_ranks(args) -> int:
     started before anything touches the GPU; returns the job's exit code.  A rank that
     fails ends the others (they would wait in the barrier)."""
     n = args.gpus
-    if not args.cpu_standin:
+    share = os.environ.get("PBS_BENCH_SHARE_GPU") == "1"
+    if not args.cpu_standin and not share:
         import torch
         have = torch.cuda.device_count()  # counts devices without initialising HIP
         if have < n:
@@ -527,7 +528,7 @@ def launch_ranks(args) -> int:
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        if args.cpu_standin:  # gloo on the loopback device (the hostname may not resolve)
+        if args.cpu_standin or share:  # gloo on the loopback device (the hostname may not resolve)
             env.setdefault("GLOO_SOCKET_IFNAME", "lo")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
@@ -631,7 +632,13 @@ def main():
     import numpy as np
     import torch
 
-    if torch.cuda.device_count() < max(world, local + 1):
+    # TEST ONLY (PBS_BENCH_SHARE_GPU=1): every rank on GPU 0 and gloo instead of RCCL -- a
+    # rehearsal of the N-rank GPU path on a one-GPU box (the ranks share one HBM, so the
+    # line is not a scaling measurement and says so)
+    share = world > 1 and os.environ.get("PBS_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
+    if torch.cuda.device_count() < (1 if share else max(world, local + 1)):
         print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible",
               file=sys.stderr)
         sys.exit(2)
@@ -639,10 +646,14 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    red_dev = torch.device("cpu") if share else dev  # gloo reduces CPU tensors
 
     import pbschunk
 
@@ -686,7 +697,7 @@ def main():
     elapsed, cuts = timed_steps(step, args, dist, torch.cuda.synchronize, after)
     recs = per_rank_records({"rank": rank, "seed": seed, "elapsed_s": round(elapsed, 6),
                              "bytes": work_bytes, "chunks": last.get("ncuts", 0)}, dist, world)
-    elapsed, total_bytes = aggregate(elapsed, work_bytes, dist, dev)
+    elapsed, total_bytes = aggregate(elapsed, work_bytes, dist, red_dev)
 
     value = total_bytes * args.steps / (1 << 30) / elapsed
     avg_scan_s = float(np.mean(scan_ms)) / 1e3 if scan_ms else float("nan")
@@ -725,7 +736,7 @@ def main():
         return
     default_cfg = (args.size_gib == 64.0 and args.avg == 4 * 1024 * 1024
                    and args.workload == "vmimage" and args.mode == "streams")
-    metric = METRIC if default_cfg else (
+    metric = METRIC if default_cfg and not share else ("REHEARSAL (ranks share one GPU, gloo): " if share else "") + (
         f"GiB/s chunked (device-resident), {args.avg >> 10} KiB mean, {args.size_gib:g} GiB "
         f"{args.workload} stream ({args.mode}); boundaries bit-exact")
     out = base_line(
@@ -744,6 +755,8 @@ def main():
                        "kernel": "scan_fused_kernel" if fused and all(fused) else "scan_main_kernel",
                        "avg_launch_ms": round(avg_scan_s * 1e3, 4)}
     out["build_id"] = pbschunk.build_id()
+    if share:
+        out["rehearsal"] = "TEST ONLY: all ranks on GPU 0 over gloo; not a scaling measurement"
     if world > 1:
         out["per_rank"] = recs
     if host_incl is not None:
