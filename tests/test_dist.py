@@ -98,3 +98,38 @@ def test_bench_refuses_world_mismatch():
     rc, out, err = _run_bench(["--gpus", "4", "--cpu-standin", "--steps", "1"],
                               env={"WORLD_SIZE": "2", "RANK": "0"}, timeout=120)
     assert rc == 2 and "disagrees" in err
+
+
+def test_bench_share_gpu_refuses_without_gpu():
+    """The one-GPU rehearsal (PBS_BENCH_SHARE_GPU=1) still needs a GPU: here it fails
+    loudly instead of falling back to anything."""
+    if _has_gpu():
+        pytest.skip("a GPU is visible")
+    rc, out, err = _run_bench(["--gpus", "2", "--steps", "1", "--size-gib", "0.01"],
+                              env={"PBS_BENCH_SHARE_GPU": "1"}, timeout=180)
+    assert rc == 2 and out is None and "GPU" in err
+
+
+def _has_gpu():
+    import torch
+    return torch.cuda.device_count() > 0
+
+
+@pytest.mark.gpu
+def test_bench_share_gpu_rehearsal():
+    """The N-rank GPU path of bench.py with both ranks on GPU 0 over gloo: one line from
+    rank 0, labelled as a rehearsal, n_gpus 2, per-rank seeds and cut lists, MAX/SUM
+    aggregation (the RCCL all-reduce is the only part it does not exercise)."""
+    rc, out, err = _run_bench(["--gpus", "2", "--size-gib", "0.25", "--steps", "2", "--warmup", "1",
+                               "--cpu-baseline", "0", "--host-inclusive-gib", "0",
+                               "--secondary-random", "0"],
+                              env={"PBS_BENCH_SHARE_GPU": "1"}, timeout=240)
+    assert rc == 0, err[-2000:]
+    assert out["n_gpus"] == 2 and out["metric"].startswith("REHEARSAL") and "rehearsal" in out
+    recs = sorted(out["per_rank"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in recs] == [0, 1]
+    assert recs[1]["seed"] == recs[0]["seed"] + 1
+    assert all(r["chunks"] > 0 for r in recs)
+    mx = max(r["elapsed_s"] for r in recs)
+    tot = sum(r["bytes"] for r in recs)
+    assert out["value"] == pytest.approx(tot * 2 / (1 << 30) / mx, rel=1e-2)
