@@ -53,7 +53,8 @@ __device__ __forceinline__ uint32_t exact_load(const uint8_t* __restrict__ data,
 }
 
 // v moved across lanes by the DPP control CTRL (rows/banks outside the masks, and lanes
-// whose source lies outside their row, read 0: the identity of XOR and OR)
+// whose source lies outside their row, read 0: the identity of XOR, OR and +).  Callers
+// run with all 64 lanes active (wave-uniform control flow), as every caller here does.
 template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, BANK_MASK, false);
