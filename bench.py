@@ -638,6 +638,9 @@ def main():
     share = world > 1 and os.environ.get("PBS_BENCH_SHARE_GPU") == "1"
     if share:
         local = 0
+        if args.mode != "streams":  # the sharded mode's all-gathers move device tensors
+            print("bench.py: PBS_BENCH_SHARE_GPU rehearses --mode streams only", file=sys.stderr)
+            sys.exit(2)
     if torch.cuda.device_count() < (1 if share else max(world, local + 1)):
         print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible",
               file=sys.stderr)
