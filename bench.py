@@ -511,16 +511,43 @@ def free_port() -> int:
         return sk.getsockname()[1]
 
 
+def kfd_gpu_count():
+    """GPUs visible to this process, counted without any HIP/torch call: the KFD topology
+    nodes with SIMDs (CPU nodes have simd_count 0), narrowed by the *_VISIBLE_DEVICES
+    lists the ROCm runtime honours.  None when the topology is not readable (the rank
+    processes then check for themselves)."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(root, node, "properties")) as f:
+                props = dict(ln.split(None, 1) for ln in f if ln.strip() and len(ln.split()) == 2)
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(args) -> int:
     """`--gpus N` without a launcher: N rank processes of this script (one per GPU),
-    started before anything touches the GPU; returns the job's exit code.  A rank that
-    fails ends the others (they would wait in the barrier)."""
+    started before anything touches the GPU -- this parent makes no HIP or torch.cuda
+    call at all (the GPU count comes from the KFD topology in sysfs, and every rank
+    checks its own device again); returns the job's exit code.  A rank that fails ends
+    the others (they would wait in the barrier)."""
     n = args.gpus
     share = os.environ.get("PBS_BENCH_SHARE_GPU") == "1"
     if not args.cpu_standin and not share:
-        import torch
-        have = torch.cuda.device_count()  # counts devices without initialising HIP
-        if have < n:
+        have = kfd_gpu_count()
+        if have is not None and have < n:
             print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
             return 2
     port = free_port()
@@ -568,6 +595,21 @@ def timed_steps(step, args, dist, sync, after=None):
     return time.perf_counter() - t0, res
 
 
+def cut_record(cuts, keep: int = 8192) -> dict:
+    """A rank's cut list (chunk END offsets, the stream end included) for the per-rank
+    record: its SHA-256 over the u64 LE values, and the list itself when it is short (the
+    multi-rank tests diff each rank's list against the oracle)."""
+    import hashlib
+
+    import numpy as np
+
+    c = np.ascontiguousarray(np.asarray(cuts, dtype=np.uint64))
+    out = {"cuts_sha256": hashlib.sha256(c.astype("<u8").tobytes()).hexdigest()}
+    if c.size <= keep:
+        out["cuts"] = [int(x) for x in c]
+    return out
+
+
 def per_rank_records(rec: dict, dist, world: int):
     if dist is None:
         return [rec]
@@ -600,7 +642,7 @@ def standin_main(args, world: int, rank: int):
            "vmimage": lambda: oracle.gen_vmimage(size, seed, 0)}[args.workload]()
     elapsed, cuts = timed_steps(lambda: oracle.chunk_feed(args.avg, buf), args, dist, lambda: None)
     recs = per_rank_records({"rank": rank, "seed": seed, "elapsed_s": elapsed, "bytes": size,
-                             "chunks": int(cuts.size)}, dist, world)
+                             "chunks": int(cuts.size), **cut_record(cuts)}, dist, world)
     mx, total = aggregate(elapsed, size, dist, torch.device("cpu"))
     if rank == 0:
         out = base_line(args, "STAND-IN (CPU oracle over gloo, not a GPU measurement): GiB/s chunked",
@@ -637,16 +679,16 @@ def main():
     # line is not a scaling measurement and says so)
     share = world > 1 and os.environ.get("PBS_BENCH_SHARE_GPU") == "1"
     if share:
-        local = 0
-        if args.mode != "streams":  # the sharded mode's all-gathers move device tensors
-            print("bench.py: PBS_BENCH_SHARE_GPU rehearses --mode streams only", file=sys.stderr)
-            sys.exit(2)
+        local = 0  # (--mode sharded stages its all-gathers through host memory: shard.py)
     if torch.cuda.device_count() < (1 if share else max(world, local + 1)):
         print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible",
               file=sys.stderr)
         sys.exit(2)
     dist = None
-    if world > 1:
+    # TEST ONLY (PBS_BENCH_DIST_WORLD1=1, under torch.distributed.run): a one-rank job still
+    # creates its RCCL group, so the device-tensor barrier / all-reduce / all-gather path of
+    # the multi-GPU run executes on a one-GPU box (tests/test_dist.py)
+    if world > 1 or (world == 1 and env_world is not None and os.environ.get("PBS_BENCH_DIST_WORLD1") == "1"):
         import torch.distributed as dist
         torch.cuda.set_device(local)
         if share:
@@ -699,7 +741,8 @@ def main():
 
     elapsed, cuts = timed_steps(step, args, dist, torch.cuda.synchronize, after)
     recs = per_rank_records({"rank": rank, "seed": seed, "elapsed_s": round(elapsed, 6),
-                             "bytes": work_bytes, "chunks": last.get("ncuts", 0)}, dist, world)
+                             "bytes": work_bytes, "chunks": last.get("ncuts", 0),
+                             **cut_record(cuts)}, dist, world)
     elapsed, total_bytes = aggregate(elapsed, work_bytes, dist, red_dev)
 
     value = total_bytes * args.steps / (1 << 30) / elapsed
@@ -760,8 +803,9 @@ def main():
     out["build_id"] = pbschunk.build_id()
     if share:
         out["rehearsal"] = "TEST ONLY: all ranks on GPU 0 over gloo; not a scaling measurement"
-    if world > 1:
+    if dist is not None:
         out["per_rank"] = recs
+        out["backend"] = dist.get_backend()
     if host_incl is not None:
         out["host_inclusive_gib_s"] = round(host_incl, 3)
     if args.digest and args.mode == "streams":

@@ -37,6 +37,7 @@
 #include <map>
 #include <mutex>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include "pbs_blob.h"
@@ -115,17 +116,36 @@ const CrcTables* device_tables(int dev) {
     return d;
 }
 
-// counter of the dynamic chunk order, one per stream, allocated on the stream's own
-// device and zeroed by a 8-byte memset on that stream before every launch (launches on
-// one stream are ordered, so a counter is never shared by two running launches, and an
-// aborted launch cannot leave a stale value behind).  release_stream_counter() frees
-// a stream's entry before the stream is destroyed (pbs_pipeline.cpp).
+// counter of the dynamic chunk order, one per (device, stream), allocated on the stream's
+// own device and zeroed by a 8-byte memset on that stream before every launch (launches
+// on one stream are ordered, so a counter is never shared by two running launches, and
+// an aborted launch cannot leave a stale value behind).  The null stream and
+// hipStreamPerThread are the same handle on every device and in every thread, so their
+// key also names the calling thread: two threads on the null stream would otherwise
+// interleave memset, memset, launch, launch on one counter.  release_stream_counter()
+// frees a stream's entry before the stream is destroyed (pbs_pipeline.cpp).
+struct CtrKey {
+    int dev;
+    hipStream_t st;
+    std::thread::id th;
+    bool operator<(const CtrKey& o) const {
+        if (dev != o.dev) return dev < o.dev;
+        if (st != o.st) return st < o.st;
+        return th < o.th;
+    }
+};
 std::mutex g_ctr_mu;
-std::map<hipStream_t, unsigned long long*> g_ctrs;
+std::map<CtrKey, unsigned long long*> g_ctrs;
+
+CtrKey ctr_key(hipStream_t st, int dev) {
+    const bool shared = st == nullptr || st == hipStreamPerThread;
+    return CtrKey{dev, st, shared ? std::this_thread::get_id() : std::thread::id()};
+}
 
 unsigned long long* stream_counter(hipStream_t st, int dev) {
     std::lock_guard<std::mutex> g(g_ctr_mu);
-    auto it = g_ctrs.find(st);
+    const CtrKey key = ctr_key(st, dev);
+    auto it = g_ctrs.find(key);
     if (it != g_ctrs.end()) return it->second;
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess) return nullptr;
@@ -134,15 +154,17 @@ unsigned long long* stream_counter(hipStream_t st, int dev) {
     const bool ok = hipMalloc(&d, sizeof(unsigned long long)) == hipSuccess;
     if (cur != dev) (void)hipSetDevice(cur);
     if (!ok) return nullptr;
-    g_ctrs[st] = d;
+    g_ctrs[key] = d;
     return d;
 }
 
 }  // namespace
 
 void release_stream_counter(hipStream_t st) {
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess) return;
     std::lock_guard<std::mutex> g(g_ctr_mu);
-    auto it = g_ctrs.find(st);
+    auto it = g_ctrs.find(ctr_key(st, dev));
     if (it == g_ctrs.end()) return;
     (void)hipFree(it->second);
     g_ctrs.erase(it);

@@ -150,7 +150,8 @@ struct pbs_chunker {
     int scan_dyn_env = -1;         // PBS_SCAN_DYN=0/1: force the static / dynamic tile order
     uint64_t fused_min_bytes = 0;  // smallest batch for the fused pass (PBS_FUSED_MIN_BYTES)  // smallest average served by the fused pass (PBS_FUSED_MIN_AVG: A/B)
     uint64_t susp_cap = 0, cand_cap = 0;
-    uint64_t batch_limit = 0;  // bytes per batch (0 = batch_max); shrunk when a batch is too dense
+    uint64_t batch_limit = 0;  // bytes per batch (0 = batch_max); shrunk when a batch is too
+                               // dense, reset at the start of every find_cuts / scan call
     bool too_dense = false;    // the last scan found more than kMaxBatchCand candidates
     uint64_t* h_small = nullptr;  // pinned + mapped: [0] counters, [8..19] results, [24..31] tail
     uint64_t* h_cuts = nullptr;   // pinned + mapped: cut list of the small resolve
@@ -998,6 +999,7 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
     server_stop(c);
     c->timing = pbs_timing{};
     c->timing_pending = false;
+    c->batch_limit = 0;  // a dense batch shortens batches for this call only
     HIP_TRY(c, hipEventRecord(c->ev[5], c->stream));
     const uint64_t end = c->consumed + len;
     uint64_t pos = std::max(c->consumed, c->scanned_end);
@@ -1283,6 +1285,7 @@ size_t pbs_chunker_scan(pbs_chunker* c, const uint8_t* data, size_t len) {
     const uint64_t end = c->consumed + len;
     if (end > c->scanned_end) {
         c->timing = pbs_timing{};
+        c->batch_limit = 0;  // a dense batch shortens batches for this call only
         // No cut can fall before chunk_start + min_eff - 1, and no window of a later position
         // reaches back before that minus 63: those bytes only update the 63-byte history
         // (exact for every later chunk too, whose starts are later)

@@ -208,6 +208,27 @@ hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, ui
                               uint32_t minimum, uint64_t last_seq, uint64_t idle_ticks,
                               hipStream_t stream);
 
+// Makes `dev` the calling thread's current device for a scope (allocations and stream /
+// event creation land on the current device, not on the device of the stream a call was
+// handed) and restores the previous one.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            prev = -1;
+            return;
+        }
+        ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+        if (prev == dev) prev = -1;  // nothing to restore
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 // pbs_blob.hip: free the blob-CRC chunk counter kept for `st` (call before destroying it)
 void release_stream_counter(hipStream_t st);
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,

@@ -663,28 +663,39 @@ struct HostStage {
     std::vector<uint8_t*> buf;  // 2 * kSlice each
     std::vector<hipStream_t> st;
     std::vector<hipEvent_t> ev;  // 2 per thread
+    // streams and events are created on device dv (the caller's stream's device), not
+    // on whatever device the calling thread has current
     bool grow(int dv, int t) {
         if (dev != dv) {
             release();
             dev = dv;
         }
-        while ((int)buf.size() < t) {
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess) return false;
+        if (cur != dv && hipSetDevice(dv) != hipSuccess) return false;
+        bool ok = true;
+        while (ok && (int)buf.size() < t) {
             uint8_t* b = nullptr;
             hipStream_t s = nullptr;
             hipEvent_t e0 = nullptr, e1 = nullptr;
-            if (hipHostMalloc(&b, 2 * kSlice, hipHostMallocDefault) != hipSuccess) return false;
+            if (hipHostMalloc(&b, 2 * kSlice, hipHostMallocDefault) != hipSuccess) {
+                ok = false;
+                break;
+            }
             if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
                 hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) {
                 (void)hipHostFree(b);
-                return false;
+                ok = false;
+                break;
             }
             buf.push_back(b);
             st.push_back(s);
             ev.push_back(e0);
             ev.push_back(e1);
         }
-        return true;
+        if (cur != dv) (void)hipSetDevice(cur);
+        return ok;
     }
     void release() {
         for (auto b : buf) (void)hipHostFree(b);
@@ -766,6 +777,10 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
     const double agg = std::min(threads * host_rate, host_data ? 1e12 : 14e9);
     hipStream_t st = (hipStream_t)hip_stream;
     auto clen = [&](uint32_t i) { return bounds[i + 1] - bounds[i]; };
+    int sdev = 0;
+    if (hipStreamGetDevice(st, &sdev) != hipSuccess) return PBS_ERR_NO_DEVICE;
+    pbs::DeviceGuard dg(sdev);  // the scratch below belongs on the stream's device
+    if (!dg.ok) return PBS_ERR_NO_DEVICE;
 
     std::vector<uint32_t> order(n);
     std::iota(order.begin(), order.end(), 0u);
@@ -786,6 +801,15 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
         hipMalloc(&d_dig, n * 32) != hipSuccess || (m && hipMalloc(&d_flags, m) != hipSuccess))
         fail(PBS_ERR_NOMEM);
     std::vector<uint8_t> zf(m, 0);
+    // the host share's D2H copies run on the HostStage streams, which do not wait for the
+    // caller's stream: this event marks the point on `st` after the caller's producer
+    // work (recorded before anything of ours, so the copies do not also wait for the GPU
+    // digest launch)
+    hipEvent_t ready = nullptr;
+    if (rc == PBS_OK && !host_data && threads > 0 &&
+        (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess ||
+         hipEventRecord(ready, st) != hipSuccess))
+        fail(PBS_ERR_HIP);
     if (rc == PBS_OK && (hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
                          hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess))
         fail(PBS_ERR_HIP);
@@ -865,9 +889,15 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
             std::lock_guard<std::mutex> lk(hs.mu);
             int dv = 0;
             const int t = (int)std::min<size_t>((size_t)threads, h);
-            if (hipGetDevice(&dv) != hipSuccess || !hs.grow(dv, t)) {
+            bool waits = true;
+            if (hipStreamGetDevice(st, &dv) != hipSuccess || !hs.grow(dv, t)) {
                 fail(PBS_ERR_NOMEM);
             } else {
+                for (int j = 0; j < t; ++j)
+                    waits = waits && hipStreamWaitEvent(hs.st[j], ready, 0) == hipSuccess;
+                if (!waits) fail(PBS_ERR_HIP);
+            }
+            if (rc == PBS_OK) {
                 std::atomic<size_t> next{0};
                 std::atomic<bool> bad{false};
                 auto run = [&](int j) {
@@ -903,6 +933,7 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
             if (d.first != d.second) std::memcpy(digests + 32 * (size_t)d.first, digests + 32 * (size_t)d.second, 32);
     for (auto e : ev)
         if (e) (void)hipEventDestroy(e);
+    if (ready) (void)hipEventDestroy(ready);
     for (void* p : {(void*)d_bounds, (void*)d_order, (void*)d_dig, (void*)d_flags})
         if (p) (void)hipFree(p);
     if (timing) {

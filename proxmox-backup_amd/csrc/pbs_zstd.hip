@@ -567,8 +567,11 @@ extern "C" size_t pbs_zstd_frame_bound(size_t len) { return (size_t)zstd::frame_
 extern "C" void pbs_blob_encode_release(void) {
     ZScratch& z = zscratch();
     std::lock_guard<std::mutex> lk(z.mu);
-    for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.seqs_out, (void*)z.zt})
-        if (p) (void)hipFree(p);
+    if (z.dev >= 0) {
+        DeviceGuard dg(z.dev);
+        for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.seqs_out, (void*)z.zt})
+            if (p) (void)hipFree(p);
+    }
     z.slots = nullptr;
     z.seqs = nullptr;
     z.seqs_out = nullptr;
@@ -606,8 +609,11 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     if (hipStreamGetDevice(st, &dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return PBS_ERR_NO_DEVICE;
+    // every allocation of this call (and the cached scratch) lives on the stream's device
+    DeviceGuard dg(dev);
+    if (!dg.ok) return PBS_ERR_NO_DEVICE;
 
-    // items: (chunk, 128 KiB block) pairs; an empty chunk is one item
+    // items: (chunk, 64 KiB block) pairs; an empty chunk is one item
     std::vector<uint64_t> items, first(n + 1);
     for (size_t i = 0; i < n; ++i) {
         first[i] = items.size();
@@ -646,7 +652,12 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     std::lock_guard<std::mutex> lk(zs.mu);
     const unsigned grid = (unsigned)std::min<uint64_t>(ni, (uint64_t)ncu * kZGroupsPerCu);
     if (rc == PBS_OK && compress) {
-        if (zs.dev != dev) {  // first use on this device (or another device): fresh scratch
+        if (zs.dev != dev) {  // first use, or another device: free the old scratch there
+            if (zs.dev >= 0) {
+                DeviceGuard og(zs.dev);
+                for (void* p : {(void*)zs.slots, (void*)zs.seqs, (void*)zs.seqs_out, (void*)zs.zt})
+                    if (p) (void)hipFree(p);
+            }
             zs.slots = nullptr;
             zs.slots_cap = 0;
             zs.seqs = nullptr;

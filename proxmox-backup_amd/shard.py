@@ -15,7 +15,9 @@ chunker.rs:146: once the window is full, rotl by 64 is the identity), so:
 
 The result equals one chunker over the concatenated stream (tests/test_shard.py).
 Collectives go through ``torch.distributed`` (RCCL over xGMI with the "nccl" backend on
-the GPU box, gloo in the CPU tests); nothing else crosses GPUs.
+the GPU box, gloo in the CPU tests); nothing else crosses GPUs.  gloo reduces CPU tensors
+only, so with a gloo group (the CPU tests, and bench.py's one-GPU rehearsal) the halo and
+the candidate lists are staged through host memory around each collective.
 """
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -36,18 +38,29 @@ def shard_ranges(total: int, world: int, align: int = 8) -> List[Tuple[int, int]
     return out
 
 
-def exchange_halo(tail: "torch.Tensor", dist, rank: int, world: int) -> bytes:
-    """All-gather every rank's last <= 63 bytes (uint8 tensor on the collective's
-    device) and return the left neighbour's (b"" on rank 0)."""
+def collective_device(dist, device):
+    """Where the collectives' tensors must live: the data's device for RCCL ("nccl"),
+    the host for gloo (which does not take device tensors)."""
     import torch
 
+    if dist is not None and dist.is_initialized() and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return device
+
+
+def exchange_halo(tail: "torch.Tensor", dist, rank: int, world: int) -> bytes:
+    """All-gather every rank's last <= 63 bytes and return the left neighbour's (b"" on
+    rank 0)."""
+    import torch
+
+    tail = tail.to(collective_device(dist, tail.device))
     buf = torch.zeros(HALO + 1, dtype=torch.uint8, device=tail.device)
     n = int(tail.numel())
     if n > HALO:
         raise ValueError("tail longer than the halo")
     buf[:n] = tail
     buf[HALO] = n
-    if dist is None or world == 1:
+    if dist is None:
         return b""
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)
@@ -58,11 +71,14 @@ def exchange_halo(tail: "torch.Tensor", dist, rank: int, world: int) -> bytes:
 
 
 def gather_candidates(cand: "torch.Tensor", dist, world: int) -> "torch.Tensor":
-    """All-gather variable-length int64 candidate lists and concatenate in rank order."""
+    """All-gather variable-length int64 candidate lists and concatenate in rank order
+    (the result on ``cand``'s device)."""
     import torch
 
-    if dist is None or world == 1:
+    if dist is None:
         return cand
+    home = cand.device
+    cand = cand.to(collective_device(dist, home))
     cnt = torch.tensor([cand.numel()], dtype=torch.int64, device=cand.device)
     counts = [torch.empty_like(cnt) for _ in range(world)]
     dist.all_gather(counts, cnt)
@@ -72,7 +88,7 @@ def gather_candidates(cand: "torch.Tensor", dist, world: int) -> "torch.Tensor":
     pad[: cand.numel()] = cand
     parts = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(parts, pad)
-    return torch.cat([p[:c] for p, c in zip(parts, counts)])
+    return torch.cat([p[:c] for p, c in zip(parts, counts)]).to(home)
 
 
 def phase_a(ch, dev_ptr: int, length: int, base: int, pre: bytes, device,

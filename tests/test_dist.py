@@ -115,21 +115,108 @@ def _has_gpu():
     return torch.cuda.device_count() > 0
 
 
+def _oracle_cuts(oracle, workload, seed, size, avg):
+    import numpy as np
+    gen = {"vmimage": oracle.gen_vmimage, "random": oracle.gen_random}[workload]
+    ref = oracle.chunk_feed(avg, gen(size, seed, 0))
+    if ref.size == 0 or int(ref[-1]) != size:
+        ref = np.append(ref, np.uint64(size))
+    return [int(x) for x in ref]
+
+
+def test_kfd_gpu_count_without_hip():
+    """The launcher counts GPUs from sysfs only; the visible-devices lists narrow it."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    n = bench.kfd_gpu_count()
+    assert n is None or n >= 0
+    if n:
+        old = os.environ.get("HIP_VISIBLE_DEVICES")
+        os.environ["HIP_VISIBLE_DEVICES"] = "0"
+        try:
+            assert bench.kfd_gpu_count() == 1
+        finally:
+            if old is None:
+                os.environ.pop("HIP_VISIBLE_DEVICES")
+            else:
+                os.environ["HIP_VISIBLE_DEVICES"] = old
+
+
+def test_standin_records_cut_lists(oracle):
+    """Every rank's record carries its cut list (and its SHA-256), so the multi-rank runs
+    can be diffed against the oracle rank by rank."""
+    size = int(0.01 * (1 << 30)) // 8 * 8
+    rc, out, err = _run_bench(["--gpus", "2", "--cpu-standin", "--size-gib", "0.01", "--avg", "65536",
+                               "--steps", "1", "--warmup", "0"])
+    assert rc == 0, err[-2000:]
+    for r in out["per_rank"]:  # (the stand-in's list is the oracle's: no tail entry)
+        ref = oracle.chunk_feed(65536, oracle.gen_vmimage(size, r["seed"], 0))
+        assert r["cuts"] == [int(x) for x in ref] and r["chunks"] == ref.size
+
+
 @pytest.mark.gpu
-def test_bench_share_gpu_rehearsal():
+@pytest.mark.parametrize("mode", ["streams", "sharded"])
+def test_bench_share_gpu_rehearsal(oracle, mode):
     """The N-rank GPU path of bench.py with both ranks on GPU 0 over gloo: one line from
-    rank 0, labelled as a rehearsal, n_gpus 2, per-rank seeds and cut lists, MAX/SUM
-    aggregation (the RCCL all-reduce is the only part it does not exercise)."""
-    rc, out, err = _run_bench(["--gpus", "2", "--size-gib", "0.25", "--steps", "2", "--warmup", "1",
-                               "--cpu-baseline", "0", "--host-inclusive-gib", "0",
+    rank 0, labelled as a rehearsal, n_gpus 2, MAX/SUM aggregation, and every rank's cut
+    list equal to the oracle's -- its own stream (seed + rank) in the streams mode, the
+    whole stream in the sharded mode (halo and candidate all-gathers staged through host
+    memory, since gloo takes CPU tensors).  The RCCL collectives are covered by
+    test_bench_rccl_world1."""
+    gib = 0.25
+    size = int(gib * (1 << 30)) // 8 * 8
+    rc, out, err = _run_bench(["--gpus", "2", "--size-gib", str(gib), "--steps", "2", "--warmup", "1",
+                               "--mode", mode, "--cpu-baseline", "0", "--host-inclusive-gib", "0",
                                "--secondary-random", "0"],
                               env={"PBS_BENCH_SHARE_GPU": "1"}, timeout=240)
     assert rc == 0, err[-2000:]
     assert out["n_gpus"] == 2 and out["metric"].startswith("REHEARSAL") and "rehearsal" in out
+    assert out["backend"] == "gloo"
     recs = sorted(out["per_rank"], key=lambda r: r["rank"])
     assert [r["rank"] for r in recs] == [0, 1]
-    assert recs[1]["seed"] == recs[0]["seed"] + 1
-    assert all(r["chunks"] > 0 for r in recs)
+    if mode == "streams":
+        assert recs[1]["seed"] == recs[0]["seed"] + 1
+        for r in recs:
+            assert r["bytes"] == size
+            assert r["cuts"] == _oracle_cuts(oracle, "vmimage", r["seed"], size, 4 << 20), r["rank"]
+    else:
+        ref = _oracle_cuts(oracle, "vmimage", recs[0]["seed"], size, 4 << 20)
+        assert sum(r["bytes"] for r in recs) == size
+        for r in recs:
+            assert r["cuts"] == ref, r["rank"]
     mx = max(r["elapsed_s"] for r in recs)
     tot = sum(r["bytes"] for r in recs)
     assert out["value"] == pytest.approx(tot * 2 / (1 << 30) / mx, rel=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["streams", "sharded"])
+def test_bench_rccl_world1(oracle, mode):
+    """bench.py under torch.distributed.run with one rank and its RCCL ("nccl") group
+    (PBS_BENCH_DIST_WORLD1=1): the device-tensor barrier, MAX/SUM all-reduces, the
+    per-rank all_gather_object and (sharded) the halo and candidate all-gathers all run
+    through RCCL on the GPU -- the collectives of the 8-GPU run, at world size 1."""
+    import subprocess
+    import sys
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gib = 0.25
+    size = int(gib * (1 << 30)) // 8 * 8
+    e = dict(os.environ, PBS_BENCH_DIST_WORLD1="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PBS_BENCH_SHARE_GPU"):
+        e.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "1", "--size-gib", str(gib), "--steps", "2",
+           "--warmup", "1", "--mode", mode, "--cpu-baseline", "0", "--host-inclusive-gib", "0",
+           "--secondary-random", "0"]
+    p = subprocess.run(cmd, env=e, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["backend"] == "nccl"
+    (r,) = out["per_rank"]
+    assert r["bytes"] == size
+    assert r["cuts"] == _oracle_cuts(oracle, "vmimage", r["seed"], size, 4 << 20)
+    assert out["value"] == pytest.approx(size * 2 / (1 << 30) / r["elapsed_s"], rel=1e-2)
