@@ -48,6 +48,7 @@ constexpr uint32_t kSub = 8192;     // one GPU wave's sub-block
 constexpr uint32_t kHist = 16384;   // window before a sub-block (reaches into the previous block)
 constexpr uint32_t kRound = 256, kMaxStep = 8;
 constexpr uint32_t kHashLog = 12, kCap = 32, kMinMatch = 5;
+constexpr uint32_t kHufStreams = 48 * 1024;  // largest Huffman stream bytes of a block
 
 // ------------------------------------------------------------------------ parse
 inline uint32_t rd32(const uint8_t* p) {
@@ -72,6 +73,7 @@ inline uint32_t prefix(const uint8_t* s, uint32_t a, uint32_t b, uint32_t lim) {
 }
 
 // src = the block (n bytes); src[-avail .. -1] = the chunk bytes before it
+uint64_t g_hist_inserts = 0;
 void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seqs) {
     const uint32_t hb = 5;
     const uint8_t* const b = src - avail;  // positions P = p + avail
@@ -81,8 +83,27 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
         const uint32_t se = std::min(s0 + kSub, N);
         std::fill(table.begin(), table.end(), 0u);
         const uint32_t wlo = s0 - std::min(s0, kHist);  // the sub-block's window start
-        for (uint32_t P = wlo; P < s0; ++P)  // history
-            if (P + hb <= N) table[hash5(b + P)] = P + 1;
+        // history: the window before the sub-block enters the table in rounds like the
+        // parse's (lookups before inserts; step 1 after a round in which some position's 5
+        // bytes equal its table or run candidate's, doubling to kMaxStep without)
+        for (uint32_t r0 = wlo, rn, hs = 1; r0 < s0; r0 = rn) {
+            rn = r0 + kRound * hs;
+            uint32_t pos[kRound], cand[kRound], np = 0;
+            for (uint32_t j = 0; j < kRound && r0 + j * hs < s0; ++j) pos[np++] = r0 + j * hs;
+            for (uint32_t k = 0; k < np; ++k) cand[k] = pos[k] + hb <= N ? table[hash5(b + pos[k])] : 0;
+            bool hit = false;
+            for (uint32_t k = 0; k < np; ++k) {
+                const uint32_t p = pos[k];
+                if (p + hb > N) continue;
+                uint32_t& t = table[hash5(b + p)];
+                if (p + 1 > t) t = p + 1;
+                // (5 equal bytes -- a run -- never count: runs need no dense history)
+                const bool run = rd32(b + p) == b[p] * 0x01010101u && b[p + 4] == b[p];
+                hit |= !run && cand[k] && std::memcmp(b + cand[k] - 1, b + p, 5) == 0;
+            }
+            g_hist_inserts += np;
+            hs = hit ? 1 : std::min(hs * 2, kMaxStep);
+        }
         uint32_t cur = s0, step = 1, rep = 0;  // rep 0: no offset in this sub-block yet
         for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
             rn = r0 + kRound * step;
@@ -571,6 +592,7 @@ void literals(std::vector<uint8_t>& o, const std::vector<uint8_t>& lit) {
         return;
     }
     const bool four = n >= 256;
+    const size_t desc = body.size();
     if (!four) {
         huf_stream(h, lit.data(), n, body);
     } else {
@@ -587,6 +609,11 @@ void literals(std::vector<uint8_t>& o, const std::vector<uint8_t>& lit) {
         for (int k = 0; k < 4; ++k) body.insert(body.end(), st[k].begin(), st[k].end());
     }
     const uint32_t c = (uint32_t)body.size();
+    // the GPU stages the streams in 48 KiB of LDS: longer ones are written raw
+    if (c - desc - (four ? 6 : 0) > kHufStreams) {
+        raw_literals(o, lit.data(), n, 0);
+        return;
+    }
     // header: type 2, size format 0 (1 stream, 10+10 bits), 1 (4 streams, 10+10), 2 (14+14),
     // 3 (18+18)
     const uint32_t mx = std::max(n, c);
@@ -867,6 +894,8 @@ size_t frame_header(uint8_t* o, uint64_t len) {
 }  // namespace
 
 extern "C" {
+
+uint64_t zstd_twin_hist_inserts(void) { return g_hist_inserts; }
 
 uint64_t zstd_twin_bound(uint64_t len) {
     const uint64_t nb = len ? (len + kBlock - 1) / kBlock : 1;

@@ -5,32 +5,41 @@
 // chunk, else the uncompressed blob {UNCOMPRESSED_BLOB_MAGIC_1_0, CRC, bytes}; the CRC
 // (`compute_crc`, :70-75) covers everything after the header.  C ABI: include/pbs_blob.h.
 //
-// The frame (zstd_enc.h) is built from independent 64 KiB zstd blocks, one workgroup per
-// block (a 64 GiB stream is 1 M blocks), the block staged in LDS (16-byte loads of its
-// aligned span; every byte and word read after that is LDS: 2 workgroups per CU):
-//   1. RLE test (every byte equal: a 4-byte RLE block -- the zero pages of a VM image);
-//   2. each wave parses its own 16 KiB sub-block with its own 512-entry LDS table, in
-//      rounds of 256 sampled positions (4 per lane; every step-th byte: step 1 after a
-//      round with a match, doubling to 8 while rounds find none): hash of the 4 bytes at
-//      p -> candidate = the last sampled position of an earlier round with that hash
-//      (`ds_max` inserts after the round's lookups) or the run candidate p - 1, the
-//      longer match winning; the 4-byte compares and all LDS reads issued
-//      unconditionally; matches capped at 32
-//      and at the sub-block end; positions inside a chosen match skipped;
-//   3. the wave's greedy parse over the round's match masks (ballots, registers): from
-//      the current position the next matching position starts a sequence, a capped match
-//      is extended 256 bytes per step (a word per lane, ballot of mismatches) -- no
-//      workgroup barrier until the four waves' sequences are combined (literals carry
-//      over sub-block ends);
-//   4. wave 0 lane 0 writes the FSE-coded sequences (predefined tables) while waves 1-3
-//      copy the literal runs; raw block if that is not shorter.
+// The frame is built from 64 KiB zstd blocks, one 512-thread workgroup per block at a
+// time (one per CU: 154 KiB of LDS).  Per block:
+//   stage   the block and up to 16 KiB of the chunk before it (the match window of its
+//           first sub-blocks) in LDS -- every later byte read is LDS;
+//   RLE     every byte equal: a 4-byte RLE block (the zero pages of a VM image);
+//   parse   each of the 8 waves parses one 8 KiB sub-block with its own 4096-entry table
+//           of 16-bit window positions: the 16 KiB before the sub-block first enter the
+//           table in accelerated rounds, then rounds of 256 sampled positions (step 1
+//           after a round with a match, doubling to 8 without): candidates = the table
+//           (hash of 5 bytes; the last position of an EARLIER round) and the run
+//           candidate p - 1, the longer (capped at 32) winning; the wave's greedy walk
+//           over the round's match masks (ballots) checks the positions before the next
+//           match for a match at the sub-block's last offset (a repeat match, one ballot),
+//           extends a taken table match backwards over the literals (one ballot) and every
+//           match forwards to its end (256 bytes per step);
+//   literals the literal bytes (a bitmap of the matched bytes, per-thread popcounts and a
+//           block scan give each literal its index): RLE, raw, or Huffman-coded (RFC 8878
+//           4.2) -- histogram, a two-queue Huffman merge limited to 11 bits, canonical
+//           codes, weights direct or FSE-coded, then every thread ORs the codes of its
+//           literals into 4 streams staged in LDS at offsets from a block scan of the
+//           code lengths (the streams are written backwards: bit offsets from the end of
+//           the literal's stream);
+//   sequences repeat-offset codes per sub-block (one lane each), code histograms, per
+//           stream (LL / OF / ML) the cheapest of predefined / RLE / own FSE table (three
+//           waves), then one lane writes the FSE bit stream;
+//   raw     when the compressed block is not shorter than its bytes.
 // Then per chunk: frame size, compressed-or-not (the reference's "only if shorter",
 // :153), blob offsets by an exclusive scan, the blocks gathered into the blob images,
 // and the blob CRC by the CRC kernel of pbs_blob.hip (12-byte header skipped).
 //
-// The parse is the host twin's (oracle/zstd_twin.cpp) step for step, so the bytes are
-// compared exactly; libzstd decodes every frame back to the chunk (tests).  The bytes are
-// not libzstd's level 1 (parity unpinned).
+// Every decision is integer-only and restated serially by the host twin
+// (oracle/zstd_twin.cpp, written separately), so the bytes are compared exactly; libzstd
+// decodes every frame back to the chunk (tests).  The bytes are not libzstd's level 1
+// (parity unpinned); their size is within a few per cent of it on
+// text, pxar-like and VM-image data (tests/test_zstd_cpu.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -52,67 +61,84 @@ namespace {
 
 using namespace zstd;
 
-constexpr int kZThreads = 256;
-constexpr uint32_t kZSub = 16384;                 // one wave's sub-block of a block
-constexpr uint32_t kZRound = 256, kZHashLog = 9, kZCap = 32, kZMaxStep = 8;
-constexpr int kZPer = kZRound / 64;              // positions per lane and round
-constexpr uint32_t kSubSeq = kZSub / 4;          // sequences one sub-block can hold
-constexpr uint32_t kWaveLdsSeq = 64;             // of them kept in LDS (the rest in global scratch)
-constexpr uint64_t kSlot = kEncBlock + 128;  // block header + up to 64 KiB + slack for 8-byte flushes
-constexpr uint32_t kMaxSeq = kEncBlock / 4;
-constexpr uint32_t kStageWords = kEncBlock / 16 + 1;  // 16-byte words covering a block at any alignment
-constexpr int kZGroupsPerCu = 2;                    // LDS: 77 KiB per workgroup
+constexpr int kZThreads = 512;
+constexpr int kZWaves = kZThreads / 64;
+constexpr uint32_t kZSub = 8192;     // one wave's sub-block
+constexpr uint32_t kZHist = 16384;   // window before a sub-block
+constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8;
+constexpr int kZPer = kZRound / 64;  // positions per lane and round
+constexpr uint32_t kZTab = 1u << kZHashLog;
+constexpr uint32_t kZStageWords = (kZHist + kEncBlock) / 16 + 3;  // 16-byte words at any alignment + 2 zero words
+constexpr uint32_t kZSubSeq = kZSub / kZMin + 2;                  // sequences one sub-block can emit
+constexpr uint32_t kZBlockSeq = kZWaves * kZSubSeq;
+constexpr uint64_t kSlot = kEncBlock + 1024;  // block header + up to 64 KiB + slack (section headers, flushes)
+constexpr uint32_t kHufStreams = 48 * 1024;  // Huffman streams staged in LDS (longer: raw literals)
+constexpr uint32_t kHufMax = 11;
+static_assert(kEncBlock / kZSub == (uint32_t)kZWaves, "one sub-block per wave");
+static_assert(kZTab * 2 * kZWaves == 64 * 1024, "the tables fill the work area");
 
 // pbs-datastore/src/file_formats.rs:9, :12
 constexpr uint8_t kUncompressedMagic[8] = {66, 171, 56, 7, 190, 131, 112, 161};
 constexpr uint8_t kCompressedMagic[8] = {49, 185, 88, 66, 111, 182, 163, 127};
 
-struct ZTables {
-    FseCTable ll, ml, of;
-};
-
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
+struct Seq {
+    uint32_t pos, ml, off;  // match start (block position), length, offset
+};
+struct Coded {
+    uint32_t ll, ml, ofv, codes;  // offset value: repeat code 1-3 or offset + 3; codes llc | mlc << 8 | ofc << 16
+};
 
-// The block staged in LDS: 16-byte words of the aligned span around it; block byte i is
-// LDS byte i + r (r = the block's address & 15).
-struct Stage {
-    const uint32_t* w;  // LDS words
+// The staged window in LDS: window byte P (P = 0 at the chunk byte `hist` before the
+// block) is LDS byte P + r.
+struct Win {
+    const uint32_t* w;
     uint32_t r;
-    __device__ __forceinline__ uint32_t byte(uint32_t i) const {
-        return reinterpret_cast<const uint8_t*>(w)[i + r];
+    __device__ __forceinline__ uint32_t byte(uint32_t P) const {
+        return reinterpret_cast<const uint8_t*>(w)[P + r];
     }
-    // little-endian 4 bytes at block position i (i + 3 inside the staged span)
-    __device__ __forceinline__ uint32_t word(uint32_t i) const {
-        const uint32_t o = i + r;
+    __device__ __forceinline__ uint32_t word(uint32_t P) const {  // 4 bytes little-endian
+        const uint32_t o = P + r;
         return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
     }
 };
 
-// Common prefix of the block at positions c < p, at most lim bytes: word compares, the
-// first differing byte from the lowest set bit of the XOR.
-__device__ __forceinline__ uint32_t common_prefix(const Stage& s, uint32_t c, uint32_t p, uint32_t lim) {
+__device__ __forceinline__ uint32_t hash5(uint32_t w, uint32_t b4) {
+    return ((w * 2654435761u) ^ (b4 * 2246822519u)) >> (32 - kZHashLog);
+}
+
+// table[h] = max(table[h], v) for this wave's lanes: write, read back, repeat while a
+// smaller value of another lane of the same instruction landed (lockstep: the survivors
+// only ever raise it)
+__device__ __forceinline__ void tab_max(uint16_t* e, uint32_t v) {
+    volatile uint16_t* ve = e;
+    for (;;) {
+        *ve = (uint16_t)v;
+        if (*ve >= v) break;
+    }
+}
+
+// common prefix of window positions a < b, at most lim bytes (word compares)
+__device__ __forceinline__ uint32_t win_prefix(const Win& W, uint32_t a, uint32_t b, uint32_t lim) {
     uint32_t L = 0;
     while (L + 4 <= lim) {
-        const uint32_t x = s.word(c + L) ^ s.word(p + L);
+        const uint32_t x = W.word(a + L) ^ W.word(b + L);
         if (x) return L + ((uint32_t)__builtin_ctz(x) >> 3);
         L += 4;
     }
-    while (L < lim && s.byte(c + L) == s.byte(p + L)) ++L;
+    while (L < lim && W.byte(a + L) == W.byte(b + L)) ++L;
     return L;
 }
 
-// cnt bytes of the staged block from position `from` to global dst: head bytes up to a
-// 4-aligned dst, then dword stores (one LDS word read each), then the tail; threads t of nt.
-__device__ __forceinline__ void copy_from_stage(uint8_t* dst, const Stage& S, uint32_t from, uint32_t cnt,
-                                                uint32_t t, uint32_t nt) {
-    uint32_t head = (uint32_t)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3);
-    if (head > cnt) head = cnt;
-    if (t < head) dst[t] = (uint8_t)S.byte(from + t);
-    const uint32_t nwd = (cnt - head) >> 2;
-    uint32_t* const dw = reinterpret_cast<uint32_t*>(dst + head);
-    for (uint32_t w = t; w < nwd; w += nt) dw[w] = S.word(from + head + 4 * w);
-    for (uint32_t i = head + 4 * nwd + t; i < cnt; i += nt) dst[i] = (uint8_t)S.byte(from + i);
+// inclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_incl(uint32_t x, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
 }
 
 // n bytes global -> global at any alignments: 16-byte stores at 16-aligned dst, each built
@@ -143,56 +169,480 @@ __device__ __forceinline__ void copy_global(uint8_t* dst, const uint8_t* src, ui
     for (uint64_t i = head + 16 * nq + t; i < n; i += nt) dst[i] = src[i];
 }
 
-// PBS_ZSTD_PROBE=1 (diagnostics): workgroup 0 adds wall-clock ticks (100 MHz) per phase
-// into g_zprobe: 0 stage, 1 RLE test, 2 wave 0's sub-block (lookups, matches, parse), 3
-// combine (barrier included), 4 encode + literal copy, 5 raw copy, 6 items, 7 sequences.
-__device__ unsigned long long g_zprobe[8];
+// ---------------------------------------------------------------- bit writers
+// Backward bit stream of RFC 8878 4.1 as an encoder writes it (fields at increasing bit
+// positions, bytes little-endian), one lane, to global memory.
+struct GBits {
+    uint64_t acc;
+    uint32_t n;
+    uint8_t* p;
+    __device__ void init(uint8_t* dst) {
+        acc = 0;
+        n = 0;
+        p = dst;
+    }
+    __device__ void put(uint64_t v, uint32_t nb) {
+        acc |= (v & ((1ull << nb) - 1ull)) << n;  // nb <= 32
+        n += nb;
+        if (n >= 32) {
+            p[0] = (uint8_t)acc;
+            p[1] = (uint8_t)(acc >> 8);
+            p[2] = (uint8_t)(acc >> 16);
+            p[3] = (uint8_t)(acc >> 24);
+            p += 4;
+            acc >>= 32;
+            n -= 32;
+        }
+    }
+    __device__ void close() {
+        put(1, 1);
+        while (n > 0) {
+            *p++ = (uint8_t)acc;
+            acc >>= 8;
+            n = n > 8 ? n - 8 : 0;
+        }
+    }
+};
 
-template <bool PROBE>
+// the same into an LDS byte buffer (weights description)
+struct LBits {
+    uint64_t acc;
+    uint32_t n;
+    uint8_t* p;
+    __device__ void init(uint8_t* dst) {
+        acc = 0;
+        n = 0;
+        p = dst;
+    }
+    __device__ void put(uint64_t v, uint32_t nb) {
+        acc |= (v & ((1ull << nb) - 1ull)) << n;
+        n += nb;
+        while (n >= 8) {
+            *p++ = (uint8_t)acc;
+            acc >>= 8;
+            n -= 8;
+        }
+    }
+    __device__ void close() {
+        put(1, 1);
+        if (n) *p++ = (uint8_t)acc;
+        n = 0;
+    }
+};
+
+// ---------------------------------------------------------------- FSE (one lane)
+constexpr int kFseCells = 512;
+struct FseT {
+    uint16_t next[kFseCells];
+    int32_t dnb[53];
+    int32_t dfs[53];
+    int32_t log;
+    uint32_t mode;  // 0 predefined, 1 RLE, 2 FSE-compressed
+    uint32_t desc_len;
+    uint8_t desc[128];
+    uint8_t sym_at[kFseCells];  // construction scratch
+};
+
+__device__ __noinline__ void fse_build(FseT& t, const int16_t* norm, int nsym, int log) {
+    const int size = 1 << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    int high = size - 1;
+    int cum[54];
+    cum[0] = 0;
+    for (int s = 0; s < nsym; ++s) {
+        if (norm[s] == -1) {
+            cum[s + 1] = cum[s] + 1;
+            t.sym_at[high--] = (uint8_t)s;
+        } else {
+            cum[s + 1] = cum[s] + norm[s];
+        }
+    }
+    int pos = 0;
+    for (int s = 0; s < nsym; ++s)
+        for (int k = 0; k < norm[s]; ++k) {
+            t.sym_at[pos] = (uint8_t)s;
+            do pos = (pos + step) & mask;
+            while (pos > high);
+        }
+    for (int u = 0; u < size; ++u) t.next[cum[t.sym_at[u]]++] = (uint16_t)(size + u);
+    int total = 0;
+    for (int s = 0; s < nsym; ++s) {
+        const int c = norm[s];
+        if (c == 0) {
+            t.dnb[s] = ((log + 1) << 16) - size;
+            t.dfs[s] = 0;
+        } else if (c == -1 || c == 1) {
+            t.dnb[s] = (log << 16) - size;
+            t.dfs[s] = total - 1;
+            ++total;
+        } else {
+            const int maxbits = log - (int)highbit((uint32_t)(c - 1));
+            t.dnb[s] = (maxbits << 16) - (c << maxbits);
+            t.dfs[s] = total - c;
+            total += c;
+        }
+    }
+    t.log = log;
+}
+
+__device__ __forceinline__ uint32_t fse_init(const FseT& t, uint32_t s) {
+    const uint32_t nb = (uint32_t)((t.dnb[s] + (1 << 15)) >> 16);
+    const uint32_t v0 = (nb << 16) - (uint32_t)t.dnb[s];
+    return t.next[(v0 >> nb) + t.dfs[s]];
+}
+template <typename B>
+__device__ __forceinline__ void fse_enc(B& b, const FseT& t, uint32_t& v, uint32_t s) {
+    const uint32_t nb = (v + (uint32_t)t.dnb[s]) >> 16;
+    b.put(v, nb);
+    v = t.next[(v >> nb) + t.dfs[s]];
+}
+
+__device__ __noinline__ int fse_log(uint32_t total, uint32_t max_sym, int max_log) {
+    int log = max_log;
+    const int src = (int)highbit(total - 1) - 2;
+    const int minb = (int)min(highbit(total) + 1, highbit(max_sym) + 2);
+    if (src < log) log = src;
+    if (minb > log) log = minb;
+    return max(5, min(log, max_log));
+}
+
+__device__ __noinline__ void fse_normalize(int16_t* norm, const uint32_t* cnt, int nsym, uint32_t total, int log) {
+    const int64_t scale = 1ll << log;
+    int64_t sum = 0;
+    for (int s = 0; s < nsym; ++s) {
+        if (!cnt[s]) {
+            norm[s] = 0;
+            continue;
+        }
+        int64_t v = ((int64_t)cnt[s] * scale + total / 2) / total;
+        if (v < 1) v = 1;
+        norm[s] = (int16_t)v;
+        sum += v;
+    }
+    while (sum != scale) {
+        int big = -1;
+        for (int s = 0; s < nsym; ++s)
+            if (norm[s] > 0 && (big < 0 || norm[s] > norm[big])) big = s;
+        if (sum < scale) {
+            norm[big] = (int16_t)(norm[big] + (scale - sum));
+            sum = scale;
+        } else {
+            const int64_t take = min(sum - scale, (int64_t)norm[big] - 1);
+            norm[big] = (int16_t)(norm[big] - take);
+            sum -= take;
+        }
+    }
+}
+
+// RFC 8878 4.1.1 table description; returns its bytes
+__device__ __noinline__ uint32_t fse_ncount(uint8_t* o, const int16_t* norm, int nsym, int log) {
+    uint8_t* const o0 = o;
+    const int size = 1 << log;
+    uint64_t bs = (uint64_t)(log - 5);
+    int nb = 4;
+    int remaining = size + 1, threshold = size, nbits = log + 1, s = 0;
+    bool prev0 = false;
+    while (s < nsym && remaining > 1) {
+        if (prev0) {
+            int start = s;
+            while (s < nsym && !norm[s]) ++s;
+            while (s >= start + 24) {
+                start += 24;
+                bs |= 0xFFFFull << nb;
+                nb += 16;
+                while (nb >= 8) {
+                    *o++ = (uint8_t)bs;
+                    bs >>= 8;
+                    nb -= 8;
+                }
+            }
+            while (s >= start + 3) {
+                start += 3;
+                bs |= 3ull << nb;
+                nb += 2;
+            }
+            bs |= (uint64_t)(s - start) << nb;
+            nb += 2;
+            while (nb >= 8) {
+                *o++ = (uint8_t)bs;
+                bs >>= 8;
+                nb -= 8;
+            }
+        }
+        int count = norm[s++];
+        const int mx = (2 * threshold - 1) - remaining;
+        remaining -= count < 0 ? -count : count;
+        ++count;
+        if (count >= threshold) count += mx;
+        bs |= (uint64_t)count << nb;
+        nb += nbits;
+        nb -= count < mx;
+        prev0 = count == 1;
+        while (remaining < threshold) {
+            --nbits;
+            threshold >>= 1;
+        }
+        while (nb >= 8) {
+            *o++ = (uint8_t)bs;
+            bs >>= 8;
+            nb -= 8;
+        }
+    }
+    while (nb > 0) {
+        *o++ = (uint8_t)bs;
+        bs >>= 8;
+        nb -= 8;
+    }
+    return (uint32_t)(o - o0);
+}
+
+// Table of one sequence symbol stream: the cheapest of predefined (0), RLE (1) and own
+// FSE table (2) by the integer estimate (ties keep the earlier mode).
+__device__ __noinline__ void seq_table(FseT& t, const uint32_t* cnt, int nsym, uint32_t nseq, const int16_t* pre, int pre_log,
+                          int max_log) {
+    int distinct = 0, maxs = 0;
+    for (int s = 0; s < nsym; ++s)
+        if (cnt[s]) {
+            ++distinct;
+            maxs = s;
+        }
+    uint64_t c_pre = 0;
+    for (int s = 0; s < nsym; ++s)
+        if (cnt[s]) c_pre += (uint64_t)cnt[s] * (256u * pre_log - lg256(pre[s] < 1 ? 1 : pre[s]));
+    t.desc_len = 0;
+    if (distinct == 1 && nseq > 2) {
+        t.mode = 1;
+        t.desc[0] = (uint8_t)maxs;
+        t.desc_len = 1;
+        return;
+    }
+    if (nseq >= 16) {
+        const int log = fse_log(nseq, (uint32_t)maxs, max_log);
+        int16_t norm[53];
+        fse_normalize(norm, cnt, maxs + 1, nseq, log);
+        const uint32_t d = fse_ncount(t.desc, norm, maxs + 1, log);
+        uint64_t c = 2048ull * d;
+        for (int s = 0; s <= maxs; ++s)
+            if (cnt[s]) c += (uint64_t)cnt[s] * (256u * log - lg256((uint32_t)norm[s]));
+        if (c < c_pre) {
+            t.mode = 2;
+            t.desc_len = d;
+            fse_build(t, norm, maxs + 1, log);
+            return;
+        }
+    }
+    t.mode = 0;
+    int16_t p[53];
+    for (int s = 0; s < nsym; ++s) p[s] = pre[s];
+    fse_build(t, p, nsym, pre_log);
+}
+
+// ---------------------------------------------------------------- LDS layout
+// work area (64 KiB): the parse's tables, then the entropy stage's buffers
+struct EntropyArea {
+    uint32_t streams[kHufStreams / 4 + 4];  // Huffman streams (and, before them, per-wave literal histograms)
+    uint32_t bitmap[kEncBlock / 32];        // literal bytes of the block
+    uint32_t hist[256];
+    uint32_t keys[256];   // symbols sorted by (count, symbol)
+    uint32_t tw[512];     // Huffman merge: node weights
+    uint16_t par[512];    // ... and parents
+    uint8_t lens[256];    // code length per sorted index
+    uint8_t len[256];     // code length per symbol
+    uint16_t code[256];
+    uint32_t shist[36 + 53 + 32];  // sequence code histograms: LL, ML, OF
+};
+static_assert(sizeof(EntropyArea) <= 64 * 1024, "entropy buffers fit the work area");
+
+struct Ctl {
+    uint32_t nseq[kZWaves];     // sequences per sub-block
+    uint32_t lastend[kZWaves];  // end of the sub-block's last match (block position), 0 if none
+    uint32_t wsum[kZWaves];     // block-scan partials
+    uint32_t wsum2[kZWaves];
+    uint32_t segP[5];           // Huffman: bits before each segment boundary
+    uint32_t lit_mode, lit_size, huf_c, huf_hs, desc_len;
+    uint32_t seq_size, seq_ok;
+    int32_t root;               // Huffman merge: the root node
+    uint8_t desc[264];          // Huffman tree description (FSE form: <= ~210 bytes before the 128 check)
+};
+
+// Huffman tree description (RFC 8878 4.2.1, one lane): the weights of symbols 0 ..
+// last-1 (the last one is implied), FSE-compressed (two interleaved states) when that is
+// shorter, else in the direct 4-bit form; false when neither applies (raw literals).
+__device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scratch, uint32_t mb, uint32_t lastsym) {
+    const int nwt = (int)lastsym;
+    uint32_t wc[16] = {0};
+    uint32_t maxw = 0;
+    for (int s = 0; s < nwt; ++s) {
+        const uint32_t wv = E.len[s] ? mb + 1 - E.len[s] : 0;
+        ++wc[wv];
+        maxw = max(maxw, wv);
+    }
+    bool fse_ok = false;
+    uint32_t fl = 0;
+    if (nwt > 2) {
+        bool single = false;
+        for (int v = 0; v < 16; ++v) single |= wc[v] == (uint32_t)nwt;
+        if (!single) {
+            const int lg = fse_log((uint32_t)nwt, maxw, 6);
+            int16_t norm[16];
+            fse_normalize(norm, wc, (int)maxw + 1, (uint32_t)nwt, lg);
+            FseT& t = t_scratch;
+            fl = fse_ncount(ctl.desc + 1, norm, (int)maxw + 1, lg);
+            fse_build(t, norm, (int)maxw + 1, lg);
+            LBits bw;
+            bw.init(ctl.desc + 1 + fl);
+            auto wt = [&](int s) { return E.len[s] ? mb + 1 - E.len[s] : 0u; };
+            uint32_t v1, v2;
+            int i = nwt;
+            if (nwt & 1) {
+                v1 = fse_init(t, wt(--i));
+                v2 = fse_init(t, wt(--i));
+                fse_enc(bw, t, v1, wt(--i));
+            } else {
+                v2 = fse_init(t, wt(--i));
+                v1 = fse_init(t, wt(--i));
+            }
+            while (i > 0) {
+                fse_enc(bw, t, v2, wt(--i));
+                fse_enc(bw, t, v1, wt(--i));
+            }
+            bw.put(v2, (uint32_t)t.log);
+            bw.put(v1, (uint32_t)t.log);
+            bw.close();
+            fl = (uint32_t)(bw.p - ctl.desc - 1);
+            fse_ok = fl < 128;
+        }
+    }
+    const uint32_t direct = nwt <= 128 ? 1 + (uint32_t)(nwt + 1) / 2 : 0xFFFFFFFFu;
+    if (fse_ok && fl + 1 < direct) {
+        ctl.desc[0] = (uint8_t)fl;
+        ctl.desc_len = fl + 1;
+    } else if (direct != 0xFFFFFFFFu) {
+        ctl.desc[0] = (uint8_t)(127 + nwt);
+        for (int s = 0; s < nwt; s += 2) {
+            const uint32_t a = E.len[s] ? mb + 1 - E.len[s] : 0;
+            const uint32_t b = s + 1 < nwt && E.len[s + 1] ? mb + 1 - E.len[s + 1] : 0;
+            ctl.desc[1 + s / 2] = (uint8_t)(a << 4 | b);
+        }
+        ctl.desc_len = direct;
+    } else {
+        return false;  // no description fits: raw literals
+    }
+    return true;
+}
+
+// Sequences section (RFC 8878 3.1.1.3.2, one lane): count, modes, table descriptions, the
+// FSE bit stream (the last sequence first); ctl.seq_ok = false once it passes the raw size.
+__device__ __noinline__ void write_sequences(Ctl& ctl, const FseT* fse, const Coded* __restrict__ coded, uint32_t nseq,
+                                             uint8_t* lit_out, uint32_t lsz, uint8_t* out, uint32_t n) {
+    uint8_t* o = lit_out + lsz;
+    uint8_t* const lim = out + 3 + n;  // past it the block is stored raw anyway
+    const uint32_t ns = nseq;
+    if (ns < 128) {
+        *o++ = (uint8_t)ns;
+    } else if (ns < 0x7F00) {
+        *o++ = (uint8_t)((ns >> 8) + 0x80);
+        *o++ = (uint8_t)ns;
+    } else {
+        *o++ = 0xFF;
+        *o++ = (uint8_t)(ns - 0x7F00);
+        *o++ = (uint8_t)((ns - 0x7F00) >> 8);
+    }
+    bool ok = true;
+    if (ns) {
+        const FseT& tl = fse[0];
+        const FseT& to = fse[1];
+        const FseT& tm = fse[2];
+        *o++ = (uint8_t)(tl.mode << 6 | to.mode << 4 | tm.mode << 2);
+        for (uint32_t i = 0; i < tl.desc_len; ++i) *o++ = tl.desc[i];
+        for (uint32_t i = 0; i < to.desc_len; ++i) *o++ = to.desc[i];
+        for (uint32_t i = 0; i < tm.desc_len; ++i) *o++ = tm.desc[i];
+        GBits b;
+        b.init(o);
+        const bool rl = tl.mode != 1, ro = to.mode != 1, rm = tm.mode != 1;
+        uint32_t vl = 0, vo = 0, vm = 0;
+        {
+            const Coded z = coded[ns - 1];
+            const uint32_t llc = z.codes & 0xFF, mlc = (z.codes >> 8) & 0xFF, ofc = z.codes >> 16;
+            if (rm) vm = fse_init(tm, mlc);
+            if (ro) vo = fse_init(to, ofc);
+            if (rl) vl = fse_init(tl, llc);
+            b.put(z.ll - kLLBase[llc], kLLBits[llc]);
+            b.put(z.ml - kMLBase[mlc], kMLBits[mlc]);
+            b.put(z.ofv - (1u << ofc), ofc);
+        }
+        Coded nx = ns >= 2 ? coded[ns - 2] : Coded{0, 0, 0, 0};
+        for (uint32_t q = ns - 1; q-- > 0;) {
+            const Coded x = nx;
+            if (q) nx = coded[q - 1];
+            const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
+            if (ro) fse_enc(b, to, vo, ofc);
+            if (rm) fse_enc(b, tm, vm, mlc);
+            if (rl) fse_enc(b, tl, vl, llc);
+            b.put(x.ll - kLLBase[llc], kLLBits[llc]);
+            b.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
+            b.put(x.ofv - (1u << ofc), ofc);
+            if (b.p > lim) {
+                ok = false;
+                break;
+            }
+        }
+        if (ok) {
+            if (rm) b.put(vm, (uint32_t)tm.log);
+            if (ro) b.put(vo, (uint32_t)to.log);
+            if (rl) b.put(vl, (uint32_t)tl.log);
+            b.close();
+            o = b.p;
+        }
+    }
+    const uint32_t body = ok ? (uint32_t)(o - lit_out) : 0xFFFFFFFFu;
+    ctl.seq_ok = ok && body < n;
+    ctl.seq_size = body;
+        
+}
+
+// Two-queue Huffman merge (one lane): leaves 0..m-1 = the symbols sorted by (count,
+// symbol) (E.tw holds their sorted keys on entry), internal nodes m.. in creation order,
+// ties taking the leaf; parents in E.par, the root in ctl.root.
+__device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) {
+        // two-queue merge: leaves 0..m-1 sorted, internal nodes m.. in creation order
+        const int m = (int)dist;
+        for (int i = 0; i < m; ++i) E.keys[i] = E.tw[i] & 0xFF;  // sorted symbols
+        for (int i = 0; i < m; ++i) E.tw[i] = E.tw[i] >> 8;      // leaf weights
+        int li = 0, ii = m, nn = m;
+        while (nn < 2 * m - 1) {
+            int a, b;
+            if (li < m && (ii >= nn || E.tw[li] <= E.tw[ii])) a = li++; else a = ii++;
+            if (li < m && (ii >= nn || E.tw[li] <= E.tw[ii])) b = li++; else b = ii++;
+            E.tw[nn] = E.tw[a] + E.tw[b];
+            E.par[a] = (uint16_t)nn;
+            E.par[b] = (uint16_t)nn;
+            ++nn;
+        }
+        ctl.root = nn - 1;
+}
+
 __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
-    const uint64_t* __restrict__ items, uint64_t nitems, const ZTables* __restrict__ zt,
-    uint8_t* __restrict__ slots, uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch,
-    Seq* __restrict__ seq_out_scratch) {
-    __shared__ uint4 blk[kStageWords + 1];
-    __shared__ uint32_t table[kZThreads / 64][1u << kZHashLog];  // one per wave
-    __shared__ uint32_t s_wave[kZThreads / 64][3];               // per wave: sequences, matched bytes, end
-    __shared__ Seq s_wseq[kZThreads / 64][kWaveLdsSeq];            // each wave's first sequences
-    __shared__ ZTables s_zt;
-    __shared__ uint32_t s_u[4];
+    const uint64_t* __restrict__ items, uint64_t nitems, uint8_t* __restrict__ slots,
+    uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch, Coded* __restrict__ coded_scratch) {
+    __shared__ uint4 stage[kZStageWords];
+    __shared__ __attribute__((aligned(16))) uint8_t work[64 * 1024];
+    __shared__ FseT fse[3];  // LL, OF, ML
+    __shared__ Ctl ctl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (uint32_t i = tid; i < sizeof(ZTables) / 4; i += kZThreads)
-        reinterpret_cast<uint32_t*>(&s_zt)[i] = reinterpret_cast<const uint32_t*>(zt)[i];
-    Seq* const wseq = seq_scratch + (uint64_t)blockIdx.x * kMaxSeq + (uint64_t)wave * kSubSeq;  // positions
-    Seq* const gseq = seq_out_scratch + (uint64_t)blockIdx.x * kMaxSeq;
+    uint16_t* const tabs = reinterpret_cast<uint16_t*>(work);
+    EntropyArea& E = *reinterpret_cast<EntropyArea*>(work);
+    Seq* const wseq_all = seq_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
+    Coded* const coded = coded_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
 
-    const bool probe = PROBE && blockIdx.x == 0 && tid == 0;
-    uint64_t tp = probe ? wall_clock64() : 0;
-    auto mark = [&](int ph) {
-        if (probe) {
-            const uint64_t t = wall_clock64();
-            g_zprobe[ph] += t - tp;
-            tp = t;
-        }
-    };
-    // the next item's metadata loads while this one is compressed
-    uint64_t it_n = blockIdx.x < nitems ? items[blockIdx.x] : 0;
-    uint64_t b0_n = blockIdx.x < nitems ? bounds[it_n >> 32] : 0, b1_n = blockIdx.x < nitems ? bounds[(it_n >> 32) + 1] : 0;
     for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
         __syncthreads();  // LDS of the previous item
-        const uint64_t it = it_n, bb0 = b0_n, bb1 = b1_n;
-        if (k + gridDim.x < nitems) {
-            it_n = items[k + gridDim.x];
-            b0_n = bounds[it_n >> 32];
-            b1_n = bounds[(it_n >> 32) + 1];
-        }
-        if (probe) g_zprobe[6] += 1;
+        const uint64_t it = items[k];
         const uint64_t ci = it >> 32, j = (uint32_t)it;
-        (void)ci;
-        const uint64_t len = bb1 - bb0, off = j * (uint64_t)kEncBlock;
+        const uint64_t c0 = bounds[ci], c1 = bounds[ci + 1];
+        const uint64_t len = c1 - c0, off = j * (uint64_t)kEncBlock;
         const uint32_t n = (uint32_t)(len > off ? (len - off < kEncBlock ? len - off : kEncBlock) : 0);
         const bool last = off + n == len;
-        const uint8_t* const src = data + (bb0 - base) + off;
         uint8_t* const out = slots + k * kSlot;
         if (n == 0) {  // the empty chunk's frame: one empty raw block
             if (tid == 0) {
@@ -201,267 +651,650 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             }
             continue;
         }
-        // stage: the aligned 16-byte words holding [src, src + n) (never past a page that
-        // holds a block byte); all of a thread's loads in flight before the LDS stores
-        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15);
-        const uint8_t* const a0 = src - r;  // pointer arithmetic keeps the loads global (not flat)
-        const uint32_t nw = (n + r + 15) >> 4;
-        for (uint32_t i0 = tid; i0 < nw; i0 += 5 * kZThreads) {  // 5 loads in flight per thread
-            v4u v[5];
+        const uint32_t hist = (uint32_t)(off < kZHist ? off : kZHist);  // window bytes before the block
+        const uint32_t N = hist + n;
+        // stage the aligned 16-byte words holding [src - hist, src + n)
+        const uint8_t* const wsrc = data + (c0 - base) + off - hist;
+        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(wsrc) & 15);
+        const uint8_t* const a0 = wsrc - r;
+        const uint32_t nw = (N + r + 15) >> 4;
+        for (uint32_t i0 = tid; i0 < nw; i0 += 4 * kZThreads) {
+            v4u v[4];
 #pragma unroll
-            for (int q = 0; q < 5; ++q) {
+            for (int q = 0; q < 4; ++q) {
                 const uint32_t i = i0 + kZThreads * q;
                 if (i < nw) v[q] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(a0) + i);
             }
 #pragma unroll
-            for (int q = 0; q < 5; ++q) {
+            for (int q = 0; q < 4; ++q) {
                 const uint32_t i = i0 + kZThreads * q;
-                if (i < nw) blk[i] = make_uint4(v[q].x, v[q].y, v[q].z, v[q].w);
+                if (i < nw) stage[i] = make_uint4(v[q].x, v[q].y, v[q].z, v[q].w);
             }
         }
-        if (tid == 0) blk[nw] = make_uint4(0, 0, 0, 0);  // word reads past the end stay defined
+        if (tid < 2) stage[nw + tid] = make_uint4(0, 0, 0, 0);  // word reads past the end stay defined
         __syncthreads();
-        mark(0);
-        const Stage S{reinterpret_cast<const uint32_t*>(blk), r};
-        const uint32_t b0 = S.byte(0), b4 = b0 * 0x01010101u;
-        int same = 1;
-        for (uint32_t q = tid; q < nw; q += kZThreads) {  // staged word q = block bytes 16q - r ..
-            if (16 * q >= r && 16 * q + 16 - r <= n) {
-                const uint4 w = blk[q];
-                same &= (w.x == b4) & (w.y == b4) & (w.z == b4) & (w.w == b4);
-            } else {
-                for (uint32_t i = 0; i < 16; ++i) {
-                    const int64_t pos = (int64_t)(16 * q + i) - (int64_t)r;
-                    if (pos >= 0 && pos < (int64_t)n) same &= S.byte((uint32_t)pos) == b0;
+        const Win W{reinterpret_cast<const uint32_t*>(stage), r};
+
+        // ---- RLE block: every byte equal
+        {
+            const uint32_t b0 = W.byte(hist);
+            int same = 1;
+            for (uint32_t p = hist + 4 * tid; p < N; p += 4 * kZThreads) {
+                if (p + 4 <= N)
+                    same &= W.word(p) == b0 * 0x01010101u;
+                else
+                    for (uint32_t q = p; q < N; ++q) same &= W.byte(q) == b0;
+            }
+            if (__syncthreads_and(same)) {
+                if (tid == 0) {
+                    write_block_header(out, last, 1, n);
+                    out[3] = (uint8_t)b0;
+                    sizes[k] = 4;
                 }
+                continue;
             }
         }
-        const int rle = __syncthreads_and(same);
-        mark(1);
-        if (rle) {
-            if (tid == 0) {
-                write_block_header(out, last, 1, n);
-                out[3] = (uint8_t)b0;
-                sizes[k] = 4;
-            }
-            continue;
-        }
-        // each wave parses its own 16 KiB sub-block with its own table: no workgroup
-        // barrier until the sequences are combined (a shared 1024-position round needed two
-        // per round and left the parse to one wave)
-        const uint32_t s0 = (uint32_t)wave * kZSub;
-        uint32_t ns = 0, msum = 0, cur = s0;  // wave-uniform
-        if (s0 < n) {
-            const uint32_t se = s0 + kZSub < n ? s0 + kZSub : n;
-            uint32_t* const tw = table[wave];
+
+        // ---- parse: wave w owns the sub-block [s0, se) (window positions)
+        {
+            const uint32_t s0 = hist + (uint32_t)wave * kZSub;
+            uint32_t ns = 0, lastend = 0;
+            Seq* const wseq = wseq_all + (uint64_t)wave * kZSubSeq;
+            if (s0 < N) {
+                const uint32_t se = min(s0 + kZSub, N);
+                const uint32_t wlo = s0 - min(s0, kZHist);
+                uint16_t* const tw = tabs + wave * kZTab;
 #pragma unroll
-            for (int i = 0; i < (1 << kZHashLog) / 64; ++i) tw[lane + 64 * i] = 0;
-            const uint32_t plim = n >= 4 ? n - 4 : 0;
-            uint32_t step = 1;  // positions sampled per round: 1 after a match, doubling to 8 without
-            for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
-                rn = r0 + kZRound * step;  // the next round starts where this one's samples end
-                // branch-free lookups: every LDS read issued at a clamped address, the value
-                // selected after (conditional reads became a branch and a wait each)
-                uint32_t h[kZPer], c1[kZPer], wp[kZPer], wm[kZPer];
+                for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<uint32_t*>(tw)[lane + 64 * i] = 0;
+                // history: accelerated rounds over [wlo, s0)
+                for (uint32_t r0 = wlo, rn, hs = 1; r0 < s0; r0 = rn) {
+                    rn = r0 + kZRound * hs;
+                    uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
+                    bool ok[kZPer];
 #pragma unroll
-                for (int i = 0; i < kZPer; ++i) {
-                    const uint32_t p = r0 + (lane + 64 * i) * step;
-                    const uint32_t pc = p < plim ? p : plim;
-                    wp[i] = S.word(pc);
-                    wm[i] = S.word(pc ? pc - 1 : 0);  // p - 1: the run candidate (lane 0)
+                    for (int i = 0; i < kZPer; ++i) {
+                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
+                        ok[i] = p < s0 && p + 5 <= N;
+                        const uint32_t pc = ok[i] ? p : wlo;
+                        wp[i] = W.word(pc);
+                        b4[i] = W.byte(pc + 4);
+                        h[i] = hash5(wp[i], b4[i]);
+                        t[i] = tw[h[i]];
+                    }
+#pragma unroll
+                    for (int i = 0; i < kZPer; ++i) {
+                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
+                        if (ok[i]) tab_max(&tw[h[i]], p - wlo + 1);
+                    }
+                    bool hit = false;
+#pragma unroll
+                    for (int i = 0; i < kZPer; ++i) {
+                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
+                        const uint32_t c = ok[i] && t[i] ? wlo + t[i] - 1 : wlo;
+                        const uint32_t b = W.byte(ok[i] ? p : wlo);
+                        const bool run = wp[i] == b * 0x01010101u && b4[i] == b;
+                        hit |= ok[i] && t[i] && !run && W.word(c) == wp[i] && W.byte(c + 4) == b4[i];
+                    }
+                    hs = __ballot(hit) ? 1 : min(2 * hs, kZMaxStep);
                 }
+                // rounds + walk
+                uint32_t cur = s0, step = 1, rep = 0;
+                for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
+                    rn = r0 + kZRound * step;
+                    uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
 #pragma unroll
-                for (int i = 0; i < kZPer; ++i) {
-                    const uint32_t p = r0 + (lane + 64 * i) * step;
-                    h[i] = (wp[i] * 2654435761u) >> (32 - kZHashLog);
-                    const uint32_t t = tw[h[i]];
-                    // an AND, not a select: a select let the compiler sink the read into a branch
-                    c1[i] = t & (0u - (uint32_t)(p + 4 <= n && p < se && p >= cur));
-                }
-                uint32_t wc[kZPer], wr[kZPer];
+                    for (int i = 0; i < kZPer; ++i) {
+                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
+                        const bool ok = p < se && p + 5 <= N;
+                        const uint32_t pc = ok ? p : s0;
+                        wp[i] = W.word(pc);
+                        b4[i] = W.byte(pc + 4);
+                        h[i] = hash5(wp[i], b4[i]);
+                        t[i] = ok ? (uint32_t)tw[h[i]] : 0u;
+                    }
 #pragma unroll
-                for (int i = 0; i < kZPer; ++i) {
-                    wc[i] = S.word(c1[i] ? c1[i] - 1 : 0);
-                    const uint32_t up = (uint32_t)__shfl_up((int)wp[i], 1, 64);
-                    wr[i] = lane && step == 1 ? up : wm[i];
-                }
-                uint32_t Lm[kZPer], Cm[kZPer];
-                unsigned long long m[kZPer];
+                    for (int i = 0; i < kZPer; ++i) {
+                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
+                        if (p < se && p + 5 <= N) tab_max(&tw[h[i]], p - wlo + 1);
+                    }
+                    uint32_t Lm[kZPer], Cm[kZPer];
+                    unsigned long long m[kZPer];
 #pragma unroll
-                for (int i = 0; i < kZPer; ++i) {
-                    const uint32_t p = r0 + (lane + 64 * i) * step;
-                    const bool live = p + 4 <= n && p < se && p >= cur;
-                    const bool mt = live && c1[i] && wc[i] == wp[i];
-                    const bool mr = live && p > 0 && wr[i] == wp[i];
-                    uint32_t L = 0, c = c1[i] - 1;
-                    if (mt || mr) {  // rare: matches extended to the cap (within the sub-block);
-                        // the run candidate p - 1 wins when longer (ties: the table's)
-                        const uint32_t lim = se - p < kZCap ? se - p : kZCap;
-                        if (lim >= 4) {
-                            const uint32_t Lt = mt ? 4 + common_prefix(S, c + 4, p + 4, lim - 4) : 0;
-                            const uint32_t Lr = mr ? 4 + common_prefix(S, p + 3, p + 4, lim - 4) : 0;
+                    for (int i = 0; i < kZPer; ++i) {
+                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
+                        const bool live = p >= cur && p + 5 <= se;
+                        const uint32_t c = t[i] ? wlo + t[i] - 1 : s0;
+                        const bool rl = live && p > wlo;
+                        const uint32_t pm = rl ? p - 1 : s0;  // the run candidate (clamped when unused)
+                        const bool mt = live && t[i] && W.word(c) == wp[i] && W.byte(c + 4) == b4[i];
+                        const bool mr = rl && W.word(pm) == wp[i] && W.byte(pm + 4) == b4[i];
+                        uint32_t L = 0, C = c;
+                        if (mt || mr) {  // rare: lengths to the cap (within the sub-block)
+                            const uint32_t lim = min(se - p, kZCap);
+                            const uint32_t Lt = mt ? 5 + win_prefix(W, c + 5, p + 5, lim - 5) : 0;
+                            const uint32_t Lr = mr ? 5 + win_prefix(W, p + 4, p + 5, lim - 5) : 0;
                             L = Lt;
                             if (Lr > Lt) {
                                 L = Lr;
-                                c = p - 1;
+                                C = p - 1;
                             }
                         }
+                        Lm[i] = L;
+                        Cm[i] = C;
+                        m[i] = __ballot(L != 0);
                     }
-                    Lm[i] = L;
-                    Cm[i] = c;
-                    m[i] = __ballot(L != 0);
-                }
-                // this round's inserts, after every lookup of the round (program order)
-#pragma unroll
-                for (int i = 0; i < kZPer; ++i) {
-                    const uint32_t p = r0 + (lane + 64 * i) * step;
-                    atomicMax(&tw[h[i]], p + 4 <= n && p < se ? p + 1 : 0u);
-                }
-                // greedy parse of the round from the match masks (wave-uniform); bit q is
-                // position r0 + q * step
-                bool found = false;
-                uint32_t q = cur > r0 ? (cur - r0 + step - 1) / step : 0;
-                while (q < kZRound) {
-                    uint32_t w = q >> 6;
-                    unsigned long long mm = 0;
-                    for (; w < (uint32_t)kZPer; ++w) {
-                        mm = (w == 0 ? m[0] : w == 1 ? m[1] : w == 2 ? m[2] : m[3]) &
-                             (w == (q >> 6) ? (~0ull << (q & 63)) : ~0ull);
-                        if (mm) break;
-                    }
-                    if (!mm) break;
-                    const int l = __builtin_ctzll(mm);
-                    const uint32_t pp = r0 + (w * 64 + (uint32_t)l) * step;
-                    const uint32_t Lw = w == 0 ? Lm[0] : w == 1 ? Lm[1] : w == 2 ? Lm[2] : Lm[3];
-                    const uint32_t Cw = w == 0 ? Cm[0] : w == 1 ? Cm[1] : w == 2 ? Cm[2] : Cm[3];
-                    uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
-                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
-                    if (ml == kZCap) {  // extend to the sub-block end: a word per lane, 256 bytes a step
+                    // the greedy walk (wave-uniform); bit q = position r0 + q * step
+                    bool found = false;
+                    uint32_t q = cur > r0 ? (cur - r0 + step - 1) / step : 0;
+                    for (;;) {
+                        uint32_t wi = q >> 6;
+                        unsigned long long mm = 0;
+                        for (; wi < (uint32_t)kZPer; ++wi) {
+                            mm = (wi == 0 ? m[0] : wi == 1 ? m[1] : wi == 2 ? m[2] : m[3]) &
+                                 (wi == (q >> 6) ? (~0ull << (q & 63)) : ~0ull);
+                            if (mm) break;
+                        }
+                        const bool have = q < kZRound && mm != 0;
+                        const int l = have ? __builtin_ctzll(mm) : 0;
+                        const uint32_t ph = have ? r0 + (wi * 64 + (uint32_t)l) * step : min(rn, se);
+                        uint32_t mpos = 0, msrc = 0, mlen = 0;
+                        bool take = false;
+                        if (rep && cur < ph) {  // a repeat match in [cur, min(ph, cur + 64))
+                            const uint32_t hi = min(ph, cur + 64);
+                            const uint32_t x = cur + (uint32_t)lane;
+                            const bool okx = x < hi && x >= wlo + rep && x + 5 <= se;
+                            const uint32_t xc = okx ? x : wlo + rep;
+                            const bool eq = okx && W.word(xc) == W.word(xc - rep) && W.byte(xc + 4) == W.byte(xc - rep + 4);
+                            const unsigned long long bal = __ballot(eq);
+                            if (bal) {
+                                mpos = cur + (uint32_t)__builtin_ctzll(bal);
+                                msrc = mpos - rep;
+                                mlen = 5;
+                                take = true;
+                            }
+                        }
+                        if (!take) {
+                            if (!have) break;
+                            const uint32_t Lw = wi == 0 ? Lm[0] : wi == 1 ? Lm[1] : wi == 2 ? Lm[2] : Lm[3];
+                            const uint32_t Cw = wi == 0 ? Cm[0] : wi == 1 ? Cm[1] : wi == 2 ? Cm[2] : Cm[3];
+                            mpos = ph;
+                            mlen = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
+                            msrc = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
+                            // catch-up over the literals before it: lane k checks byte k back
+                            const uint32_t kk = (uint32_t)lane;
+                            const bool okb = mpos > cur + kk && msrc > wlo + kk;
+                            const bool eqb = okb && W.byte(okb ? mpos - 1 - kk : s0) == W.byte(okb ? msrc - 1 - kk : s0);
+                            const unsigned long long bb = __ballot(eqb);
+                            const uint32_t e = ~bb ? (uint32_t)__builtin_ctzll(~bb) : 64u;
+                            mpos -= e;
+                            msrc -= e;
+                            mlen += e;
+                        }
+                        // forwards to the end (within the sub-block): 4 bytes per lane a step
                         for (;;) {
-                            const uint32_t x = pp + ml + 4 * lane;
+                            const uint32_t x = mpos + mlen + 4 * (uint32_t)lane;
                             uint32_t mis = 4;  // first mismatching byte of my 4 (4: none)
                             if (x + 4 <= se) {
-                                const uint32_t d = S.word(c + ml + 4 * lane) ^ S.word(x);
+                                const uint32_t d = W.word(msrc + mlen + 4 * (uint32_t)lane) ^ W.word(x);
                                 if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
                             } else {
                                 mis = 0;
-                                while (x + mis < se && S.byte(c + ml + 4 * lane + mis) == S.byte(x + mis)) ++mis;
-                                if (x >= se) mis = 0;
+                                while (x + mis < se && W.byte(msrc + mlen + 4 * (uint32_t)lane + mis) == W.byte(x + mis))
+                                    ++mis;
                             }
-                            const unsigned long long bad = __ballot(mis < 4 || x + 4 > se);
+                            const unsigned long long bad = __ballot(mis < 4);
                             if (bad) {
                                 const int f = __builtin_ctzll(bad);
-                                ml += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
+                                mlen += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
                                 break;
                             }
-                            ml += 256;
+                            mlen += 256;
+                        }
+                        if (lane == 0 && ns < kZSubSeq) wseq[ns] = Seq{mpos - hist, mlen, mpos - msrc};
+                        ++ns;
+                        rep = mpos - msrc;
+                        cur = mpos + mlen;
+                        lastend = cur - hist;
+                        found = true;
+                        q = (cur - r0 + step - 1) / step;
+                    }
+                    step = found ? 1 : min(2 * step, kZMaxStep);
+                }
+            }
+            if (lane == 0) {
+                ctl.nseq[wave] = ns;
+                ctl.lastend[wave] = lastend;
+            }
+        }
+        __syncthreads();
+        __threadfence_block();
+
+        // ---- literals: bitmap of the unmatched bytes, literal index per thread range
+        for (uint32_t i = tid; i < kEncBlock / 32; i += kZThreads) {
+            const uint32_t b = 32 * i;
+            E.bitmap[i] = b + 32 <= n ? 0xFFFFFFFFu : (b >= n ? 0u : (0xFFFFFFFFu >> (32 - (n - b))));
+        }
+        for (uint32_t i = tid; i < kZWaves * 256; i += kZThreads) E.streams[i] = 0;  // per-wave histograms
+        __syncthreads();
+        {
+            const Seq* const wseq = wseq_all + (uint64_t)wave * kZSubSeq;
+            for (uint32_t q = lane; q < ctl.nseq[wave]; q += 64) {
+                const Seq e = wseq[q];
+                uint32_t a = e.pos, b = e.pos + e.ml;
+                while (a < b) {
+                    const uint32_t wd = a >> 5, lo = a & 31;
+                    const uint32_t cnt = min(32 - lo, b - a);
+                    const uint32_t mask = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << lo;
+                    if (cnt == 32)
+                        E.bitmap[wd] = 0;  // a whole word inside one match: no other match touches it
+                    else
+                        atomicAnd(&E.bitmap[wd], ~mask);
+                    a += cnt;
+                }
+            }
+        }
+        __syncthreads();
+        // thread t owns block positions [128 t, 128 t + 128): bitmap words 4t .. 4t + 3
+        uint32_t bmw[4], cnt_t = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bmw[i] = E.bitmap[4 * tid + i];
+            cnt_t += __builtin_popcount(bmw[i]);
+        }
+        uint32_t* const wh = E.streams + wave * 256;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1)
+                atomicAdd(&wh[W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2))], 1u);
+        const uint32_t incl = wave_incl(cnt_t, lane);
+        if (lane == 63) ctl.wsum[wave] = incl;
+        __syncthreads();
+        uint32_t litbase = incl - cnt_t, nlit = 0;
+        for (int w2 = 0; w2 < kZWaves; ++w2) {
+            litbase += w2 < wave ? ctl.wsum[w2] : 0u;
+            nlit += ctl.wsum[w2];
+        }
+        if (tid < 256) {
+            uint32_t c = 0;
+            for (int w2 = 0; w2 < kZWaves; ++w2) c += E.streams[w2 * 256 + tid];
+            E.hist[tid] = c;
+        }
+        __syncthreads();
+
+        // ---- literal mode (wave 0) and repeat-offset coding (wave 1, one lane per sub-block)
+        if (wave == 0) {
+            uint32_t c4[4], dist = 0, lastsym = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                c4[i] = E.hist[lane + 64 * i];
+                const unsigned long long b = __ballot(c4[i] != 0);
+                dist += (uint32_t)__builtin_popcountll(b);
+                if (b) lastsym = 64 * i + 63 - (uint32_t)__builtin_clzll(b);
+            }
+            // 0 raw, 1 RLE, 2 Huffman (if its exact size wins below)
+            uint32_t mode = 0;
+            if (nlit > 0 && dist == 1) {
+                mode = 1;
+            } else if (nlit >= 32) {
+                uint64_t est = 0;
+                const uint32_t ln = lg256(nlit);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (c4[i]) est += (uint64_t)c4[i] * (ln - lg256(c4[i]));
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) est += __shfl_xor(est, d, 64);
+                if (est / 2048 + 64 < (uint64_t)nlit - nlit / 64) mode = 2;
+            }
+            if (mode == 2) {
+                // symbols sorted by (count, symbol): rank of each key among the present ones
+                uint32_t key[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    key[i] = c4[i] << 8 | (uint32_t)(lane + 64 * i);
+                    E.keys[lane + 64 * i] = c4[i] ? key[i] : 0xFFFFFFFFu;
+                }
+                __builtin_amdgcn_wave_barrier();  // one wave: LDS ops run in order; no code motion across
+                uint32_t rk[4] = {0, 0, 0, 0};
+                for (int s2 = 0; s2 < 256; ++s2) {
+                    const uint32_t o = E.keys[s2];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) rk[i] += o < key[i];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (c4[i]) E.tw[rk[i]] = key[i];  // sorted keys (temporarily in tw)
+                if (lane == 0) huf_merge(E, ctl, dist);
+                __builtin_amdgcn_wave_barrier();
+                const int m = (int)dist, root = ctl.root;
+                // depth of each leaf (sorted index i = 4 lane + j: contiguous per lane)
+                int32_t kr = 0;
+                uint32_t L4[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int i = 4 * lane + jj;
+                    uint32_t d = 0;
+                    if (i < m)
+                        for (int nd = i; nd != root; nd = E.par[nd]) ++d;
+                    L4[jj] = i < m ? min(d, kHufMax) : 0u;
+                    if (i < m) kr += 1 << (kHufMax - L4[jj]);
+                }
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) kr += __shfl_xor(kr, d, 64);
+                kr -= 1 << kHufMax;
+                while (kr > 0) {  // lengthen the longest code under the limit, least frequent first
+                    uint32_t best = 0;
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) {
+                        const uint32_t i = 4 * lane + jj;
+                        if ((int)i < m && L4[jj] < kHufMax) best = max(best, L4[jj] << 16 | (0xFFFFu - i));
+                    }
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, d, 64));
+                    const uint32_t bi = 0xFFFFu - (best & 0xFFFFu), bl = best >> 16;
+                    kr -= 1 << (kHufMax - bl - 1);
+                    if ((bi >> 2) == (uint32_t)lane) {
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj)
+                            if ((bi & 3) == (uint32_t)jj) ++L4[jj];
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) E.lens[4 * lane + jj] = (uint8_t)L4[jj];
+                if (lane == 0 && kr < 0) {  // shorten: most frequent first, while the deficit allows
+                    while (kr < 0)
+                        for (int i = m - 1; i >= 0 && kr < 0; --i) {
+                            uint32_t L = E.lens[i];
+                            while (L > 1 && (1 << (kHufMax - L)) <= -kr) {
+                                kr += 1 << (kHufMax - L);
+                                --L;
+                            }
+                            E.lens[i] = (uint8_t)L;
+                        }
+                }
+                __builtin_amdgcn_wave_barrier();
+                // per symbol lengths
+#pragma unroll
+                for (int i = 0; i < 4; ++i) E.len[lane + 64 * i] = 0;
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int i = 4 * lane + jj;
+                    if (i < m) E.len[E.keys[i]] = E.lens[i];
+                }
+                __builtin_amdgcn_wave_barrier();
+                // canonical codes: by (length descending, symbol ascending), increasing
+                uint32_t ls[4], mb = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    ls[i] = E.len[lane + 64 * i];
+                    mb = max(mb, ls[i]);
+                }
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, d, 64));
+                uint32_t start[kHufMax + 2];
+                {
+                    uint32_t cntL[kHufMax + 2];
+                    for (uint32_t L = 0; L <= kHufMax + 1; ++L) cntL[L] = 0;
+                    for (uint32_t L = 1; L <= kHufMax; ++L) {
+                        uint32_t c = 0;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) c += (uint32_t)__builtin_popcountll(__ballot(ls[i] == L));
+                        cntL[L] = c;
+                    }
+                    uint32_t prevL = 0, s = 0;
+                    for (uint32_t L = mb; L >= 1; --L) {
+                        if (!cntL[L]) continue;
+                        start[L] = prevL ? (s >> (prevL - L)) : 0u;
+                        s = start[L] + cntL[L];
+                        prevL = L;
+                    }
+                }
+                // rank among the same length by symbol (symbols lane + 64 i): per length, the
+                // ballots of the four symbol groups in order
+                {
+                    uint32_t rk[4] = {0, 0, 0, 0};
+                    const unsigned long long lt = (1ull << lane) - 1ull;
+                    for (uint32_t L = 1; L <= mb; ++L) {
+                        uint32_t acc = 0;
+#pragma unroll
+                        for (int i2 = 0; i2 < 4; ++i2) {
+                            const unsigned long long b = __ballot(ls[i2] == L);
+                            if (ls[i2] == L) rk[i2] = acc + (uint32_t)__builtin_popcountll(b & lt);
+                            acc += (uint32_t)__builtin_popcountll(b);
                         }
                     }
-                    if (lane == 0) {  // position form: ll comes later
-                        if (ns < kWaveLdsSeq)
-                            s_wseq[wave][ns] = Seq{pp, ml, pp - c};
-                        else
-                            wseq[ns] = Seq{pp, ml, pp - c};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (ls[i]) E.code[lane + 64 * i] = (uint16_t)(start[ls[i]] + rk[i]);
+                }
+                if (lane == 0 && !huf_describe(E, ctl, fse[0], mb, lastsym)) mode = 0;
+            }
+            if (lane == 0) ctl.lit_mode = mode;  // (lane 0's: it may have fallen back to raw)
+        } else if (wave == 1 && lane < kZWaves) {
+            // repeat-offset coding of sub-block `lane` (reps tracked per sub-block)
+            const uint32_t w2 = (uint32_t)lane;
+            uint32_t first = 0, lit_end = 0;
+            for (uint32_t v = 0; v < w2; ++v) {
+                first += min(ctl.nseq[v], kZSubSeq);
+                if (ctl.nseq[v]) lit_end = ctl.lastend[v];
+            }
+            const Seq* const ws = wseq_all + (uint64_t)w2 * kZSubSeq;
+            uint32_t rp[3] = {0, 0, 0};
+            const uint32_t cnt = min(ctl.nseq[w2], kZSubSeq);
+            for (uint32_t q = 0; q < cnt; ++q) {
+                const Seq e = ws[q];
+                Coded c;
+                c.ll = e.pos - lit_end;
+                c.ml = e.ml;
+                const uint32_t o = e.off;
+                const bool ll0 = c.ll == 0;
+                c.ofv = o + 3;
+                if (!ll0 && rp[0] == o) c.ofv = 1;
+                else if (rp[1] && rp[1] == o) c.ofv = ll0 ? 1 : 2;
+                else if (rp[2] && rp[2] == o) c.ofv = ll0 ? 2 : 3;
+                else if (ll0 && rp[0] > 1 && rp[0] - 1 == o) c.ofv = 3;
+                if (c.ofv > 3) {
+                    rp[2] = rp[1];
+                    rp[1] = rp[0];
+                    rp[0] = o;
+                } else {
+                    const uint32_t rc = c.ofv - 1 + (ll0 ? 1u : 0u);
+                    if (rc > 0) {
+                        const uint32_t cu = rc == 3 ? rp[0] - 1 : rp[rc];
+                        if (rc >= 2) rp[2] = rp[1];
+                        rp[1] = rp[0];
+                        rp[0] = cu;
                     }
-                    ++ns;
-                    msum += ml;
-                    cur = pp + ml;
-                    q = (cur - r0 + step - 1) / step;
-                    found = true;
                 }
-                step = found ? 1 : (2 * step < kZMaxStep ? 2 * step : kZMaxStep);
+                c.codes = ll_code(c.ll) | ml_code(c.ml) << 8 | highbit(c.ofv) << 16;
+                coded[first + q] = c;
+                lit_end = e.pos + e.ml;
             }
         }
-        if (lane == 0) {
-            s_wave[wave][0] = ns;
-            s_wave[wave][1] = msum;
-            s_wave[wave][2] = cur;
-        }
-        mark(2);
+        for (uint32_t i = tid; i < 36 + 53 + 32; i += kZThreads) E.shist[i] = 0;
         __syncthreads();
-        // combine the waves' sequences: literal length = position - end of the previous
-        // match (across sub-blocks: literals carry over), into LDS (the tables are free) or,
-        // when they do not fit, a contiguous global list
-        static_assert(kZThreads / 64 == 4, "four sub-blocks per block");
-        const uint32_t b1 = s_wave[0][0], b2 = b1 + s_wave[1][0], b3 = b2 + s_wave[2][0];
-        const uint32_t matched = s_wave[0][1] + s_wave[1][1] + s_wave[2][1] + s_wave[3][1];
-        ns = b3 + s_wave[3][0];
-        if (probe) g_zprobe[7] += ns;
-        constexpr uint32_t kLdsSeq = sizeof(table) / sizeof(Seq);
-        Seq* const sq = ns <= kLdsSeq ? reinterpret_cast<Seq*>(&table[0][0]) : gseq;
-        const Seq* const pos0 = seq_scratch + (uint64_t)blockIdx.x * kMaxSeq;
-        auto at = [&](uint32_t q) -> Seq {  // q-th sequence (position form), selects only
-            const uint32_t w = (uint32_t)(q >= b1) + (uint32_t)(q >= b2) + (uint32_t)(q >= b3);
-            const uint32_t b = w == 0 ? 0 : w == 1 ? b1 : w == 2 ? b2 : b3;
-            const uint32_t j = q - b;
-            return j < kWaveLdsSeq ? s_wseq[w][j] : pos0[(uint64_t)w * kSubSeq + j];
-        };
-        for (uint32_t q = tid; q < ns; q += kZThreads) {
-            const Seq e = at(q);
-            uint32_t prev_end = 0;
-            if (q) {
-                const Seq f = at(q - 1);
-                prev_end = f.ll + f.ml;
-            }
-            sq[q] = Seq{e.ll - prev_end, e.ml, e.off};
+        __threadfence_block();
+        uint32_t nseq = 0;
+        for (int w2 = 0; w2 < kZWaves; ++w2) nseq += min(ctl.nseq[w2], kZSubSeq);
+        for (uint32_t q = tid; q < nseq; q += kZThreads) {
+            const uint32_t cc = coded[q].codes;
+            atomicAdd(&E.shist[cc & 0xFF], 1u);
+            atomicAdd(&E.shist[36 + ((cc >> 8) & 0xFF)], 1u);
+            atomicAdd(&E.shist[36 + 53 + (cc >> 16)], 1u);
         }
-        uint32_t tail_start = 0;  // end of the last match
-        for (int w = kZThreads / 64 - 1; w >= 0; --w)
-            if (s_wave[w][0]) {
-                tail_start = s_wave[w][2];
-                break;
-            }
+        // ---- Huffman sizes: per-thread code-length sums, block scan, segment totals
+        const uint32_t lit_mode = ctl.lit_mode;
+        uint32_t bits_t = 0;
+        if (lit_mode == 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1)
+                    bits_t += E.len[W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2))];
+        }
+        const uint32_t bincl = wave_incl(bits_t, lane);
+        if (lane == 63) ctl.wsum2[wave] = bincl;
+        const bool four = nlit >= 256;
+        const uint32_t seg = four ? (nlit + 3) / 4 : nlit;
         __syncthreads();
-        mark(3);
-        const uint32_t nlit = n - matched;
-        const uint32_t lith = nlit < 32 ? 1 : nlit < 4096 ? 2 : 3;
-        const uint32_t seq_at = 3 + lith + nlit;
-        bool raw = seq_at - 3 >= n;
-        if (!raw) {
-            if (wave == 0) {
-                if (lane == 0) {
-                    const size_t sz = write_sequences(out + seq_at, sq, ns, s_zt.ll, s_zt.ml, s_zt.of,
-                                                      out + 3 + n);
-                    s_u[3] = sz == SIZE_MAX ? 0xFFFFFFFFu : (uint32_t)sz;
-                }
-            } else {  // waves 1-3: the literal runs in order (run ns: after the last match)
-                uint8_t* const lo = out + 3 + lith;
-                uint32_t from = 0, to = 0;
-                for (uint32_t q = 0; q <= ns; ++q) {
-                    uint32_t cnt;
-                    if (q < ns) {
-                        const Seq e = sq[q];
-                        cnt = e.ll;
-                        copy_from_stage(lo + to, S, from, cnt, tid - 64, kZThreads - 64);
-                        from += cnt + e.ml;
-                    } else {
-                        cnt = n - tail_start;
-                        copy_from_stage(lo + to, S, tail_start, cnt, tid - 64, kZThreads - 64);
+        uint32_t bbase = bincl - bits_t;
+        for (int w2 = 0; w2 < wave; ++w2) bbase += ctl.wsum2[w2];
+        if (lit_mode == 2) {
+            // the thread holding literal index seg * s records the bits before it
+            if (tid == 0) {
+                ctl.segP[0] = 0;
+                uint32_t tot = 0;
+                for (int w2 = 0; w2 < kZWaves; ++w2) tot += ctl.wsum2[w2];
+                ctl.segP[4] = tot;
+                if (!four) ctl.segP[1] = tot;
+            }
+            if (four) {
+                uint32_t idx = litbase, pb = bbase;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1) {
+                        if (idx == seg || idx == 2 * seg || idx == 3 * seg) ctl.segP[idx / seg] = pb;
+                        pb += E.len[W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2))];
+                        ++idx;
                     }
-                    to += cnt;
+            }
+        }
+        // sequence tables: LL on wave 1, OF on wave 2, ML on wave 3 (lane 0 each)
+        __syncthreads();
+        if (lane == 0 && wave >= 1 && wave <= 3 && nseq > 0) {
+            if (wave == 1) seq_table(fse[0], E.shist, 36, nseq, kLLNorm, kLLLog, kLLMaxLog);
+            if (wave == 2) seq_table(fse[1], E.shist + 36 + 53, 29, nseq, kOFNorm, kOFLog, kOFMaxLog);
+            if (wave == 3) seq_table(fse[2], E.shist + 36, 53, nseq, kMLNorm, kMLLog, kMLMaxLog);
+        }
+        // literal section: size decision (thread 0)
+        if (tid == 0) {
+            uint32_t lm = lit_mode, sz = 0;
+            const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+            if (lm == 2) {
+                uint32_t sb = 0;
+                const int ns4 = four ? 4 : 1;
+                for (int s = 0; s < ns4; ++s) sb += (ctl.segP[four ? s + 1 : 4] - ctl.segP[s] + 8) / 8;
+                const uint32_t c = ctl.desc_len + (four ? 6u : 0u) + sb;
+                const uint32_t mx = max(nlit, c);
+                const uint32_t hs = mx < 1024 ? 3u : mx < 16384 ? 4u : 5u;
+                if (sb > kHufStreams || hs + c >= rawh + nlit) {
+                    lm = 0;
+                } else {
+                    sz = hs + c;
+                    ctl.huf_c = c;   // the header's compressed size
+                    ctl.huf_hs = hs; // header bytes
                 }
+            }
+            if (lm == 0) sz = rawh + nlit;
+            if (lm == 1) sz = rawh + 1;
+            ctl.lit_mode = lm;
+            ctl.lit_size = sz;
+        }
+        __syncthreads();
+        const uint32_t lm = ctl.lit_mode, lsz = ctl.lit_size;
+        uint8_t* const lit_out = out + 3;
+        // ---- write the literal section (all threads but wave 7 lane 0's sequence encode runs after)
+        if (lm == 2) {
+            const uint32_t words = kHufStreams / 4 + 4;
+            for (uint32_t i = tid; i < words; i += kZThreads) E.streams[i] = 0;
+            __syncthreads();
+            // stream s starts at byte S_s of the LDS buffer
+            uint32_t S[5];
+            S[0] = 0;
+            for (int s = 0; s < 4; ++s) {
+                const uint32_t bits = (four || s == 0) ? ctl.segP[four ? s + 1 : 4] - ctl.segP[s] : 0u;
+                S[s + 1] = S[s] + ((four || s == 0) ? (bits + 8) / 8 : 0u);
+            }
+            uint32_t idx = litbase, pb = bbase;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1) {
+                    const uint32_t sym = W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2));
+                    const uint32_t L = E.len[sym], cv = E.code[sym];
+                    const uint32_t sg = four ? min(idx / seg, 3u) : 0u;
+                    const uint32_t endP = four ? ctl.segP[sg + 1] : ctl.segP[4];
+                    const uint32_t o = 8 * S[sg] + (endP - pb - L);
+                    const uint64_t v = (uint64_t)cv << (o & 31);
+                    atomicOr(&E.streams[o >> 5], (uint32_t)v);
+                    if ((o & 31) + L > 32) atomicOr(&E.streams[(o >> 5) + 1], (uint32_t)(v >> 32));
+                    pb += L;
+                    ++idx;
+                }
+            if (tid < (four ? 4 : 1)) {  // end marks
+                const uint32_t bits = ctl.segP[four ? tid + 1 : 4] - ctl.segP[tid];
+                const uint32_t o = 8 * S[tid] + bits;
+                atomicOr(&E.streams[o >> 5], 1u << (o & 31));
             }
             __syncthreads();
-            mark(4);
-            const uint32_t sz = s_u[3];
-            if (sz == 0xFFFFFFFFu || seq_at + sz - 3 >= n) {
-                raw = true;
-            } else if (tid == 0) {
-                write_block_header(out, last, 2, seq_at + sz - 3);
-                write_raw_literals_header(out + 3, nlit);
-                sizes[k] = seq_at + sz;
+            const uint32_t hs = ctl.huf_hs, c = ctl.huf_c;
+            const uint32_t dl = ctl.desc_len;
+            uint8_t* const body = lit_out + hs;
+            if (tid == 0) {
+                if (hs == 3) {
+                    const uint32_t v = 2u | (four ? 1u : 0u) << 2 | nlit << 4 | c << 14;
+                    lit_out[0] = (uint8_t)v;
+                    lit_out[1] = (uint8_t)(v >> 8);
+                    lit_out[2] = (uint8_t)(v >> 16);
+                } else if (hs == 4) {
+                    const uint32_t v = 2u | 2u << 2 | nlit << 4 | c << 18;
+                    for (int i = 0; i < 4; ++i) lit_out[i] = (uint8_t)(v >> (8 * i));
+                } else {
+                    const uint64_t v = 2u | 3u << 2 | (uint64_t)nlit << 4 | (uint64_t)c << 22;
+                    for (int i = 0; i < 5; ++i) lit_out[i] = (uint8_t)(v >> (8 * i));
+                }
+                if (four)
+                    for (int s = 0; s < 3; ++s) {
+                        const uint32_t sz = S[s + 1] - S[s];
+                        body[dl + 2 * s] = (uint8_t)sz;
+                        body[dl + 2 * s + 1] = (uint8_t)(sz >> 8);
+                    }
+            }
+            for (uint32_t i = tid; i < dl; i += kZThreads) body[i] = ctl.desc[i];
+            const uint32_t tot = four ? S[4] : S[1];
+            uint8_t* const sdst = body + dl + (four ? 6 : 0);
+            const uint8_t* const ssrc = reinterpret_cast<const uint8_t*>(E.streams);
+            for (uint32_t i = tid; i < tot; i += kZThreads) sdst[i] = ssrc[i];
+        } else {
+            const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+            if (tid == 0) {
+                const uint32_t t = lm;  // 0 raw, 1 RLE
+                if (rawh == 1) {
+                    lit_out[0] = (uint8_t)(t | nlit << 3);
+                } else if (rawh == 2) {
+                    lit_out[0] = (uint8_t)(t | 1u << 2 | nlit << 4);
+                    lit_out[1] = (uint8_t)(nlit >> 4);
+                } else {
+                    lit_out[0] = (uint8_t)(t | 3u << 2 | nlit << 4);
+                    lit_out[1] = (uint8_t)(nlit >> 4);
+                    lit_out[2] = (uint8_t)(nlit >> 12);
+                }
+            }
+            if (lm == 1) {
+                if (tid == 0) {  // the one distinct byte
+                    uint32_t s = 0;
+                    while (!E.hist[s]) ++s;
+                    lit_out[rawh] = (uint8_t)s;
+                }
+            } else {
+                uint32_t idx = litbase;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1)
+                        lit_out[rawh + idx++] = (uint8_t)W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2));
             }
         }
-        if (raw) {
-            copy_from_stage(out + 3, S, 0, n, tid, kZThreads);
+        // ---- sequences section (one lane)
+        if (tid == 0) write_sequences(ctl, fse, coded, nseq, lit_out, lsz, out, n);
+        __syncthreads();
+        if (!ctl.seq_ok) {  // raw block
+            const uint8_t* const sb = reinterpret_cast<const uint8_t*>(stage) + r + hist;
+            for (uint32_t i = tid; i < n; i += kZThreads) out[3 + i] = sb[i];
             if (tid == 0) {
                 write_block_header(out, last, 0, n);
                 sizes[k] = 3 + (uint64_t)n;
             }
-        }
-        if (PROBE) {
-            __syncthreads();
-            mark(5);
+        } else if (tid == 0) {
+            write_block_header(out, last, 2, ctl.seq_size);
+            sizes[k] = 3 + (uint64_t)ctl.seq_size;
         }
     }
 }
@@ -489,7 +1322,7 @@ __global__ void zstd_frame_sizes_kernel(const uint64_t* __restrict__ bounds, con
 }
 
 // Per item: its part of the blob image.  Compressed chunk: the block (and, for the first
-// block, the magic and the frame header); otherwise the item's 128 KiB of chunk bytes.
+// block, the magic and the frame header); otherwise the item's 64 KiB of chunk bytes.
 __global__ __launch_bounds__(kZThreads) void zstd_assemble_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, const uint64_t* __restrict__ first,
@@ -528,17 +1361,17 @@ __global__ void blob_crc_header_kernel(const uint64_t* __restrict__ boff, const 
     h[3] = (uint8_t)(v >> 24);
 }
 
-// Per-device scratch kept for the process: the block slots (~ the input size), the
-// sequence lists of the resident workgroups and the FSE tables.
+// Per-device scratch kept for the process: the block slots (~ the input size) and the
+// sequence lists of the resident workgroups.
 struct ZScratch {
     std::mutex mu;
     int dev = -1;
     uint8_t* slots = nullptr;
     size_t slots_cap = 0;
     Seq* seqs = nullptr;
-    Seq* seqs_out = nullptr;  // the combined list when it does not fit in LDS
-    size_t groups = 0;
-    ZTables* zt = nullptr;
+    size_t seqs_cap = 0;
+    Coded* coded = nullptr;
+    size_t coded_cap = 0;
 };
 ZScratch& zscratch() {
     static ZScratch* z = new ZScratch;  // never destroyed (HIP may be torn down first at exit)
@@ -569,15 +1402,13 @@ extern "C" void pbs_blob_encode_release(void) {
     std::lock_guard<std::mutex> lk(z.mu);
     if (z.dev >= 0) {
         DeviceGuard dg(z.dev);
-        for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.seqs_out, (void*)z.zt})
+        for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.coded})
             if (p) (void)hipFree(p);
     }
     z.slots = nullptr;
     z.seqs = nullptr;
-    z.seqs_out = nullptr;
-    z.zt = nullptr;
-    z.slots_cap = 0;
-    z.groups = 0;
+    z.coded = nullptr;
+    z.slots_cap = z.seqs_cap = z.coded_cap = 0;
     z.dev = -1;
 }
 
@@ -650,40 +1481,24 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
         if (rc == PBS_OK) ok(hipEventCreate(&e));
     ZScratch& zs = zscratch();
     std::lock_guard<std::mutex> lk(zs.mu);
-    const unsigned grid = (unsigned)std::min<uint64_t>(ni, (uint64_t)ncu * kZGroupsPerCu);
+    const unsigned grid = (unsigned)std::min<uint64_t>(ni, (uint64_t)ncu);  // one 512-thread workgroup per CU
     if (rc == PBS_OK && compress) {
         if (zs.dev != dev) {  // first use, or another device: free the old scratch there
             if (zs.dev >= 0) {
                 DeviceGuard og(zs.dev);
-                for (void* p : {(void*)zs.slots, (void*)zs.seqs, (void*)zs.seqs_out, (void*)zs.zt})
+                for (void* p : {(void*)zs.slots, (void*)zs.seqs, (void*)zs.coded})
                     if (p) (void)hipFree(p);
             }
             zs.slots = nullptr;
-            zs.slots_cap = 0;
             zs.seqs = nullptr;
-            zs.seqs_out = nullptr;
-            zs.groups = 0;
-            zs.zt = nullptr;
+            zs.coded = nullptr;
+            zs.slots_cap = zs.seqs_cap = zs.coded_cap = 0;
             zs.dev = dev;
         }
-        size_t seq_cap = zs.groups * kMaxSeq, run_cap = zs.groups * kMaxSeq;
-        if (!grow(&zs.slots, &zs.slots_cap, ni * kSlot) || !grow(&zs.seqs, &seq_cap, (size_t)grid * kMaxSeq) ||
-            !grow(&zs.seqs_out, &run_cap, (size_t)grid * kMaxSeq)) {
+        if (!grow(&zs.slots, &zs.slots_cap, ni * kSlot) ||
+            !grow(&zs.seqs, &zs.seqs_cap, (size_t)grid * kZBlockSeq) ||
+            !grow(&zs.coded, &zs.coded_cap, (size_t)grid * kZBlockSeq))
             fail(PBS_ERR_NOMEM);
-        } else {
-            zs.groups = std::max<size_t>(zs.groups, grid);
-        }
-        if (rc == PBS_OK && !zs.zt) {
-            ZTables h;
-            zstd::build_ctable(h.ll, zstd::kLLNorm, 36, zstd::kLLLog);
-            zstd::build_ctable(h.ml, zstd::kMLNorm, 53, zstd::kMLLog);
-            zstd::build_ctable(h.of, zstd::kOFNorm, 29, zstd::kOFLog);
-            if (hipMalloc(&zs.zt, sizeof(ZTables)) != hipSuccess ||
-                hipMemcpy(zs.zt, &h, sizeof(ZTables), hipMemcpyHostToDevice) != hipSuccess) {
-                zs.zt = nullptr;
-                fail(PBS_ERR_NOMEM);
-            }
-        }
     }
     if (rc == PBS_OK)
         ok(hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st)) &&
@@ -693,26 +1508,9 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     if (rc == PBS_OK) {
         (void)hipGetLastError();
         ok(hipEventRecord(ev[0], st));
-        static const bool probe = [] {
-            const char* e = std::getenv("PBS_ZSTD_PROBE");
-            return e && e[0] == '1';
-        }();
-        if (compress && probe) {
-            const unsigned long long z[8] = {};
-            (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
-            hipLaunchKernelGGL(zstd_block_kernel<true>, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds,
-                               d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.seqs_out);
-            unsigned long long h[8] = {};
-            (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
-            (void)hipStreamSynchronize(st);
-            std::fprintf(stderr,
-                         "zstd probe (workgroup 0, us): stage %.1f rle %.1f sub-block %.1f combine %.1f encode+lits %.1f "
-                         "raw %.1f | items %llu seqs %llu\n",
-                         h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[4] / 100.0, h[5] / 100.0, h[6], h[7]);
-        } else if (compress) {
-            hipLaunchKernelGGL(zstd_block_kernel<false>, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds,
-                               d_items, ni, zs.zt, zs.slots, d_sizes, zs.seqs, zs.seqs_out);
-        }
+        if (compress)
+            hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
+                               ni, zs.slots, d_sizes, zs.seqs, zs.coded);
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
         ok(hipGetLastError()) && ok(exclusive_sum_u64(d_tmp, &tmpb, d_bsz, d_boff,

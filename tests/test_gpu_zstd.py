@@ -28,14 +28,20 @@ def torch_dev(gpu):
 
 def _mixed():
     """Chunks of every block kind: empty, tiny, RLE (zero / 0xFF), compressible text,
-    incompressible random, periodic runs across 128 KiB blocks, VM-image pages, lengths
-    at 128 KiB +- 1 and a 16 MiB chunk."""
+    incompressible random, periodic runs across the 64 KiB blocks, VM-image pages,
+    lengths at 64 KiB +- 1 and 3 x 64 KiB (the last block full), English-like text and
+    pxar-like archives (Huffman literals; tests/corpus_gen.py), bytes above 128 (FSE-coded
+    Huffman weights), two-symbol literals, and a 16 MiB chunk."""
+    import corpus_gen
     rng = np.random.default_rng(17)
     text = np.frombuffer(b"proxmox backup chunk store " * 8000, dtype=np.uint8)
-    parts = [np.zeros(0, np.uint8), rng.integers(0, 256, 3, dtype=np.uint8), np.zeros(128 * KiB, np.uint8),
-             np.full(128 * KiB + 1, 0xFF, np.uint8), np.resize(text, 128 * KiB - 1), gen_np.gen_random(300 * KiB, 4),
+    parts = [np.zeros(0, np.uint8), rng.integers(0, 256, 3, dtype=np.uint8), np.zeros(64 * KiB, np.uint8),
+             np.full(64 * KiB + 1, 0xFF, np.uint8), np.resize(text, 64 * KiB - 1), gen_np.gen_random(300 * KiB, 4),
              np.resize(np.arange(7, dtype=np.uint8), 400 * KiB), gen_np.gen_vmimage(4 * MiB, 0x5EED0003, 0),
              gen_np.gen_counter(MiB), np.zeros(0, np.uint8), rng.integers(0, 256, 100, dtype=np.uint8),
+             corpus_gen.text(3 * 64 * KiB, 5), corpus_gen.pxar(2 * MiB + 17, 6),
+             (255 - np.minimum(rng.geometric(0.08, 200 * KiB), 200)).astype(np.uint8),
+             rng.choice(np.array([7, 200], np.uint8), 100 * KiB), corpus_gen.text(64 * KiB + 1, 7),
              gen_np.gen_vmimage(16 * MiB, 0x5EED0003, 1 << 30)]
     data = np.concatenate(parts)
     bounds = np.concatenate([[0], np.cumsum([p.size for p in parts])]).astype(np.uint64)
@@ -113,6 +119,32 @@ def test_chunker_to_blobs_vm_stream(gpu, oracle, torch_dev, avg):
     blob, offs, crcs, comp, tm = _encode(gpu, torch_dev, data, bounds)
     _check(oracle, data, bounds, blob, offs, crcs, comp)
     assert tm["bytes_out"] < n  # the zero pages compress
+
+
+@pytest.mark.parametrize("corpus", ["text", "pxar"])
+def test_chunker_to_blobs_corpus(gpu, oracle, torch_dev, corpus):
+    """Chunker -> compressed blobs on 24 MiB of English-like text / a pxar-like archive
+    (tests/corpus_gen.py) at 1 MiB: Huffman literals, FSE sequence tables and repeat codes
+    in every block, bit-exact with the twin, and the payloads within 10 % of libzstd
+    level 1 (the reference's compressor, data_blob.rs:151)."""
+    import corpus_gen
+    n = 24 * MiB
+    data = corpus_gen.text(n, 11) if corpus == "text" else corpus_gen.pxar(n, 12)
+    n = data.size
+    t = torch_dev.from_numpy(data).to("cuda")
+    with gpu.Chunker(MiB) as c:
+        ends = c.find_cuts_device(t.data_ptr(), n, is_final=True)
+    bounds = np.concatenate([[0], ends]).astype(np.uint64)
+    blob, offs, crcs, comp, tm = _encode(gpu, torch_dev, data, bounds)
+    _check(oracle, data, bounds, blob, offs, crcs, comp)
+    L = oracle.libzstd()
+    ref = 0
+    for i in range(bounds.size - 1):
+        ch = np.ascontiguousarray(data[int(bounds[i]):int(bounds[i + 1])])
+        dst = np.empty(L.ZSTD_compressBound(ch.size), np.uint8)
+        ref += L.ZSTD_compress(dst.ctypes.data, dst.size, ch.ctypes.data, ch.size, 1)
+    ours = int(offs[-1]) - 12 * (bounds.size - 1)
+    assert ours <= ref * 1.10, (ours, ref)
 
 
 def test_blob_encode_after_release(gpu, oracle, torch_dev):
