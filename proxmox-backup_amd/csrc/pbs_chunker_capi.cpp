@@ -119,6 +119,12 @@ struct ScanServer {
     bool running = false;
     bool enabled = true;  // PBS_SCAN_SERVER=0: every scan() takes the batch path (A/B)
     bool broken = false;  // a request timed out: never used again by this handle
+    uint32_t flags = kSrvPollAll;  // PBS_SERVER_POLL=1: lane 0 of wave 0 polls alone (A/B)
+    // PBS_SERVER_PROBE=1: requests, host round trip (us) and the kernel's phases (ticks of
+    // 10 ns: request seen -> staged -> hashed -> acknowledged), printed when the handle is freed
+    uint64_t probe_n = 0;
+    double probe_rtt_us = 0;
+    uint64_t probe_ticks[3] = {0, 0, 0};
 };
 
 struct pbs_chunker {
@@ -589,7 +595,7 @@ int server_launch(pbs_chunker* c, uint64_t last) {
     ScanServer& sv = c->srv;
     __atomic_store_n(&sv.mb->exited, ~0ull, __ATOMIC_RELEASE);
     HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.slot_dev, c->prm.mask, c->prm.minimum, last,
-                                  kServerIdleTicks, sv.stream));
+                                  kServerIdleTicks, sv.flags, sv.stream));
     sv.running = true;
     return PBS_OK;
 }
@@ -638,6 +644,12 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
             return fail(c, PBS_ERR_HIP);
         }
         __builtin_ia32_pause();
+    }
+    if (sv.flags & kSrvProbe) {
+        const volatile uint64_t* pr = sv.mb->probe;
+        ++sv.probe_n;
+        sv.probe_rtt_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        for (int i = 0; i < 3; ++i) sv.probe_ticks[i] += pr[i + 1] - pr[i];
     }
     if (sv.mb->status != 0) return PBS_OK;  // too many candidates: batch path
     const uint64_t k = sv.mb->ncand;
@@ -1114,6 +1126,16 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
 
 void destroy(pbs_chunker* c) {
     server_stop(c);
+    if (c->srv.probe_n) {
+        const ScanServer& sv = c->srv;
+        const double n = (double)sv.probe_n;
+        std::fprintf(stderr,
+                     "scan server probe: %llu requests, host round trip %.2f us; kernel: staging %.2f us, "
+                     "hash %.2f us, compaction + ack %.2f us (request seen -> acknowledged %.2f us)\n",
+                     (unsigned long long)sv.probe_n, sv.probe_rtt_us / n, sv.probe_ticks[0] / n / 100.0,
+                     sv.probe_ticks[1] / n / 100.0, sv.probe_ticks[2] / n / 100.0,
+                     (sv.probe_ticks[0] + sv.probe_ticks[1] + sv.probe_ticks[2]) / n / 100.0);
+    }
     if (c->srv.stream) (void)hipStreamDestroy(c->srv.stream);
     if (c->srv.mb) (void)hipHostFree(c->srv.mb);
     if (c->srv.slot) (void)hipHostFree(c->srv.slot);
@@ -1192,6 +1214,9 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
         c->fused_force = e[0] == '1';
     }
     if (const char* e = std::getenv("PBS_SCAN_SERVER")) c->srv.enabled = e[0] != '0';
+    if (const char* e = std::getenv("PBS_SERVER_POLL")) c->srv.flags = e[0] == '1' ? 0u : kSrvPollAll;
+    if (const char* e = std::getenv("PBS_SERVER_PROBE"))
+        if (e[0] == '1') c->srv.flags |= kSrvProbe;
     c->fused_min_avg = kFusedMinAvg;
     if (const char* e = std::getenv("PBS_BALANCE")) c->balance = std::atoi(e);
     if (const char* e = std::getenv("PBS_SCAN_DYN")) c->scan_dyn_env = e[0] == '1' ? 1 : 0;

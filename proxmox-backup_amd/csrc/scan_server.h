@@ -2,21 +2,24 @@
 // chunker.rs:112-168, called by ChunkStream on every read, chunk_stream.rs:40-77).
 //
 // ONE persistent workgroup polls the mailbox (pbs_chunker_internal.h) in fine-grained
-// pinned host memory with one 16-byte load {seq, len | quit, base}.  A request then costs one
-// more PCIe round trip: the slot's history and data (host memory) are staged in LDS,
-// 32 KiB per pass, all loads in flight at once.  The cut test runs at every position --
-// one 128-byte block per lane, the blocks spread over the four SIMDs: 64 fill steps over
-// the bytes before the block (the window hash of chunker.rs:118-136), 128 roll steps
-// (:141-165) and the test (h & mask) >= mask - 2 (:185).  The hits are compacted in stream
-// order into the mailbox, and after every wave drained its stores the acknowledgement is
-// stored (system-scope release).  The host applies shall_break's min/max rule to the
-// returned candidates.  Exit: the quit flag, or idle_ticks (wall_clock64, 100 MHz) without
-// a request -- the host relaunches it on the next call (pbs_chunker_capi.cpp server_scan),
-// so a process that stops calling leaves no kernel running.
+// pinned host memory with 16-byte loads {seq, len | quit, base} -- by default lane 0 of
+// every wave, staggered, so several PCIe reads are in flight (kSrvPollAll).  A request
+// then costs one more PCIe round trip: the slot's history and data (host memory) are
+// staged in LDS, 32 KiB per pass, all loads in flight at once.  The cut test runs at
+// every position, one wave per 128-byte block (exact_block.h: the window hash as a
+// difference of prefix XORs -- one dword, 4 lookups and a DPP scan per lane instead of a
+// 192-step chain per lane; the reference's recurrence, chunker.rs:118-165, test :185).
+// The hits are compacted in stream order into the mailbox, and after every wave drained
+// its stores the acknowledgement is stored (system-scope release).  The host applies
+// shall_break's min/max rule to the returned candidates.  Exit: the quit flag, or
+// idle_ticks (wall_clock64, 100 MHz) without a request -- the host relaunches it on the
+// next call (pbs_chunker_capi.cpp server_scan), so a process that stops calling leaves
+// no kernel running.  kSrvProbe: per-request phase stamps (PBS_SERVER_PROBE=1).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "exact_block.h"
 #include "pbs_chunker_internal.h"
 
 namespace pbs {
@@ -24,30 +27,7 @@ namespace pbs {
 constexpr int kSrvThreads = 256;  // 4 waves, one per SIMD
 constexpr int kSrvPass = 32 * 1024;  // bytes staged per pass
 constexpr int kSrvBlocks = kSrvPass / 128;
-static_assert(kSrvBlocks == kSrvThreads, "one block per thread");
-
-// hits of the 128-byte block at sd[B .. B+128) (LDS; sd[B-64 .. B) readable): bit i = the
-// window ending at byte B + i passes the test
-__device__ __forceinline__ uint4 lane_block_hits(const uint8_t* sd, int B, const uint32_t* tab,
-                                                 uint32_t mask, uint32_t minimum) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(sd + B - 64);
-    uint32_t d[48];
-#pragma unroll
-    for (int k = 0; k < 48; ++k) d[k] = w[k];
-    uint32_t h = 0;
-#pragma unroll
-    for (int i = 0; i < 64; ++i)
-        h = __builtin_amdgcn_alignbit(h, h, 31) ^ tab[(d[i >> 2] >> (8 * (i & 3))) & 0xffu];
-    uint32_t hw[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int i = 0; i < 128; ++i) {
-        const uint32_t out = (d[i >> 2] >> (8 * (i & 3))) & 0xffu;
-        const uint32_t in = (d[(i + 64) >> 2] >> (8 * (i & 3))) & 0xffu;
-        h = __builtin_amdgcn_alignbit(h, h, 31) ^ tab[out] ^ tab[in];
-        hw[i >> 5] |= ((h & mask) >= minimum ? 1u : 0u) << (i & 31);
-    }
-    return make_uint4(hw[0], hw[1], hw[2], hw[3]);
-}
+static_assert(kSrvBlocks == kSrvThreads, "one block per thread in the compaction");
 
 typedef uint32_t srv_u32x4 __attribute__((ext_vector_type(4)));
 
@@ -55,43 +35,58 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                                                                   const uint8_t* __restrict__ slot,
                                                                   uint32_t mask, uint32_t minimum,
                                                                   uint64_t last_seq,
-                                                                  uint64_t idle_ticks) {
+                                                                  uint64_t idle_ticks, uint32_t flags) {
     __shared__ uint32_t tab[256];
     __shared__ __attribute__((aligned(16))) uint8_t st[kServerHist + kSrvPass + 128];
     __shared__ uint4 hv[kSrvBlocks];
     __shared__ uint32_t wsum[kSrvThreads / 64];
-    __shared__ uint64_t ctl[3];  // [0] command (1 serve, 2 exit) [1] seq | len << 32 [2] base
+    __shared__ uint32_t s_go;    // 0 polling, 1 serve, 2 exit
+    __shared__ uint64_t ctl[2];  // [0] seq | len << 32 [1] base
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool poll_all = (flags & kSrvPollAll) != 0, probe = (flags & kSrvProbe) != 0;
     for (int i = tid; i < 256; i += kSrvThreads) tab[i] = kBuzhashTable[i];
+    if (tid == 0) s_go = 0;
+    __syncthreads();
     uint32_t last = (uint32_t)last_seq;
     uint64_t t_idle = wall_clock64();
     for (;;) {
-        if (tid == 0) {
-            uint64_t cmd = 2;
-            srv_u32x4 r = {last, 0u, 0u, 0u};
+        // poll the request record (one 16-byte load {seq, len | quit, base}); with
+        // kSrvPollAll lane 0 of every wave polls, the waves staggered so that several
+        // PCIe reads are in flight and a new request is seen sooner
+        if (lane == 0 && (poll_all || wave == 0)) {
+            if (poll_all)
+                for (int d = 0; d < wave; ++d) __builtin_amdgcn_s_sleep(8);
             for (;;) {
-                r = *reinterpret_cast<volatile srv_u32x4*>(&mb->req_seq);  // {seq, len, base}
-                if (r.y & kServerQuit) break;
-                if (r.x != last) {
-                    cmd = 1;
+                if (__hip_atomic_load(&s_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                const srv_u32x4 r = *reinterpret_cast<volatile srv_u32x4*>(&mb->req_seq);  // {seq, len, base}
+                uint32_t go = 0;
+                if (r.y & kServerQuit) {
+                    go = 2;
+                } else if (r.x != last) {
+                    ctl[0] = (uint64_t)r.x | ((uint64_t)r.y << 32);
+                    ctl[1] = (uint64_t)r.z | ((uint64_t)r.w << 32);
+                    go = 1;
+                } else if (wall_clock64() - t_idle > idle_ticks) {
+                    go = 2;
+                }
+                if (go) {
+                    __hip_atomic_store(&s_go, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
-                if (wall_clock64() - t_idle > idle_ticks) break;
-                __builtin_amdgcn_s_sleep(2);
+                if (!poll_all) __builtin_amdgcn_s_sleep(2);
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the slot is read after the record
-            ctl[0] = cmd;
-            ctl[1] = (uint64_t)r.x | ((uint64_t)r.y << 32);
-            ctl[2] = (uint64_t)r.z | ((uint64_t)r.w << 32);
         }
         __syncthreads();
-        if (ctl[0] != 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the slot is read after the record
+        if (s_go != 1) {
             if (tid == 0)
                 __hip_atomic_store(&mb->exited, (uint64_t)last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             return;  // uniform
         }
-        const uint32_t seq = (uint32_t)ctl[1], len = (uint32_t)(ctl[1] >> 32);
-        const uint64_t base = ctl[2];
+        const uint64_t t_seen = probe ? wall_clock64() : 0;
+        uint64_t t_staged = 0, t_hashed = 0;
+        const uint32_t seq = (uint32_t)ctl[0], len = (uint32_t)(ctl[0] >> 32);
+        const uint64_t base = ctl[1];
         uint32_t total = 0;
         for (uint32_t off = 0; off < len; off += kSrvPass) {
             const uint32_t plen = len - off < (uint32_t)kSrvPass ? len - off : (uint32_t)kSrvPass;
@@ -126,25 +121,28 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             }
             for (uint32_t i = n16 * 16 + tid; i < nbytes; i += kSrvThreads) st[dst0 + i] = slot[src0 + i];
             __syncthreads();
+            if (probe && off == 0) t_staged = wall_clock64();
             const int nblk = (int)((plen + 127) / 128);
-            {
-                // block b runs on lane b/4 of wave b%4: small requests use all four SIMDs
-                const int b = (tid & 63) * 4 + (tid >> 6);
-                if (b < nblk) {
-                    uint4 h = lane_block_hits(st + kServerHist, b * 128, tab, mask, minimum);
-                    uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+            // the cut test at every position: block b (128 bytes) by wave b % 4, one wave per
+            // block -- lane l < 48 takes window dword l, 4 lookups, a DPP prefix XOR
+            // (exact_block.h; the reference's own window hash, chunker.rs:141-165, and test :185)
+            for (int b = wave; b < nblk; b += kSrvThreads / 64) {
+                const uint8_t* const wb = st + kServerHist + 128 * b - 64;  // window bytes [B - 64, B + 128)
+                const uint32_t wv = lane < 48 ? *reinterpret_cast<const uint32_t*>(wb + 4 * lane) : 0u;
+                const uint4 h = exact_hits<false>(wv, ~0ull >> 1, 0, 64, tab, mask, minimum, lane);
+                uint32_t hw[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {  // reportable positions [lo_ok, plen)
-                        const int p0 = b * 128 + 32 * q;
-                        const int lo = (int)lo_ok - p0, up = (int)plen - p0;
-                        const uint32_t keep_lo = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
-                        const uint32_t keep_hi = up >= 32 ? 0xFFFFFFFFu : (up <= 0 ? 0u : (0xFFFFFFFFu >> (32 - up)));
-                        hw[q] &= keep_lo & keep_hi;
-                    }
-                    hv[b] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                for (int q = 0; q < 4; ++q) {  // reportable positions [lo_ok, plen)
+                    const int p0 = b * 128 + 32 * q;
+                    const int lo = (int)lo_ok - p0, up = (int)plen - p0;
+                    const uint32_t keep_lo = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
+                    const uint32_t keep_hi = up >= 32 ? 0xFFFFFFFFu : (up <= 0 ? 0u : (0xFFFFFFFFu >> (32 - up)));
+                    hw[q] &= keep_lo & keep_hi;
                 }
+                if (lane == 0) hv[b] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
             }
             __syncthreads();
+            if (probe && off == 0) t_hashed = wall_clock64();
             // stream-order compaction: thread t owns block t
             const uint4 h = tid < nblk ? hv[tid] : make_uint4(0, 0, 0, 0);
             const uint32_t c = __builtin_popcount(h.x) + __builtin_popcount(h.y) +
@@ -184,8 +182,16 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
         if (tid == 0) {
             mb->ncand = total < kServerCand ? total : kServerCand;
             mb->status = total > kServerCand ? 1u : 0u;
+            if (probe) {
+                mb->probe[0] = t_seen;
+                mb->probe[1] = t_staged;
+                mb->probe[2] = t_hashed;
+                mb->probe[3] = wall_clock64();
+            }
+            s_go = 0;
             __hip_atomic_store(&mb->ack_seq, (uint64_t)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        __syncthreads();
         last = seq;
         t_idle = wall_clock64();
     }

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void server(const Req* req, const uint8_t* pay
         const u32x4* p = reinterpret_cast<const u32x4*>(payload);
         for (uint32_t i = tid; i < len / 16; i += 256) {
             const u32x4 v = __builtin_nontemporal_load(p + i);
-            s += v.x + v.y + v.z + v.w;
+            s += (uint64_t)v.x + v.y + v.z + v.w;
         }
         for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
         if ((tid & 63) == 0) part[tid >> 6] = s;
@@ -87,6 +87,74 @@ __global__ __launch_bounds__(256) void server(const Req* req, const uint8_t* pay
             ack->t_seen = ts;
             ack->t_staged = tg;
             ack->t_done = wall_clock64();
+            __hip_atomic_store(&ack->seq, (uint64_t)last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        t0 = wall_clock64();
+    }
+}
+
+// mode 3: every wave's lane 0 polls (staggered: ~4 loads in flight over PCIe instead of
+// one), the first to see the request raises an LDS flag; the payload is read with all of
+// a thread's loads in flight before any is used
+__global__ __launch_bounds__(256) void server4(const Req* req, const uint8_t* payload, Ack* ack, uint64_t idle) {
+    __shared__ uint32_t s_go, s_len, s_seq;
+    __shared__ uint64_t part[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t last = 0;
+    if (tid == 0) s_go = 0;
+    __syncthreads();
+    uint64_t t0 = wall_clock64();
+    for (;;) {
+        if (lane == 0) {
+            for (int d = 0; d < wave; ++d) __builtin_amdgcn_s_sleep(8);  // stagger the pollers
+            for (;;) {
+                if (__hip_atomic_load(&s_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                const u32x4 r = *reinterpret_cast<const volatile u32x4*>(req);
+                if (r.z) {
+                    __hip_atomic_store(&s_go, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                if (r.x != last) {
+                    s_len = r.y;
+                    s_seq = r.x;
+                    __hip_atomic_store(&s_go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                if (wall_clock64() - t0 > idle) {
+                    __hip_atomic_store(&s_go, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (s_go != 1) return;
+        const uint64_t ts = wall_clock64();
+        const uint32_t len = s_len;
+        last = s_seq;
+        const u32x4* p = reinterpret_cast<const u32x4*>(payload);
+        const uint32_t n16 = len / 16;
+        uint64_t s = 0;
+        for (uint32_t i0 = tid; i0 < n16; i0 += 16 * 256) {  // 16 loads in flight per thread
+            u32x4 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (i0 + 256 * u < n16) v[u] = __builtin_nontemporal_load(p + i0 + 256 * u);
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (i0 + 256 * u < n16) s += (uint64_t)v[u].x + v[u].y + v[u].z + v[u].w;
+        }
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) part[wave] = s;
+        __syncthreads();
+        const uint64_t tg = wall_clock64();
+        if (tid == 0) {
+            ack->sum = part[0] + part[1] + part[2] + part[3];
+            ack->t_seen = ts;
+            ack->t_staged = tg;
+            ack->t_done = wall_clock64();
+            s_go = 0;
             __hip_atomic_store(&ack->seq, (uint64_t)last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
@@ -106,7 +174,7 @@ static int run(int mode, uint32_t len, int iters) {
     uint8_t* pay_h = nullptr;  // host's view
     uint8_t* pay_d = nullptr;
     void* dev_alloc[2] = {nullptr, nullptr};
-    if (mode == 0) {
+    if (mode == 0 || mode == 3) {
         CK(hipHostMalloc((void**)&req_h, sizeof(Req), fl));
         CK(hipHostMalloc((void**)&pay_h, 1 << 20, fl));
         CK(hipHostGetDevicePointer((void**)&req_d, req_h, 0));
@@ -148,7 +216,10 @@ static int run(int mode, uint32_t len, int iters) {
     }
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    hipLaunchKernelGGL(server, dim3(1), dim3(256), 0, st, req_d, pay_d, ack_d, (uint64_t)200000000);
+    if (mode == 3)
+        hipLaunchKernelGGL(server4, dim3(1), dim3(256), 0, st, req_d, pay_d, ack_d, (uint64_t)200000000);
+    else
+        hipLaunchKernelGGL(server, dim3(1), dim3(256), 0, st, req_d, pay_d, ack_d, (uint64_t)200000000);
     CK(hipGetLastError());
     double tot = 0, t_seen_staged = 0, t_staged_done = 0;
     int bad = 0;
@@ -193,7 +264,7 @@ static int run(int mode, uint32_t len, int iters) {
 
 int main() {
     int rc = 0;
-    for (int mode : {0, 1, 2})
+    for (int mode : {0, 3})
         for (uint32_t len : {0u, 8192u, 65536u}) rc |= run(mode, len, 3000);
     return rc;
 }

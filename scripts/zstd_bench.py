@@ -1,0 +1,72 @@
+"""Throughput and ratio of the GPU blob stage (zstd frames + CRC, pbs_blob_encode_chunks_device)
+on text-like and pxar-like data (tests/corpus_gen.py): a seeded 32 MiB corpus tiled to
+--gib GiB in HBM (a chunk's window never reaches a neighbouring tile), cut by the GPU
+chunker at --avg, encoded --reps times (best wall clock), with libzstd level 1 on the
+host over the first 64 MiB for the ratio.
+
+    python scripts/zstd_bench.py [--corpus text|pxar|both] [--gib 1] [--avg 4194304]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "proxmox-backup_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--corpus", default="both")
+    ap.add_argument("--gib", type=float, default=1.0)
+    ap.add_argument("--avg", type=int, default=4 << 20)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import corpus_gen
+    import oracle
+    import pbschunk
+
+    torch.cuda.set_device(0)
+    L = oracle.libzstd()
+    for name in (["text", "pxar"] if a.corpus == "both" else [a.corpus]):
+        t0 = time.time()
+        base = corpus_gen.text(32 << 20, 21) if name == "text" else corpus_gen.pxar(32 << 20, 22)
+        n = int(a.gib * (1 << 30)) // base.size * base.size
+        host = np.tile(base, n // base.size)
+        gen_s = time.time() - t0
+        dev = torch.from_numpy(host).to("cuda")
+        with pbschunk.Chunker(a.avg) as c:
+            ends = c.find_cuts_device(dev.data_ptr(), n, is_final=True)
+        bounds = np.concatenate([[0], ends]).astype(np.uint64)
+        cap = pbschunk.blob_stream_bound(bounds)
+        out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        pbschunk.blob_encode_chunks_device(dev.data_ptr(), n, bounds, out.data_ptr(), cap)  # warm-up
+        best = None
+        for _ in range(a.reps):
+            offs, crcs, comp, tm = pbschunk.blob_encode_chunks_device(dev.data_ptr(), n, bounds, out.data_ptr(), cap)
+            if best is None or tm["total_ms"] < best["total_ms"]:
+                best = tm
+        # ratio against libzstd level 1 on the first 64 MiB of chunks
+        take = int(np.searchsorted(bounds, 64 << 20))
+        ours = int(offs[take]) - 12 * take
+        ref = 0
+        for i in range(take):
+            ch = np.ascontiguousarray(host[int(bounds[i]):int(bounds[i + 1])])
+            dst = np.empty(L.ZSTD_compressBound(ch.size), np.uint8)
+            ref += L.ZSTD_compress(dst.ctypes.data, dst.size, ch.ctypes.data, ch.size, 1)
+        print(json.dumps({"corpus": name, "bytes": n, "chunks": int(bounds.size - 1), "gen_s": round(gen_s, 1),
+                          "GiB/s": round(n / (1 << 30) / (best["total_ms"] / 1e3), 2),
+                          "ms": {k: round(best[k], 2) for k in ("total_ms", "compress_ms", "assemble_ms", "crc_ms")},
+                          "out_in": round(best["bytes_out"] / n, 4),
+                          "sample_payload": {"ours": ours, "libzstd_level1": ref, "ratio": round(ours / ref, 4),
+                                             "chunks": take}}), flush=True)
+        del dev, out
+        pbschunk.blob_encode_release()
+
+
+if __name__ == "__main__":
+    main()
