@@ -119,7 +119,7 @@ struct ScanServer {
     bool running = false;
     bool enabled = true;  // PBS_SCAN_SERVER=0: every scan() takes the batch path (A/B)
     bool broken = false;  // a request timed out: never used again by this handle
-    uint32_t flags = kSrvPollAll;  // PBS_SERVER_POLL=1: lane 0 of wave 0 polls alone (A/B)
+    uint32_t flags = 0;  // PBS_SERVER_POLL=4: lane 0 of every wave polls, staggered (A/B; no faster)
     // PBS_SERVER_PROBE=1: requests, host round trip (us) and the kernel's phases (ticks of
     // 10 ns: request seen -> staged -> hashed -> acknowledged), printed when the handle is freed
     uint64_t probe_n = 0;
@@ -628,8 +628,10 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
     }
     __atomic_store_n(&sv.mb->req_seq, seq, __ATOMIC_RELEASE);
     const auto t0 = std::chrono::steady_clock::now();
+    uint64_t ack = 0;
     for (uint32_t spin = 0;; ++spin) {
-        if (__atomic_load_n(&sv.mb->ack_seq, __ATOMIC_ACQUIRE) == seq) break;
+        ack = __atomic_load_n(&sv.mb->ack_seq, __ATOMIC_ACQUIRE);
+        if ((uint32_t)ack == seq) break;
         if (__atomic_load_n(&sv.mb->exited, __ATOMIC_ACQUIRE) == (uint32_t)(seq - 1)) {
             // it went idle just before this request: relaunch, the request is still there
             HIP_TRY(c, hipStreamSynchronize(sv.stream));
@@ -651,8 +653,8 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
         sv.probe_rtt_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         for (int i = 0; i < 3; ++i) sv.probe_ticks[i] += pr[i + 1] - pr[i];
     }
-    if (sv.mb->status != 0) return PBS_OK;  // too many candidates: batch path
-    const uint64_t k = sv.mb->ncand;
+    if (ack >> 63) return PBS_OK;  // too many candidates: batch path
+    const uint64_t k = (ack >> 32) & 0x7FFFFFFFull;
     const size_t old = c->pending.size();
     c->pending.resize(old + k);
     std::memcpy(c->pending.data() + old, sv.mb->cand, k * 8);
@@ -1214,7 +1216,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
         c->fused_force = e[0] == '1';
     }
     if (const char* e = std::getenv("PBS_SCAN_SERVER")) c->srv.enabled = e[0] != '0';
-    if (const char* e = std::getenv("PBS_SERVER_POLL")) c->srv.flags = e[0] == '1' ? 0u : kSrvPollAll;
+    if (const char* e = std::getenv("PBS_SERVER_POLL")) c->srv.flags = e[0] == '4' ? kSrvPollAll : 0u;
     if (const char* e = std::getenv("PBS_SERVER_PROBE"))
         if (e[0] == '1') c->srv.flags |= kSrvProbe;
     c->fused_min_avg = kFusedMinAvg;

@@ -198,10 +198,10 @@ struct alignas(64) ServerMailbox {
                         // stream bytes before it, right-aligned in the slot's first 64 bytes
     uint32_t pad0[12];
     // device -> host
-    alignas(64) uint64_t ack_seq;  // = req_seq once served (release)
+    alignas(64) uint64_t ack_seq;  // once served (release): req_seq | ncand << 32 | overflow << 63,
+                                   // ncand = candidates in cand[] (ascending, absolute), overflow:
+                                   // more than kServerCand (nothing usable)
     uint64_t exited;               // last served request when the kernel exited; ~0 while up
-    uint64_t ncand;                // candidates in cand[] (ascending, absolute)
-    uint64_t status;               // 0 ok, 1 more than kServerCand candidates (nothing usable)
     uint64_t probe[4];             // kSrvProbe: wall_clock64 at request seen, staged, hashed, acked
     uint64_t cand[kServerCand];
 };

@@ -240,13 +240,28 @@ struct FseT {
     uint32_t mode;  // 0 predefined, 1 RLE, 2 FSE-compressed
     uint32_t desc_len;
     uint8_t desc[128];
-    uint8_t sym_at[kFseCells];  // construction scratch
+    uint8_t sym_at[kFseCells];  // construction scratch (LDS: no private arrays on the serial paths)
+    int16_t norm[64];
+    int32_t cum[64];
+};
+// a predefined table (RFC 8878 3.1.1.3.2.2), built once per launch
+struct PreT {
+    uint16_t next[64];
+    int32_t dnb[53];
+    int32_t dfs[53];
+    int32_t log;
+};
+struct FseView {
+    const uint16_t* next;
+    const int32_t* dnb;
+    const int32_t* dfs;
+    uint32_t log;
 };
 
 __device__ __noinline__ void fse_build(FseT& t, const int16_t* norm, int nsym, int log) {
     const int size = 1 << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
     int high = size - 1;
-    int cum[54];
+    int32_t* const cum = t.cum;
     cum[0] = 0;
     for (int s = 0; s < nsym; ++s) {
         if (norm[s] == -1) {
@@ -284,13 +299,16 @@ __device__ __noinline__ void fse_build(FseT& t, const int16_t* norm, int nsym, i
     t.log = log;
 }
 
-__device__ __forceinline__ uint32_t fse_init(const FseT& t, uint32_t s) {
+__device__ __forceinline__ FseView view(const FseT& t) { return FseView{t.next, t.dnb, t.dfs, (uint32_t)t.log}; }
+__device__ __forceinline__ FseView view(const PreT& t) { return FseView{t.next, t.dnb, t.dfs, (uint32_t)t.log}; }
+
+__device__ __forceinline__ uint32_t fse_init(const FseView& t, uint32_t s) {
     const uint32_t nb = (uint32_t)((t.dnb[s] + (1 << 15)) >> 16);
     const uint32_t v0 = (nb << 16) - (uint32_t)t.dnb[s];
     return t.next[(v0 >> nb) + t.dfs[s]];
 }
 template <typename B>
-__device__ __forceinline__ void fse_enc(B& b, const FseT& t, uint32_t& v, uint32_t s) {
+__device__ __forceinline__ void fse_enc(B& b, const FseView& t, uint32_t& v, uint32_t s) {
     const uint32_t nb = (v + (uint32_t)t.dnb[s]) >> 16;
     b.put(v, nb);
     v = t.next[(v >> nb) + t.dfs[s]];
@@ -396,9 +414,10 @@ __device__ __noinline__ uint32_t fse_ncount(uint8_t* o, const int16_t* norm, int
 }
 
 // Table of one sequence symbol stream: the cheapest of predefined (0), RLE (1) and own
-// FSE table (2) by the integer estimate (ties keep the earlier mode).
-__device__ __noinline__ void seq_table(FseT& t, const uint32_t* cnt, int nsym, uint32_t nseq, const int16_t* pre, int pre_log,
-                          int max_log) {
+// FSE table (2) by the integer estimate (ties keep the earlier mode).  Mode 0 leaves the
+// table to the launch's predefined one.
+__device__ __noinline__ void seq_table(FseT& t, const uint32_t* cnt, int nsym, uint32_t nseq, const int16_t* pre,
+                                       int pre_log, int max_log) {
     int distinct = 0, maxs = 0;
     for (int s = 0; s < nsym; ++s)
         if (cnt[s]) {
@@ -409,6 +428,7 @@ __device__ __noinline__ void seq_table(FseT& t, const uint32_t* cnt, int nsym, u
     for (int s = 0; s < nsym; ++s)
         if (cnt[s]) c_pre += (uint64_t)cnt[s] * (256u * pre_log - lg256(pre[s] < 1 ? 1 : pre[s]));
     t.desc_len = 0;
+    t.mode = 0;
     if (distinct == 1 && nseq > 2) {
         t.mode = 1;
         t.desc[0] = (uint8_t)maxs;
@@ -417,23 +437,17 @@ __device__ __noinline__ void seq_table(FseT& t, const uint32_t* cnt, int nsym, u
     }
     if (nseq >= 16) {
         const int log = fse_log(nseq, (uint32_t)maxs, max_log);
-        int16_t norm[53];
-        fse_normalize(norm, cnt, maxs + 1, nseq, log);
-        const uint32_t d = fse_ncount(t.desc, norm, maxs + 1, log);
+        fse_normalize(t.norm, cnt, maxs + 1, nseq, log);
+        const uint32_t d = fse_ncount(t.desc, t.norm, maxs + 1, log);
         uint64_t c = 2048ull * d;
         for (int s = 0; s <= maxs; ++s)
-            if (cnt[s]) c += (uint64_t)cnt[s] * (256u * log - lg256((uint32_t)norm[s]));
+            if (cnt[s]) c += (uint64_t)cnt[s] * (256u * log - lg256((uint32_t)t.norm[s]));
         if (c < c_pre) {
             t.mode = 2;
             t.desc_len = d;
-            fse_build(t, norm, maxs + 1, log);
-            return;
+            fse_build(t, t.norm, maxs + 1, log);
         }
     }
-    t.mode = 0;
-    int16_t p[53];
-    for (int s = 0; s < nsym; ++s) p[s] = pre[s];
-    fse_build(t, p, nsym, pre_log);
 }
 
 // ---------------------------------------------------------------- LDS layout
@@ -459,7 +473,7 @@ struct Ctl {
     uint32_t wsum2[kZWaves];
     uint32_t segP[5];           // Huffman: bits before each segment boundary
     uint32_t lit_mode, lit_size, huf_c, huf_hs, desc_len;
-    uint32_t seq_size, seq_ok;
+    uint32_t seq_size, seq_ok, seq_hdr, seq_last[3];  // sequences: body size, fits, header bytes, final states
     int32_t root;               // Huffman merge: the root node
     uint8_t desc[264];          // Huffman tree description (FSE form: <= ~210 bytes before the 128 check)
 };
@@ -469,7 +483,8 @@ struct Ctl {
 // shorter, else in the direct 4-bit form; false when neither applies (raw literals).
 __device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scratch, uint32_t mb, uint32_t lastsym) {
     const int nwt = (int)lastsym;
-    uint32_t wc[16] = {0};
+    uint32_t* const wc = reinterpret_cast<uint32_t*>(t_scratch.cum);  // weight counts (LDS)
+    for (int v = 0; v < 16; ++v) wc[v] = 0;
     uint32_t maxw = 0;
     for (int s = 0; s < nwt; ++s) {
         const uint32_t wv = E.len[s] ? mb + 1 - E.len[s] : 0;
@@ -483,27 +498,28 @@ __device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scra
         for (int v = 0; v < 16; ++v) single |= wc[v] == (uint32_t)nwt;
         if (!single) {
             const int lg = fse_log((uint32_t)nwt, maxw, 6);
-            int16_t norm[16];
-            fse_normalize(norm, wc, (int)maxw + 1, (uint32_t)nwt, lg);
             FseT& t = t_scratch;
+            int16_t* const norm = t.norm;
+            fse_normalize(norm, wc, (int)maxw + 1, (uint32_t)nwt, lg);
             fl = fse_ncount(ctl.desc + 1, norm, (int)maxw + 1, lg);
-            fse_build(t, norm, (int)maxw + 1, lg);
+            fse_build(t, norm, (int)maxw + 1, lg);  // (overwrites wc: no longer needed)
+            const FseView tv = view(t);
             LBits bw;
             bw.init(ctl.desc + 1 + fl);
             auto wt = [&](int s) { return E.len[s] ? mb + 1 - E.len[s] : 0u; };
             uint32_t v1, v2;
             int i = nwt;
             if (nwt & 1) {
-                v1 = fse_init(t, wt(--i));
-                v2 = fse_init(t, wt(--i));
-                fse_enc(bw, t, v1, wt(--i));
+                v1 = fse_init(tv, wt(--i));
+                v2 = fse_init(tv, wt(--i));
+                fse_enc(bw, tv, v1, wt(--i));
             } else {
-                v2 = fse_init(t, wt(--i));
-                v1 = fse_init(t, wt(--i));
+                v2 = fse_init(tv, wt(--i));
+                v1 = fse_init(tv, wt(--i));
             }
             while (i > 0) {
-                fse_enc(bw, t, v2, wt(--i));
-                fse_enc(bw, t, v1, wt(--i));
+                fse_enc(bw, tv, v2, wt(--i));
+                fse_enc(bw, tv, v1, wt(--i));
             }
             bw.put(v2, (uint32_t)t.log);
             bw.put(v1, (uint32_t)t.log);
@@ -530,75 +546,75 @@ __device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scra
     return true;
 }
 
-// Sequences section (RFC 8878 3.1.1.3.2, one lane): count, modes, table descriptions, the
-// FSE bit stream (the last sequence first); ctl.seq_ok = false once it passes the raw size.
-__device__ __noinline__ void write_sequences(Ctl& ctl, const FseT* fse, const Coded* __restrict__ coded, uint32_t nseq,
-                                             uint8_t* lit_out, uint32_t lsz, uint8_t* out, uint32_t n) {
-    uint8_t* o = lit_out + lsz;
-    uint8_t* const lim = out + 3 + n;  // past it the block is stored raw anyway
-    const uint32_t ns = nseq;
-    if (ns < 128) {
-        *o++ = (uint8_t)ns;
-    } else if (ns < 0x7F00) {
-        *o++ = (uint8_t)((ns >> 8) + 0x80);
-        *o++ = (uint8_t)ns;
-    } else {
-        *o++ = 0xFF;
-        *o++ = (uint8_t)(ns - 0x7F00);
-        *o++ = (uint8_t)((ns - 0x7F00) >> 8);
-    }
-    bool ok = true;
-    if (ns) {
-        const FseT& tl = fse[0];
-        const FseT& to = fse[1];
-        const FseT& tm = fse[2];
-        *o++ = (uint8_t)(tl.mode << 6 | to.mode << 4 | tm.mode << 2);
-        for (uint32_t i = 0; i < tl.desc_len; ++i) *o++ = tl.desc[i];
-        for (uint32_t i = 0; i < to.desc_len; ++i) *o++ = to.desc[i];
-        for (uint32_t i = 0; i < tm.desc_len; ++i) *o++ = tm.desc[i];
-        GBits b;
-        b.init(o);
-        const bool rl = tl.mode != 1, ro = to.mode != 1, rm = tm.mode != 1;
-        uint32_t vl = 0, vo = 0, vm = 0;
-        {
-            const Coded z = coded[ns - 1];
-            const uint32_t llc = z.codes & 0xFF, mlc = (z.codes >> 8) & 0xFF, ofc = z.codes >> 16;
-            if (rm) vm = fse_init(tm, mlc);
-            if (ro) vo = fse_init(to, ofc);
-            if (rl) vl = fse_init(tl, llc);
-            b.put(z.ll - kLLBase[llc], kLLBits[llc]);
-            b.put(z.ml - kMLBase[mlc], kMLBits[mlc]);
-            b.put(z.ofv - (1u << ofc), ofc);
-        }
-        Coded nx = ns >= 2 ? coded[ns - 2] : Coded{0, 0, 0, 0};
-        for (uint32_t q = ns - 1; q-- > 0;) {
-            const Coded x = nx;
-            if (q) nx = coded[q - 1];
-            const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
-            if (ro) fse_enc(b, to, vo, ofc);
-            if (rm) fse_enc(b, tm, vm, mlc);
-            if (rl) fse_enc(b, tl, vl, llc);
-            b.put(x.ll - kLLBase[llc], kLLBits[llc]);
-            b.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
-            b.put(x.ofv - (1u << ofc), ofc);
-            if (b.p > lim) {
-                ok = false;
-                break;
+// One FSE state chain of the sequences bit stream (one lane): the state is initialised
+// from the last sequence's code and then encodes sequences ns-2 .. 0; chain[q] = the bits
+// it emits for sequence q (value | count << 16), *last = the final state (flushed after
+// sequence 0).  `shift` picks the code byte (0 LL, 8 ML, 16 OF).
+__device__ __noinline__ void seq_chain(FseView t, const Coded* __restrict__ coded, uint32_t ns, uint32_t shift,
+                                       uint32_t* __restrict__ chain, uint32_t* last) {
+    uint32_t v = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
+    uint32_t q = ns - 1;
+    while (q > 0) {
+        // the next 8 codes' loads in flight together
+        uint32_t c8[8];
+        const uint32_t nq = q < 8 ? q : 8;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if ((uint32_t)u < nq) c8[u] = (coded[q - 1 - u].codes >> shift) & 0xFF;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if ((uint32_t)u < nq) {
+                const uint32_t sym = c8[u];
+                const uint32_t nb = (v + (uint32_t)t.dnb[sym]) >> 16;
+                chain[q - 1 - u] = (v & ((1u << nb) - 1u)) | nb << 16;
+                v = t.next[(v >> nb) + t.dfs[sym]];
             }
-        }
-        if (ok) {
-            if (rm) b.put(vm, (uint32_t)tm.log);
-            if (ro) b.put(vo, (uint32_t)to.log);
-            if (rl) b.put(vl, (uint32_t)tl.log);
-            b.close();
-            o = b.p;
+        q -= nq;
+    }
+    *last = v;
+}
+
+// bits of sequence q in the stream: its three state fields (none for the last sequence,
+// nor for an RLE-mode stream) and its extra bits
+__device__ __forceinline__ uint32_t seq_bits(const Coded& x, uint32_t q, uint32_t ns, const uint32_t* chains,
+                                             uint32_t stride, const uint32_t* mode) {
+    const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
+    uint32_t b = kLLBits[llc] + kMLBits[mlc] + ofc;
+    if (q + 1 < ns) {
+        if (mode[0] != 1) b += chains[q] >> 16;
+        if (mode[1] != 1) b += chains[stride + q] >> 16;
+        if (mode[2] != 1) b += chains[2 * stride + q] >> 16;
+    }
+    return b;
+}
+
+// a thread's bits into the zeroed stream words (atomicOr: its first and last words are
+// shared with its neighbours)
+struct OrBits {
+    uint32_t* w;
+    uint32_t wi;
+    uint64_t acc;
+    uint32_t n;
+    __device__ void init(uint32_t* words, uint32_t bit) {
+        w = words;
+        wi = bit >> 5;
+        n = bit & 31;
+        acc = 0;
+    }
+    __device__ void put(uint64_t v, uint32_t nb) {
+        acc |= (v & ((1ull << nb) - 1ull)) << n;  // nb <= 31
+        n += nb;
+        if (n >= 32) {
+            if ((uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
+            ++wi;
+            acc >>= 32;
+            n -= 32;
         }
     }
-    const uint32_t body = ok ? (uint32_t)(o - lit_out) : 0xFFFFFFFFu;
-    ctl.seq_ok = ok && body < n;
-    ctl.seq_size = body;
-        
-}
+    __device__ void done() {
+        if (n && (uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
+    }
+};
 
 // Two-queue Huffman merge (one lane): leaves 0..m-1 = the symbols sorted by (count,
 // symbol) (E.tw holds their sorted keys on entry), internal nodes m.. in creation order,
@@ -624,16 +640,32 @@ __device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) 
 __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, uint8_t* __restrict__ slots,
-    uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch, Coded* __restrict__ coded_scratch) {
+    uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch, Coded* __restrict__ coded_scratch,
+    uint32_t* __restrict__ chain_scratch) {
     __shared__ uint4 stage[kZStageWords];
     __shared__ __attribute__((aligned(16))) uint8_t work[64 * 1024];
     __shared__ FseT fse[3];  // LL, OF, ML
+    __shared__ PreT pre[3];  // the predefined tables, same order
     __shared__ Ctl ctl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint16_t* const tabs = reinterpret_cast<uint16_t*>(work);
     EntropyArea& E = *reinterpret_cast<EntropyArea*>(work);
     Seq* const wseq_all = seq_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
     Coded* const coded = coded_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
+    uint32_t* const chains = chain_scratch + (uint64_t)blockIdx.x * 3 * kZBlockSeq;  // per stream, per sequence
+    if (wave == 0 && lane < 3) {  // the predefined tables, once per launch (fse[] as scratch)
+        FseT& t = fse[lane];
+        if (lane == 0) fse_build(t, kLLNorm, 36, kLLLog);
+        if (lane == 1) fse_build(t, kOFNorm, 29, kOFLog);
+        if (lane == 2) fse_build(t, kMLNorm, 53, kMLLog);
+        PreT& q = pre[lane];
+        for (int i = 0; i < 64; ++i) q.next[i] = t.next[i];
+        for (int i = 0; i < 53; ++i) {
+            q.dnb[i] = t.dnb[i];
+            q.dfs[i] = t.dfs[i];
+        }
+        q.log = t.log;
+    }
 
     for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
         __syncthreads();  // LDS of the previous item
@@ -865,9 +897,9 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 ctl.nseq[wave] = ns;
                 ctl.lastend[wave] = lastend;
             }
+            __threadfence();  // the sequence list (global) before the other waves read it
         }
         __syncthreads();
-        __threadfence_block();
 
         // ---- literals: bitmap of the unmatched bytes, literal index per thread range
         for (uint32_t i = tid; i < kEncBlock / 32; i += kZThreads) {
@@ -1110,10 +1142,10 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 coded[first + q] = c;
                 lit_end = e.pos + e.ml;
             }
+            __threadfence();
         }
         for (uint32_t i = tid; i < 36 + 53 + 32; i += kZThreads) E.shist[i] = 0;
         __syncthreads();
-        __threadfence_block();
         uint32_t nseq = 0;
         for (int w2 = 0; w2 < kZWaves; ++w2) nseq += min(ctl.nseq[w2], kZSubSeq);
         for (uint32_t q = tid; q < nseq; q += kZThreads) {
@@ -1192,6 +1224,43 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         __syncthreads();
         const uint32_t lm = ctl.lit_mode, lsz = ctl.lit_size;
         uint8_t* const lit_out = out + 3;
+        // ---- sequences: the three FSE state chains (lane 0 of waves 1-3), the section
+        // header (count, modes, table descriptions; wave 0 lane 0)
+        if (lane == 0 && wave >= 1 && wave <= 3 && nseq >= 2 && fse[wave - 1].mode != 1) {
+            const int k = wave - 1;  // 0 LL, 1 OF, 2 ML
+            const FseView tv = fse[k].mode == 2 ? view(fse[k]) : view(pre[k]);
+            seq_chain(tv, coded, nseq, k == 0 ? 0u : k == 1 ? 16u : 8u, chains + (uint64_t)k * kZBlockSeq,
+                      &ctl.seq_last[k]);
+            __threadfence();
+        }
+        if (tid == 0) {
+            uint8_t* o = lit_out + lsz;
+            uint8_t* const o0 = o;
+            const uint32_t ns = nseq;
+            if (ns < 128) {
+                *o++ = (uint8_t)ns;
+            } else if (ns < 0x7F00) {
+                *o++ = (uint8_t)((ns >> 8) + 0x80);
+                *o++ = (uint8_t)ns;
+            } else {
+                *o++ = 0xFF;
+                *o++ = (uint8_t)(ns - 0x7F00);
+                *o++ = (uint8_t)((ns - 0x7F00) >> 8);
+            }
+            if (ns) {
+                *o++ = (uint8_t)(fse[0].mode << 6 | fse[1].mode << 4 | fse[2].mode << 2);
+                for (int k = 0; k < 3; ++k)
+                    for (uint32_t i = 0; i < fse[k].desc_len; ++i) *o++ = fse[k].desc[i];
+            }
+            ctl.seq_hdr = (uint32_t)(o - o0);
+            if (ns >= 1)  // a single sequence's states come from its own codes
+                for (int k = 0; k < 3; ++k)
+                    if (fse[k].mode != 1 && ns == 1) {
+                        const uint32_t sh = k == 0 ? 0u : k == 1 ? 16u : 8u;
+                        const FseView tv = fse[k].mode == 2 ? view(fse[k]) : view(pre[k]);
+                        ctl.seq_last[k] = fse_init(tv, (coded[0].codes >> sh) & 0xFF);
+                    }
+        }
         // ---- write the literal section (all threads but wave 7 lane 0's sequence encode runs after)
         if (lm == 2) {
             const uint32_t words = kHufStreams / 4 + 4;
@@ -1282,8 +1351,80 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                         lit_out[rawh + idx++] = (uint8_t)W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2));
             }
         }
-        // ---- sequences section (one lane)
-        if (tid == 0) write_sequences(ctl, fse, coded, nseq, lit_out, lsz, out, n);
+        // ---- sequences bit stream: per-sequence bit counts, a block scan, then every
+        // thread writes its range of sequences (the last sequence first in the stream) with
+        // atomicOr into the zeroed words
+        __syncthreads();
+        {
+            const uint32_t ns = nseq, hdr = ctl.seq_hdr;
+            const uint32_t mode[3] = {fse[0].mode, fse[1].mode, fse[2].mode};
+            const uint32_t per = (ns + kZThreads - 1) / kZThreads;
+            const uint32_t q0 = min(ns, (uint32_t)tid * per), q1 = min(ns, q0 + per);
+            uint32_t st = 0;
+            for (uint32_t q = q0; q < q1; ++q) st += seq_bits(coded[q], q, ns, chains, kZBlockSeq, mode);
+            const uint32_t si = wave_incl(st, lane);
+            if (lane == 63) ctl.wsum[wave] = si;
+            __syncthreads();
+            uint32_t pt = si - st, T = 0;
+            for (int w2 = 0; w2 < kZWaves; ++w2) {
+                pt += w2 < wave ? ctl.wsum[w2] : 0u;
+                T += ctl.wsum[w2];
+            }
+            uint32_t flushb = 0;
+            for (int k = 0; k < 3; ++k)
+                if (ns && mode[k] != 1) flushb += (uint32_t)(mode[k] == 2 ? fse[k].log : pre[k].log);
+            const uint32_t sbytes = ns ? (T + flushb + 1 + 7) / 8 : 0u;
+            const uint32_t body = lsz + hdr + sbytes;
+            const bool ok = body < n;
+            if (ok && ns) {
+                uint8_t* const S0 = lit_out + lsz + hdr;
+                uint32_t* const A = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(S0) & ~(uintptr_t)3);
+                const uint32_t off0 = 8u * (uint32_t)(S0 - reinterpret_cast<uint8_t*>(A));
+                const uint32_t lastw = (off0 + T + flushb + 1 - 1) >> 5;
+                if (tid == 0)
+                    for (uint8_t* b = S0; b < reinterpret_cast<uint8_t*>(A + 1); ++b) *b = 0;
+                for (uint32_t wdx = 1 + tid; wdx <= lastw; wdx += kZThreads) A[wdx] = 0;
+                __threadfence();  // the zeros (and the section header) at L2 before any atomicOr
+                __syncthreads();
+                OrBits ob;
+                ob.init(A, off0 + (T - pt - st));
+                for (uint32_t q = q1; q-- > q0;) {
+                    const Coded x = coded[q];
+                    const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
+                    if (q + 1 < ns) {
+                        if (mode[1] != 1) {
+                            const uint32_t c = chains[kZBlockSeq + q];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                        if (mode[2] != 1) {
+                            const uint32_t c = chains[2 * kZBlockSeq + q];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                        if (mode[0] != 1) {
+                            const uint32_t c = chains[q];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                    }
+                    ob.put(x.ll - kLLBase[llc], kLLBits[llc]);
+                    ob.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
+                    ob.put(x.ofv - (1u << ofc), ofc);
+                }
+                ob.done();
+                if (tid == kZThreads - 1) {  // the final states (ML, OF, LL) and the end mark
+                    OrBits fb;
+                    fb.init(A, off0 + T);
+                    if (mode[2] != 1) fb.put(ctl.seq_last[2], (uint32_t)(mode[2] == 2 ? fse[2].log : pre[2].log));
+                    if (mode[1] != 1) fb.put(ctl.seq_last[1], (uint32_t)(mode[1] == 2 ? fse[1].log : pre[1].log));
+                    if (mode[0] != 1) fb.put(ctl.seq_last[0], (uint32_t)(mode[0] == 2 ? fse[0].log : pre[0].log));
+                    fb.put(1, 1);
+                    fb.done();
+                }
+            }
+            if (tid == 0) {
+                ctl.seq_ok = ok;
+                ctl.seq_size = body;
+            }
+        }
         __syncthreads();
         if (!ctl.seq_ok) {  // raw block
             const uint8_t* const sb = reinterpret_cast<const uint8_t*>(stage) + r + hist;
@@ -1372,6 +1513,8 @@ struct ZScratch {
     size_t seqs_cap = 0;
     Coded* coded = nullptr;
     size_t coded_cap = 0;
+    uint32_t* chains = nullptr;
+    size_t chains_cap = 0;
 };
 ZScratch& zscratch() {
     static ZScratch* z = new ZScratch;  // never destroyed (HIP may be torn down first at exit)
@@ -1402,13 +1545,14 @@ extern "C" void pbs_blob_encode_release(void) {
     std::lock_guard<std::mutex> lk(z.mu);
     if (z.dev >= 0) {
         DeviceGuard dg(z.dev);
-        for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.coded})
+        for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.coded, (void*)z.chains})
             if (p) (void)hipFree(p);
     }
     z.slots = nullptr;
     z.seqs = nullptr;
     z.coded = nullptr;
-    z.slots_cap = z.seqs_cap = z.coded_cap = 0;
+    z.chains = nullptr;
+    z.slots_cap = z.seqs_cap = z.coded_cap = z.chains_cap = 0;
     z.dev = -1;
 }
 
@@ -1486,18 +1630,20 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
         if (zs.dev != dev) {  // first use, or another device: free the old scratch there
             if (zs.dev >= 0) {
                 DeviceGuard og(zs.dev);
-                for (void* p : {(void*)zs.slots, (void*)zs.seqs, (void*)zs.coded})
+                for (void* p : {(void*)zs.slots, (void*)zs.seqs, (void*)zs.coded, (void*)zs.chains})
                     if (p) (void)hipFree(p);
             }
             zs.slots = nullptr;
             zs.seqs = nullptr;
             zs.coded = nullptr;
-            zs.slots_cap = zs.seqs_cap = zs.coded_cap = 0;
+            zs.chains = nullptr;
+            zs.slots_cap = zs.seqs_cap = zs.coded_cap = zs.chains_cap = 0;
             zs.dev = dev;
         }
         if (!grow(&zs.slots, &zs.slots_cap, ni * kSlot) ||
             !grow(&zs.seqs, &zs.seqs_cap, (size_t)grid * kZBlockSeq) ||
-            !grow(&zs.coded, &zs.coded_cap, (size_t)grid * kZBlockSeq))
+            !grow(&zs.coded, &zs.coded_cap, (size_t)grid * kZBlockSeq) ||
+            !grow(&zs.chains, &zs.chains_cap, (size_t)grid * 3 * kZBlockSeq))
             fail(PBS_ERR_NOMEM);
     }
     if (rc == PBS_OK)
@@ -1510,7 +1656,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
         ok(hipEventRecord(ev[0], st));
         if (compress)
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
-                               ni, zs.slots, d_sizes, zs.seqs, zs.coded);
+                               ni, zs.slots, d_sizes, zs.seqs, zs.coded, zs.chains);
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
         ok(hipGetLastError()) && ok(exclusive_sum_u64(d_tmp, &tmpb, d_bsz, d_boff,

@@ -2,15 +2,16 @@
 // chunker.rs:112-168, called by ChunkStream on every read, chunk_stream.rs:40-77).
 //
 // ONE persistent workgroup polls the mailbox (pbs_chunker_internal.h) in fine-grained
-// pinned host memory with 16-byte loads {seq, len | quit, base} -- by default lane 0 of
-// every wave, staggered, so several PCIe reads are in flight (kSrvPollAll).  A request
+// pinned host memory with 16-byte loads {seq, len | quit, base} (kSrvPollAll: lane 0 of
+// every wave, staggered -- measured no faster, off by default).  A request
 // then costs one more PCIe round trip: the slot's history and data (host memory) are
 // staged in LDS, 32 KiB per pass, all loads in flight at once.  The cut test runs at
-// every position, one wave per 128-byte block (exact_block.h: the window hash as a
-// difference of prefix XORs -- one dword, 4 lookups and a DPP scan per lane instead of a
-// 192-step chain per lane; the reference's recurrence, chunker.rs:118-165, test :185).
+// every position, each of the 256 threads over S = 32, 64 or 128 bytes (the shortest
+// that covers the pass: an 8 KiB read is 64 + 32 steps per lane; the reference's
+// recurrence, chunker.rs:118-165, test :185).
 // The hits are compacted in stream order into the mailbox, and after every wave drained
-// its stores the acknowledgement is stored (system-scope release).  The host applies
+// its stores the acknowledgement -- seq, candidate count and overflow flag in one 8-byte
+// word -- is stored (system-scope release).  The host applies
 // shall_break's min/max rule to the returned candidates.  Exit: the quit flag, or
 // idle_ticks (wall_clock64, 100 MHz) without a request -- the host relaunches it on the
 // next call (pbs_chunker_capi.cpp server_scan), so a process that stops calling leaves
@@ -26,10 +27,35 @@ namespace pbs {
 
 constexpr int kSrvThreads = 256;  // 4 waves, one per SIMD
 constexpr int kSrvPass = 32 * 1024;  // bytes staged per pass
-constexpr int kSrvBlocks = kSrvPass / 128;
-static_assert(kSrvBlocks == kSrvThreads, "one block per thread in the compaction");
+static_assert(kSrvPass == 128 * kSrvThreads, "a pass is at most 128 bytes per thread");
 
 typedef uint32_t srv_u32x4 __attribute__((ext_vector_type(4)));
+
+// hits of the S bytes at sd[B .. B+S) (LDS; sd[B-64 .. B) readable): bit i of word i / 32
+// = the window ending at byte B + i passes the test -- 64 fill steps over the bytes before
+// the segment (the window hash of chunker.rs:118-136), S roll steps (:141-165), the test
+// (:185); one lane per segment, every lane of the workgroup busy
+template <int S>
+__device__ __forceinline__ uint4 lane_hits(const uint8_t* sd, int B, const uint32_t* tab, uint32_t mask,
+                                           uint32_t minimum) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(sd + B - 64);
+    uint32_t d[(64 + S) / 4];
+#pragma unroll
+    for (int k = 0; k < (64 + S) / 4; ++k) d[k] = w[k];
+    uint32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < 64; ++i)
+        h = __builtin_amdgcn_alignbit(h, h, 31) ^ tab[(d[i >> 2] >> (8 * (i & 3))) & 0xffu];
+    uint32_t hw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const uint32_t out = (d[i >> 2] >> (8 * (i & 3))) & 0xffu;
+        const uint32_t in = (d[(i + 64) >> 2] >> (8 * (i & 3))) & 0xffu;
+        h = __builtin_amdgcn_alignbit(h, h, 31) ^ tab[out] ^ tab[in];
+        hw[i >> 5] |= ((h & mask) >= minimum ? 1u : 0u) << (i & 31);
+    }
+    return make_uint4(hw[0], hw[1], hw[2], hw[3]);
+}
 
 __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox* mb,
                                                                   const uint8_t* __restrict__ slot,
@@ -38,7 +64,6 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                                                                   uint64_t idle_ticks, uint32_t flags) {
     __shared__ uint32_t tab[256];
     __shared__ __attribute__((aligned(16))) uint8_t st[kServerHist + kSrvPass + 128];
-    __shared__ uint4 hv[kSrvBlocks];
     __shared__ uint32_t wsum[kSrvThreads / 64];
     __shared__ uint32_t s_go;    // 0 polling, 1 serve, 2 exit
     __shared__ uint64_t ctl[2];  // [0] seq | len << 32 [1] base
@@ -122,29 +147,28 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             for (uint32_t i = n16 * 16 + tid; i < nbytes; i += kSrvThreads) st[dst0 + i] = slot[src0 + i];
             __syncthreads();
             if (probe && off == 0) t_staged = wall_clock64();
-            const int nblk = (int)((plen + 127) / 128);
-            // the cut test at every position: block b (128 bytes) by wave b % 4, one wave per
-            // block -- lane l < 48 takes window dword l, 4 lookups, a DPP prefix XOR
-            // (exact_block.h; the reference's own window hash, chunker.rs:141-165, and test :185)
-            for (int b = wave; b < nblk; b += kSrvThreads / 64) {
-                const uint8_t* const wb = st + kServerHist + 128 * b - 64;  // window bytes [B - 64, B + 128)
-                const uint32_t wv = lane < 48 ? *reinterpret_cast<const uint32_t*>(wb + 4 * lane) : 0u;
-                const uint4 h = exact_hits<false>(wv, ~0ull >> 1, 0, 64, tab, mask, minimum, lane);
+            // the cut test at every position: thread t takes the S bytes at t * S (S = 32,
+            // 64 or 128: the shortest that covers the pass with the 256 threads)
+            const uint32_t S = plen <= 32 * kSrvThreads ? 32u : plen <= 64 * kSrvThreads ? 64u : 128u;
+            uint4 h = make_uint4(0, 0, 0, 0);
+            if (tid * S < plen) {
+                const uint8_t* const sd = st + kServerHist;
+                h = S == 32 ? lane_hits<32>(sd, (int)(tid * S), tab, mask, minimum)
+                    : S == 64 ? lane_hits<64>(sd, (int)(tid * S), tab, mask, minimum)
+                              : lane_hits<128>(sd, (int)(tid * S), tab, mask, minimum);
                 uint32_t hw[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {  // reportable positions [lo_ok, plen)
-                    const int p0 = b * 128 + 32 * q;
+                    const int p0 = (int)(tid * S) + 32 * q;
                     const int lo = (int)lo_ok - p0, up = (int)plen - p0;
                     const uint32_t keep_lo = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
                     const uint32_t keep_hi = up >= 32 ? 0xFFFFFFFFu : (up <= 0 ? 0u : (0xFFFFFFFFu >> (32 - up)));
-                    hw[q] &= keep_lo & keep_hi;
+                    hw[q] &= q < (int)(S / 32) ? keep_lo & keep_hi : 0u;
                 }
-                if (lane == 0) hv[b] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                h = make_uint4(hw[0], hw[1], hw[2], hw[3]);
             }
-            __syncthreads();
             if (probe && off == 0) t_hashed = wall_clock64();
-            // stream-order compaction: thread t owns block t
-            const uint4 h = tid < nblk ? hv[tid] : make_uint4(0, 0, 0, 0);
+            // stream-order compaction: thread t owns positions [t S, t S + S)
             const uint32_t c = __builtin_popcount(h.x) + __builtin_popcount(h.y) +
                                __builtin_popcount(h.z) + __builtin_popcount(h.w);
             uint32_t x = c;
@@ -169,7 +193,7 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                 while (m) {
                     const int bit = __builtin_ctz(m);
                     m &= m - 1;
-                    if (o < kServerCand) mb->cand[o] = pos0 + (uint64_t)(tid * 128 + q * 32 + bit);
+                    if (o < kServerCand) mb->cand[o] = pos0 + (uint64_t)(tid * S + q * 32 + bit);
                     ++o;
                 }
             }
@@ -180,8 +204,6 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            mb->ncand = total < kServerCand ? total : kServerCand;
-            mb->status = total > kServerCand ? 1u : 0u;
             if (probe) {
                 mb->probe[0] = t_seen;
                 mb->probe[1] = t_staged;
@@ -189,7 +211,10 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                 mb->probe[3] = wall_clock64();
             }
             s_go = 0;
-            __hip_atomic_store(&mb->ack_seq, (uint64_t)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            // ONE 8-byte store: seq, candidate count, overflow flag (the host reads them together)
+            const uint64_t ack = (uint64_t)seq | (uint64_t)(total < kServerCand ? total : kServerCand) << 32 |
+                                 (total > kServerCand ? 1ull << 63 : 0ull);
+            __hip_atomic_store(&mb->ack_seq, ack, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
         last = seq;
