@@ -169,6 +169,23 @@ __device__ __forceinline__ void copy_global(uint8_t* dst, const uint8_t* src, ui
     for (uint64_t i = head + 16 * nq + t; i < n; i += nt) dst[i] = src[i];
 }
 
+// cnt bytes of an LDS buffer (4-byte aligned) to global dst at any alignment: head bytes
+// up to a 4-aligned dst, then dword stores (each built from two LDS dwords), then the tail
+__device__ __forceinline__ void lds_to_global(uint8_t* dst, const uint32_t* src, uint32_t cnt, uint32_t t,
+                                              uint32_t nt) {
+    const uint8_t* const sb = reinterpret_cast<const uint8_t*>(src);
+    uint32_t head = (uint32_t)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3);
+    if (head > cnt) head = cnt;
+    if (t < head) dst[t] = sb[t];
+    const uint32_t nwd = (cnt - head) >> 2;
+    uint32_t* const dw = reinterpret_cast<uint32_t*>(dst + head);
+    for (uint32_t w = t; w < nwd; w += nt) {
+        const uint32_t o = head + 4 * w;
+        dw[w] = __builtin_amdgcn_alignbyte(src[(o >> 2) + 1], src[o >> 2], o & 3);
+    }
+    for (uint32_t i = head + 4 * nwd + t; i < cnt; i += nt) dst[i] = sb[i];
+}
+
 // ---------------------------------------------------------------- bit writers
 // Backward bit stream of RFC 8878 4.1 as an encoder writes it (fields at increasing bit
 // positions, bytes little-endian), one lane, to global memory.
@@ -546,32 +563,66 @@ __device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scra
     return true;
 }
 
-// One FSE state chain of the sequences bit stream (one lane): the state is initialised
-// from the last sequence's code and then encodes sequences ns-2 .. 0; chain[q] = the bits
-// it emits for sequence q (value | count << 16), *last = the final state (flushed after
-// sequence 0).  `shift` picks the code byte (0 LL, 8 ML, 16 OF).
-__device__ __noinline__ void seq_chain(FseView t, const Coded* __restrict__ coded, uint32_t ns, uint32_t shift,
-                                       uint32_t* __restrict__ chain, uint32_t* last) {
-    uint32_t v = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
-    uint32_t q = ns - 1;
-    while (q > 0) {
-        // the next 8 codes' loads in flight together
-        uint32_t c8[8];
-        const uint32_t nq = q < 8 ? q : 8;
+// One FSE state chain of the sequences bit stream, by ONE WAVE: the state is initialised
+// from the last sequence's code and then encodes sequences ns-2 .. 0 (steps j = 0 .. m-1,
+// sequence ns-2-j); chain[q] = the bits it emits for sequence q (value | count << 16),
+// *last = the final state (flushed after sequence 0).  `shift` picks the code byte (0 LL,
+// 8 ML, 16 OF).  The chain is serial, but tANS states forget their past quickly (every
+// encode maps many states to one), so lane l runs steps [l seg, (l+1) seg) from a guessed
+// state, recording the state before each step; then, in rounds, a lane whose start state
+// differs from its left neighbour's end re-runs from that end until its state meets the
+// recorded one (the rest of its record is then already right).  Lane 0 starts from the
+// true state, so after r rounds lanes 0..r are exact; usually one round settles all.
+__device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__ coded, uint32_t ns,
+                                            uint32_t shift, uint32_t* __restrict__ chain,
+                                            uint16_t* __restrict__ states, uint32_t* last, int lane) {
+    const uint32_t m = ns - 1;
+    const uint32_t seg = (m + 63) / 64;
+    const uint32_t a = min(m, (uint32_t)lane * seg), b = min(m, a + seg);
+    const uint32_t x0 = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
+    auto run = [&](uint32_t x, bool stop_on_meet) -> uint32_t {  // returns the end state, ~0u: met
+        for (uint32_t j = a; j < b;) {
+            uint32_t c8[8];
+            const uint32_t nj = min(8u, b - j);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if ((uint32_t)u < nq) c8[u] = (coded[q - 1 - u].codes >> shift) & 0xFF;
+            for (int u = 0; u < 8; ++u)
+                if ((uint32_t)u < nj) c8[u] = (coded[ns - 2 - (j + u)].codes >> shift) & 0xFF;
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if ((uint32_t)u < nq) {
-                const uint32_t sym = c8[u];
-                const uint32_t nb = (v + (uint32_t)t.dnb[sym]) >> 16;
-                chain[q - 1 - u] = (v & ((1u << nb) - 1u)) | nb << 16;
-                v = t.next[(v >> nb) + t.dfs[sym]];
-            }
-        q -= nq;
+            for (int u = 0; u < 8; ++u)
+                if ((uint32_t)u < nj) {
+                    if (stop_on_meet && states[j + u] == x) return ~0u;
+                    states[j + u] = (uint16_t)x;
+                    const uint32_t sym = c8[u];
+                    const uint32_t nb = (x + (uint32_t)t.dnb[sym]) >> 16;
+                    chain[ns - 2 - (j + u)] = (x & ((1u << nb) - 1u)) | nb << 16;
+                    x = t.next[(x >> nb) + t.dfs[sym]];
+                }
+            j += nj;
+        }
+        return x;
+    };
+    // pass 1: lane 0 from the true state, the others from the table's first state
+    uint32_t start = lane == 0 ? x0 : (1u << t.log);
+    uint32_t end = run(start, false);
+    for (int round = 0; round < 64; ++round) {
+        // the true start of lane l is lane l-1's end (lane 0: x0)
+        const uint32_t left = (uint32_t)__shfl_up((int)end, 1, 64);
+        const uint32_t want = lane == 0 ? x0 : left;
+        const bool redo = want != start && a < b;
+        if (!__ballot(redo)) break;
+        if (redo) {
+            start = want;
+            const uint32_t e = run(start, true);
+            if (e != ~0u) end = e;  // never met: the whole segment changed, so does its end
+        } else if (a >= b) {
+            end = want;  // an empty segment passes its start through
+            start = want;
+        }
     }
-    *last = v;
+    // the final state: the end of the last non-empty segment
+    const uint32_t lastlane = m ? (m - 1) / seg : 0;
+    const uint32_t fin = (uint32_t)__shfl((int)end, (int)lastlane, 64);
+    if (lane == 0) *last = m ? fin : x0;
 }
 
 // bits of sequence q in the stream: its three state fields (none for the last sequence,
@@ -637,22 +688,475 @@ __device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) 
         ctl.root = nn - 1;
 }
 
+// The parse of one 8 KiB sub-block by ONE WAVE (wave w: window positions [s0, se)):
+// history rounds, then the rounds + greedy walk; the sequences go to wseq (block
+// positions), their count to *ns_out, the end of the last match to *lastend_out.
+__device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ tabs, Seq* __restrict__ wseq_all,
+                                            uint32_t hist, uint32_t N, int wave, int lane, uint32_t* ns_out,
+                                            uint32_t* lastend_out) {
+    const uint32_t s0 = hist + (uint32_t)wave * kZSub;
+    uint32_t ns = 0, lastend = 0;
+    Seq* const wseq = wseq_all + (uint64_t)wave * kZSubSeq;
+    if (s0 < N) {
+        const uint32_t se = min(s0 + kZSub, N);
+        const uint32_t wlo = s0 - min(s0, kZHist);
+        uint16_t* const tw = tabs + wave * kZTab;
+#pragma unroll
+        for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<uint32_t*>(tw)[lane + 64 * i] = 0;
+        // history: accelerated rounds over [wlo, s0)
+        for (uint32_t r0 = wlo, rn, hs = 1; r0 < s0; r0 = rn) {
+            rn = r0 + kZRound * hs;
+            uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
+            bool ok[kZPer];
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
+                ok[i] = p < s0 && p + 5 <= N;
+                const uint32_t pc = ok[i] ? p : wlo;
+                wp[i] = W.word(pc);
+                b4[i] = W.byte(pc + 4);
+                h[i] = hash5(wp[i], b4[i]);
+                t[i] = tw[h[i]];
+            }
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
+                if (ok[i]) tab_max(&tw[h[i]], p - wlo + 1);
+            }
+            bool hit = false;
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
+                const uint32_t c = ok[i] && t[i] ? wlo + t[i] - 1 : wlo;
+                const uint32_t b = W.byte(ok[i] ? p : wlo);
+                const bool run = wp[i] == b * 0x01010101u && b4[i] == b;
+                hit |= ok[i] && t[i] && !run && W.word(c) == wp[i] && W.byte(c + 4) == b4[i];
+            }
+            hs = __ballot(hit) ? 1 : min(2 * hs, kZMaxStep);
+        }
+        // rounds + walk
+        uint32_t cur = s0, step = 1, lstep = 0, rep = 0;
+        for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
+            rn = r0 + kZRound * step;
+            uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
+                const bool ok = p < se && p + 5 <= N;
+                const uint32_t pc = ok ? p : s0;
+                wp[i] = W.word(pc);
+                b4[i] = W.byte(pc + 4);
+                h[i] = hash5(wp[i], b4[i]);
+                t[i] = ok ? (uint32_t)tw[h[i]] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
+                if (p < se && p + 5 <= N) tab_max(&tw[h[i]], p - wlo + 1);
+            }
+            uint32_t Lm[kZPer], Cm[kZPer];
+            unsigned long long m[kZPer];
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
+                const bool live = p >= cur && p + 5 <= se;
+                const uint32_t c = t[i] ? wlo + t[i] - 1 : s0;
+                const bool rl = live && p > wlo;
+                const uint32_t pm = rl ? p - 1 : s0;  // the run candidate (clamped when unused)
+                const bool mt = live && t[i] && W.word(c) == wp[i] && W.byte(c + 4) == b4[i];
+                const bool mr = rl && W.word(pm) == wp[i] && W.byte(pm + 4) == b4[i];
+                uint32_t L = 0, C = c;
+                if (mt || mr) {  // rare: lengths to the cap (within the sub-block)
+                    const uint32_t lim = min(se - p, kZCap);
+                    const uint32_t Lt = mt ? 5 + win_prefix(W, c + 5, p + 5, lim - 5) : 0;
+                    const uint32_t Lr = mr ? 5 + win_prefix(W, p + 4, p + 5, lim - 5) : 0;
+                    L = Lt;
+                    if (Lr > Lt) {
+                        L = Lr;
+                        C = p - 1;
+                    }
+                }
+                Lm[i] = L;
+                Cm[i] = C;
+                m[i] = __ballot(L != 0);
+            }
+            // the greedy walk (wave-uniform); bit q = position r0 + q * step
+            bool found = false;
+            uint32_t q = cur > r0 ? (cur - r0 + step - 1) >> lstep : 0;
+            for (;;) {
+                uint32_t wi = q >> 6;
+                unsigned long long mm = 0;
+                for (; wi < (uint32_t)kZPer; ++wi) {
+                    mm = (wi == 0 ? m[0] : wi == 1 ? m[1] : wi == 2 ? m[2] : m[3]) &
+                         (wi == (q >> 6) ? (~0ull << (q & 63)) : ~0ull);
+                    if (mm) break;
+                }
+                const bool have = q < kZRound && mm != 0;
+                const int l = have ? __builtin_ctzll(mm) : 0;
+                const uint32_t ph = have ? r0 + (wi * 64 + (uint32_t)l) * step : min(rn, se);
+                uint32_t mpos = 0, msrc = 0, mlen = 0;
+                bool take = false;
+                if (rep && cur < ph) {  // a repeat match in [cur, min(ph, cur + 64))
+                    const uint32_t hi = min(ph, cur + 64);
+                    const uint32_t x = cur + (uint32_t)lane;
+                    const bool okx = x < hi && x >= wlo + rep && x + 5 <= se;
+                    const uint32_t xc = okx ? x : wlo + rep;
+                    const bool eq = okx && W.word(xc) == W.word(xc - rep) && W.byte(xc + 4) == W.byte(xc - rep + 4);
+                    const unsigned long long bal = __ballot(eq);
+                    if (bal) {
+                        mpos = cur + (uint32_t)__builtin_ctzll(bal);
+                        msrc = mpos - rep;
+                        mlen = 5;
+                        take = true;
+                    }
+                }
+                if (!take) {
+                    if (!have) break;
+                    const uint32_t Lw = wi == 0 ? Lm[0] : wi == 1 ? Lm[1] : wi == 2 ? Lm[2] : Lm[3];
+                    const uint32_t Cw = wi == 0 ? Cm[0] : wi == 1 ? Cm[1] : wi == 2 ? Cm[2] : Cm[3];
+                    mpos = ph;
+                    mlen = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
+                    msrc = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
+                    // catch-up over the literals before it: lane k checks byte k back
+                    const uint32_t kk = (uint32_t)lane;
+                    const bool okb = mpos > cur + kk && msrc > wlo + kk;
+                    const bool eqb = okb && W.byte(okb ? mpos - 1 - kk : s0) == W.byte(okb ? msrc - 1 - kk : s0);
+                    const unsigned long long bb = __ballot(eqb);
+                    const uint32_t e = ~bb ? (uint32_t)__builtin_ctzll(~bb) : 64u;
+                    mpos -= e;
+                    msrc -= e;
+                    mlen += e;
+                }
+                // forwards to the end (within the sub-block): 4 bytes per lane a step
+                for (;;) {
+                    const uint32_t x = mpos + mlen + 4 * (uint32_t)lane;
+                    uint32_t mis = 4;  // first mismatching byte of my 4 (4: none)
+                    if (x + 4 <= se) {
+                        const uint32_t d = W.word(msrc + mlen + 4 * (uint32_t)lane) ^ W.word(x);
+                        if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
+                    } else {
+                        mis = 0;
+                        while (x + mis < se && W.byte(msrc + mlen + 4 * (uint32_t)lane + mis) == W.byte(x + mis))
+                            ++mis;
+                    }
+                    const unsigned long long bad = __ballot(mis < 4);
+                    if (bad) {
+                        const int f = __builtin_ctzll(bad);
+                        mlen += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
+                        break;
+                    }
+                    mlen += 256;
+                }
+                if (lane == 0 && ns < kZSubSeq) wseq[ns] = Seq{mpos - hist, mlen, mpos - msrc};
+                ++ns;
+                rep = mpos - msrc;
+                cur = mpos + mlen;
+                lastend = cur - hist;
+                found = true;
+                q = (cur - r0 + step - 1) >> lstep;
+            }
+            step = found ? 1 : min(2 * step, kZMaxStep);
+            lstep = 31 - __builtin_clz(step);
+        }
+    }
+    *ns_out = ns;
+    *lastend_out = lastend;
+}
+
+// Literal section mode of a block (ONE WAVE): RLE (one distinct byte), raw, or Huffman
+// when the entropy estimate says it may pay -- then the code lengths (two-queue merge,
+// limited to 11 bits), canonical codes and the tree description.  ctl.lit_mode = lane 0's.
+__device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& fsc, uint32_t nlit, int lane) {
+    uint32_t c4[4], dist = 0, lastsym = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        c4[i] = E.hist[lane + 64 * i];
+        const unsigned long long b = __ballot(c4[i] != 0);
+        dist += (uint32_t)__builtin_popcountll(b);
+        if (b) lastsym = 64 * i + 63 - (uint32_t)__builtin_clzll(b);
+    }
+    // 0 raw, 1 RLE, 2 Huffman (if its exact size wins below)
+    uint32_t mode = 0;
+    if (nlit > 0 && dist == 1) {
+        mode = 1;
+    } else if (nlit >= 32) {
+        uint64_t est = 0;
+        const uint32_t ln = lg256(nlit);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (c4[i]) est += (uint64_t)c4[i] * (ln - lg256(c4[i]));
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) est += __shfl_xor(est, d, 64);
+        if (est / 2048 + 64 < (uint64_t)nlit - nlit / 64) mode = 2;
+    }
+    if (mode == 2) {
+        // symbols sorted by (count, symbol): rank of each key among the present ones
+        uint32_t key[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            key[i] = c4[i] << 8 | (uint32_t)(lane + 64 * i);
+            E.keys[lane + 64 * i] = c4[i] ? key[i] : 0xFFFFFFFFu;
+        }
+        __builtin_amdgcn_wave_barrier();  // one wave: LDS ops run in order; no code motion across
+        uint32_t rk[4] = {0, 0, 0, 0};
+        for (int s2 = 0; s2 < 256; ++s2) {
+            const uint32_t o = E.keys[s2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rk[i] += o < key[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (c4[i]) E.tw[rk[i]] = key[i];  // sorted keys (temporarily in tw)
+        if (lane == 0) huf_merge(E, ctl, dist);
+        __builtin_amdgcn_wave_barrier();
+        const int m = (int)dist, root = ctl.root;
+        // depth of each leaf (sorted index i = 4 lane + j: contiguous per lane)
+        int32_t kr = 0;
+        uint32_t L4[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int i = 4 * lane + jj;
+            uint32_t d = 0;
+            if (i < m)
+                for (int nd = i; nd != root; nd = E.par[nd]) ++d;
+            L4[jj] = i < m ? min(d, kHufMax) : 0u;
+            if (i < m) kr += 1 << (kHufMax - L4[jj]);
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) kr += __shfl_xor(kr, d, 64);
+        kr -= 1 << kHufMax;
+        while (kr > 0) {  // lengthen the longest code under the limit, least frequent first
+            uint32_t best = 0;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const uint32_t i = 4 * lane + jj;
+                if ((int)i < m && L4[jj] < kHufMax) best = max(best, L4[jj] << 16 | (0xFFFFu - i));
+            }
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, d, 64));
+            const uint32_t bi = 0xFFFFu - (best & 0xFFFFu), bl = best >> 16;
+            kr -= 1 << (kHufMax - bl - 1);
+            if ((bi >> 2) == (uint32_t)lane) {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    if ((bi & 3) == (uint32_t)jj) ++L4[jj];
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) E.lens[4 * lane + jj] = (uint8_t)L4[jj];
+        if (lane == 0 && kr < 0) {  // shorten: most frequent first, while the deficit allows
+            while (kr < 0)
+                for (int i = m - 1; i >= 0 && kr < 0; --i) {
+                    uint32_t L = E.lens[i];
+                    while (L > 1 && (1 << (kHufMax - L)) <= -kr) {
+                        kr += 1 << (kHufMax - L);
+                        --L;
+                    }
+                    E.lens[i] = (uint8_t)L;
+                }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // per symbol lengths
+#pragma unroll
+        for (int i = 0; i < 4; ++i) E.len[lane + 64 * i] = 0;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int i = 4 * lane + jj;
+            if (i < m) E.len[E.keys[i]] = E.lens[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+        // canonical codes: by (length descending, symbol ascending), increasing
+        uint32_t ls[4], mb = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ls[i] = E.len[lane + 64 * i];
+            mb = max(mb, ls[i]);
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, d, 64));
+        uint32_t start[kHufMax + 2];
+        {
+            uint32_t cntL[kHufMax + 2];
+            for (uint32_t L = 0; L <= kHufMax + 1; ++L) cntL[L] = 0;
+            for (uint32_t L = 1; L <= kHufMax; ++L) {
+                uint32_t c = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) c += (uint32_t)__builtin_popcountll(__ballot(ls[i] == L));
+                cntL[L] = c;
+            }
+            uint32_t prevL = 0, s = 0;
+            for (uint32_t L = mb; L >= 1; --L) {
+                if (!cntL[L]) continue;
+                start[L] = prevL ? (s >> (prevL - L)) : 0u;
+                s = start[L] + cntL[L];
+                prevL = L;
+            }
+        }
+        // rank among the same length by symbol (symbols lane + 64 i): per length, the
+        // ballots of the four symbol groups in order
+        {
+            uint32_t rk[4] = {0, 0, 0, 0};
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            for (uint32_t L = 1; L <= mb; ++L) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int i2 = 0; i2 < 4; ++i2) {
+                    const unsigned long long b = __ballot(ls[i2] == L);
+                    if (ls[i2] == L) rk[i2] = acc + (uint32_t)__builtin_popcountll(b & lt);
+                    acc += (uint32_t)__builtin_popcountll(b);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (ls[i]) E.code[lane + 64 * i] = (uint16_t)(start[ls[i]] + rk[i]);
+        }
+        if (lane == 0 && !huf_describe(E, ctl, fsc, mb, lastsym)) mode = 0;
+    }
+    if (lane == 0) ctl.lit_mode = mode;  // (lane 0's: it may have fallen back to raw)
+}
+
+// The literal section (all threads): Huffman streams ORed into LDS at offsets from the
+// block scan of code lengths and copied out, or raw bytes compacted through LDS, or the
+// RLE byte.  Thread t's literals are the set bits of bm (block positions 128 t ..).
+__device__ __noinline__ void write_literals(EntropyArea& E, const Ctl& ctl, const Win W, uint32_t hist, uint4 bm4,
+                                            uint32_t litbase, uint32_t bbase, uint32_t nlit, uint32_t lm, bool four,
+                                            uint32_t seg, uint8_t* lit_out, int tid) {
+    const uint32_t bmw[4] = {bm4.x, bm4.y, bm4.z, bm4.w};
+    if (lm == 2) {
+        const uint32_t words = kHufStreams / 4 + 4;
+        for (uint32_t i = tid; i < words; i += kZThreads) E.streams[i] = 0;
+        __syncthreads();
+        // stream s starts at byte S_s of the LDS buffer
+        // (scalars, not an array: a dynamically indexed array would live in scratch memory)
+        const uint32_t S0 = 0;
+        const uint32_t S1 = four ? (ctl.segP[1] - ctl.segP[0] + 8) / 8 : (ctl.segP[4] - ctl.segP[0] + 8) / 8;
+        const uint32_t S2 = four ? S1 + (ctl.segP[2] - ctl.segP[1] + 8) / 8 : S1;
+        const uint32_t S3 = four ? S2 + (ctl.segP[3] - ctl.segP[2] + 8) / 8 : S1;
+        const uint32_t S4 = four ? S3 + (ctl.segP[4] - ctl.segP[3] + 8) / 8 : S1;
+        auto Sat = [&](uint32_t g) { return g == 0 ? S0 : g == 1 ? S1 : g == 2 ? S2 : g == 3 ? S3 : S4; };
+        uint32_t idx = litbase, pb = bbase;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1) {
+                const uint32_t sym = W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2));
+                const uint32_t L = E.len[sym], cv = E.code[sym];
+                const uint32_t sg = four ? min(idx / seg, 3u) : 0u;
+                const uint32_t endP = four ? ctl.segP[sg + 1] : ctl.segP[4];
+                const uint32_t o = 8 * Sat(sg) + (endP - pb - L);
+                const uint64_t v = (uint64_t)cv << (o & 31);
+                atomicOr(&E.streams[o >> 5], (uint32_t)v);
+                if ((o & 31) + L > 32) atomicOr(&E.streams[(o >> 5) + 1], (uint32_t)(v >> 32));
+                pb += L;
+                ++idx;
+            }
+        if (tid < (four ? 4 : 1)) {  // end marks
+            const uint32_t bits = ctl.segP[four ? tid + 1 : 4] - ctl.segP[tid];
+            const uint32_t o = 8 * Sat((uint32_t)tid) + bits;
+            atomicOr(&E.streams[o >> 5], 1u << (o & 31));
+        }
+        __syncthreads();
+        const uint32_t hs = ctl.huf_hs, c = ctl.huf_c;
+        const uint32_t dl = ctl.desc_len;
+        uint8_t* const body = lit_out + hs;
+        if (tid == 0) {
+            if (hs == 3) {
+                const uint32_t v = 2u | (four ? 1u : 0u) << 2 | nlit << 4 | c << 14;
+                lit_out[0] = (uint8_t)v;
+                lit_out[1] = (uint8_t)(v >> 8);
+                lit_out[2] = (uint8_t)(v >> 16);
+            } else if (hs == 4) {
+                const uint32_t v = 2u | 2u << 2 | nlit << 4 | c << 18;
+                for (int i = 0; i < 4; ++i) lit_out[i] = (uint8_t)(v >> (8 * i));
+            } else {
+                const uint64_t v = 2u | 3u << 2 | (uint64_t)nlit << 4 | (uint64_t)c << 22;
+                for (int i = 0; i < 5; ++i) lit_out[i] = (uint8_t)(v >> (8 * i));
+            }
+            if (four)
+                for (int s = 0; s < 3; ++s) {
+                    const uint32_t sz = Sat((uint32_t)s + 1) - Sat((uint32_t)s);
+                    body[dl + 2 * s] = (uint8_t)sz;
+                    body[dl + 2 * s + 1] = (uint8_t)(sz >> 8);
+                }
+        }
+        for (uint32_t i = tid; i < dl; i += kZThreads) body[i] = ctl.desc[i];
+        const uint32_t tot = four ? S4 : S1;
+        lds_to_global(body + dl + (four ? 6 : 0), E.streams, tot, (uint32_t)tid, kZThreads);
+    } else {
+        const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+        if (tid == 0) {
+            const uint32_t t = lm;  // 0 raw, 1 RLE
+            if (rawh == 1) {
+                lit_out[0] = (uint8_t)(t | nlit << 3);
+            } else if (rawh == 2) {
+                lit_out[0] = (uint8_t)(t | 1u << 2 | nlit << 4);
+                lit_out[1] = (uint8_t)(nlit >> 4);
+            } else {
+                lit_out[0] = (uint8_t)(t | 3u << 2 | nlit << 4);
+                lit_out[1] = (uint8_t)(nlit >> 4);
+                lit_out[2] = (uint8_t)(nlit >> 12);
+            }
+        }
+        if (lm == 1) {
+            if (tid == 0) {  // the one distinct byte
+                uint32_t s = 0;
+                while (!E.hist[s]) ++s;
+                lit_out[rawh] = (uint8_t)s;
+            }
+        } else {
+            // compacted through LDS (the stream buffer, free here) in pieces of 48 KiB, then
+            // copied out with dword stores: scattered global byte stores cost a line each
+            uint8_t* const lb = reinterpret_cast<uint8_t*>(E.streams);
+            for (uint32_t pb = 0; pb < nlit; pb += kHufStreams) {
+                const uint32_t pe = min(nlit, pb + kHufStreams);
+                uint32_t idx = litbase;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1, ++idx)
+                        if (idx >= pb && idx < pe)
+                            lb[idx - pb] = (uint8_t)W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2));
+                __syncthreads();
+                lds_to_global(lit_out + rawh + pb, E.streams, pe - pb, (uint32_t)tid, kZThreads);
+                __syncthreads();
+            }
+        }
+    }
+}
+
+// PBS_ZSTD_PROBE=1 (diagnostics): workgroup 0, thread 0 adds the wall-clock ticks (100 MHz)
+// of each phase into g_zprobe: 0 stage + RLE, 1 parse, 2 literal bitmap + histogram,
+// 3 literal mode / Huffman code + repeat codes, 4 code histograms + Huffman sizes,
+// 5 sequence tables, 6 state chains + literal size, 7 literal section, 8 sequence bit
+// stream, 9 block end; 10 blocks, 11 sequences, 12 literals.
+__device__ unsigned long long g_zprobe[16];
+#define ZMARK(ph)                                  \
+    do {                                           \
+        if (probe) {                               \
+            const uint64_t t_ = wall_clock64();    \
+            g_zprobe[ph] += t_ - tp;               \
+            tp = t_;                               \
+        }                                          \
+    } while (0)
+
 __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, uint8_t* __restrict__ slots,
     uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch, Coded* __restrict__ coded_scratch,
-    uint32_t* __restrict__ chain_scratch) {
+    uint32_t* __restrict__ chain_scratch, int probe_on) {
     __shared__ uint4 stage[kZStageWords];
     __shared__ __attribute__((aligned(16))) uint8_t work[64 * 1024];
     __shared__ FseT fse[3];  // LL, OF, ML
     __shared__ PreT pre[3];  // the predefined tables, same order
     __shared__ Ctl ctl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool probe = probe_on && blockIdx.x == 0 && tid == 0;
+    uint64_t tp = probe ? wall_clock64() : 0;
     uint16_t* const tabs = reinterpret_cast<uint16_t*>(work);
     EntropyArea& E = *reinterpret_cast<EntropyArea*>(work);
     Seq* const wseq_all = seq_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
     Coded* const coded = coded_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
-    uint32_t* const chains = chain_scratch + (uint64_t)blockIdx.x * 3 * kZBlockSeq;  // per stream, per sequence
+    // per stream, per sequence: the emitted bits, then (as u16) the state before each step
+    uint32_t* const chains = chain_scratch + (uint64_t)blockIdx.x * 6 * kZBlockSeq;
     if (wave == 0 && lane < 3) {  // the predefined tables, once per launch (fse[] as scratch)
         FseT& t = fse[lane];
         if (lane == 0) fse_build(t, kLLNorm, 36, kLLLog);
@@ -669,6 +1173,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
 
     for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
         __syncthreads();  // LDS of the previous item
+        ZMARK(9);
         const uint64_t it = items[k];
         const uint64_t ci = it >> 32, j = (uint32_t)it;
         const uint64_t c0 = bounds[ci], c1 = bounds[ci + 1];
@@ -705,6 +1210,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         }
         if (tid < 2) stage[nw + tid] = make_uint4(0, 0, 0, 0);  // word reads past the end stay defined
         __syncthreads();
+        ZMARK(0);
         const Win W{reinterpret_cast<const uint32_t*>(stage), r};
 
         // ---- RLE block: every byte equal
@@ -729,177 +1235,16 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
 
         // ---- parse: wave w owns the sub-block [s0, se) (window positions)
         {
-            const uint32_t s0 = hist + (uint32_t)wave * kZSub;
             uint32_t ns = 0, lastend = 0;
-            Seq* const wseq = wseq_all + (uint64_t)wave * kZSubSeq;
-            if (s0 < N) {
-                const uint32_t se = min(s0 + kZSub, N);
-                const uint32_t wlo = s0 - min(s0, kZHist);
-                uint16_t* const tw = tabs + wave * kZTab;
-#pragma unroll
-                for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<uint32_t*>(tw)[lane + 64 * i] = 0;
-                // history: accelerated rounds over [wlo, s0)
-                for (uint32_t r0 = wlo, rn, hs = 1; r0 < s0; r0 = rn) {
-                    rn = r0 + kZRound * hs;
-                    uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
-                    bool ok[kZPer];
-#pragma unroll
-                    for (int i = 0; i < kZPer; ++i) {
-                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
-                        ok[i] = p < s0 && p + 5 <= N;
-                        const uint32_t pc = ok[i] ? p : wlo;
-                        wp[i] = W.word(pc);
-                        b4[i] = W.byte(pc + 4);
-                        h[i] = hash5(wp[i], b4[i]);
-                        t[i] = tw[h[i]];
-                    }
-#pragma unroll
-                    for (int i = 0; i < kZPer; ++i) {
-                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
-                        if (ok[i]) tab_max(&tw[h[i]], p - wlo + 1);
-                    }
-                    bool hit = false;
-#pragma unroll
-                    for (int i = 0; i < kZPer; ++i) {
-                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
-                        const uint32_t c = ok[i] && t[i] ? wlo + t[i] - 1 : wlo;
-                        const uint32_t b = W.byte(ok[i] ? p : wlo);
-                        const bool run = wp[i] == b * 0x01010101u && b4[i] == b;
-                        hit |= ok[i] && t[i] && !run && W.word(c) == wp[i] && W.byte(c + 4) == b4[i];
-                    }
-                    hs = __ballot(hit) ? 1 : min(2 * hs, kZMaxStep);
-                }
-                // rounds + walk
-                uint32_t cur = s0, step = 1, rep = 0;
-                for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
-                    rn = r0 + kZRound * step;
-                    uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
-#pragma unroll
-                    for (int i = 0; i < kZPer; ++i) {
-                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
-                        const bool ok = p < se && p + 5 <= N;
-                        const uint32_t pc = ok ? p : s0;
-                        wp[i] = W.word(pc);
-                        b4[i] = W.byte(pc + 4);
-                        h[i] = hash5(wp[i], b4[i]);
-                        t[i] = ok ? (uint32_t)tw[h[i]] : 0u;
-                    }
-#pragma unroll
-                    for (int i = 0; i < kZPer; ++i) {
-                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
-                        if (p < se && p + 5 <= N) tab_max(&tw[h[i]], p - wlo + 1);
-                    }
-                    uint32_t Lm[kZPer], Cm[kZPer];
-                    unsigned long long m[kZPer];
-#pragma unroll
-                    for (int i = 0; i < kZPer; ++i) {
-                        const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
-                        const bool live = p >= cur && p + 5 <= se;
-                        const uint32_t c = t[i] ? wlo + t[i] - 1 : s0;
-                        const bool rl = live && p > wlo;
-                        const uint32_t pm = rl ? p - 1 : s0;  // the run candidate (clamped when unused)
-                        const bool mt = live && t[i] && W.word(c) == wp[i] && W.byte(c + 4) == b4[i];
-                        const bool mr = rl && W.word(pm) == wp[i] && W.byte(pm + 4) == b4[i];
-                        uint32_t L = 0, C = c;
-                        if (mt || mr) {  // rare: lengths to the cap (within the sub-block)
-                            const uint32_t lim = min(se - p, kZCap);
-                            const uint32_t Lt = mt ? 5 + win_prefix(W, c + 5, p + 5, lim - 5) : 0;
-                            const uint32_t Lr = mr ? 5 + win_prefix(W, p + 4, p + 5, lim - 5) : 0;
-                            L = Lt;
-                            if (Lr > Lt) {
-                                L = Lr;
-                                C = p - 1;
-                            }
-                        }
-                        Lm[i] = L;
-                        Cm[i] = C;
-                        m[i] = __ballot(L != 0);
-                    }
-                    // the greedy walk (wave-uniform); bit q = position r0 + q * step
-                    bool found = false;
-                    uint32_t q = cur > r0 ? (cur - r0 + step - 1) / step : 0;
-                    for (;;) {
-                        uint32_t wi = q >> 6;
-                        unsigned long long mm = 0;
-                        for (; wi < (uint32_t)kZPer; ++wi) {
-                            mm = (wi == 0 ? m[0] : wi == 1 ? m[1] : wi == 2 ? m[2] : m[3]) &
-                                 (wi == (q >> 6) ? (~0ull << (q & 63)) : ~0ull);
-                            if (mm) break;
-                        }
-                        const bool have = q < kZRound && mm != 0;
-                        const int l = have ? __builtin_ctzll(mm) : 0;
-                        const uint32_t ph = have ? r0 + (wi * 64 + (uint32_t)l) * step : min(rn, se);
-                        uint32_t mpos = 0, msrc = 0, mlen = 0;
-                        bool take = false;
-                        if (rep && cur < ph) {  // a repeat match in [cur, min(ph, cur + 64))
-                            const uint32_t hi = min(ph, cur + 64);
-                            const uint32_t x = cur + (uint32_t)lane;
-                            const bool okx = x < hi && x >= wlo + rep && x + 5 <= se;
-                            const uint32_t xc = okx ? x : wlo + rep;
-                            const bool eq = okx && W.word(xc) == W.word(xc - rep) && W.byte(xc + 4) == W.byte(xc - rep + 4);
-                            const unsigned long long bal = __ballot(eq);
-                            if (bal) {
-                                mpos = cur + (uint32_t)__builtin_ctzll(bal);
-                                msrc = mpos - rep;
-                                mlen = 5;
-                                take = true;
-                            }
-                        }
-                        if (!take) {
-                            if (!have) break;
-                            const uint32_t Lw = wi == 0 ? Lm[0] : wi == 1 ? Lm[1] : wi == 2 ? Lm[2] : Lm[3];
-                            const uint32_t Cw = wi == 0 ? Cm[0] : wi == 1 ? Cm[1] : wi == 2 ? Cm[2] : Cm[3];
-                            mpos = ph;
-                            mlen = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
-                            msrc = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
-                            // catch-up over the literals before it: lane k checks byte k back
-                            const uint32_t kk = (uint32_t)lane;
-                            const bool okb = mpos > cur + kk && msrc > wlo + kk;
-                            const bool eqb = okb && W.byte(okb ? mpos - 1 - kk : s0) == W.byte(okb ? msrc - 1 - kk : s0);
-                            const unsigned long long bb = __ballot(eqb);
-                            const uint32_t e = ~bb ? (uint32_t)__builtin_ctzll(~bb) : 64u;
-                            mpos -= e;
-                            msrc -= e;
-                            mlen += e;
-                        }
-                        // forwards to the end (within the sub-block): 4 bytes per lane a step
-                        for (;;) {
-                            const uint32_t x = mpos + mlen + 4 * (uint32_t)lane;
-                            uint32_t mis = 4;  // first mismatching byte of my 4 (4: none)
-                            if (x + 4 <= se) {
-                                const uint32_t d = W.word(msrc + mlen + 4 * (uint32_t)lane) ^ W.word(x);
-                                if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
-                            } else {
-                                mis = 0;
-                                while (x + mis < se && W.byte(msrc + mlen + 4 * (uint32_t)lane + mis) == W.byte(x + mis))
-                                    ++mis;
-                            }
-                            const unsigned long long bad = __ballot(mis < 4);
-                            if (bad) {
-                                const int f = __builtin_ctzll(bad);
-                                mlen += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
-                                break;
-                            }
-                            mlen += 256;
-                        }
-                        if (lane == 0 && ns < kZSubSeq) wseq[ns] = Seq{mpos - hist, mlen, mpos - msrc};
-                        ++ns;
-                        rep = mpos - msrc;
-                        cur = mpos + mlen;
-                        lastend = cur - hist;
-                        found = true;
-                        q = (cur - r0 + step - 1) / step;
-                    }
-                    step = found ? 1 : min(2 * step, kZMaxStep);
-                }
-            }
+            parse_subblock(W, tabs, wseq_all, hist, N, wave, lane, &ns, &lastend);
             if (lane == 0) {
                 ctl.nseq[wave] = ns;
                 ctl.lastend[wave] = lastend;
             }
-            __threadfence();  // the sequence list (global) before the other waves read it
+            __threadfence_block();  // the sequence list (global) before the other waves read it (workgroup scope: an agent-scope fence writes back L2)
         }
         __syncthreads();
+        ZMARK(1);
 
         // ---- literals: bitmap of the unmatched bytes, literal index per thread range
         for (uint32_t i = tid; i < kEncBlock / 32; i += kZThreads) {
@@ -952,156 +1297,11 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             E.hist[tid] = c;
         }
         __syncthreads();
+        ZMARK(2);
 
         // ---- literal mode (wave 0) and repeat-offset coding (wave 1, one lane per sub-block)
         if (wave == 0) {
-            uint32_t c4[4], dist = 0, lastsym = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                c4[i] = E.hist[lane + 64 * i];
-                const unsigned long long b = __ballot(c4[i] != 0);
-                dist += (uint32_t)__builtin_popcountll(b);
-                if (b) lastsym = 64 * i + 63 - (uint32_t)__builtin_clzll(b);
-            }
-            // 0 raw, 1 RLE, 2 Huffman (if its exact size wins below)
-            uint32_t mode = 0;
-            if (nlit > 0 && dist == 1) {
-                mode = 1;
-            } else if (nlit >= 32) {
-                uint64_t est = 0;
-                const uint32_t ln = lg256(nlit);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (c4[i]) est += (uint64_t)c4[i] * (ln - lg256(c4[i]));
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) est += __shfl_xor(est, d, 64);
-                if (est / 2048 + 64 < (uint64_t)nlit - nlit / 64) mode = 2;
-            }
-            if (mode == 2) {
-                // symbols sorted by (count, symbol): rank of each key among the present ones
-                uint32_t key[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    key[i] = c4[i] << 8 | (uint32_t)(lane + 64 * i);
-                    E.keys[lane + 64 * i] = c4[i] ? key[i] : 0xFFFFFFFFu;
-                }
-                __builtin_amdgcn_wave_barrier();  // one wave: LDS ops run in order; no code motion across
-                uint32_t rk[4] = {0, 0, 0, 0};
-                for (int s2 = 0; s2 < 256; ++s2) {
-                    const uint32_t o = E.keys[s2];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) rk[i] += o < key[i];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (c4[i]) E.tw[rk[i]] = key[i];  // sorted keys (temporarily in tw)
-                if (lane == 0) huf_merge(E, ctl, dist);
-                __builtin_amdgcn_wave_barrier();
-                const int m = (int)dist, root = ctl.root;
-                // depth of each leaf (sorted index i = 4 lane + j: contiguous per lane)
-                int32_t kr = 0;
-                uint32_t L4[4];
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const int i = 4 * lane + jj;
-                    uint32_t d = 0;
-                    if (i < m)
-                        for (int nd = i; nd != root; nd = E.par[nd]) ++d;
-                    L4[jj] = i < m ? min(d, kHufMax) : 0u;
-                    if (i < m) kr += 1 << (kHufMax - L4[jj]);
-                }
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) kr += __shfl_xor(kr, d, 64);
-                kr -= 1 << kHufMax;
-                while (kr > 0) {  // lengthen the longest code under the limit, least frequent first
-                    uint32_t best = 0;
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const uint32_t i = 4 * lane + jj;
-                        if ((int)i < m && L4[jj] < kHufMax) best = max(best, L4[jj] << 16 | (0xFFFFu - i));
-                    }
-#pragma unroll
-                    for (int d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, d, 64));
-                    const uint32_t bi = 0xFFFFu - (best & 0xFFFFu), bl = best >> 16;
-                    kr -= 1 << (kHufMax - bl - 1);
-                    if ((bi >> 2) == (uint32_t)lane) {
-#pragma unroll
-                        for (int jj = 0; jj < 4; ++jj)
-                            if ((bi & 3) == (uint32_t)jj) ++L4[jj];
-                    }
-                }
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) E.lens[4 * lane + jj] = (uint8_t)L4[jj];
-                if (lane == 0 && kr < 0) {  // shorten: most frequent first, while the deficit allows
-                    while (kr < 0)
-                        for (int i = m - 1; i >= 0 && kr < 0; --i) {
-                            uint32_t L = E.lens[i];
-                            while (L > 1 && (1 << (kHufMax - L)) <= -kr) {
-                                kr += 1 << (kHufMax - L);
-                                --L;
-                            }
-                            E.lens[i] = (uint8_t)L;
-                        }
-                }
-                __builtin_amdgcn_wave_barrier();
-                // per symbol lengths
-#pragma unroll
-                for (int i = 0; i < 4; ++i) E.len[lane + 64 * i] = 0;
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const int i = 4 * lane + jj;
-                    if (i < m) E.len[E.keys[i]] = E.lens[i];
-                }
-                __builtin_amdgcn_wave_barrier();
-                // canonical codes: by (length descending, symbol ascending), increasing
-                uint32_t ls[4], mb = 0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    ls[i] = E.len[lane + 64 * i];
-                    mb = max(mb, ls[i]);
-                }
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, d, 64));
-                uint32_t start[kHufMax + 2];
-                {
-                    uint32_t cntL[kHufMax + 2];
-                    for (uint32_t L = 0; L <= kHufMax + 1; ++L) cntL[L] = 0;
-                    for (uint32_t L = 1; L <= kHufMax; ++L) {
-                        uint32_t c = 0;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) c += (uint32_t)__builtin_popcountll(__ballot(ls[i] == L));
-                        cntL[L] = c;
-                    }
-                    uint32_t prevL = 0, s = 0;
-                    for (uint32_t L = mb; L >= 1; --L) {
-                        if (!cntL[L]) continue;
-                        start[L] = prevL ? (s >> (prevL - L)) : 0u;
-                        s = start[L] + cntL[L];
-                        prevL = L;
-                    }
-                }
-                // rank among the same length by symbol (symbols lane + 64 i): per length, the
-                // ballots of the four symbol groups in order
-                {
-                    uint32_t rk[4] = {0, 0, 0, 0};
-                    const unsigned long long lt = (1ull << lane) - 1ull;
-                    for (uint32_t L = 1; L <= mb; ++L) {
-                        uint32_t acc = 0;
-#pragma unroll
-                        for (int i2 = 0; i2 < 4; ++i2) {
-                            const unsigned long long b = __ballot(ls[i2] == L);
-                            if (ls[i2] == L) rk[i2] = acc + (uint32_t)__builtin_popcountll(b & lt);
-                            acc += (uint32_t)__builtin_popcountll(b);
-                        }
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (ls[i]) E.code[lane + 64 * i] = (uint16_t)(start[ls[i]] + rk[i]);
-                }
-                if (lane == 0 && !huf_describe(E, ctl, fse[0], mb, lastsym)) mode = 0;
-            }
-            if (lane == 0) ctl.lit_mode = mode;  // (lane 0's: it may have fallen back to raw)
+            literal_mode_wave(E, ctl, fse[0], nlit, lane);
         } else if (wave == 1 && lane < kZWaves) {
             // repeat-offset coding of sub-block `lane` (reps tracked per sub-block)
             const uint32_t w2 = (uint32_t)lane;
@@ -1111,41 +1311,51 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 if (ctl.nseq[v]) lit_end = ctl.lastend[v];
             }
             const Seq* const ws = wseq_all + (uint64_t)w2 * kZSubSeq;
-            uint32_t rp[3] = {0, 0, 0};
             const uint32_t cnt = min(ctl.nseq[w2], kZSubSeq);
-            for (uint32_t q = 0; q < cnt; ++q) {
-                const Seq e = ws[q];
-                Coded c;
-                c.ll = e.pos - lit_end;
-                c.ml = e.ml;
-                const uint32_t o = e.off;
-                const bool ll0 = c.ll == 0;
-                c.ofv = o + 3;
-                if (!ll0 && rp[0] == o) c.ofv = 1;
-                else if (rp[1] && rp[1] == o) c.ofv = ll0 ? 1 : 2;
-                else if (rp[2] && rp[2] == o) c.ofv = ll0 ? 2 : 3;
-                else if (ll0 && rp[0] > 1 && rp[0] - 1 == o) c.ofv = 3;
-                if (c.ofv > 3) {
-                    rp[2] = rp[1];
-                    rp[1] = rp[0];
-                    rp[0] = o;
-                } else {
-                    const uint32_t rc = c.ofv - 1 + (ll0 ? 1u : 0u);
-                    if (rc > 0) {
-                        const uint32_t cu = rc == 3 ? rp[0] - 1 : rp[rc];
-                        if (rc >= 2) rp[2] = rp[1];
-                        rp[1] = rp[0];
-                        rp[0] = cu;
+            // (registers only: a dynamically indexed array would live in scratch memory)
+            uint32_t ra = 0, rb = 0, rc3 = 0;  // repeat offsets 1..3 (0: not set in this sub-block)
+            for (uint32_t q0 = 0; q0 < cnt; q0 += 8) {
+                Seq e8[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)  // 8 loads in flight
+                    if (q0 + u < cnt) e8[u] = ws[q0 + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    if (q0 + u >= cnt) break;
+                    const Seq e = e8[u];
+                    Coded c;
+                    c.ll = e.pos - lit_end;
+                    c.ml = e.ml;
+                    const uint32_t o = e.off;
+                    const bool ll0 = c.ll == 0;
+                    c.ofv = o + 3;
+                    if (!ll0 && ra == o) c.ofv = 1;
+                    else if (rb && rb == o) c.ofv = ll0 ? 1 : 2;
+                    else if (rc3 && rc3 == o) c.ofv = ll0 ? 2 : 3;
+                    else if (ll0 && ra > 1 && ra - 1 == o) c.ofv = 3;
+                    if (c.ofv > 3) {
+                        rc3 = rb;
+                        rb = ra;
+                        ra = o;
+                    } else {
+                        const uint32_t rcode = c.ofv - 1 + (ll0 ? 1u : 0u);
+                        if (rcode > 0) {
+                            const uint32_t cu = rcode == 3 ? ra - 1 : rcode == 1 ? rb : rc3;
+                            if (rcode >= 2) rc3 = rb;
+                            rb = ra;
+                            ra = cu;
+                        }
                     }
+                    c.codes = ll_code(c.ll) | ml_code(c.ml) << 8 | highbit(c.ofv) << 16;
+                    coded[first + q0 + u] = c;
+                    lit_end = e.pos + e.ml;
                 }
-                c.codes = ll_code(c.ll) | ml_code(c.ml) << 8 | highbit(c.ofv) << 16;
-                coded[first + q] = c;
-                lit_end = e.pos + e.ml;
             }
-            __threadfence();
+            __threadfence_block();
         }
         for (uint32_t i = tid; i < 36 + 53 + 32; i += kZThreads) E.shist[i] = 0;
         __syncthreads();
+        ZMARK(3);
         uint32_t nseq = 0;
         for (int w2 = 0; w2 < kZWaves; ++w2) nseq += min(ctl.nseq[w2], kZSubSeq);
         for (uint32_t q = tid; q < nseq; q += kZThreads) {
@@ -1168,6 +1378,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         const bool four = nlit >= 256;
         const uint32_t seg = four ? (nlit + 3) / 4 : nlit;
         __syncthreads();
+        ZMARK(4);
         uint32_t bbase = bincl - bits_t;
         for (int w2 = 0; w2 < wave; ++w2) bbase += ctl.wsum2[w2];
         if (lit_mode == 2) {
@@ -1192,6 +1403,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         }
         // sequence tables: LL on wave 1, OF on wave 2, ML on wave 3 (lane 0 each)
         __syncthreads();
+        ZMARK(5);
         if (lane == 0 && wave >= 1 && wave <= 3 && nseq > 0) {
             if (wave == 1) seq_table(fse[0], E.shist, 36, nseq, kLLNorm, kLLLog, kLLMaxLog);
             if (wave == 2) seq_table(fse[1], E.shist + 36 + 53, 29, nseq, kOFNorm, kOFLog, kOFMaxLog);
@@ -1222,16 +1434,23 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             ctl.lit_size = sz;
         }
         __syncthreads();
+        ZMARK(6);
         const uint32_t lm = ctl.lit_mode, lsz = ctl.lit_size;
         uint8_t* const lit_out = out + 3;
+        if (probe) {
+            g_zprobe[10] += 1;
+            g_zprobe[11] += nseq;
+            g_zprobe[12] += nlit;
+        }
         // ---- sequences: the three FSE state chains (lane 0 of waves 1-3), the section
         // header (count, modes, table descriptions; wave 0 lane 0)
-        if (lane == 0 && wave >= 1 && wave <= 3 && nseq >= 2 && fse[wave - 1].mode != 1) {
+        if (wave >= 1 && wave <= 3 && nseq >= 2 && fse[wave - 1].mode != 1) {
             const int k = wave - 1;  // 0 LL, 1 OF, 2 ML
             const FseView tv = fse[k].mode == 2 ? view(fse[k]) : view(pre[k]);
-            seq_chain(tv, coded, nseq, k == 0 ? 0u : k == 1 ? 16u : 8u, chains + (uint64_t)k * kZBlockSeq,
-                      &ctl.seq_last[k]);
-            __threadfence();
+            seq_chain_wave(tv, coded, nseq, k == 0 ? 0u : k == 1 ? 16u : 8u, chains + (uint64_t)k * kZBlockSeq,
+                           reinterpret_cast<uint16_t*>(chains + 3ull * kZBlockSeq) + (uint64_t)k * kZBlockSeq,
+                           &ctl.seq_last[k], lane);
+            __threadfence_block();
         }
         if (tid == 0) {
             uint8_t* o = lit_out + lsz;
@@ -1261,100 +1480,14 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                         ctl.seq_last[k] = fse_init(tv, (coded[0].codes >> sh) & 0xFF);
                     }
         }
-        // ---- write the literal section (all threads but wave 7 lane 0's sequence encode runs after)
-        if (lm == 2) {
-            const uint32_t words = kHufStreams / 4 + 4;
-            for (uint32_t i = tid; i < words; i += kZThreads) E.streams[i] = 0;
-            __syncthreads();
-            // stream s starts at byte S_s of the LDS buffer
-            uint32_t S[5];
-            S[0] = 0;
-            for (int s = 0; s < 4; ++s) {
-                const uint32_t bits = (four || s == 0) ? ctl.segP[four ? s + 1 : 4] - ctl.segP[s] : 0u;
-                S[s + 1] = S[s] + ((four || s == 0) ? (bits + 8) / 8 : 0u);
-            }
-            uint32_t idx = litbase, pb = bbase;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1) {
-                    const uint32_t sym = W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2));
-                    const uint32_t L = E.len[sym], cv = E.code[sym];
-                    const uint32_t sg = four ? min(idx / seg, 3u) : 0u;
-                    const uint32_t endP = four ? ctl.segP[sg + 1] : ctl.segP[4];
-                    const uint32_t o = 8 * S[sg] + (endP - pb - L);
-                    const uint64_t v = (uint64_t)cv << (o & 31);
-                    atomicOr(&E.streams[o >> 5], (uint32_t)v);
-                    if ((o & 31) + L > 32) atomicOr(&E.streams[(o >> 5) + 1], (uint32_t)(v >> 32));
-                    pb += L;
-                    ++idx;
-                }
-            if (tid < (four ? 4 : 1)) {  // end marks
-                const uint32_t bits = ctl.segP[four ? tid + 1 : 4] - ctl.segP[tid];
-                const uint32_t o = 8 * S[tid] + bits;
-                atomicOr(&E.streams[o >> 5], 1u << (o & 31));
-            }
-            __syncthreads();
-            const uint32_t hs = ctl.huf_hs, c = ctl.huf_c;
-            const uint32_t dl = ctl.desc_len;
-            uint8_t* const body = lit_out + hs;
-            if (tid == 0) {
-                if (hs == 3) {
-                    const uint32_t v = 2u | (four ? 1u : 0u) << 2 | nlit << 4 | c << 14;
-                    lit_out[0] = (uint8_t)v;
-                    lit_out[1] = (uint8_t)(v >> 8);
-                    lit_out[2] = (uint8_t)(v >> 16);
-                } else if (hs == 4) {
-                    const uint32_t v = 2u | 2u << 2 | nlit << 4 | c << 18;
-                    for (int i = 0; i < 4; ++i) lit_out[i] = (uint8_t)(v >> (8 * i));
-                } else {
-                    const uint64_t v = 2u | 3u << 2 | (uint64_t)nlit << 4 | (uint64_t)c << 22;
-                    for (int i = 0; i < 5; ++i) lit_out[i] = (uint8_t)(v >> (8 * i));
-                }
-                if (four)
-                    for (int s = 0; s < 3; ++s) {
-                        const uint32_t sz = S[s + 1] - S[s];
-                        body[dl + 2 * s] = (uint8_t)sz;
-                        body[dl + 2 * s + 1] = (uint8_t)(sz >> 8);
-                    }
-            }
-            for (uint32_t i = tid; i < dl; i += kZThreads) body[i] = ctl.desc[i];
-            const uint32_t tot = four ? S[4] : S[1];
-            uint8_t* const sdst = body + dl + (four ? 6 : 0);
-            const uint8_t* const ssrc = reinterpret_cast<const uint8_t*>(E.streams);
-            for (uint32_t i = tid; i < tot; i += kZThreads) sdst[i] = ssrc[i];
-        } else {
-            const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
-            if (tid == 0) {
-                const uint32_t t = lm;  // 0 raw, 1 RLE
-                if (rawh == 1) {
-                    lit_out[0] = (uint8_t)(t | nlit << 3);
-                } else if (rawh == 2) {
-                    lit_out[0] = (uint8_t)(t | 1u << 2 | nlit << 4);
-                    lit_out[1] = (uint8_t)(nlit >> 4);
-                } else {
-                    lit_out[0] = (uint8_t)(t | 3u << 2 | nlit << 4);
-                    lit_out[1] = (uint8_t)(nlit >> 4);
-                    lit_out[2] = (uint8_t)(nlit >> 12);
-                }
-            }
-            if (lm == 1) {
-                if (tid == 0) {  // the one distinct byte
-                    uint32_t s = 0;
-                    while (!E.hist[s]) ++s;
-                    lit_out[rawh] = (uint8_t)s;
-                }
-            } else {
-                uint32_t idx = litbase;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1)
-                        lit_out[rawh + idx++] = (uint8_t)W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2));
-            }
-        }
+        // ---- the literal section
+        write_literals(E, ctl, W, hist, make_uint4(bmw[0], bmw[1], bmw[2], bmw[3]), litbase, bbase, nlit, lm, four, seg,
+                       lit_out, tid);
         // ---- sequences bit stream: per-sequence bit counts, a block scan, then every
         // thread writes its range of sequences (the last sequence first in the stream) with
         // atomicOr into the zeroed words
         __syncthreads();
+        ZMARK(7);
         {
             const uint32_t ns = nseq, hdr = ctl.seq_hdr;
             const uint32_t mode[3] = {fse[0].mode, fse[1].mode, fse[2].mode};
@@ -1384,7 +1517,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
                 if (tid == 0)
                     for (uint8_t* b = S0; b < reinterpret_cast<uint8_t*>(A + 1); ++b) *b = 0;
                 for (uint32_t wdx = 1 + tid; wdx <= lastw; wdx += kZThreads) A[wdx] = 0;
-                __threadfence();  // the zeros (and the section header) at L2 before any atomicOr
+                __threadfence_block();  // the zeros (and the section header) stored before any atomicOr
                 __syncthreads();
                 OrBits ob;
                 ob.init(A, off0 + (T - pt - st));
@@ -1426,6 +1559,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             }
         }
         __syncthreads();
+        ZMARK(8);
         if (!ctl.seq_ok) {  // raw block
             const uint8_t* const sb = reinterpret_cast<const uint8_t*>(stage) + r + hist;
             for (uint32_t i = tid; i < n; i += kZThreads) out[3 + i] = sb[i];
@@ -1643,7 +1777,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
         if (!grow(&zs.slots, &zs.slots_cap, ni * kSlot) ||
             !grow(&zs.seqs, &zs.seqs_cap, (size_t)grid * kZBlockSeq) ||
             !grow(&zs.coded, &zs.coded_cap, (size_t)grid * kZBlockSeq) ||
-            !grow(&zs.chains, &zs.chains_cap, (size_t)grid * 3 * kZBlockSeq))
+            !grow(&zs.chains, &zs.chains_cap, (size_t)grid * 6 * kZBlockSeq))
             fail(PBS_ERR_NOMEM);
     }
     if (rc == PBS_OK)
@@ -1654,9 +1788,30 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     if (rc == PBS_OK) {
         (void)hipGetLastError();
         ok(hipEventRecord(ev[0], st));
+        static const bool zprobe = [] {
+            const char* e = std::getenv("PBS_ZSTD_PROBE");
+            return e && e[0] == '1';
+        }();
+        if (compress && zprobe) {
+            const unsigned long long z[16] = {};
+            (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
+        }
         if (compress)
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
-                               ni, zs.slots, d_sizes, zs.seqs, zs.coded, zs.chains);
+                               ni, zs.slots, d_sizes, zs.seqs, zs.coded, zs.chains, zprobe ? 1 : 0);
+        if (compress && zprobe) {
+            unsigned long long h[16] = {};
+            (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
+            (void)hipStreamSynchronize(st);
+            const double nb = h[10] ? (double)h[10] : 1.0;
+            std::fprintf(stderr,
+                         "zstd probe (workgroup 0, us per block over %llu blocks, %.0f sequences, %.0f literals per "
+                         "block): stage %.1f parse %.1f litmap %.1f litmode %.1f codehist %.1f tables %.1f chains %.1f "
+                         "literals %.1f seqstream %.1f end %.1f\n",
+                         h[10], h[11] / nb, h[12] / nb, h[0] / nb / 100, h[1] / nb / 100, h[2] / nb / 100,
+                         h[3] / nb / 100, h[4] / nb / 100, h[5] / nb / 100, h[6] / nb / 100, h[7] / nb / 100,
+                         h[8] / nb / 100, h[9] / nb / 100);
+        }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
         ok(hipGetLastError()) && ok(exclusive_sum_u64(d_tmp, &tmpb, d_bsz, d_boff,
