@@ -17,7 +17,9 @@
 //            two-queue Huffman merge limited to 11 bits, weights in the direct 4-bit form
 //            when at most 128 are transmitted else FSE-compressed (two interleaved states,
 //            accuracy <= 6); 1 stream below 256 literals, else 4 streams + jump table;
-//            Huffman only when its estimate beats raw;
+//            Huffman only when its estimate beats raw -- first on the literals at block
+//            positions divisible by 4 (cheap: random literals never build a histogram of
+//            all bytes), then on all of them;
 //   sequences per stream (LL / OF / ML) the cheapest of predefined, RLE and FSE-compressed
 //            (own table, normalised counts), by an integer cost estimate; offsets as
 //            repeat codes when they equal a repeat offset set EARLIER IN THE SAME BLOCK
@@ -560,8 +562,21 @@ void raw_literals(std::vector<uint8_t>& o, const uint8_t* lit, uint32_t n, uint3
         o.push_back(lit[0]);
 }
 
-void literals(std::vector<uint8_t>& o, const std::vector<uint8_t>& lit) {
+// samp = the literal bytes at block positions divisible by 4 (a first, cheap estimate)
+void literals(std::vector<uint8_t>& o, const std::vector<uint8_t>& lit, const std::vector<uint8_t>& samp) {
     const uint32_t n = (uint32_t)lit.size();
+    if (n >= 32 && !samp.empty()) {  // sampled estimate: clearly incompressible literals stay raw
+        uint32_t cs[256] = {0};
+        for (uint8_t c : samp) ++cs[c];
+        const uint32_t m = (uint32_t)samp.size(), lm = lg256(m);
+        uint64_t es = 0;
+        for (int s = 0; s < 256; ++s)
+            if (cs[s]) es += (uint64_t)cs[s] * (lm - lg256(cs[s]));
+        if (es * n / m / 2048 + 64 >= (uint64_t)n - n / 64) {
+            raw_literals(o, lit.data(), n, 0);
+            return;
+        }
+    }
     uint32_t cnt[256] = {0};
     for (uint8_t c : lit) ++cnt[c];
     int distinct = 0;
@@ -845,15 +860,19 @@ size_t block(const uint8_t* src, uint32_t n, uint32_t avail, bool last, uint8_t*
     }
     std::vector<Seq> seqs;
     parse(src, n, avail, seqs);
-    std::vector<uint8_t> lit;
+    std::vector<uint8_t> lit, samp;
     uint32_t at = 0;
+    auto run = [&](uint32_t a, uint32_t e) {
+        lit.insert(lit.end(), src + a, src + e);
+        for (uint32_t p = (a + 3) & ~3u; p < e; p += 4) samp.push_back(src[p]);
+    };
     for (const Seq& e : seqs) {
-        lit.insert(lit.end(), src + at, src + e.pos);
+        run(at, e.pos);
         at = e.pos + e.ml;
     }
-    lit.insert(lit.end(), src + at, src + n);
+    run(at, n);
     std::vector<uint8_t> body;
-    literals(body, lit);
+    literals(body, lit, samp);
     sequences(body, code_sequences(seqs));
     if (body.size() >= n) {
         block_header(out, last, 0, n);

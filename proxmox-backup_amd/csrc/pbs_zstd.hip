@@ -74,6 +74,7 @@ constexpr uint32_t kZBlockSeq = kZWaves * kZSubSeq;
 constexpr uint64_t kSlot = kEncBlock + 1024;  // block header + up to 64 KiB + slack (section headers, flushes)
 constexpr uint32_t kHufStreams = 48 * 1024;  // Huffman streams staged in LDS (longer: raw literals)
 constexpr uint32_t kHufMax = 11;
+constexpr uint32_t kZRuns = 64;  // blocks with fewer sequences copy raw literals run by run
 static_assert(kEncBlock / kZSub == (uint32_t)kZWaves, "one sub-block per wave");
 static_assert(kZTab * 2 * kZWaves == 64 * 1024, "the tables fill the work area");
 
@@ -184,6 +185,19 @@ __device__ __forceinline__ void lds_to_global(uint8_t* dst, const uint32_t* src,
         dw[w] = __builtin_amdgcn_alignbyte(src[(o >> 2) + 1], src[o >> 2], o & 3);
     }
     for (uint32_t i = head + 4 * nwd + t; i < cnt; i += nt) dst[i] = sb[i];
+}
+
+// cnt bytes of the staged window from position `from` to global dst at any alignment: head
+// bytes up to a 4-aligned dst, then dword stores (W.word), then the tail; threads t of nt
+__device__ __forceinline__ void stage_to_global(uint8_t* dst, const Win& W, uint32_t from, uint32_t cnt, uint32_t t,
+                                                uint32_t nt) {
+    uint32_t head = (uint32_t)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3);
+    if (head > cnt) head = cnt;
+    if (t < head) dst[t] = (uint8_t)W.byte(from + t);
+    const uint32_t nwd = (cnt - head) >> 2;
+    uint32_t* const dw = reinterpret_cast<uint32_t*>(dst + head);
+    for (uint32_t w = t; w < nwd; w += nt) dw[w] = W.word(from + head + 4 * w);
+    for (uint32_t i = head + 4 * nwd + t; i < cnt; i += nt) dst[i] = (uint8_t)W.byte(from + i);
 }
 
 // ---------------------------------------------------------------- bit writers
@@ -489,7 +503,8 @@ struct Ctl {
     uint32_t wsum[kZWaves];     // block-scan partials
     uint32_t wsum2[kZWaves];
     uint32_t segP[5];           // Huffman: bits before each segment boundary
-    uint32_t lit_mode, lit_size, huf_c, huf_hs, desc_len;
+    uint32_t lit_mode, lit_size, huf_c, huf_hs, desc_len, need_full;
+    uint32_t run_start[kZRuns], run_len[kZRuns], run_out[kZRuns];  // literal runs of a block with few sequences
     uint32_t seq_size, seq_ok, seq_hdr, seq_last[3];  // sequences: body size, fits, header bytes, final states
     int32_t root;               // Huffman merge: the root node
     uint8_t desc[264];          // Huffman tree description (FSE form: <= ~210 bytes before the 128 check)
@@ -577,6 +592,19 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
                                             uint32_t shift, uint32_t* __restrict__ chain,
                                             uint16_t* __restrict__ states, uint32_t* last, int lane) {
     const uint32_t m = ns - 1;
+    if (m < 128) {  // short: one lane, serially (the rounds would cost more than they save)
+        if (lane == 0) {
+            uint32_t x = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
+            for (uint32_t j = 0; j < m; ++j) {
+                const uint32_t sym = (coded[ns - 2 - j].codes >> shift) & 0xFF;
+                const uint32_t nb = (x + (uint32_t)t.dnb[sym]) >> 16;
+                chain[ns - 2 - j] = (x & ((1u << nb) - 1u)) | nb << 16;
+                x = t.next[(x >> nb) + t.dfs[sym]];
+            }
+            *last = x;
+        }
+        return;
+    }
     const uint32_t seg = (m + 63) / 64;
     const uint32_t a = min(m, (uint32_t)lane * seg), b = min(m, a + seg);
     const uint32_t x0 = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
@@ -693,7 +721,9 @@ __device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) 
 // positions), their count to *ns_out, the end of the last match to *lastend_out.
 __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ tabs, Seq* __restrict__ wseq_all,
                                             uint32_t hist, uint32_t N, int wave, int lane, uint32_t* ns_out,
-                                            uint32_t* lastend_out) {
+                                            uint32_t* lastend_out, unsigned long long* probe) {
+    const uint64_t t_in = probe ? wall_clock64() : 0;
+    uint64_t t_hist = t_in;
     const uint32_t s0 = hist + (uint32_t)wave * kZSub;
     uint32_t ns = 0, lastend = 0;
     Seq* const wseq = wseq_all + (uint64_t)wave * kZSubSeq;
@@ -734,6 +764,7 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
             }
             hs = __ballot(hit) ? 1 : min(2 * hs, kZMaxStep);
         }
+        if (probe) t_hist = wall_clock64();
         // rounds + walk
         uint32_t cur = s0, step = 1, lstep = 0, rep = 0;
         for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
@@ -858,6 +889,10 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
             step = found ? 1 : min(2 * step, kZMaxStep);
             lstep = 31 - __builtin_clz(step);
         }
+    }
+    if (probe && lane == 0 && s0 < N) {  // wave 0 of workgroup 0: history / rounds + walk
+        probe[13] += t_hist - t_in;
+        probe[14] += wall_clock64() - t_hist;
     }
     *ns_out = ns;
     *lastend_out = lastend;
@@ -1021,7 +1056,7 @@ __device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& f
 // RLE byte.  Thread t's literals are the set bits of bm (block positions 128 t ..).
 __device__ __noinline__ void write_literals(EntropyArea& E, const Ctl& ctl, const Win W, uint32_t hist, uint4 bm4,
                                             uint32_t litbase, uint32_t bbase, uint32_t nlit, uint32_t lm, bool four,
-                                            uint32_t seg, uint8_t* lit_out, int tid) {
+                                            uint32_t seg, uint8_t* lit_out, int tid, uint32_t nruns) {
     const uint32_t bmw[4] = {bm4.x, bm4.y, bm4.z, bm4.w};
     if (lm == 2) {
         const uint32_t words = kHufStreams / 4 + 4;
@@ -1103,6 +1138,11 @@ __device__ __noinline__ void write_literals(EntropyArea& E, const Ctl& ctl, cons
                 while (!E.hist[s]) ++s;
                 lit_out[rawh] = (uint8_t)s;
             }
+        } else if (nruns) {
+            // few sequences: run by run, every thread on each run (coalesced dword stores)
+            for (uint32_t r = 0; r < nruns; ++r)
+                stage_to_global(lit_out + rawh + ctl.run_out[r], W, hist + ctl.run_start[r], ctl.run_len[r],
+                                (uint32_t)tid, kZThreads);
         } else {
             // compacted through LDS (the stream buffer, free here) in pieces of 48 KiB, then
             // copied out with dword stores: scattered global byte stores cost a line each
@@ -1236,7 +1276,8 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         // ---- parse: wave w owns the sub-block [s0, se) (window positions)
         {
             uint32_t ns = 0, lastend = 0;
-            parse_subblock(W, tabs, wseq_all, hist, N, wave, lane, &ns, &lastend);
+            parse_subblock(W, tabs, wseq_all, hist, N, wave, lane, &ns, &lastend,
+                           probe_on && blockIdx.x == 0 && wave == 0 ? g_zprobe : nullptr);
             if (lane == 0) {
                 ctl.nseq[wave] = ns;
                 ctl.lastend[wave] = lastend;
@@ -1278,18 +1319,30 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             bmw[i] = E.bitmap[4 * tid + i];
             cnt_t += __builtin_popcount(bmw[i]);
         }
+        // the sampled histogram first: literals at block positions divisible by 4 (one
+        // predicated LDS atomic per 4 positions); the full one only when the sample says
+        // Huffman may pay (random literals never need it)
         uint32_t* const wh = E.streams + wave * 256;
+        uint32_t samp_t = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1)
-                atomicAdd(&wh[W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2))], 1u);
+        for (int k = 0; k < 32; ++k) {
+            if ((bmw[k >> 3] >> ((4 * k) & 31)) & 1u) {
+                atomicAdd(&wh[W.byte(hist + 128 * tid + 4 * k)], 1u);
+                ++samp_t;
+            }
+        }
         const uint32_t incl = wave_incl(cnt_t, lane);
-        if (lane == 63) ctl.wsum[wave] = incl;
+        const uint32_t sincl = wave_incl(samp_t, lane);
+        if (lane == 63) {
+            ctl.wsum[wave] = incl;
+            ctl.wsum2[wave] = sincl;
+        }
         __syncthreads();
-        uint32_t litbase = incl - cnt_t, nlit = 0;
+        uint32_t litbase = incl - cnt_t, nlit = 0, nsamp = 0;
         for (int w2 = 0; w2 < kZWaves; ++w2) {
             litbase += w2 < wave ? ctl.wsum[w2] : 0u;
             nlit += ctl.wsum[w2];
+            nsamp += ctl.wsum2[w2];
         }
         if (tid < 256) {
             uint32_t c = 0;
@@ -1297,11 +1350,46 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             E.hist[tid] = c;
         }
         __syncthreads();
+        if (wave == 0) {  // 1: the full histogram is needed; 0: raw literals
+            uint32_t need = nlit > 0;
+            if (nlit >= 32 && nsamp > 0) {
+                uint64_t es = 0;
+                const uint32_t lm = lg256(nsamp);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t c = E.hist[lane + 64 * i];
+                    if (c) es += (uint64_t)c * (lm - lg256(c));
+                }
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) es += __shfl_xor(es, d, 64);
+                if (es * nlit / nsamp / 2048 + 64 >= (uint64_t)nlit - nlit / 64) need = 0;
+            }
+            if (lane == 0) {
+                ctl.need_full = need;
+                ctl.lit_mode = 0;
+            }
+        }
+        __syncthreads();
+        if (ctl.need_full) {
+            for (uint32_t i = tid; i < kZWaves * 256; i += kZThreads) E.streams[i] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1)
+                    atomicAdd(&wh[W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2))], 1u);
+            __syncthreads();
+            if (tid < 256) {
+                uint32_t c = 0;
+                for (int w2 = 0; w2 < kZWaves; ++w2) c += E.streams[w2 * 256 + tid];
+                E.hist[tid] = c;
+            }
+            __syncthreads();
+        }
         ZMARK(2);
 
         // ---- literal mode (wave 0) and repeat-offset coding (wave 1, one lane per sub-block)
         if (wave == 0) {
-            literal_mode_wave(E, ctl, fse[0], nlit, lane);
+            if (ctl.need_full) literal_mode_wave(E, ctl, fse[0], nlit, lane);
         } else if (wave == 1 && lane < kZWaves) {
             // repeat-offset coding of sub-block `lane` (reps tracked per sub-block)
             const uint32_t w2 = (uint32_t)lane;
@@ -1363,6 +1451,17 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             atomicAdd(&E.shist[cc & 0xFF], 1u);
             atomicAdd(&E.shist[36 + ((cc >> 8) & 0xFF)], 1u);
             atomicAdd(&E.shist[36 + 53 + (cc >> 16)], 1u);
+        }
+        // literal runs (few sequences: the raw literals are copied run by run, coalesced)
+        if (wave == 0 && nseq < kZRuns) {
+            const Coded x = (uint32_t)lane < nseq ? coded[lane] : Coded{0, 0, 0, 0};
+            const uint32_t span = x.ll + x.ml, lit = x.ll;
+            const uint32_t si = wave_incl(span, lane), li = wave_incl(lit, lane);
+            if ((uint32_t)lane <= nseq) {
+                ctl.run_start[lane] = si - span;
+                ctl.run_out[lane] = li - lit;
+                ctl.run_len[lane] = (uint32_t)lane < nseq ? lit : n - (si - span);
+            }
         }
         // ---- Huffman sizes: per-thread code-length sums, block scan, segment totals
         const uint32_t lit_mode = ctl.lit_mode;
@@ -1482,7 +1581,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         }
         // ---- the literal section
         write_literals(E, ctl, W, hist, make_uint4(bmw[0], bmw[1], bmw[2], bmw[3]), litbase, bbase, nlit, lm, four, seg,
-                       lit_out, tid);
+                       lit_out, tid, nseq < kZRuns ? nseq + 1 : 0u);
         // ---- sequences bit stream: per-sequence bit counts, a block scan, then every
         // thread writes its range of sequences (the last sequence first in the stream) with
         // atomicOr into the zeroed words
@@ -1807,10 +1906,10 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
             std::fprintf(stderr,
                          "zstd probe (workgroup 0, us per block over %llu blocks, %.0f sequences, %.0f literals per "
                          "block): stage %.1f parse %.1f litmap %.1f litmode %.1f codehist %.1f tables %.1f chains %.1f "
-                         "literals %.1f seqstream %.1f end %.1f\n",
+                         "literals %.1f seqstream %.1f end %.1f | wave 0: history %.1f rounds+walk %.1f\n",
                          h[10], h[11] / nb, h[12] / nb, h[0] / nb / 100, h[1] / nb / 100, h[2] / nb / 100,
                          h[3] / nb / 100, h[4] / nb / 100, h[5] / nb / 100, h[6] / nb / 100, h[7] / nb / 100,
-                         h[8] / nb / 100, h[9] / nb / 100);
+                         h[8] / nb / 100, h[9] / nb / 100, h[13] / nb / 100, h[14] / nb / 100);
         }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
