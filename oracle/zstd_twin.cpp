@@ -28,7 +28,9 @@
 //
 // Parse (per 64 KiB block; 16 KiB sub-blocks = one GPU wave each, own hash table):
 //   rounds of kRound positions sampled every `step` bytes (step 1 after a round with a
-//   match, doubling to kMaxStep without); per position the candidates are (a) the table
+//   match, doubling to kMaxStep without -- kHistMaxStep in the history before the
+//   sub-block, whose last step the sub-block's first round keeps, up to kMaxStep; a round starts at the end of a match that ran past the previous one, the
+//   positions inside it are not searched); per position the candidates are (a) the table
 //   (1 + the last position of an EARLIER round with the same hash of kHashBytes bytes),
 //   (b) the run candidate p - 1; lengths = common prefix capped at kCap (and the
 //   sub-block end), a candidate counts from kMinMatch bytes; the longer wins (ties: the
@@ -48,7 +50,7 @@ namespace {
 constexpr uint32_t kBlock = 64 * 1024;
 constexpr uint32_t kSub = 8192;     // one GPU wave's sub-block
 constexpr uint32_t kHist = 16384;   // window before a sub-block (reaches into the previous block)
-constexpr uint32_t kRound = 256, kMaxStep = 8;
+constexpr uint32_t kRound = 256, kMaxStep = 8, kHistMaxStep = 32;
 constexpr uint32_t kHashLog = 12, kCap = 32, kMinMatch = 5;
 constexpr uint32_t kHufStreams = 48 * 1024;  // largest Huffman stream bytes of a block
 
@@ -87,8 +89,9 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
         const uint32_t wlo = s0 - std::min(s0, kHist);  // the sub-block's window start
         // history: the window before the sub-block enters the table in rounds like the
         // parse's (lookups before inserts; step 1 after a round in which some position's 5
-        // bytes equal its table or run candidate's, doubling to kMaxStep without)
-        for (uint32_t r0 = wlo, rn, hs = 1; r0 < s0; r0 = rn) {
+        // bytes equal its table or run candidate's, doubling to kHistMaxStep without)
+        uint32_t hs = 1;
+        for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kRound * hs;
             uint32_t pos[kRound], cand[kRound], np = 0;
             for (uint32_t j = 0; j < kRound && r0 + j * hs < s0; ++j) pos[np++] = r0 + j * hs;
@@ -104,12 +107,13 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
                 hit |= !run && cand[k] && std::memcmp(b + cand[k] - 1, b + p, 5) == 0;
             }
             g_hist_inserts += np;
-            hs = hit ? 1 : std::min(hs * 2, kMaxStep);
+            hs = hit ? 1 : std::min(hs * 2, kHistMaxStep);
         }
-        uint32_t cur = s0, step = 1, rep = 0;  // rep 0: no offset in this sub-block yet
+        // the first rounds keep the history's step; rep 0: no offset in this sub-block yet
+        uint32_t cur = s0, step = std::min(hs, kMaxStep), rep = 0;
         for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
             rn = r0 + kRound * step;
-            uint32_t pos[1024], cand[1024], len[1024], np = 0;
+            uint32_t pos[kRound], cand[kRound], len[kRound], np = 0;
             for (uint32_t j = 0; j < kRound && r0 + j * step < se; ++j) pos[np++] = r0 + j * step;
             for (uint32_t k = 0; k < np; ++k) {
                 const uint32_t p = pos[k];
@@ -176,6 +180,7 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
                 found = true;
             }
             step = found ? 1 : std::min(step * 2, kMaxStep);
+            if (cur > rn) rn = cur;  // positions inside a match that ran past the round: not searched
         }
     }
 }

@@ -65,7 +65,7 @@ constexpr int kZThreads = 512;
 constexpr int kZWaves = kZThreads / 64;
 constexpr uint32_t kZSub = 8192;     // one wave's sub-block
 constexpr uint32_t kZHist = 16384;   // window before a sub-block
-constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8;
+constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8, kZHistMaxStep = 32;
 constexpr int kZPer = kZRound / 64;  // positions per lane and round
 constexpr uint32_t kZTab = 1u << kZHashLog;
 constexpr uint32_t kZStageWords = (kZHist + kEncBlock) / 16 + 3;  // 16-byte words at any alignment + 2 zero words
@@ -103,6 +103,13 @@ struct Win {
         const uint32_t o = P + r;
         return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
     }
+    // the 4 bytes at P and (b4) the byte after them: one pair of LDS words
+    __device__ __forceinline__ uint32_t word5(uint32_t P, uint32_t& b4) const {
+        const uint32_t o = P + r;
+        const uint32_t lo = w[o >> 2], hi = w[(o >> 2) + 1];
+        b4 = (hi >> (8 * (o & 3))) & 0xFF;
+        return __builtin_amdgcn_alignbyte(hi, lo, o & 3);
+    }
 };
 
 __device__ __forceinline__ uint32_t hash5(uint32_t w, uint32_t b4) {
@@ -131,6 +138,9 @@ __device__ __forceinline__ uint32_t win_prefix(const Win& W, uint32_t a, uint32_
     while (L < lim && W.byte(a + L) == W.byte(b + L)) ++L;
     return L;
 }
+
+// a wave-uniform value, provably so (SGPR)
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
 // inclusive prefix sum over the wave
 __device__ __forceinline__ uint32_t wave_incl(uint32_t x, int lane) {
@@ -610,13 +620,13 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
     const uint32_t x0 = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
     auto run = [&](uint32_t x, bool stop_on_meet) -> uint32_t {  // returns the end state, ~0u: met
         for (uint32_t j = a; j < b;) {
-            uint32_t c8[8];
-            const uint32_t nj = min(8u, b - j);
+            uint32_t c8[16];
+            const uint32_t nj = min(16u, b - j);
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < 16; ++u)  // 16 loads in flight
                 if ((uint32_t)u < nj) c8[u] = (coded[ns - 2 - (j + u)].codes >> shift) & 0xFF;
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < 16; ++u)
                 if ((uint32_t)u < nj) {
                     if (stop_on_meet && states[j + u] == x) return ~0u;
                     states[j + u] = (uint16_t)x;
@@ -734,7 +744,8 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
 #pragma unroll
         for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<uint32_t*>(tw)[lane + 64 * i] = 0;
         // history: accelerated rounds over [wlo, s0)
-        for (uint32_t r0 = wlo, rn, hs = 1; r0 < s0; r0 = rn) {
+        uint32_t hs = 1;
+        for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kZRound * hs;
             uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
             bool ok[kZPer];
@@ -743,8 +754,7 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
                 ok[i] = p < s0 && p + 5 <= N;
                 const uint32_t pc = ok[i] ? p : wlo;
-                wp[i] = W.word(pc);
-                b4[i] = W.byte(pc + 4);
+                wp[i] = W.word5(pc, b4[i]);
                 h[i] = hash5(wp[i], b4[i]);
                 t[i] = tw[h[i]];
             }
@@ -758,15 +768,18 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
             for (int i = 0; i < kZPer; ++i) {
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
                 const uint32_t c = ok[i] && t[i] ? wlo + t[i] - 1 : wlo;
-                const uint32_t b = W.byte(ok[i] ? p : wlo);
+                const uint32_t b = wp[i] & 0xFF;
                 const bool run = wp[i] == b * 0x01010101u && b4[i] == b;
-                hit |= ok[i] && t[i] && !run && W.word(c) == wp[i] && W.byte(c + 4) == b4[i];
+                uint32_t c4;
+                const uint32_t cw = W.word5(c, c4);
+                hit |= ok[i] && t[i] && !run && cw == wp[i] && c4 == b4[i];
             }
-            hs = __ballot(hit) ? 1 : min(2 * hs, kZMaxStep);
+            hs = __ballot(hit) ? 1 : min(2 * hs, kZHistMaxStep);
         }
         if (probe) t_hist = wall_clock64();
         // rounds + walk
-        uint32_t cur = s0, step = 1, lstep = 0, rep = 0;
+        // (the first rounds keep the history's step: no matches there, few here)
+        uint32_t cur = s0, step = min(hs, kZMaxStep), lstep = 31 - __builtin_clz(step), rep = 0;
         for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
             rn = r0 + kZRound * step;
             uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
@@ -775,8 +788,7 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
                 const bool ok = p < se && p + 5 <= N;
                 const uint32_t pc = ok ? p : s0;
-                wp[i] = W.word(pc);
-                b4[i] = W.byte(pc + 4);
+                wp[i] = W.word5(pc, b4[i]);
                 h[i] = hash5(wp[i], b4[i]);
                 t[i] = ok ? (uint32_t)tw[h[i]] : 0u;
             }
@@ -792,10 +804,13 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
                 const bool live = p >= cur && p + 5 <= se;
                 const uint32_t c = t[i] ? wlo + t[i] - 1 : s0;
-                const bool rl = live && p > wlo;
-                const uint32_t pm = rl ? p - 1 : s0;  // the run candidate (clamped when unused)
-                const bool mt = live && t[i] && W.word(c) == wp[i] && W.byte(c + 4) == b4[i];
-                const bool mr = rl && W.word(pm) == wp[i] && W.byte(pm + 4) == b4[i];
+                uint32_t c4;
+                const uint32_t cw = W.word5(c, c4);
+                const bool mt = live && t[i] && cw == wp[i] && c4 == b4[i];
+                // the run candidate p - 1 matches 5 bytes iff bytes p - 1 .. p + 4 are equal
+                const uint32_t b = wp[i] & 0xFF;
+                bool mr = live && p > wlo && wp[i] == b * 0x01010101u && b4[i] == b;
+                if (mr) mr = W.byte(p - 1) == b;
                 uint32_t L = 0, C = c;
                 if (mt || mr) {  // rare: lengths to the cap (within the sub-block)
                     const uint32_t lim = min(se - p, kZCap);
@@ -813,8 +828,12 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
             }
             // the greedy walk (wave-uniform); bit q = position r0 + q * step
             bool found = false;
-            uint32_t q = cur > r0 ? (cur - r0 + step - 1) >> lstep : 0;
+            // (the walk's state is wave-uniform: readfirstlane keeps it in SGPRs, so its
+            // branches are scalar)
+            uint32_t q = uni(cur > r0 ? (cur - r0 + step - 1) >> lstep : 0);
             for (;;) {
+                cur = uni(cur);
+                rep = uni(rep);
                 uint32_t wi = q >> 6;
                 unsigned long long mm = 0;
                 for (; wi < (uint32_t)kZPer; ++wi) {
@@ -824,52 +843,65 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 }
                 const bool have = q < kZRound && mm != 0;
                 const int l = have ? __builtin_ctzll(mm) : 0;
-                const uint32_t ph = have ? r0 + (wi * 64 + (uint32_t)l) * step : min(rn, se);
-                uint32_t mpos = 0, msrc = 0, mlen = 0;
-                bool take = false;
-                if (rep && cur < ph) {  // a repeat match in [cur, min(ph, cur + 64))
-                    const uint32_t hi = min(ph, cur + 64);
-                    const uint32_t x = cur + (uint32_t)lane;
-                    const bool okx = x < hi && x >= wlo + rep && x + 5 <= se;
-                    const uint32_t xc = okx ? x : wlo + rep;
-                    const bool eq = okx && W.word(xc) == W.word(xc - rep) && W.byte(xc + 4) == W.byte(xc - rep + 4);
-                    const unsigned long long bal = __ballot(eq);
-                    if (bal) {
-                        mpos = cur + (uint32_t)__builtin_ctzll(bal);
-                        msrc = mpos - rep;
-                        mlen = 5;
-                        take = true;
-                    }
-                }
-                if (!take) {
-                    if (!have) break;
+                const uint32_t ph = uni(have ? r0 + (wi * 64 + (uint32_t)l) * step : min(rn, se));
+                // every LDS read of the step issued before the first ballot: the repeat-match
+                // test over [cur, min(ph, cur + 64)), and for the hash match at ph the
+                // catch-up bytes before it and the first 256 bytes after its capped length
+                uint32_t hl = 0, hsrc = 0;
+                if (have) {
                     const uint32_t Lw = wi == 0 ? Lm[0] : wi == 1 ? Lm[1] : wi == 2 ? Lm[2] : Lm[3];
                     const uint32_t Cw = wi == 0 ? Cm[0] : wi == 1 ? Cm[1] : wi == 2 ? Cm[2] : Cm[3];
-                    mpos = ph;
-                    mlen = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
-                    msrc = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
-                    // catch-up over the literals before it: lane k checks byte k back
-                    const uint32_t kk = (uint32_t)lane;
-                    const bool okb = mpos > cur + kk && msrc > wlo + kk;
-                    const bool eqb = okb && W.byte(okb ? mpos - 1 - kk : s0) == W.byte(okb ? msrc - 1 - kk : s0);
-                    const unsigned long long bb = __ballot(eqb);
-                    const uint32_t e = ~bb ? (uint32_t)__builtin_ctzll(~bb) : 64u;
-                    mpos -= e;
-                    msrc -= e;
-                    mlen += e;
+                    hl = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
+                    hsrc = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
                 }
-                // forwards to the end (within the sub-block): 4 bytes per lane a step
-                for (;;) {
-                    const uint32_t x = mpos + mlen + 4 * (uint32_t)lane;
-                    uint32_t mis = 4;  // first mismatching byte of my 4 (4: none)
-                    if (x + 4 <= se) {
-                        const uint32_t d = W.word(msrc + mlen + 4 * (uint32_t)lane) ^ W.word(x);
+                const uint32_t kk = (uint32_t)lane;
+                const uint32_t x = cur + kk;
+                const bool okx = rep && x < min(ph, cur + 64) && x >= wlo + rep && x + 5 <= se;
+                const uint32_t xc = okx ? x : wlo + rep;
+                const uint32_t ra = W.word(xc), rbw = W.word(xc - rep), r4 = W.byte(xc + 4), r4b = W.byte(xc - rep + 4);
+                const bool okb = have && ph > cur + kk && hsrc > wlo + kk;
+                const uint32_t ba = W.byte(okb ? ph - 1 - kk : s0), bbv = W.byte(okb ? hsrc - 1 - kk : s0);
+                auto fwd_mis = [&](uint32_t src, uint32_t dst) {  // first mismatch of my 4 bytes (4: none)
+                    const uint32_t xf = dst + 4 * kk;
+                    uint32_t mis = 4;
+                    if (xf + 4 <= se) {
+                        const uint32_t d = W.word(src + 4 * kk) ^ W.word(xf);
                         if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
                     } else {
                         mis = 0;
-                        while (x + mis < se && W.byte(msrc + mlen + 4 * (uint32_t)lane + mis) == W.byte(x + mis))
-                            ++mis;
+                        while (xf + mis < se && W.byte(src + 4 * kk + mis) == W.byte(xf + mis)) ++mis;
                     }
+                    return mis;
+                };
+                const uint32_t mis0 = have ? fwd_mis(hsrc + hl, ph + hl) : 0u;
+                const unsigned long long bal = __ballot(okx && ra == rbw && r4 == r4b);
+                uint32_t mpos, msrc, mlen;
+                bool ext;  // the forward extension continues from mpos + mlen
+                if (bal) {  // a repeat match
+                    mpos = cur + (uint32_t)__builtin_ctzll(bal);
+                    msrc = mpos - rep;
+                    mlen = 5;
+                    ext = true;
+                } else {
+                    if (!have) break;
+                    const unsigned long long bb = __ballot(okb && ba == bbv);
+                    const uint32_t e = ~bb ? (uint32_t)__builtin_ctzll(~bb) : 64u;
+                    const unsigned long long bad = __ballot(mis0 < 4);
+                    mlen = hl;
+                    ext = !bad;
+                    if (bad) {
+                        const int f = __builtin_ctzll(bad);
+                        mlen += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis0, f);
+                    } else {
+                        mlen += 256;
+                    }
+                    mpos = ph - e;
+                    msrc = hsrc - e;
+                    mlen += e;
+                }
+                // forwards to the end (within the sub-block): 4 bytes per lane a step
+                while (ext) {
+                    const uint32_t mis = fwd_mis(msrc + mlen, mpos + mlen);
                     const unsigned long long bad = __ballot(mis < 4);
                     if (bad) {
                         const int f = __builtin_ctzll(bad);
@@ -878,16 +910,20 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                     }
                     mlen += 256;
                 }
+                mpos = uni(mpos);
+                msrc = uni(msrc);
+                mlen = uni(mlen);
                 if (lane == 0 && ns < kZSubSeq) wseq[ns] = Seq{mpos - hist, mlen, mpos - msrc};
                 ++ns;
                 rep = mpos - msrc;
                 cur = mpos + mlen;
                 lastend = cur - hist;
                 found = true;
-                q = (cur - r0 + step - 1) >> lstep;
+                q = uni((cur - r0 + step - 1) >> lstep);
             }
             step = found ? 1 : min(2 * step, kZMaxStep);
             lstep = 31 - __builtin_clz(step);
+            if (cur > rn) rn = cur;  // positions inside a match that ran past the round: not searched
         }
     }
     if (probe && lane == 0 && s0 < N) {  // wave 0 of workgroup 0: history / rounds + walk
@@ -1163,12 +1199,65 @@ __device__ __noinline__ void write_literals(EntropyArea& E, const Ctl& ctl, cons
     }
 }
 
+// Repeat-offset coding of sub-block w2 (one lane; the repeat offsets are tracked per
+// sub-block, so the eight run at once): literal lengths, offset values, codes.
+__device__ __noinline__ void rep_code_subblock(const Ctl& ctl, const Seq* __restrict__ wseq_all,
+                                               Coded* __restrict__ coded, uint32_t w2) {
+    uint32_t first = 0, lit_end = 0;
+    for (uint32_t v = 0; v < w2; ++v) {
+        first += min(ctl.nseq[v], kZSubSeq);
+        if (ctl.nseq[v]) lit_end = ctl.lastend[v];
+    }
+    const Seq* const ws = wseq_all + (uint64_t)w2 * kZSubSeq;
+    const uint32_t cnt = min(ctl.nseq[w2], kZSubSeq);
+    // (registers only: a dynamically indexed array would live in scratch memory)
+    uint32_t ra = 0, rb = 0, rc3 = 0;  // repeat offsets 1..3 (0: not set in this sub-block)
+    for (uint32_t q0 = 0; q0 < cnt; q0 += 16) {
+        Seq e8[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)  // 16 loads in flight
+            if (q0 + u < cnt) e8[u] = ws[q0 + u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            if (q0 + u >= cnt) break;
+            const Seq e = e8[u];
+            Coded c;
+            c.ll = e.pos - lit_end;
+            c.ml = e.ml;
+            const uint32_t o = e.off;
+            const bool ll0 = c.ll == 0;
+            c.ofv = o + 3;
+            if (!ll0 && ra == o) c.ofv = 1;
+            else if (rb && rb == o) c.ofv = ll0 ? 1 : 2;
+            else if (rc3 && rc3 == o) c.ofv = ll0 ? 2 : 3;
+            else if (ll0 && ra > 1 && ra - 1 == o) c.ofv = 3;
+            if (c.ofv > 3) {
+                rc3 = rb;
+                rb = ra;
+                ra = o;
+            } else {
+                const uint32_t rcode = c.ofv - 1 + (ll0 ? 1u : 0u);
+                if (rcode > 0) {
+                    const uint32_t cu = rcode == 3 ? ra - 1 : rcode == 1 ? rb : rc3;
+                    if (rcode >= 2) rc3 = rb;
+                    rb = ra;
+                    ra = cu;
+                }
+            }
+            c.codes = ll_code(c.ll) | ml_code(c.ml) << 8 | highbit(c.ofv) << 16;
+            coded[first + q0 + u] = c;
+            lit_end = e.pos + e.ml;
+        }
+    }
+}
+
 // PBS_ZSTD_PROBE=1 (diagnostics): workgroup 0, thread 0 adds the wall-clock ticks (100 MHz)
 // of each phase into g_zprobe: 0 stage + RLE, 1 parse, 2 literal bitmap + histogram,
 // 3 literal mode / Huffman code + repeat codes, 4 code histograms + Huffman sizes,
 // 5 sequence tables, 6 state chains + literal size, 7 literal section, 8 sequence bit
-// stream, 9 block end; 10 blocks, 11 sequences, 12 literals.
-__device__ unsigned long long g_zprobe[16];
+// stream, 9 block end; 10 blocks, 11 sequences, 12 literals; 13/14 wave 0's history and
+// rounds + walk; 15 literal bitmap, 16 sampled histogram (both inside 2).
+__device__ unsigned long long g_zprobe[24];
 #define ZMARK(ph)                                  \
     do {                                           \
         if (probe) {                               \
@@ -1295,23 +1384,47 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         for (uint32_t i = tid; i < kZWaves * 256; i += kZThreads) E.streams[i] = 0;  // per-wave histograms
         __syncthreads();
         {
+            // lane per match: its partial end words by atomics, up to 4 whole words by
+            // stores (no other match touches them); longer runs of whole words by the wave
             const Seq* const wseq = wseq_all + (uint64_t)wave * kZSubSeq;
-            for (uint32_t q = lane; q < ctl.nseq[wave]; q += 64) {
-                const Seq e = wseq[q];
-                uint32_t a = e.pos, b = e.pos + e.ml;
-                while (a < b) {
-                    const uint32_t wd = a >> 5, lo = a & 31;
-                    const uint32_t cnt = min(32 - lo, b - a);
-                    const uint32_t mask = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << lo;
-                    if (cnt == 32)
-                        E.bitmap[wd] = 0;  // a whole word inside one match: no other match touches it
-                    else
-                        atomicAnd(&E.bitmap[wd], ~mask);
-                    a += cnt;
+            const uint32_t nsw = min(ctl.nseq[wave], kZSubSeq);
+            for (uint32_t q0 = 0; q0 < nsw; q0 += 64) {
+                uint32_t a = 0, b = 0;
+                if (q0 + lane < nsw) {
+                    const Seq e = wseq[q0 + lane];
+                    a = e.pos;
+                    b = e.pos + e.ml;
+                }
+                uint32_t wa = 0, wb = 0;
+                if (a < b) {
+                    if ((a >> 5) == ((b - 1) >> 5)) {
+                        const uint32_t cnt = b - a;
+                        const uint32_t mask = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << (a & 31);
+                        if (cnt == 32)
+                            E.bitmap[a >> 5] = 0;
+                        else
+                            atomicAnd(&E.bitmap[a >> 5], ~mask);
+                    } else {
+                        if (a & 31) atomicAnd(&E.bitmap[a >> 5], (1u << (a & 31)) - 1u);
+                        if (b & 31) atomicAnd(&E.bitmap[b >> 5], ~((1u << (b & 31)) - 1u));
+                        wa = (a + 31) >> 5;
+                        wb = b >> 5;
+                        if (wb - wa <= 4) {
+                            for (uint32_t w = wa; w < wb; ++w) E.bitmap[w] = 0;
+                            wb = wa;
+                        }
+                    }
+                }
+                for (unsigned long long lg = __ballot(wb > wa); lg; lg &= lg - 1) {
+                    const int l = __builtin_ctzll(lg);
+                    const uint32_t la = (uint32_t)__builtin_amdgcn_readlane((int)wa, l);
+                    const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)wb, l);
+                    for (uint32_t w = la + lane; w < lb; w += 64) E.bitmap[w] = 0;
                 }
             }
         }
         __syncthreads();
+        ZMARK(15);
         // thread t owns block positions [128 t, 128 t + 128): bitmap words 4t .. 4t + 3
         uint32_t bmw[4], cnt_t = 0;
 #pragma unroll
@@ -1350,6 +1463,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             E.hist[tid] = c;
         }
         __syncthreads();
+        ZMARK(16);
         if (wave == 0) {  // 1: the full histogram is needed; 0: raw literals
             uint32_t need = nlit > 0;
             if (nlit >= 32 && nsamp > 0) {
@@ -1391,54 +1505,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         if (wave == 0) {
             if (ctl.need_full) literal_mode_wave(E, ctl, fse[0], nlit, lane);
         } else if (wave == 1 && lane < kZWaves) {
-            // repeat-offset coding of sub-block `lane` (reps tracked per sub-block)
-            const uint32_t w2 = (uint32_t)lane;
-            uint32_t first = 0, lit_end = 0;
-            for (uint32_t v = 0; v < w2; ++v) {
-                first += min(ctl.nseq[v], kZSubSeq);
-                if (ctl.nseq[v]) lit_end = ctl.lastend[v];
-            }
-            const Seq* const ws = wseq_all + (uint64_t)w2 * kZSubSeq;
-            const uint32_t cnt = min(ctl.nseq[w2], kZSubSeq);
-            // (registers only: a dynamically indexed array would live in scratch memory)
-            uint32_t ra = 0, rb = 0, rc3 = 0;  // repeat offsets 1..3 (0: not set in this sub-block)
-            for (uint32_t q0 = 0; q0 < cnt; q0 += 8) {
-                Seq e8[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u)  // 8 loads in flight
-                    if (q0 + u < cnt) e8[u] = ws[q0 + u];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    if (q0 + u >= cnt) break;
-                    const Seq e = e8[u];
-                    Coded c;
-                    c.ll = e.pos - lit_end;
-                    c.ml = e.ml;
-                    const uint32_t o = e.off;
-                    const bool ll0 = c.ll == 0;
-                    c.ofv = o + 3;
-                    if (!ll0 && ra == o) c.ofv = 1;
-                    else if (rb && rb == o) c.ofv = ll0 ? 1 : 2;
-                    else if (rc3 && rc3 == o) c.ofv = ll0 ? 2 : 3;
-                    else if (ll0 && ra > 1 && ra - 1 == o) c.ofv = 3;
-                    if (c.ofv > 3) {
-                        rc3 = rb;
-                        rb = ra;
-                        ra = o;
-                    } else {
-                        const uint32_t rcode = c.ofv - 1 + (ll0 ? 1u : 0u);
-                        if (rcode > 0) {
-                            const uint32_t cu = rcode == 3 ? ra - 1 : rcode == 1 ? rb : rc3;
-                            if (rcode >= 2) rc3 = rb;
-                            rb = ra;
-                            ra = cu;
-                        }
-                    }
-                    c.codes = ll_code(c.ll) | ml_code(c.ml) << 8 | highbit(c.ofv) << 16;
-                    coded[first + q0 + u] = c;
-                    lit_end = e.pos + e.ml;
-                }
-            }
+            rep_code_subblock(ctl, wseq_all, coded, (uint32_t)lane);
             __threadfence_block();
         }
         for (uint32_t i = tid; i < 36 + 53 + 32; i += kZThreads) E.shist[i] = 0;
@@ -1892,24 +1959,26 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
             return e && e[0] == '1';
         }();
         if (compress && zprobe) {
-            const unsigned long long z[16] = {};
+            const unsigned long long z[24] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
         }
         if (compress)
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
                                ni, zs.slots, d_sizes, zs.seqs, zs.coded, zs.chains, zprobe ? 1 : 0);
         if (compress && zprobe) {
-            unsigned long long h[16] = {};
+            unsigned long long h[24] = {};
             (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
             (void)hipStreamSynchronize(st);
             const double nb = h[10] ? (double)h[10] : 1.0;
             std::fprintf(stderr,
                          "zstd probe (workgroup 0, us per block over %llu blocks, %.0f sequences, %.0f literals per "
                          "block): stage %.1f parse %.1f litmap %.1f litmode %.1f codehist %.1f tables %.1f chains %.1f "
-                         "literals %.1f seqstream %.1f end %.1f | wave 0: history %.1f rounds+walk %.1f\n",
+                         "literals %.1f seqstream %.1f end %.1f | wave 0: history %.1f rounds+walk %.1f | litmap: bitmap %.1f "
+                         "sampled %.1f\n",
                          h[10], h[11] / nb, h[12] / nb, h[0] / nb / 100, h[1] / nb / 100, h[2] / nb / 100,
                          h[3] / nb / 100, h[4] / nb / 100, h[5] / nb / 100, h[6] / nb / 100, h[7] / nb / 100,
-                         h[8] / nb / 100, h[9] / nb / 100, h[13] / nb / 100, h[14] / nb / 100);
+                         h[8] / nb / 100, h[9] / nb / 100, h[13] / nb / 100, h[14] / nb / 100, h[15] / nb / 100,
+                         h[16] / nb / 100);
         }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 3h: zstd phase probe (PBS_ZSTD_PROBE=1) on text / pxar / VM image, LDS-staged raw literals.
+# Round 3h/3i: zstd phase probe (PBS_ZSTD_PROBE=1) on text / pxar / VM image.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-R="$(pwd)"; export TMPDIR=/tmp; O=${OUT:-gpurun_out/r03h}; mkdir -p $O
+R="$(pwd)"; export TMPDIR=/tmp; O=${OUT:-gpurun_out/r03i}; mkdir -p $O
 step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
 step pytest_zstd 400 python -u -m pytest tests/test_gpu_zstd.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1
 step zstd_corpus_probe 400 env PBS_ZSTD_PROBE=1 python -u scripts/zstd_bench.py --gib 1 --reps 1 || exit 1

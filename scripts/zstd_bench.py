@@ -4,7 +4,7 @@ on text-like and pxar-like data (tests/corpus_gen.py): a seeded 32 MiB corpus ti
 chunker at --avg, encoded --reps times (best wall clock), with libzstd level 1 on the
 host over the first 64 MiB for the ratio.
 
-    python scripts/zstd_bench.py [--corpus text|pxar|both] [--gib 1] [--avg 4194304]
+    python scripts/zstd_bench.py [--corpus text|pxar|vm|both|text,vm,...] [--gib 1] [--avg 4194304]
 """
 import argparse
 import json
@@ -32,9 +32,11 @@ def main():
 
     torch.cuda.set_device(0)
     L = oracle.libzstd()
-    for name in (["text", "pxar"] if a.corpus == "both" else [a.corpus]):
+    import gen_np
+    for name in (["text", "pxar"] if a.corpus == "both" else a.corpus.split(",")):
         t0 = time.time()
-        base = corpus_gen.text(32 << 20, 21) if name == "text" else corpus_gen.pxar(32 << 20, 22)
+        base = {"text": lambda: corpus_gen.text(32 << 20, 21), "pxar": lambda: corpus_gen.pxar(32 << 20, 22),
+                "vm": lambda: gen_np.gen_vmimage(32 << 20, 0x5EED0003, 0)}[name]()
         n = int(a.gib * (1 << 30)) // base.size * base.size
         host = np.tile(base, n // base.size)
         gen_s = time.time() - t0
