@@ -340,6 +340,86 @@ __device__ __noinline__ void fse_build(FseT& t, const int16_t* norm, int nsym, i
     t.log = log;
 }
 
+// fse_build by ONE WAVE (nsym <= 64), same table: symbol s's cells are the (cs_s + i)-th
+// positions of the spread sequence (j * step) & mask that are <= high (cs = exclusive
+// prefix of the positive counts); next[] takes, per symbol, its cells in increasing order
+// (rank among the same symbol by ballots, 64 cells at a time).
+__device__ __noinline__ void fse_build_wave(FseT& t, const int16_t* norm, int nsym, int log, int lane) {
+    const uint32_t size = 1u << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    const int c = lane < nsym ? norm[lane] : 0;
+    const uint32_t cells = c == -1 ? 1u : (c > 0 ? (uint32_t)c : 0u);
+    const uint32_t spread = c > 0 ? (uint32_t)c : 0u, low = c == -1 ? 1u : 0u;
+    const uint32_t ci = wave_incl(cells, lane), si = wave_incl(spread, lane), li = wave_incl(low, lane);
+    const uint32_t nlow = (uint32_t)__builtin_amdgcn_readlane((int)li, 63);
+    const uint32_t high = size - 1 - nlow;
+    uint16_t* const spc = t.next;  // (scratch until next[] is written below)
+    if (lane < nsym) {
+        t.cum[lane] = (int32_t)(ci - cells);
+        spc[lane] = (uint16_t)(si - spread);
+        if (low) t.sym_at[size - 1 - (li - low)] = (uint8_t)lane;
+        t.dfs[lane] = (int32_t)(ci - cells);  // running next[] slot per symbol (dfs is set last)
+    }
+    __builtin_amdgcn_wave_barrier();
+    // spread: placement k at the k-th position <= high
+    const uint32_t nspread = (uint32_t)__builtin_amdgcn_readlane((int)si, 63);
+    uint32_t kb = 0;
+    for (uint32_t j0 = 0; j0 < size; j0 += 64) {
+        const uint32_t j = j0 + (uint32_t)lane;
+        const uint32_t P = (j * step) & mask;
+        const bool ok = j < size && P <= high;
+        const unsigned long long b = __ballot(ok);
+        const uint32_t k = kb + (uint32_t)__builtin_popcountll(b & ((1ull << lane) - 1ull));
+        if (ok && k < nspread) {
+            int lo = 0, hi = nsym - 1;  // the last symbol with spc <= k (and a positive count)
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (spc[mid] <= k) lo = mid; else hi = mid - 1;
+            }
+            while (norm[lo] <= 0) --lo;  // (symbols without spread cells share its spc)
+            t.sym_at[P] = (uint8_t)lo;
+        }
+        kb += (uint32_t)__builtin_popcountll(b);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // next: the cells of each symbol in increasing order
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint32_t u0 = 0; u0 < size; u0 += 64) {
+        const uint32_t u = u0 + (uint32_t)lane;
+        const uint32_t sy = u < size ? t.sym_at[u] : 0xFFFFu;
+        unsigned long long rem = __ballot(u < size);
+        uint32_t slot = 0;
+        while (rem) {
+            const int f = __builtin_ctzll(rem);
+            const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)sy, f);
+            const unsigned long long mm = __ballot(sy == s0) & rem;
+            const uint32_t base = (uint32_t)t.dfs[s0];
+            if (sy == s0) slot = base + (uint32_t)__builtin_popcountll(mm & lt);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == f) t.dfs[s0] = (int32_t)(base + (uint32_t)__builtin_popcountll(mm));
+            __builtin_amdgcn_wave_barrier();
+            rem &= ~mm;
+        }
+        if (u < size) t.next[slot] = (uint16_t)(size + u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nsym) {
+        const uint32_t total = ci - cells;
+        if (c == 0) {
+            t.dnb[lane] = (int32_t)(((uint32_t)log + 1) << 16) - (int32_t)size;
+            t.dfs[lane] = 0;
+        } else if (c == -1 || c == 1) {
+            t.dnb[lane] = (int32_t)((uint32_t)log << 16) - (int32_t)size;
+            t.dfs[lane] = (int32_t)total - 1;
+        } else {
+            const int maxbits = log - (int)highbit((uint32_t)(c - 1));
+            t.dnb[lane] = (maxbits << 16) - (c << maxbits);
+            t.dfs[lane] = (int32_t)total - c;
+        }
+    }
+    if (lane == 0) t.log = log;
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ FseView view(const FseT& t) { return FseView{t.next, t.dnb, t.dfs, (uint32_t)t.log}; }
 __device__ __forceinline__ FseView view(const PreT& t) { return FseView{t.next, t.dnb, t.dfs, (uint32_t)t.log}; }
 
@@ -456,39 +536,77 @@ __device__ __noinline__ uint32_t fse_ncount(uint8_t* o, const int16_t* norm, int
 
 // Table of one sequence symbol stream: the cheapest of predefined (0), RLE (1) and own
 // FSE table (2) by the integer estimate (ties keep the earlier mode).  Mode 0 leaves the
-// table to the launch's predefined one.
-__device__ __noinline__ void seq_table(FseT& t, const uint32_t* cnt, int nsym, uint32_t nseq, const int16_t* pre,
-                                       int pre_log, int max_log) {
-    int distinct = 0, maxs = 0;
-    for (int s = 0; s < nsym; ++s)
-        if (cnt[s]) {
-            ++distinct;
-            maxs = s;
-        }
-    uint64_t c_pre = 0;
-    for (int s = 0; s < nsym; ++s)
-        if (cnt[s]) c_pre += (uint64_t)cnt[s] * (256u * pre_log - lg256(pre[s] < 1 ? 1 : pre[s]));
-    t.desc_len = 0;
-    t.mode = 0;
+// table to the launch's predefined one.  ONE WAVE, a lane per symbol (nsym <= 64): the
+// normalisation's rounding, its fix-up (the largest count, first on ties), the estimate;
+// lane 0 writes the description, the wave builds the table.
+__device__ __noinline__ void seq_table_wave(FseT& t, const uint32_t* cnt, int nsym, uint32_t nseq, const int16_t* pre,
+                                            int pre_log, int max_log, int lane) {
+    const uint32_t c = lane < nsym ? cnt[lane] : 0u;
+    const unsigned long long present = __ballot(c != 0);
+    const int distinct = __builtin_popcountll(present);
+    const int maxs = present ? 63 - __builtin_clzll(present) : 0;
+    uint64_t cp = c ? (uint64_t)c * (256u * pre_log - lg256(pre[lane] < 1 ? 1 : pre[lane])) : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cp += __shfl_xor(cp, d, 64);
+    if (lane == 0) {
+        t.desc_len = 0;
+        t.mode = 0;
+    }
     if (distinct == 1 && nseq > 2) {
-        t.mode = 1;
-        t.desc[0] = (uint8_t)maxs;
-        t.desc_len = 1;
+        if (lane == 0) {
+            t.mode = 1;
+            t.desc[0] = (uint8_t)maxs;
+            t.desc_len = 1;
+        }
+        __builtin_amdgcn_wave_barrier();
         return;
     }
     if (nseq >= 16) {
         const int log = fse_log(nseq, (uint32_t)maxs, max_log);
-        fse_normalize(t.norm, cnt, maxs + 1, nseq, log);
-        const uint32_t d = fse_ncount(t.desc, t.norm, maxs + 1, log);
-        uint64_t c = 2048ull * d;
-        for (int s = 0; s <= maxs; ++s)
-            if (cnt[s]) c += (uint64_t)cnt[s] * (256u * log - lg256((uint32_t)t.norm[s]));
-        if (c < c_pre) {
-            t.mode = 2;
-            t.desc_len = d;
-            fse_build(t, t.norm, maxs + 1, log);
+        const int64_t scale = 1ll << log;
+        int64_t v = 0;
+        if (c) {
+            v = ((int64_t)c * scale + nseq / 2) / nseq;
+            if (v < 1) v = 1;
+        }
+        int64_t sum = v;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+        while (sum != scale) {  // wave-uniform
+            uint32_t key = v > 0 ? (uint32_t)v << 8 | (255u - (uint32_t)lane) : 0u;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, d, 64));
+            const int big = 255 - (int)(key & 255u);
+            const int64_t vb = (int64_t)(key >> 8);
+            int64_t nv = vb;
+            if (sum < scale) {
+                nv = vb + (scale - sum);
+                sum = scale;
+            } else {
+                const int64_t take = min(sum - scale, vb - 1);
+                nv = vb - take;
+                sum -= take;
+            }
+            if (lane == big) v = nv;
+        }
+        if (lane < nsym) t.norm[lane] = (int16_t)(lane <= maxs ? v : 0);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t d = 0;
+        if (lane == 0) d = fse_ncount(t.desc, t.norm, maxs + 1, log);
+        d = uni(d);
+        uint64_t cc = c ? (uint64_t)c * (256u * log - lg256((uint32_t)v)) : 0ull;
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) cc += __shfl_xor(cc, k, 64);
+        cc += 2048ull * d;
+        if (cc < cp) {
+            if (lane == 0) {
+                t.mode = 2;
+                t.desc_len = d;
+            }
+            fse_build_wave(t, t.norm, maxs + 1, log, lane);
         }
     }
+    __builtin_amdgcn_wave_barrier();
 }
 
 // ---------------------------------------------------------------- LDS layout
@@ -600,19 +718,27 @@ __device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scra
 // true state, so after r rounds lanes 0..r are exact; usually one round settles all.
 __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__ coded, uint32_t ns,
                                             uint32_t shift, uint32_t* __restrict__ chain,
-                                            uint16_t* __restrict__ states, uint32_t* last, int lane) {
+                                            uint16_t* __restrict__ states, uint32_t* last, int lane,
+                                            unsigned long long* probe) {
     const uint32_t m = ns - 1;
     if (m < 128) {  // short: one lane, serially (the rounds would cost more than they save)
-        if (lane == 0) {
-            uint32_t x = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
-            for (uint32_t j = 0; j < m; ++j) {
-                const uint32_t sym = (coded[ns - 2 - j].codes >> shift) & 0xFF;
+        // the wave loads 64 codes at a time, lane 0 takes them by readlane
+        uint32_t x = 0;
+        for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+            const uint32_t jl = j0 + (uint32_t)lane;
+            const uint32_t mine = jl < m ? (coded[ns - 2 - jl].codes >> shift) & 0xFF : 0u;
+            if (j0 == 0) x = fse_init(t, (uni(coded[ns - 1].codes) >> shift) & 0xFF);
+            uint32_t mine_bits = 0;
+            const uint32_t nj = min(64u, m - j0);
+            for (uint32_t u = 0; u < nj; ++u) {
+                const uint32_t sym = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)u);
                 const uint32_t nb = (x + (uint32_t)t.dnb[sym]) >> 16;
-                chain[ns - 2 - j] = (x & ((1u << nb) - 1u)) | nb << 16;
+                if ((uint32_t)lane == u) mine_bits = (x & ((1u << nb) - 1u)) | nb << 16;
                 x = t.next[(x >> nb) + t.dfs[sym]];
             }
-            *last = x;
+            if (jl < m) chain[ns - 2 - jl] = mine_bits;
         }
+        if (lane == 0) *last = m ? x : fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
         return;
     }
     const uint32_t seg = (m + 63) / 64;
@@ -620,15 +746,18 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
     const uint32_t x0 = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
     auto run = [&](uint32_t x, bool stop_on_meet) -> uint32_t {  // returns the end state, ~0u: met
         for (uint32_t j = a; j < b;) {
-            uint32_t c8[16];
+            uint32_t c8[16], s8[16];
             const uint32_t nj = min(16u, b - j);
 #pragma unroll
-            for (int u = 0; u < 16; ++u)  // 16 loads in flight
-                if ((uint32_t)u < nj) c8[u] = (coded[ns - 2 - (j + u)].codes >> shift) & 0xFF;
+            for (int u = 0; u < 16; ++u)  // 16 loads in flight (and the recorded states)
+                if ((uint32_t)u < nj) {
+                    c8[u] = (coded[ns - 2 - (j + u)].codes >> shift) & 0xFF;
+                    s8[u] = stop_on_meet ? states[j + u] : 0u;
+                }
 #pragma unroll
             for (int u = 0; u < 16; ++u)
                 if ((uint32_t)u < nj) {
-                    if (stop_on_meet && states[j + u] == x) return ~0u;
+                    if (stop_on_meet && s8[u] == x) return ~0u;
                     states[j + u] = (uint16_t)x;
                     const uint32_t sym = c8[u];
                     const uint32_t nb = (x + (uint32_t)t.dnb[sym]) >> 16;
@@ -641,8 +770,11 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
     };
     // pass 1: lane 0 from the true state, the others from the table's first state
     uint32_t start = lane == 0 ? x0 : (1u << t.log);
+    const uint64_t tp0 = probe ? wall_clock64() : 0;
     uint32_t end = run(start, false);
-    for (int round = 0; round < 64; ++round) {
+    const uint64_t tp1 = probe ? wall_clock64() : 0;
+    int round = 0;
+    for (; round < 64; ++round) {
         // the true start of lane l is lane l-1's end (lane 0: x0)
         const uint32_t left = (uint32_t)__shfl_up((int)end, 1, 64);
         const uint32_t want = lane == 0 ? x0 : left;
@@ -656,6 +788,12 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
             end = want;  // an empty segment passes its start through
             start = want;
         }
+    }
+    if (probe && lane == 0) {
+        probe[22] += tp1 - tp0;
+        probe[23] += wall_clock64() - tp1;
+        probe[24] += (unsigned long long)round;
+        probe[25] += 1;
     }
     // the final state: the end of the last non-empty segment
     const uint32_t lastlane = m ? (m - 1) / seg : 0;
@@ -937,7 +1075,16 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
 // Literal section mode of a block (ONE WAVE): RLE (one distinct byte), raw, or Huffman
 // when the entropy estimate says it may pay -- then the code lengths (two-queue merge,
 // limited to 11 bits), canonical codes and the tree description.  ctl.lit_mode = lane 0's.
-__device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& fsc, uint32_t nlit, int lane) {
+__device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& fsc, uint32_t nlit, int lane,
+                                               unsigned long long* probe) {
+    uint64_t tq = probe ? wall_clock64() : 0;
+    auto mark = [&](int idx) {
+        if (probe && lane == 0) {
+            const uint64_t t2 = wall_clock64();
+            probe[idx] += t2 - tq;
+            tq = t2;
+        }
+    };
     uint32_t c4[4], dist = 0, lastsym = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -978,8 +1125,10 @@ __device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& f
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if (c4[i]) E.tw[rk[i]] = key[i];  // sorted keys (temporarily in tw)
+        mark(26);
         if (lane == 0) huf_merge(E, ctl, dist);
         __builtin_amdgcn_wave_barrier();
+        mark(27);
         const int m = (int)dist, root = ctl.root;
         // depth of each leaf (sorted index i = 4 lane + j: contiguous per lane)
         int32_t kr = 0;
@@ -1027,6 +1176,7 @@ __device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& f
                 }
         }
         __builtin_amdgcn_wave_barrier();
+        mark(28);
         // per symbol lengths
 #pragma unroll
         for (int i = 0; i < 4; ++i) E.len[lane + 64 * i] = 0;
@@ -1082,7 +1232,9 @@ __device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& f
             for (int i = 0; i < 4; ++i)
                 if (ls[i]) E.code[lane + 64 * i] = (uint16_t)(start[ls[i]] + rk[i]);
         }
+        mark(29);
         if (lane == 0 && !huf_describe(E, ctl, fsc, mb, lastsym)) mode = 0;
+        mark(30);
     }
     if (lane == 0) ctl.lit_mode = mode;  // (lane 0's: it may have fallen back to raw)
 }
@@ -1199,10 +1351,36 @@ __device__ __noinline__ void write_literals(EntropyArea& E, const Ctl& ctl, cons
     }
 }
 
-// Repeat-offset coding of sub-block w2 (one lane; the repeat offsets are tracked per
-// sub-block, so the eight run at once): literal lengths, offset values, codes.
-__device__ __noinline__ void rep_code_subblock(const Ctl& ctl, const Seq* __restrict__ wseq_all,
-                                               Coded* __restrict__ coded, uint32_t w2) {
+// Repeat-offset coding of sub-block w2 by ONE WAVE (the repeat offsets are tracked per
+// sub-block): literal lengths, offset values, codes.  The offsets are a serial state
+// machine, but its state is the last three offsets, so it forgets its past: lane l codes
+// the sequences [l seg, (l+1) seg) from the state reached by running the machine over the
+// 8 sequences before them from empty (lane 0: the true start); then, in rounds, a lane
+// whose start differs from its left neighbour's end re-codes from that end.
+__device__ __forceinline__ void rep_step(uint32_t& ra, uint32_t& rb, uint32_t& rc3, uint32_t o, bool ll0,
+                                         uint32_t& ofv) {
+    ofv = o + 3;
+    if (!ll0 && ra == o) ofv = 1;
+    else if (rb && rb == o) ofv = ll0 ? 1 : 2;
+    else if (rc3 && rc3 == o) ofv = ll0 ? 2 : 3;
+    else if (ll0 && ra > 1 && ra - 1 == o) ofv = 3;
+    if (ofv > 3) {
+        rc3 = rb;
+        rb = ra;
+        ra = o;
+    } else {
+        const uint32_t rcode = ofv - 1 + (ll0 ? 1u : 0u);
+        if (rcode > 0) {
+            const uint32_t cu = rcode == 3 ? ra - 1 : rcode == 1 ? rb : rc3;
+            if (rcode >= 2) rc3 = rb;
+            rb = ra;
+            ra = cu;
+        }
+    }
+}
+
+__device__ __noinline__ void rep_code_wave(const Ctl& ctl, const Seq* __restrict__ wseq_all, Coded* __restrict__ coded,
+                                           uint32_t w2, int lane) {
     uint32_t first = 0, lit_end = 0;
     for (uint32_t v = 0; v < w2; ++v) {
         first += min(ctl.nseq[v], kZSubSeq);
@@ -1210,43 +1388,57 @@ __device__ __noinline__ void rep_code_subblock(const Ctl& ctl, const Seq* __rest
     }
     const Seq* const ws = wseq_all + (uint64_t)w2 * kZSubSeq;
     const uint32_t cnt = min(ctl.nseq[w2], kZSubSeq);
-    // (registers only: a dynamically indexed array would live in scratch memory)
-    uint32_t ra = 0, rb = 0, rc3 = 0;  // repeat offsets 1..3 (0: not set in this sub-block)
-    for (uint32_t q0 = 0; q0 < cnt; q0 += 16) {
-        Seq e8[16];
+    if (!cnt) return;
+    const uint32_t seg = (cnt + 63) / 64;
+    const uint32_t a = min(cnt, (uint32_t)lane * seg), b = min(cnt, a + seg);
+    constexpr uint32_t kWarm = 8;
+    // codes [from, to) from state (ra, rb, rc3); write: store the Coded entries
+    auto run = [&](uint32_t from, uint32_t to, uint32_t& ra, uint32_t& rb, uint32_t& rc3, bool write) {
+        uint32_t prev_end = from == 0 ? lit_end : 0u;
+        if (from > 0) {
+            const Seq p = ws[from - 1];
+            prev_end = p.pos + p.ml;
+        }
+        for (uint32_t q0 = from; q0 < to; q0 += 8) {
+            Seq e8[8];
 #pragma unroll
-        for (int u = 0; u < 16; ++u)  // 16 loads in flight
-            if (q0 + u < cnt) e8[u] = ws[q0 + u];
+            for (int u = 0; u < 8; ++u)  // 8 loads in flight
+                if (q0 + u < to) e8[u] = ws[q0 + u];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            if (q0 + u >= cnt) break;
-            const Seq e = e8[u];
-            Coded c;
-            c.ll = e.pos - lit_end;
-            c.ml = e.ml;
-            const uint32_t o = e.off;
-            const bool ll0 = c.ll == 0;
-            c.ofv = o + 3;
-            if (!ll0 && ra == o) c.ofv = 1;
-            else if (rb && rb == o) c.ofv = ll0 ? 1 : 2;
-            else if (rc3 && rc3 == o) c.ofv = ll0 ? 2 : 3;
-            else if (ll0 && ra > 1 && ra - 1 == o) c.ofv = 3;
-            if (c.ofv > 3) {
-                rc3 = rb;
-                rb = ra;
-                ra = o;
-            } else {
-                const uint32_t rcode = c.ofv - 1 + (ll0 ? 1u : 0u);
-                if (rcode > 0) {
-                    const uint32_t cu = rcode == 3 ? ra - 1 : rcode == 1 ? rb : rc3;
-                    if (rcode >= 2) rc3 = rb;
-                    rb = ra;
-                    ra = cu;
+            for (int u = 0; u < 8; ++u) {
+                if (q0 + u >= to) break;
+                const Seq e = e8[u];
+                Coded c;
+                c.ll = e.pos - prev_end;
+                c.ml = e.ml;
+                rep_step(ra, rb, rc3, e.off, c.ll == 0, c.ofv);
+                if (write) {
+                    c.codes = ll_code(c.ll) | ml_code(c.ml) << 8 | highbit(c.ofv) << 16;
+                    coded[first + q0 + u] = c;
                 }
+                prev_end = e.pos + e.ml;
             }
-            c.codes = ll_code(c.ll) | ml_code(c.ml) << 8 | highbit(c.ofv) << 16;
-            coded[first + q0 + u] = c;
-            lit_end = e.pos + e.ml;
+        }
+    };
+    uint32_t sa = 0, sb = 0, sc = 0;  // the start state
+    if (a < b && a > 0) run(a > kWarm ? a - kWarm : 0u, a, sa, sb, sc, false);
+    uint32_t ea = sa, eb = sb, ec = sc;  // the end state
+    if (a < b) run(a, b, ea, eb, ec, true);
+    for (int round = 0; round < 64; ++round) {
+        // the true start of lane l is lane l-1's end (lane 0: empty); empty segments pass it on
+        const uint32_t la = (uint32_t)__shfl_up((int)ea, 1, 64), lb = (uint32_t)__shfl_up((int)eb, 1, 64),
+                       lc = (uint32_t)__shfl_up((int)ec, 1, 64);
+        const uint32_t wa = lane == 0 ? 0u : la, wb = lane == 0 ? 0u : lb, wc = lane == 0 ? 0u : lc;
+        const bool differ = a < b && (wa != sa || wb != sb || wc != sc);  // (empty segments: trailing)
+        if (!__ballot(differ)) break;
+        if (differ) {
+            sa = wa;
+            sb = wb;
+            sc = wc;
+            ea = sa;
+            eb = sb;
+            ec = sc;
+            run(a, b, ea, eb, ec, true);
         }
     }
 }
@@ -1256,8 +1448,12 @@ __device__ __noinline__ void rep_code_subblock(const Ctl& ctl, const Seq* __rest
 // 3 literal mode / Huffman code + repeat codes, 4 code histograms + Huffman sizes,
 // 5 sequence tables, 6 state chains + literal size, 7 literal section, 8 sequence bit
 // stream, 9 block end; 10 blocks, 11 sequences, 12 literals; 13/14 wave 0's history and
-// rounds + walk; 15 literal bitmap, 16 sampled histogram (both inside 2).
-__device__ unsigned long long g_zprobe[24];
+// rounds + walk; 15 literal bitmap, 16 sampled histogram (both inside 2); per role (lane 0
+// of the wave doing it): 17 literal mode (wave 0), 18 repeat coding (wave 1), 19 LL table
+// (wave 1), 20 LL state chain (wave 1), 21 literal section (wave 0); long LL chains: 22 pass
+// 1, 23 rounds (ticks), 24 rounds, 25 chains; Huffman (wave 0): 26 rank, 27 merge, 28
+// lengths, 29 canonical codes, 30 description.
+__device__ unsigned long long g_zprobe[32];
 #define ZMARK(ph)                                  \
     do {                                           \
         if (probe) {                               \
@@ -1502,11 +1698,21 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         ZMARK(2);
 
         // ---- literal mode (wave 0) and repeat-offset coding (wave 1, one lane per sub-block)
+        const bool role_probe = probe_on && blockIdx.x == 0;
+        uint64_t zt = role_probe ? wall_clock64() : 0;
+        auto role_end = [&](int idx) {
+            if (role_probe && lane == 0) {
+                const uint64_t t2 = wall_clock64();
+                atomicAdd(&g_zprobe[idx], t2 - zt);
+                zt = t2;
+            }
+        };
+        rep_code_wave(ctl, wseq_all, coded, (uint32_t)wave, lane);
+        __threadfence_block();
+        if (wave == 1) role_end(18);
         if (wave == 0) {
-            if (ctl.need_full) literal_mode_wave(E, ctl, fse[0], nlit, lane);
-        } else if (wave == 1 && lane < kZWaves) {
-            rep_code_subblock(ctl, wseq_all, coded, (uint32_t)lane);
-            __threadfence_block();
+            if (ctl.need_full) literal_mode_wave(E, ctl, fse[0], nlit, lane, role_probe ? g_zprobe : nullptr);
+            role_end(17);
         }
         for (uint32_t i = tid; i < 36 + 53 + 32; i += kZThreads) E.shist[i] = 0;
         __syncthreads();
@@ -1570,10 +1776,12 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         // sequence tables: LL on wave 1, OF on wave 2, ML on wave 3 (lane 0 each)
         __syncthreads();
         ZMARK(5);
-        if (lane == 0 && wave >= 1 && wave <= 3 && nseq > 0) {
-            if (wave == 1) seq_table(fse[0], E.shist, 36, nseq, kLLNorm, kLLLog, kLLMaxLog);
-            if (wave == 2) seq_table(fse[1], E.shist + 36 + 53, 29, nseq, kOFNorm, kOFLog, kOFMaxLog);
-            if (wave == 3) seq_table(fse[2], E.shist + 36, 53, nseq, kMLNorm, kMLLog, kMLMaxLog);
+        if (role_probe) zt = wall_clock64();
+        if (wave >= 1 && wave <= 3 && nseq > 0) {
+            if (wave == 1) seq_table_wave(fse[0], E.shist, 36, nseq, kLLNorm, kLLLog, kLLMaxLog, lane);
+            if (wave == 2) seq_table_wave(fse[1], E.shist + 36 + 53, 29, nseq, kOFNorm, kOFLog, kOFMaxLog, lane);
+            if (wave == 3) seq_table_wave(fse[2], E.shist + 36, 53, nseq, kMLNorm, kMLLog, kMLMaxLog, lane);
+            if (wave == 1) role_end(19);
         }
         // literal section: size decision (thread 0)
         if (tid == 0) {
@@ -1615,9 +1823,11 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             const FseView tv = fse[k].mode == 2 ? view(fse[k]) : view(pre[k]);
             seq_chain_wave(tv, coded, nseq, k == 0 ? 0u : k == 1 ? 16u : 8u, chains + (uint64_t)k * kZBlockSeq,
                            reinterpret_cast<uint16_t*>(chains + 3ull * kZBlockSeq) + (uint64_t)k * kZBlockSeq,
-                           &ctl.seq_last[k], lane);
+                           &ctl.seq_last[k], lane, role_probe && k == 0 ? g_zprobe : nullptr);
             __threadfence_block();
         }
+        if (wave == 1) role_end(20);
+        if (wave == 0 && role_probe) zt = wall_clock64();
         if (tid == 0) {
             uint8_t* o = lit_out + lsz;
             uint8_t* const o0 = o;
@@ -1649,6 +1859,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         // ---- the literal section
         write_literals(E, ctl, W, hist, make_uint4(bmw[0], bmw[1], bmw[2], bmw[3]), litbase, bbase, nlit, lm, four, seg,
                        lit_out, tid, nseq < kZRuns ? nseq + 1 : 0u);
+        if (wave == 0) role_end(21);
         // ---- sequences bit stream: per-sequence bit counts, a block scan, then every
         // thread writes its range of sequences (the last sequence first in the stream) with
         // atomicOr into the zeroed words
@@ -1959,14 +2170,14 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
             return e && e[0] == '1';
         }();
         if (compress && zprobe) {
-            const unsigned long long z[24] = {};
+            const unsigned long long z[32] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
         }
         if (compress)
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
                                ni, zs.slots, d_sizes, zs.seqs, zs.coded, zs.chains, zprobe ? 1 : 0);
         if (compress && zprobe) {
-            unsigned long long h[24] = {};
+            unsigned long long h[32] = {};
             (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
             (void)hipStreamSynchronize(st);
             const double nb = h[10] ? (double)h[10] : 1.0;
@@ -1974,11 +2185,16 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
                          "zstd probe (workgroup 0, us per block over %llu blocks, %.0f sequences, %.0f literals per "
                          "block): stage %.1f parse %.1f litmap %.1f litmode %.1f codehist %.1f tables %.1f chains %.1f "
                          "literals %.1f seqstream %.1f end %.1f | wave 0: history %.1f rounds+walk %.1f | litmap: bitmap %.1f "
-                         "sampled %.1f\n",
+                         "sampled %.1f | roles: litmode %.1f repcode %.1f LLtable %.1f LLchain %.1f litsection %.1f | long LL "
+                         "chains %llu: pass 1 %.1f rounds %.1f (%.2f rounds) | Huffman: rank %.1f merge %.1f lengths %.1f codes "
+                         "%.1f describe %.1f\n",
                          h[10], h[11] / nb, h[12] / nb, h[0] / nb / 100, h[1] / nb / 100, h[2] / nb / 100,
                          h[3] / nb / 100, h[4] / nb / 100, h[5] / nb / 100, h[6] / nb / 100, h[7] / nb / 100,
                          h[8] / nb / 100, h[9] / nb / 100, h[13] / nb / 100, h[14] / nb / 100, h[15] / nb / 100,
-                         h[16] / nb / 100);
+                         h[16] / nb / 100, h[17] / nb / 100, h[18] / nb / 100, h[19] / nb / 100, h[20] / nb / 100,
+                         h[21] / nb / 100, h[25], h[25] ? h[22] / (double)h[25] / 100 : 0.0,
+                         h[25] ? h[23] / (double)h[25] / 100 : 0.0, h[25] ? h[24] / (double)h[25] : 0.0,
+                         h[26] / nb / 100, h[27] / nb / 100, h[28] / nb / 100, h[29] / nb / 100, h[30] / nb / 100);
         }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
