@@ -18,7 +18,7 @@
 //            when at most 128 are transmitted else FSE-compressed (two interleaved states,
 //            accuracy <= 6); 1 stream below 256 literals, else 4 streams + jump table;
 //            Huffman only when its estimate beats raw -- first on the literals at block
-//            positions divisible by 4 (cheap: random literals never build a histogram of
+//            positions divisible by 16 (cheap: random literals never build a histogram of
 //            all bytes), then on all of them;
 //   sequences per stream (LL / OF / ML) the cheapest of predefined, RLE and FSE-compressed
 //            (own table, normalised counts), by an integer cost estimate; offsets as
@@ -29,7 +29,8 @@
 // Parse (per 64 KiB block; 16 KiB sub-blocks = one GPU wave each, own hash table):
 //   rounds of kRound positions sampled every `step` bytes (step 1 after a round with a
 //   match, doubling to kMaxStep without -- kHistMaxStep in the history before the
-//   sub-block, whose last step the sub-block's first round keeps, up to kMaxStep; a round starts at the end of a match that ran past the previous one, the
+//   sub-block, in rounds of kHistRound, whose last step the sub-block's first round keeps,
+//   up to kMaxStep; a round starts at the end of a match that ran past the previous one, the
 //   positions inside it are not searched); per position the candidates are (a) the table
 //   (1 + the last position of an EARLIER round with the same hash of kHashBytes bytes),
 //   (b) the run candidate p - 1; lengths = common prefix capped at kCap (and the
@@ -50,7 +51,7 @@ namespace {
 constexpr uint32_t kBlock = 64 * 1024;
 constexpr uint32_t kSub = 8192;     // one GPU wave's sub-block
 constexpr uint32_t kHist = 16384;   // window before a sub-block (reaches into the previous block)
-constexpr uint32_t kRound = 256, kMaxStep = 8, kHistMaxStep = 32;
+constexpr uint32_t kRound = 256, kHistRound = 512, kMaxStep = 8, kHistMaxStep = 32;
 constexpr uint32_t kHashLog = 12, kCap = 32, kMinMatch = 5;
 constexpr uint32_t kHufStreams = 48 * 1024;  // largest Huffman stream bytes of a block
 
@@ -92,9 +93,9 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
         // bytes equal its table or run candidate's, doubling to kHistMaxStep without)
         uint32_t hs = 1;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
-            rn = r0 + kRound * hs;
-            uint32_t pos[kRound], cand[kRound], np = 0;
-            for (uint32_t j = 0; j < kRound && r0 + j * hs < s0; ++j) pos[np++] = r0 + j * hs;
+            rn = r0 + kHistRound * hs;
+            uint32_t pos[kHistRound], cand[kHistRound], np = 0;
+            for (uint32_t j = 0; j < kHistRound && r0 + j * hs < s0; ++j) pos[np++] = r0 + j * hs;
             for (uint32_t k = 0; k < np; ++k) cand[k] = pos[k] + hb <= N ? table[hash5(b + pos[k])] : 0;
             bool hit = false;
             for (uint32_t k = 0; k < np; ++k) {
@@ -567,7 +568,7 @@ void raw_literals(std::vector<uint8_t>& o, const uint8_t* lit, uint32_t n, uint3
         o.push_back(lit[0]);
 }
 
-// samp = the literal bytes at block positions divisible by 4 (a first, cheap estimate)
+// samp = the literal bytes at block positions divisible by 16 (a first, cheap estimate)
 void literals(std::vector<uint8_t>& o, const std::vector<uint8_t>& lit, const std::vector<uint8_t>& samp) {
     const uint32_t n = (uint32_t)lit.size();
     if (n >= 32 && !samp.empty()) {  // sampled estimate: clearly incompressible literals stay raw
@@ -869,7 +870,7 @@ size_t block(const uint8_t* src, uint32_t n, uint32_t avail, bool last, uint8_t*
     uint32_t at = 0;
     auto run = [&](uint32_t a, uint32_t e) {
         lit.insert(lit.end(), src + a, src + e);
-        for (uint32_t p = (a + 3) & ~3u; p < e; p += 4) samp.push_back(src[p]);
+        for (uint32_t p = (a + 15) & ~15u; p < e; p += 16) samp.push_back(src[p]);
     };
     for (const Seq& e : seqs) {
         run(at, e.pos);

@@ -67,6 +67,8 @@ constexpr uint32_t kZSub = 8192;     // one wave's sub-block
 constexpr uint32_t kZHist = 16384;   // window before a sub-block
 constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8, kZHistMaxStep = 32;
 constexpr int kZPer = kZRound / 64;  // positions per lane and round
+constexpr uint32_t kZHistRound = 512;  // history rounds (no walk: wider, fewer)
+constexpr int kZPerH = kZHistRound / 64;
 constexpr uint32_t kZTab = 1u << kZHashLog;
 constexpr uint32_t kZStageWords = (kZHist + kEncBlock) / 16 + 3;  // 16-byte words at any alignment + 2 zero words
 constexpr uint32_t kZSubSeq = kZSub / kZMin + 2;                  // sequences one sub-block can emit
@@ -884,11 +886,11 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
         // history: accelerated rounds over [wlo, s0)
         uint32_t hs = 1;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
-            rn = r0 + kZRound * hs;
-            uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
-            bool ok[kZPer];
+            rn = r0 + kZHistRound * hs;
+            uint32_t h[kZPerH], t[kZPerH], wp[kZPerH], b4[kZPerH];
+            bool ok[kZPerH];
 #pragma unroll
-            for (int i = 0; i < kZPer; ++i) {
+            for (int i = 0; i < kZPerH; ++i) {
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
                 ok[i] = p < s0 && p + 5 <= N;
                 const uint32_t pc = ok[i] ? p : wlo;
@@ -897,13 +899,13 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 t[i] = tw[h[i]];
             }
 #pragma unroll
-            for (int i = 0; i < kZPer; ++i) {
+            for (int i = 0; i < kZPerH; ++i) {
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
                 if (ok[i]) tab_max(&tw[h[i]], p - wlo + 1);
             }
             bool hit = false;
 #pragma unroll
-            for (int i = 0; i < kZPer; ++i) {
+            for (int i = 0; i < kZPerH; ++i) {
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
                 const uint32_t c = ok[i] && t[i] ? wlo + t[i] - 1 : wlo;
                 const uint32_t b = wp[i] & 0xFF;
@@ -935,7 +937,10 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
                 if (p < se && p + 5 <= N) tab_max(&tw[h[i]], p - wlo + 1);
             }
-            uint32_t Lm[kZPer], Cm[kZPer];
+            // per position: its table candidate and which candidates match 5 bytes (bit 2i:
+            // the table's, 2i + 1: the run's p - 1); the lengths are measured by the walk,
+            // for the positions it takes only
+            uint32_t Cm[kZPer], F = 0;
             unsigned long long m[kZPer];
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
@@ -949,20 +954,14 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 const uint32_t b = wp[i] & 0xFF;
                 bool mr = live && p > wlo && wp[i] == b * 0x01010101u && b4[i] == b;
                 if (mr) mr = W.byte(p - 1) == b;
-                uint32_t L = 0, C = c;
-                if (mt || mr) {  // rare: lengths to the cap (within the sub-block)
-                    const uint32_t lim = min(se - p, kZCap);
-                    const uint32_t Lt = mt ? 5 + win_prefix(W, c + 5, p + 5, lim - 5) : 0;
-                    const uint32_t Lr = mr ? 5 + win_prefix(W, p + 4, p + 5, lim - 5) : 0;
-                    L = Lt;
-                    if (Lr > Lt) {
-                        L = Lr;
-                        C = p - 1;
-                    }
-                }
-                Lm[i] = L;
-                Cm[i] = C;
-                m[i] = __ballot(L != 0);
+                Cm[i] = c;
+                F |= (mt ? 1u : 0u) << (2 * i) | (mr ? 2u : 0u) << (2 * i);
+                m[i] = __ballot(mt || mr);
+            }
+            uint64_t t_walk = 0;
+            if (probe) {
+                t_walk = wall_clock64();
+                probe[33] += 1;  // rounds
             }
             // the greedy walk (wave-uniform); bit q = position r0 + q * step
             bool found = false;
@@ -982,15 +981,39 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 const bool have = q < kZRound && mm != 0;
                 const int l = have ? __builtin_ctzll(mm) : 0;
                 const uint32_t ph = uni(have ? r0 + (wi * 64 + (uint32_t)l) * step : min(rn, se));
+                if (!have && !(rep && cur < ph)) break;  // nothing left in this round
                 // every LDS read of the step issued before the first ballot: the repeat-match
                 // test over [cur, min(ph, cur + 64)), and for the hash match at ph the
                 // catch-up bytes before it and the first 256 bytes after its capped length
                 uint32_t hl = 0, hsrc = 0;
                 if (have) {
-                    const uint32_t Lw = wi == 0 ? Lm[0] : wi == 1 ? Lm[1] : wi == 2 ? Lm[2] : Lm[3];
                     const uint32_t Cw = wi == 0 ? Cm[0] : wi == 1 ? Cm[1] : wi == 2 ? Cm[2] : Cm[3];
-                    hl = (uint32_t)__builtin_amdgcn_readlane((int)Lw, l);
-                    hsrc = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
+                    const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
+                    const uint32_t f = ((uint32_t)__builtin_amdgcn_readlane((int)F, l) >> (2 * wi)) & 3u;
+                    hl = 5;
+                    hsrc = f & 1u ? ct : ph - 1;
+                    if (f == 3u) {
+                        // both: the longer within the cap (and the sub-block) wins, ties the
+                        // table's -- lanes 0-7 measure the table's, 8-15 the run's, 4 bytes each
+                        const uint32_t lim = min(se - ph, kZCap);
+                        const uint32_t k = (uint32_t)lane & 7u;
+                        const uint32_t src = lane < 8 ? ct : ph - 1;
+                        const uint32_t x = ph + 4 * k;
+                        uint32_t mis = 4;
+                        if (lane < 16) {
+                            const uint32_t d = W.word(src + 4 * k) ^ W.word(x);
+                            if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
+                        }
+                        const unsigned long long bt = __ballot(lane < 8 && mis < 4);
+                        const unsigned long long br = __ballot(lane >= 8 && lane < 16 && mis < 4) >> 8;
+                        const uint32_t ft = bt ? (uint32_t)__builtin_ctzll(bt) : 8u;
+                        const uint32_t fr = br ? (uint32_t)__builtin_ctzll(br) : 8u;
+                        const uint32_t Lt = min(lim, 4 * ft + (bt ? (uint32_t)__builtin_amdgcn_readlane((int)mis, (int)ft) : 0u));
+                        const uint32_t Lr =
+                            min(lim, 4 * fr + (br ? (uint32_t)__builtin_amdgcn_readlane((int)mis, (int)(8 + fr)) : 0u));
+                        hsrc = Lr > Lt ? ph - 1 : ct;
+                        hl = Lr > Lt ? Lr : Lt;
+                    }
                 }
                 const uint32_t kk = (uint32_t)lane;
                 const uint32_t x = cur + kk;
@@ -1059,6 +1082,7 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 found = true;
                 q = uni((cur - r0 + step - 1) >> lstep);
             }
+            if (probe) probe[32] += wall_clock64() - t_walk;  // walk time
             step = found ? 1 : min(2 * step, kZMaxStep);
             lstep = 31 - __builtin_clz(step);
             if (cur > rn) rn = cur;  // positions inside a match that ran past the round: not searched
@@ -1452,8 +1476,9 @@ __device__ __noinline__ void rep_code_wave(const Ctl& ctl, const Seq* __restrict
 // of the wave doing it): 17 literal mode (wave 0), 18 repeat coding (wave 1), 19 LL table
 // (wave 1), 20 LL state chain (wave 1), 21 literal section (wave 0); long LL chains: 22 pass
 // 1, 23 rounds (ticks), 24 rounds, 25 chains; Huffman (wave 0): 26 rank, 27 merge, 28
-// lengths, 29 canonical codes, 30 description.
-__device__ unsigned long long g_zprobe[32];
+// lengths, 29 canonical codes, 30 description; 32/33 wave 0's walk ticks / rounds, 34 + w
+// wave w's parse.
+__device__ unsigned long long g_zprobe[48];
 #define ZMARK(ph)                                  \
     do {                                           \
         if (probe) {                               \
@@ -1520,6 +1545,17 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
         const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(wsrc) & 15);
         const uint8_t* const a0 = wsrc - r;
         const uint32_t nw = (N + r + 15) >> 4;
+        // (with the RLE test: every block byte, LDS bytes [r + hist, r + N), equal to the first)
+        const uint32_t b0 = data[(c0 - base) + off];
+        const uint32_t bb = b0 * 0x01010101u, blo = r + hist, bhi = r + N;
+        auto same_dw = [&](uint32_t a, uint32_t val) {  // the dword at LDS byte a
+            if (a + 4 <= blo || a >= bhi) return true;
+            uint32_t mk = 0xFFFFFFFFu;
+            if (a < blo) mk &= 0xFFFFFFFFu << (8 * (blo - a));
+            if (a + 4 > bhi) mk &= 0xFFFFFFFFu >> (8 * (a + 4 - bhi));
+            return ((val ^ bb) & mk) == 0;
+        };
+        bool same = true;
         for (uint32_t i0 = tid; i0 < nw; i0 += 4 * kZThreads) {
             v4u v[4];
 #pragma unroll
@@ -1530,39 +1566,34 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint32_t i = i0 + kZThreads * q;
-                if (i < nw) stage[i] = make_uint4(v[q].x, v[q].y, v[q].z, v[q].w);
+                if (i < nw) {
+                    stage[i] = make_uint4(v[q].x, v[q].y, v[q].z, v[q].w);
+                    same = same && same_dw(16 * i, v[q].x) && same_dw(16 * i + 4, v[q].y) &&
+                           same_dw(16 * i + 8, v[q].z) && same_dw(16 * i + 12, v[q].w);
+                }
             }
         }
         if (tid < 2) stage[nw + tid] = make_uint4(0, 0, 0, 0);  // word reads past the end stay defined
-        __syncthreads();
+        // ---- RLE block: every byte equal
+        if (__syncthreads_and(same)) {
+            ZMARK(0);
+            if (tid == 0) {
+                write_block_header(out, last, 1, n);
+                out[3] = (uint8_t)b0;
+                sizes[k] = 4;
+            }
+            continue;
+        }
         ZMARK(0);
         const Win W{reinterpret_cast<const uint32_t*>(stage), r};
-
-        // ---- RLE block: every byte equal
-        {
-            const uint32_t b0 = W.byte(hist);
-            int same = 1;
-            for (uint32_t p = hist + 4 * tid; p < N; p += 4 * kZThreads) {
-                if (p + 4 <= N)
-                    same &= W.word(p) == b0 * 0x01010101u;
-                else
-                    for (uint32_t q = p; q < N; ++q) same &= W.byte(q) == b0;
-            }
-            if (__syncthreads_and(same)) {
-                if (tid == 0) {
-                    write_block_header(out, last, 1, n);
-                    out[3] = (uint8_t)b0;
-                    sizes[k] = 4;
-                }
-                continue;
-            }
-        }
 
         // ---- parse: wave w owns the sub-block [s0, se) (window positions)
         {
             uint32_t ns = 0, lastend = 0;
+            const uint64_t tw0 = probe_on && blockIdx.x == 0 ? wall_clock64() : 0;
             parse_subblock(W, tabs, wseq_all, hist, N, wave, lane, &ns, &lastend,
                            probe_on && blockIdx.x == 0 && wave == 0 ? g_zprobe : nullptr);
+            if (probe_on && blockIdx.x == 0 && lane == 0) atomicAdd(&g_zprobe[34 + wave], wall_clock64() - tw0);
             if (lane == 0) {
                 ctl.nseq[wave] = ns;
                 ctl.lastend[wave] = lastend;
@@ -1628,15 +1659,15 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
             bmw[i] = E.bitmap[4 * tid + i];
             cnt_t += __builtin_popcount(bmw[i]);
         }
-        // the sampled histogram first: literals at block positions divisible by 4 (one
-        // predicated LDS atomic per 4 positions); the full one only when the sample says
+        // the sampled histogram first: literals at block positions divisible by 16 (one
+        // predicated LDS atomic per 16 positions); the full one only when the sample says
         // Huffman may pay (random literals never need it)
         uint32_t* const wh = E.streams + wave * 256;
         uint32_t samp_t = 0;
 #pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            if ((bmw[k >> 3] >> ((4 * k) & 31)) & 1u) {
-                atomicAdd(&wh[W.byte(hist + 128 * tid + 4 * k)], 1u);
+        for (int k = 0; k < 8; ++k) {
+            if ((bmw[k >> 1] >> ((16 * k) & 31)) & 1u) {
+                atomicAdd(&wh[W.byte(hist + 128 * tid + 16 * k)], 1u);
                 ++samp_t;
             }
         }
@@ -2170,14 +2201,14 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
             return e && e[0] == '1';
         }();
         if (compress && zprobe) {
-            const unsigned long long z[32] = {};
+            const unsigned long long z[48] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
         }
         if (compress)
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
                                ni, zs.slots, d_sizes, zs.seqs, zs.coded, zs.chains, zprobe ? 1 : 0);
         if (compress && zprobe) {
-            unsigned long long h[32] = {};
+            unsigned long long h[48] = {};
             (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
             (void)hipStreamSynchronize(st);
             const double nb = h[10] ? (double)h[10] : 1.0;
@@ -2187,14 +2218,16 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
                          "literals %.1f seqstream %.1f end %.1f | wave 0: history %.1f rounds+walk %.1f | litmap: bitmap %.1f "
                          "sampled %.1f | roles: litmode %.1f repcode %.1f LLtable %.1f LLchain %.1f litsection %.1f | long LL "
                          "chains %llu: pass 1 %.1f rounds %.1f (%.2f rounds) | Huffman: rank %.1f merge %.1f lengths %.1f codes "
-                         "%.1f describe %.1f\n",
+                         "%.1f describe %.1f | wave 0 walk %.1f in %.1f rounds | parse by wave %.1f %.1f %.1f %.1f %.1f %.1f %.1f %.1f\n",
                          h[10], h[11] / nb, h[12] / nb, h[0] / nb / 100, h[1] / nb / 100, h[2] / nb / 100,
                          h[3] / nb / 100, h[4] / nb / 100, h[5] / nb / 100, h[6] / nb / 100, h[7] / nb / 100,
                          h[8] / nb / 100, h[9] / nb / 100, h[13] / nb / 100, h[14] / nb / 100, h[15] / nb / 100,
                          h[16] / nb / 100, h[17] / nb / 100, h[18] / nb / 100, h[19] / nb / 100, h[20] / nb / 100,
                          h[21] / nb / 100, h[25], h[25] ? h[22] / (double)h[25] / 100 : 0.0,
                          h[25] ? h[23] / (double)h[25] / 100 : 0.0, h[25] ? h[24] / (double)h[25] : 0.0,
-                         h[26] / nb / 100, h[27] / nb / 100, h[28] / nb / 100, h[29] / nb / 100, h[30] / nb / 100);
+                         h[26] / nb / 100, h[27] / nb / 100, h[28] / nb / 100, h[29] / nb / 100, h[30] / nb / 100,
+                         h[32] / nb / 100, h[33] / nb, h[34] / nb / 100, h[35] / nb / 100, h[36] / nb / 100,
+                         h[37] / nb / 100, h[38] / nb / 100, h[39] / nb / 100, h[40] / nb / 100, h[41] / nb / 100);
         }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);
