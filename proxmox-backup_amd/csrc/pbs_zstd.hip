@@ -121,24 +121,37 @@ __device__ __forceinline__ uint32_t hash5(uint32_t w, uint32_t b4) {
 // table[h] = max(table[h], v) for this wave's lanes: write, read back, repeat while a
 // smaller value of another lane of the same instruction landed (lockstep: the survivors
 // only ever raise it)
+// (the LDS address space spelled out: a volatile generic access is not narrowed to LDS by
+// the compiler and would go out as flat loads and stores, waiting on the memory counter)
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 __device__ __forceinline__ void tab_max(uint16_t* e, uint32_t v) {
-    volatile uint16_t* ve = e;
+    volatile lds_u16* ve = (volatile lds_u16*)e;
     for (;;) {
         *ve = (uint16_t)v;
         if (*ve >= v) break;
     }
 }
 
-// common prefix of window positions a < b, at most lim bytes (word compares)
-__device__ __forceinline__ uint32_t win_prefix(const Win& W, uint32_t a, uint32_t b, uint32_t lim) {
-    uint32_t L = 0;
-    while (L + 4 <= lim) {
-        const uint32_t x = W.word(a + L) ^ W.word(b + L);
-        if (x) return L + ((uint32_t)__builtin_ctz(x) >> 3);
-        L += 4;
-    }
-    while (L < lim && W.byte(a + L) == W.byte(b + L)) ++L;
-    return L;
+// tab_max over a lane's K positions: all writes, then all read-backs (in order: LDS ops of
+// a wave complete in issue order), then the rare retries
+template <int K>
+__device__ __forceinline__ void tab_max_batch(uint16_t* tw, const uint32_t* h, const uint32_t* v, const bool* ok) {
+#if PBS_ZV_SERIALTAB
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        if (ok[i]) tab_max(&tw[h[i]], v[i]);
+    return;
+#endif
+    volatile lds_u16* const base = (volatile lds_u16*)tw;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        if (ok[i]) base[h[i]] = (uint16_t)v[i];
+    uint32_t rb[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) rb[i] = ok[i] ? (uint32_t)base[h[i]] : 0xFFFFu;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        if (rb[i] < v[i]) tab_max(&tw[h[i]], v[i]);
 }
 
 // a wave-uniform value, provably so (SGPR)
@@ -294,17 +307,25 @@ struct PreT {
     int32_t dfs[53];
     int32_t log;
 };
+// Address spaces spelled out where a noinline function receives LDS or global pointers:
+// the compiler cannot always narrow a generic pointer and would emit flat accesses, which
+// wait on both counters (an LDS lookup then waits for every outstanding global load).
+typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+typedef __attribute__((address_space(3))) const int32_t lds_ci32;
+#define PBS_GLOBAL __attribute__((address_space(1)))
 struct FseView {
-    const uint16_t* next;
-    const int32_t* dnb;
-    const int32_t* dfs;
+    lds_cu16* next;
+    lds_ci32* dnb;
+    lds_ci32* dfs;
     uint32_t log;
 };
 
-__device__ __noinline__ void fse_build(FseT& t, const int16_t* norm, int nsym, int log) {
+// (norm: the predefined counts in global memory, or a table's own counts in LDS)
+__device__ __noinline__ void fse_build(FseT& t_g, const int16_t* norm, int nsym, int log) {
+    __attribute__((address_space(3))) FseT& t = *(__attribute__((address_space(3))) FseT*)&t_g;
     const int size = 1 << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
     int high = size - 1;
-    int32_t* const cum = t.cum;
+    __attribute__((address_space(3))) int32_t* const cum = t.cum;
     cum[0] = 0;
     for (int s = 0; s < nsym; ++s) {
         if (norm[s] == -1) {
@@ -346,7 +367,9 @@ __device__ __noinline__ void fse_build(FseT& t, const int16_t* norm, int nsym, i
 // positions of the spread sequence (j * step) & mask that are <= high (cs = exclusive
 // prefix of the positive counts); next[] takes, per symbol, its cells in increasing order
 // (rank among the same symbol by ballots, 64 cells at a time).
-__device__ __noinline__ void fse_build_wave(FseT& t, const int16_t* norm, int nsym, int log, int lane) {
+__device__ __noinline__ void fse_build_wave(FseT& t_g, const int16_t* norm_g, int nsym, int log, int lane) {
+    __attribute__((address_space(3))) FseT& t = *(__attribute__((address_space(3))) FseT*)&t_g;
+    const __attribute__((address_space(3))) int16_t* const norm = (const __attribute__((address_space(3))) int16_t*)norm_g;
     const uint32_t size = 1u << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
     const int c = lane < nsym ? norm[lane] : 0;
     const uint32_t cells = c == -1 ? 1u : (c > 0 ? (uint32_t)c : 0u);
@@ -354,7 +377,7 @@ __device__ __noinline__ void fse_build_wave(FseT& t, const int16_t* norm, int ns
     const uint32_t ci = wave_incl(cells, lane), si = wave_incl(spread, lane), li = wave_incl(low, lane);
     const uint32_t nlow = (uint32_t)__builtin_amdgcn_readlane((int)li, 63);
     const uint32_t high = size - 1 - nlow;
-    uint16_t* const spc = t.next;  // (scratch until next[] is written below)
+    __attribute__((address_space(3))) uint16_t* const spc = t.next;  // (scratch until next[] is written below)
     if (lane < nsym) {
         t.cum[lane] = (int32_t)(ci - cells);
         spc[lane] = (uint16_t)(si - spread);
@@ -422,8 +445,12 @@ __device__ __noinline__ void fse_build_wave(FseT& t, const int16_t* norm, int ns
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ FseView view(const FseT& t) { return FseView{t.next, t.dnb, t.dfs, (uint32_t)t.log}; }
-__device__ __forceinline__ FseView view(const PreT& t) { return FseView{t.next, t.dnb, t.dfs, (uint32_t)t.log}; }
+__device__ __forceinline__ FseView view(const FseT& t) {
+    return FseView{(lds_cu16*)t.next, (lds_ci32*)t.dnb, (lds_ci32*)t.dfs, (uint32_t)t.log};
+}
+__device__ __forceinline__ FseView view(const PreT& t) {
+    return FseView{(lds_cu16*)t.next, (lds_ci32*)t.dnb, (lds_ci32*)t.dfs, (uint32_t)t.log};
+}
 
 __device__ __forceinline__ uint32_t fse_init(const FseView& t, uint32_t s) {
     const uint32_t nb = (uint32_t)((t.dnb[s] + (1 << 15)) >> 16);
@@ -718,10 +745,13 @@ __device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scra
 // differs from its left neighbour's end re-runs from that end until its state meets the
 // recorded one (the rest of its record is then already right).  Lane 0 starts from the
 // true state, so after r rounds lanes 0..r are exact; usually one round settles all.
-__device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__ coded, uint32_t ns,
-                                            uint32_t shift, uint32_t* __restrict__ chain,
-                                            uint16_t* __restrict__ states, uint32_t* last, int lane,
+__device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__ coded_g, uint32_t ns,
+                                            uint32_t shift, uint32_t* __restrict__ chain_g,
+                                            uint16_t* __restrict__ states_g, uint32_t* last, int lane,
                                             unsigned long long* probe) {
+    const PBS_GLOBAL Coded* const coded = (const PBS_GLOBAL Coded*)coded_g;
+    PBS_GLOBAL uint32_t* const chain = (PBS_GLOBAL uint32_t*)chain_g;
+    PBS_GLOBAL uint16_t* const states = (PBS_GLOBAL uint16_t*)states_g;
     const uint32_t m = ns - 1;
     if (m < 128) {  // short: one lane, serially (the rounds would cost more than they save)
         // the wave loads 64 codes at a time, lane 0 takes them by readlane
@@ -820,12 +850,12 @@ __device__ __forceinline__ uint32_t seq_bits(const Coded& x, uint32_t q, uint32_
 // a thread's bits into the zeroed stream words (atomicOr: its first and last words are
 // shared with its neighbours)
 struct OrBits {
-    uint32_t* w;
+    PBS_GLOBAL uint32_t* w;
     uint32_t wi;
     uint64_t acc;
     uint32_t n;
     __device__ void init(uint32_t* words, uint32_t bit) {
-        w = words;
+        w = (PBS_GLOBAL uint32_t*)words;
         wi = bit >> 5;
         n = bit & 31;
         acc = 0;
@@ -834,14 +864,14 @@ struct OrBits {
         acc |= (v & ((1ull << nb) - 1ull)) << n;  // nb <= 31
         n += nb;
         if (n >= 32) {
-            if ((uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
+            if ((uint32_t)acc) __hip_atomic_fetch_or(&w[wi], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ++wi;
             acc >>= 32;
             n -= 32;
         }
     }
     __device__ void done() {
-        if (n && (uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
+        if (n && (uint32_t)acc) __hip_atomic_fetch_or(&w[wi], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 };
 
@@ -868,15 +898,15 @@ __device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) 
 
 // The parse of one 8 KiB sub-block by ONE WAVE (wave w: window positions [s0, se)):
 // history rounds, then the rounds + greedy walk; the sequences go to wseq (block
-// positions), their count to *ns_out, the end of the last match to *lastend_out.
-__device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ tabs, Seq* __restrict__ wseq_all,
-                                            uint32_t hist, uint32_t N, int wave, int lane, uint32_t* ns_out,
-                                            uint32_t* lastend_out, unsigned long long* probe) {
+// positions); returns their count | the end of the last match (block position) << 32.
+__device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restrict__ tabs, Seq* __restrict__ wseq_g,
+                                                uint32_t hist, uint32_t N, int wave, int lane,
+                                                unsigned long long* probe) {
+    PBS_GLOBAL uint32_t* const wseq_w = (PBS_GLOBAL uint32_t*)(wseq_g + (uint64_t)wave * kZSubSeq);
     const uint64_t t_in = probe ? wall_clock64() : 0;
     uint64_t t_hist = t_in;
     const uint32_t s0 = hist + (uint32_t)wave * kZSub;
     uint32_t ns = 0, lastend = 0;
-    Seq* const wseq = wseq_all + (uint64_t)wave * kZSubSeq;
     if (s0 < N) {
         const uint32_t se = min(s0 + kZSub, N);
         const uint32_t wlo = s0 - min(s0, kZHist);
@@ -887,32 +917,52 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
         uint32_t hs = 1;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kZHistRound * hs;
-            uint32_t h[kZPerH], t[kZPerH], wp[kZPerH], b4[kZPerH];
+            uint32_t h[kZPerH], t[kZPerH], wp[kZPerH], b4[kZPerH], lo[kZPerH], hi[kZPerH], o3[kZPerH];
             bool ok[kZPerH];
+            // all the round's LDS reads in flight together (the scheduler would otherwise
+            // wait for each before issuing the next)
 #pragma unroll
             for (int i = 0; i < kZPerH; ++i) {
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
                 ok[i] = p < s0 && p + 5 <= N;
-                const uint32_t pc = ok[i] ? p : wlo;
-                wp[i] = W.word5(pc, b4[i]);
+                const uint32_t o = (ok[i] ? p : wlo) + W.r;
+                lo[i] = W.w[o >> 2];
+                hi[i] = W.w[(o >> 2) + 1];
+                o3[i] = o & 3;
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * kZPerH, 0);  // the DS reads first
+#pragma unroll
+            for (int i = 0; i < kZPerH; ++i) {
+                b4[i] = (hi[i] >> (8 * o3[i])) & 0xFF;
+                wp[i] = __builtin_amdgcn_alignbyte(hi[i], lo[i], o3[i]);
                 h[i] = hash5(wp[i], b4[i]);
                 t[i] = tw[h[i]];
             }
+            {
+                uint32_t v[kZPerH];
+#pragma unroll
+                for (int i = 0; i < kZPerH; ++i) v[i] = r0 + ((uint32_t)lane + 64 * i) * hs - wlo + 1;
+                tab_max_batch<kZPerH>(tw, h, v, ok);
+            }
+            // the candidates' words: all reads first
+            uint32_t cw[kZPerH], c4[kZPerH];
 #pragma unroll
             for (int i = 0; i < kZPerH; ++i) {
-                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
-                if (ok[i]) tab_max(&tw[h[i]], p - wlo + 1);
+                const uint32_t c = ok[i] && t[i] ? wlo + t[i] - 1 : wlo;
+                const uint32_t o = c + W.r;
+                lo[i] = W.w[o >> 2];
+                hi[i] = W.w[(o >> 2) + 1];
+                o3[i] = o & 3;
             }
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * kZPerH, 0);
             bool hit = false;
 #pragma unroll
             for (int i = 0; i < kZPerH; ++i) {
-                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
-                const uint32_t c = ok[i] && t[i] ? wlo + t[i] - 1 : wlo;
+                c4[i] = (hi[i] >> (8 * o3[i])) & 0xFF;
+                cw[i] = __builtin_amdgcn_alignbyte(hi[i], lo[i], o3[i]);
                 const uint32_t b = wp[i] & 0xFF;
                 const bool run = wp[i] == b * 0x01010101u && b4[i] == b;
-                uint32_t c4;
-                const uint32_t cw = W.word5(c, c4);
-                hit |= ok[i] && t[i] && !run && cw == wp[i] && c4 == b4[i];
+                hit |= ok[i] && t[i] && !run && cw[i] == wp[i] && c4[i] == b4[i];
             }
             hs = __ballot(hit) ? 1 : min(2 * hs, kZHistMaxStep);
         }
@@ -920,23 +970,44 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
         // rounds + walk
         // (the first rounds keep the history's step: no matches there, few here)
         uint32_t cur = s0, step = min(hs, kZMaxStep), lstep = 31 - __builtin_clz(step), rep = 0;
+        uint32_t rep_chk = 0;  // [cur, rep_chk) already tested for a repeat match: none there
         for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
             rn = r0 + kZRound * step;
-            uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer];
+            uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer], lo[kZPer], hi[kZPer], o3[kZPer], pm1[kZPer];
+            bool okp[kZPer];
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
-                const bool ok = p < se && p + 5 <= N;
-                const uint32_t pc = ok ? p : s0;
-                wp[i] = W.word5(pc, b4[i]);
+                okp[i] = p < se && p + 5 <= N;
+                const uint32_t o = (okp[i] ? p : s0) + W.r;
+                lo[i] = W.w[o >> 2];
+                hi[i] = W.w[(o >> 2) + 1];
+                o3[i] = o & 3;
+                pm1[i] = W.byte(p > wlo && okp[i] ? p - 1 : s0);  // (the run candidate's first byte)
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 3 * kZPer, 0);
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                b4[i] = (hi[i] >> (8 * o3[i])) & 0xFF;
+                wp[i] = __builtin_amdgcn_alignbyte(hi[i], lo[i], o3[i]);
                 h[i] = hash5(wp[i], b4[i]);
-                t[i] = ok ? (uint32_t)tw[h[i]] : 0u;
+                t[i] = okp[i] ? (uint32_t)tw[h[i]] : 0u;
             }
+            {
+                uint32_t v[kZPer];
+#pragma unroll
+                for (int i = 0; i < kZPer; ++i) v[i] = r0 + ((uint32_t)lane + 64 * i) * step - wlo + 1;
+                tab_max_batch<kZPer>(tw, h, v, okp);
+            }
+            // the table candidates' words: all reads first
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
-                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
-                if (p < se && p + 5 <= N) tab_max(&tw[h[i]], p - wlo + 1);
+                const uint32_t o = (t[i] ? wlo + t[i] - 1 : s0) + W.r;
+                lo[i] = W.w[o >> 2];
+                hi[i] = W.w[(o >> 2) + 1];
+                o3[i] = o & 3;
             }
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * kZPer, 0);
             // per position: its table candidate and which candidates match 5 bytes (bit 2i:
             // the table's, 2i + 1: the run's p - 1); the lengths are measured by the walk,
             // for the positions it takes only
@@ -947,13 +1018,12 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
                 const bool live = p >= cur && p + 5 <= se;
                 const uint32_t c = t[i] ? wlo + t[i] - 1 : s0;
-                uint32_t c4;
-                const uint32_t cw = W.word5(c, c4);
+                const uint32_t c4 = (hi[i] >> (8 * o3[i])) & 0xFF;
+                const uint32_t cw = __builtin_amdgcn_alignbyte(hi[i], lo[i], o3[i]);
                 const bool mt = live && t[i] && cw == wp[i] && c4 == b4[i];
                 // the run candidate p - 1 matches 5 bytes iff bytes p - 1 .. p + 4 are equal
                 const uint32_t b = wp[i] & 0xFF;
-                bool mr = live && p > wlo && wp[i] == b * 0x01010101u && b4[i] == b;
-                if (mr) mr = W.byte(p - 1) == b;
+                const bool mr = live && p > wlo && wp[i] == b * 0x01010101u && b4[i] == b && pm1[i] == b;
                 Cm[i] = c;
                 F |= (mt ? 1u : 0u) << (2 * i) | (mr ? 2u : 0u) << (2 * i);
                 m[i] = __ballot(mt || mr);
@@ -981,7 +1051,12 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 const bool have = q < kZRound && mm != 0;
                 const int l = have ? __builtin_ctzll(mm) : 0;
                 const uint32_t ph = uni(have ? r0 + (wi * 64 + (uint32_t)l) * step : min(rn, se));
-                if (!have && !(rep && cur < ph)) break;  // nothing left in this round
+                const uint32_t rep_hi = min(ph, cur + 64);  // the repeat test's window end
+#if PBS_ZV_NOREPCHK
+                rep_chk = 0;
+#endif
+                const bool rep_try = rep && rep_hi > max(cur, rep_chk);
+                if (!have && !rep_try) break;  // nothing left in this round
                 // every LDS read of the step issued before the first ballot: the repeat-match
                 // test over [cur, min(ph, cur + 64)), and for the hash match at ph the
                 // catch-up bytes before it and the first 256 bytes after its capped length
@@ -1017,7 +1092,7 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 }
                 const uint32_t kk = (uint32_t)lane;
                 const uint32_t x = cur + kk;
-                const bool okx = rep && x < min(ph, cur + 64) && x >= wlo + rep && x + 5 <= se;
+                const bool okx = rep_try && x < rep_hi && x >= rep_chk && x >= wlo + rep && x + 5 <= se;
                 const uint32_t xc = okx ? x : wlo + rep;
                 const uint32_t ra = W.word(xc), rbw = W.word(xc - rep), r4 = W.byte(xc + 4), r4b = W.byte(xc - rep + 4);
                 const bool okb = have && ph > cur + kk && hsrc > wlo + kk;
@@ -1044,6 +1119,7 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                     mlen = 5;
                     ext = true;
                 } else {
+                    rep_chk = uni(max(rep_chk, rep_hi));  // (no repeat match up to there)
                     if (!have) break;
                     const unsigned long long bb = __ballot(okb && ba == bbv);
                     const uint32_t e = ~bb ? (uint32_t)__builtin_ctzll(~bb) : 64u;
@@ -1074,9 +1150,14 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
                 mpos = uni(mpos);
                 msrc = uni(msrc);
                 mlen = uni(mlen);
-                if (lane == 0 && ns < kZSubSeq) wseq[ns] = Seq{mpos - hist, mlen, mpos - msrc};
+                if (lane == 0 && ns < kZSubSeq) {
+                    wseq_w[3 * ns] = mpos - hist;
+                    wseq_w[3 * ns + 1] = mlen;
+                    wseq_w[3 * ns + 2] = mpos - msrc;
+                }
                 ++ns;
                 rep = mpos - msrc;
+                rep_chk = 0;
                 cur = mpos + mlen;
                 lastend = cur - hist;
                 found = true;
@@ -1092,8 +1173,7 @@ __device__ __noinline__ void parse_subblock(const Win W, uint16_t* __restrict__ 
         probe[13] += t_hist - t_in;
         probe[14] += wall_clock64() - t_hist;
     }
-    *ns_out = ns;
-    *lastend_out = lastend;
+    return (uint64_t)ns | (uint64_t)lastend << 32;
 }
 
 // Literal section mode of a block (ONE WAVE): RLE (one distinct byte), raw, or Huffman
@@ -1403,14 +1483,24 @@ __device__ __forceinline__ void rep_step(uint32_t& ra, uint32_t& rb, uint32_t& r
     }
 }
 
-__device__ __noinline__ void rep_code_wave(const Ctl& ctl, const Seq* __restrict__ wseq_all, Coded* __restrict__ coded,
+__device__ __forceinline__ Seq ld_seq(const PBS_GLOBAL Seq* p) {
+    const PBS_GLOBAL uint32_t* q = (const PBS_GLOBAL uint32_t*)p;
+    return Seq{q[0], q[1], q[2]};
+}
+__device__ __forceinline__ void st_coded(PBS_GLOBAL Coded* p, const Coded& c) {
+    *(PBS_GLOBAL v4u*)p = v4u{c.ll, c.ml, c.ofv, c.codes};
+}
+
+__device__ __noinline__ void rep_code_wave(const Ctl& ctl, const Seq* __restrict__ wseq_g, Coded* __restrict__ coded_g,
                                            uint32_t w2, int lane) {
+    const PBS_GLOBAL Seq* const wseq_all = (const PBS_GLOBAL Seq*)wseq_g;
+    PBS_GLOBAL Coded* const coded = (PBS_GLOBAL Coded*)coded_g;
     uint32_t first = 0, lit_end = 0;
     for (uint32_t v = 0; v < w2; ++v) {
         first += min(ctl.nseq[v], kZSubSeq);
         if (ctl.nseq[v]) lit_end = ctl.lastend[v];
     }
-    const Seq* const ws = wseq_all + (uint64_t)w2 * kZSubSeq;
+    const PBS_GLOBAL Seq* const ws = wseq_all + (uint64_t)w2 * kZSubSeq;
     const uint32_t cnt = min(ctl.nseq[w2], kZSubSeq);
     if (!cnt) return;
     const uint32_t seg = (cnt + 63) / 64;
@@ -1420,14 +1510,14 @@ __device__ __noinline__ void rep_code_wave(const Ctl& ctl, const Seq* __restrict
     auto run = [&](uint32_t from, uint32_t to, uint32_t& ra, uint32_t& rb, uint32_t& rc3, bool write) {
         uint32_t prev_end = from == 0 ? lit_end : 0u;
         if (from > 0) {
-            const Seq p = ws[from - 1];
+            const Seq p = ld_seq(ws + from - 1);
             prev_end = p.pos + p.ml;
         }
         for (uint32_t q0 = from; q0 < to; q0 += 8) {
             Seq e8[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u)  // 8 loads in flight
-                if (q0 + u < to) e8[u] = ws[q0 + u];
+                if (q0 + u < to) e8[u] = ld_seq(ws + q0 + u);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 if (q0 + u >= to) break;
@@ -1438,7 +1528,7 @@ __device__ __noinline__ void rep_code_wave(const Ctl& ctl, const Seq* __restrict
                 rep_step(ra, rb, rc3, e.off, c.ll == 0, c.ofv);
                 if (write) {
                     c.codes = ll_code(c.ll) | ml_code(c.ml) << 8 | highbit(c.ofv) << 16;
-                    coded[first + q0 + u] = c;
+                    st_coded(coded + first + q0 + u, c);
                 }
                 prev_end = e.pos + e.ml;
             }
@@ -1488,7 +1578,7 @@ __device__ unsigned long long g_zprobe[48];
         }                                          \
     } while (0)
 
-__global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
+__global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zstd_block_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, uint8_t* __restrict__ slots,
     uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch, Coded* __restrict__ coded_scratch,
@@ -1589,10 +1679,10 @@ __global__ __launch_bounds__(kZThreads) void zstd_block_kernel(
 
         // ---- parse: wave w owns the sub-block [s0, se) (window positions)
         {
-            uint32_t ns = 0, lastend = 0;
             const uint64_t tw0 = probe_on && blockIdx.x == 0 ? wall_clock64() : 0;
-            parse_subblock(W, tabs, wseq_all, hist, N, wave, lane, &ns, &lastend,
-                           probe_on && blockIdx.x == 0 && wave == 0 ? g_zprobe : nullptr);
+            const uint64_t pr = parse_subblock(W, tabs, wseq_all, hist, N, wave, lane,
+                                               probe_on && blockIdx.x == 0 && wave == 0 ? g_zprobe : nullptr);
+            const uint32_t ns = (uint32_t)pr, lastend = (uint32_t)(pr >> 32);
             if (probe_on && blockIdx.x == 0 && lane == 0) atomicAdd(&g_zprobe[34 + wave], wall_clock64() - tw0);
             if (lane == 0) {
                 ctl.nseq[wave] = ns;
