@@ -594,7 +594,7 @@ void server_stop(pbs_chunker* c) {
 int server_launch(pbs_chunker* c, uint64_t last) {
     ScanServer& sv = c->srv;
     __atomic_store_n(&sv.mb->exited, ~0ull, __ATOMIC_RELEASE);
-    HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.slot_dev, c->prm.mask, c->prm.minimum, last,
+    HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.slot_dev, c->d_table.as<uint32_t>(), c->prm.thr, last,
                                   kServerIdleTicks, sv.flags, sv.stream));
     sv.running = true;
     return PBS_OK;
@@ -1132,7 +1132,7 @@ void destroy(pbs_chunker* c) {
         const ScanServer& sv = c->srv;
         const double n = (double)sv.probe_n;
         std::fprintf(stderr,
-                     "scan server probe: %llu requests, host round trip %.2f us; kernel: staging %.2f us, "
+                     "scan server probe: %llu requests, host round trip %.2f us; kernel: loads + chains %.2f us, "
                      "hash %.2f us, compaction + ack %.2f us (request seen -> acknowledged %.2f us)\n",
                      (unsigned long long)sv.probe_n, sv.probe_rtt_us / n, sv.probe_ticks[0] / n / 100.0,
                      sv.probe_ticks[1] / n / 100.0, sv.probe_ticks[2] / n / 100.0,

@@ -202,13 +202,13 @@ struct alignas(64) ServerMailbox {
                                    // ncand = candidates in cand[] (ascending, absolute), overflow:
                                    // more than kServerCand (nothing usable)
     uint64_t exited;               // last served request when the kernel exited; ~0 while up
-    uint64_t probe[4];             // kSrvProbe: wall_clock64 at request seen, staged, hashed, acked
+    uint64_t probe[4];             // kSrvProbe: wall_clock64 at request seen, chains done, hashed, acked
     uint64_t cand[kServerCand];
 };
 constexpr uint32_t kSrvPollAll = 1;  // launch flag: every wave polls (staggered), not one lane
 constexpr uint32_t kSrvProbe = 2;    // launch flag: per-request phase stamps into probe[]
-hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, uint32_t mask,
-                              uint32_t minimum, uint64_t last_seq, uint64_t idle_ticks,
+hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, const uint32_t* table_rot,
+                              uint32_t thr, uint64_t last_seq, uint64_t idle_ticks,
                               uint32_t flags, hipStream_t stream);
 
 // Makes `dev` the calling thread's current device for a scope (allocations and stream /

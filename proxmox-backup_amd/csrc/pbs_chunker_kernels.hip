@@ -918,12 +918,12 @@ hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid
     return hipGetLastError();
 }
 
-hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, uint32_t mask,
-                              uint32_t minimum, uint64_t last_seq, uint64_t idle_ticks,
+hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, const uint32_t* table_rot,
+                              uint32_t thr, uint64_t last_seq, uint64_t idle_ticks,
                               uint32_t flags, hipStream_t stream) {
     (void)hipGetLastError();
     hipLaunchKernelGGL(scan_server_kernel, dim3(1), dim3(kSrvThreads), 0, stream, mb_dev, slot_dev,
-                       mask, minimum, last_seq, idle_ticks, flags);
+                       table_rot, thr, last_seq, idle_ticks, flags);
     return hipGetLastError();
 }
 

@@ -3,87 +3,95 @@
 //
 // ONE persistent workgroup polls the mailbox (pbs_chunker_internal.h) in fine-grained
 // pinned host memory with 16-byte loads {seq, len | quit, base} (kSrvPollAll: lane 0 of
-// every wave, staggered -- measured no faster, off by default).  A request
-// then costs one more PCIe round trip: the slot's history and data (host memory) are
-// staged in LDS, 32 KiB per pass, all loads in flight at once.  The cut test runs at
-// every position, each of the 256 threads over S = 32, 64 or 128 bytes (the shortest
-// that covers the pass: an 8 KiB read is 64 + 32 steps per lane; the reference's
-// recurrence, chunker.rs:118-165, test :185).
+// every wave, staggered).  A request then costs one more PCIe round trip: every lane loads
+// its 32 bytes of the slot straight into registers (8 KiB per pass over 256 lanes; the
+// next kSrvAhead passes' bytes in flight while one is hashed -- a dependent load of host
+// memory takes ~1.2 us, 8 KiB ~1.6 us, scripts/microbench/mb_poll.hip).
+//
+// The hash at every position without the 64-step warm-up per lane: with the chain
+// Q(j) = rotl(Q(j-1), 1) ^ T[b_j] over the whole slot, h(j) = Q(j) ^ Q(j-64) (rotations are
+// mod 32, so the terms 64 back cancel; the reference's recurrence, chunker.rs:118-165).
+// Lane t owns the 32 bytes at 32 t and runs the chain from its first byte (Q_t); with
+// A_u = Q_u(31) and E_u = Q(32 u - 1) (so E_{u+1} = rotl(E_u, 32) ^ A_u = E_u ^ A_u),
+//     h(32 t + i) = Q_t(i) ^ Q_{t-2}(i) ^ rotl(E_t ^ E_{t-2}, i + 1),
+//     E_t ^ E_{t-2} = A_{t-2} ^ A_{t-1},
+// so a lane needs the chain of the lane two back (LDS rows) and one more total.  The 64
+// bytes before a pass are "lanes" -2 and -1: the slot's history (first pass; their chains
+// by a rotating prefix over 32-lane halves of one wave) or the previous pass's last two
+// rows.  Per byte: one address op, one table read (64 replicas, conflict-free), the
+// chain's two ops, then two for h and half a max -- against ~3x that for a warm-up of 64
+// steps per 32 bytes (the previous kernel: 8 KiB reads 1.22 GiB/s).  16 bytes per lane
+// over 512 lanes measured slower for 8 KiB reads (1.25 vs 1.43 GiB/s: eight waves to
+// synchronize; 256 KiB reads gain, 3.6 vs 2.7 GB/s, from the prefetch kept here).  The
+// table is pre-rotated by the handle (T' = rotl(T, rot)), so h' = rotl(h, rot) and the
+// test (h & mask) >= mask - 2 (:185) is h' >= thr; a max over the lane's positions
+// screens (32 positions per lane), and only lanes with a hit build their bit masks.
+//
 // The hits are compacted in stream order into the mailbox, and after every wave drained
 // its stores the acknowledgement -- seq, candidate count and overflow flag in one 8-byte
-// word -- is stored (system-scope release).  The host applies
-// shall_break's min/max rule to the returned candidates.  Exit: the quit flag, or
-// idle_ticks (wall_clock64, 100 MHz) without a request -- the host relaunches it on the
-// next call (pbs_chunker_capi.cpp server_scan), so a process that stops calling leaves
-// no kernel running.  kSrvProbe: per-request phase stamps (PBS_SERVER_PROBE=1).
+// word -- is stored (system-scope release).  The host applies shall_break's min/max rule
+// to the returned candidates.  Exit: the quit flag, or idle_ticks (wall_clock64, 100 MHz)
+// without a request -- the host relaunches it on the next call (pbs_chunker_capi.cpp
+// server_scan), so a process that stops calling leaves no kernel running.  kSrvProbe:
+// per-request phase stamps (PBS_SERVER_PROBE=1).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "exact_block.h"
 #include "pbs_chunker_internal.h"
 
 namespace pbs {
 
 constexpr int kSrvThreads = 256;  // 4 waves, one per SIMD
-constexpr int kSrvPass = 32 * 1024;  // bytes staged per pass
-static_assert(kSrvPass == 128 * kSrvThreads, "a pass is at most 128 bytes per thread");
+constexpr int kSrvLaneBytes = 32;
+constexpr int kSrvPass = kSrvLaneBytes * kSrvThreads;  // bytes per pass (8 KiB)
+constexpr int kSrvRows = kSrvThreads + 2;              // chain rows: the two before the pass, then one per lane
+constexpr int kSrvAhead = 4;                           // passes whose bytes are in flight
 
 typedef uint32_t srv_u32x4 __attribute__((ext_vector_type(4)));
 
-// hits of the S bytes at sd[B .. B+S) (LDS; sd[B-64 .. B) readable): bit i of word i / 32
-// = the window ending at byte B + i passes the test -- 64 fill steps over the bytes before
-// the segment (the window hash of chunker.rs:118-136), S roll steps (:141-165), the test
-// (:185); one lane per segment, every lane of the workgroup busy
-template <int S>
-__device__ __forceinline__ uint4 lane_hits(const uint8_t* sd, int B, const uint32_t* tab, uint32_t mask,
-                                           uint32_t minimum) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(sd + B - 64);
-    uint32_t d[(64 + S) / 4];
-#pragma unroll
-    for (int k = 0; k < (64 + S) / 4; ++k) d[k] = w[k];
-    uint32_t h = 0;
-#pragma unroll
-    for (int i = 0; i < 64; ++i)
-        h = __builtin_amdgcn_alignbit(h, h, 31) ^ tab[(d[i >> 2] >> (8 * (i & 3))) & 0xffu];
-    uint32_t hw[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        const uint32_t out = (d[i >> 2] >> (8 * (i & 3))) & 0xffu;
-        const uint32_t in = (d[(i + 64) >> 2] >> (8 * (i & 3))) & 0xffu;
-        h = __builtin_amdgcn_alignbit(h, h, 31) ^ tab[out] ^ tab[in];
-        hw[i >> 5] |= ((h & mask) >= minimum ? 1u : 0u) << (i & 31);
-    }
-    return make_uint4(hw[0], hw[1], hw[2], hw[3]);
+// chain row r (32 dwords), dwords [4k, 4k+4) at a swizzled 16-byte slot (ds_*_b128 of
+// lanes 128 bytes apart would hit the same banks)
+__device__ __forceinline__ uint32_t srv_row_off(uint32_t r, uint32_t k) {
+    return r * 128u + ((k ^ (r & 7u)) << 4);
+}
+__device__ __forceinline__ uint32_t srv_row_dw(uint32_t r, uint32_t i) {  // dword i of row r
+    return srv_row_off(r, i >> 2) + 4u * (i & 3u);
 }
 
 __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox* mb,
                                                                   const uint8_t* __restrict__ slot,
-                                                                  uint32_t mask, uint32_t minimum,
-                                                                  uint64_t last_seq,
+                                                                  const uint32_t* __restrict__ table_rot,
+                                                                  uint32_t thr, uint64_t last_seq,
                                                                   uint64_t idle_ticks, uint32_t flags) {
-    __shared__ uint32_t tab[256];
-    __shared__ __attribute__((aligned(16))) uint8_t st[kServerHist + kSrvPass + 128];
+    // T'[b] replicated 64x at byte b * 256 + lane * 4: one v_perm forms the address
+    __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t rows[kSrvRows * 128];
     __shared__ uint32_t wsum[kSrvThreads / 64];
     __shared__ uint32_t s_go;    // 0 polling, 1 serve, 2 exit
     __shared__ uint64_t ctl[2];  // [0] seq | len << 32 [1] base
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool poll_all = (flags & kSrvPollAll) != 0, probe = (flags & kSrvProbe) != 0;
-    for (int i = tid; i < 256; i += kSrvThreads) tab[i] = kBuzhashTable[i];
+    for (int i = tid; i < 256 * 64; i += kSrvThreads) tab[i] = table_rot[i >> 6];
     if (tid == 0) s_go = 0;
     __syncthreads();
+    const uint32_t lane4 = (uint32_t)lane * 4u;
+    auto lookup = [&](uint32_t word, int k) -> uint32_t {  // T'[byte k of word] (this lane's replica)
+        const uint32_t addr = __builtin_amdgcn_perm(word, lane4, 0x0C0C0000u | ((uint32_t)(4 + k) << 8));
+        return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(tab) + addr);
+    };
+    auto rd = [&](uint32_t off) -> uint32_t { return *reinterpret_cast<const uint32_t*>(rows + off); };
     uint32_t last = (uint32_t)last_seq;
     uint64_t t_idle = wall_clock64();
     for (;;) {
-        // poll the request record (one 16-byte load {seq, len | quit, base}); with
-        // kSrvPollAll lane 0 of every wave polls, the waves staggered so that several
-        // PCIe reads are in flight and a new request is seen sooner
+        // poll the request record (one 16-byte load {seq, len, base}); with kSrvPollAll
+        // lane 0 of every wave polls, the waves staggered
         if (lane == 0 && (poll_all || wave == 0)) {
             if (poll_all)
                 for (int d = 0; d < wave; ++d) __builtin_amdgcn_s_sleep(8);
             for (;;) {
                 if (__hip_atomic_load(&s_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-                const srv_u32x4 r = *reinterpret_cast<volatile srv_u32x4*>(&mb->req_seq);  // {seq, len, base}
+                const srv_u32x4 r = *reinterpret_cast<volatile srv_u32x4*>(&mb->req_seq);
                 uint32_t go = 0;
                 if (r.y & kServerQuit) {
                     go = 2;
@@ -109,96 +117,131 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             return;  // uniform
         }
         const uint64_t t_seen = probe ? wall_clock64() : 0;
-        uint64_t t_staged = 0, t_hashed = 0;
+        uint64_t t_loaded = 0, t_hashed = 0;
         const uint32_t seq = (uint32_t)ctl[0], len = (uint32_t)(ctl[0] >> 32);
         const uint64_t base = ctl[1];
+        const srv_u32x4* const src = reinterpret_cast<const srv_u32x4*>(slot + kServerHist);
+        // this lane's 32 bytes of pass p (lanes wholly past the data load nothing)
+        auto load = [&](uint32_t p, srv_u32x4 (&x)[2]) {
+            const uint32_t b = p * (uint32_t)kSrvPass + (uint32_t)tid * kSrvLaneBytes;
+            if (b < len) {
+                x[0] = __builtin_nontemporal_load(src + b / 16);
+                x[1] = __builtin_nontemporal_load(src + b / 16 + 1);
+            }
+        };
+        const uint32_t npass = (len + kSrvPass - 1) / kSrvPass;
+        srv_u32x4 ring[kSrvAhead][2];
+#pragma unroll
+        for (int k = 0; k < kSrvAhead; ++k) {
+            ring[k][0] = ring[k][1] = srv_u32x4{0u, 0u, 0u, 0u};
+            load((uint32_t)k, ring[k]);
+        }
+        // rows 0 and 1: the chains of the 64 history bytes (one byte per lane of wave 0; a
+        // rotating prefix over each 32-lane half: x = rotl(x_{l-d}, d) ^ x_l)
+        if (wave == 0) {
+            uint32_t x = lookup((uint32_t)slot[lane], 0);
+#pragma unroll
+            for (int d = 1; d < 32; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, d, 32);
+                if ((lane & 31) >= d) x ^= __builtin_amdgcn_alignbit(y, y, 32 - d);
+            }
+            *reinterpret_cast<uint32_t*>(rows + srv_row_dw((uint32_t)lane >> 5, (uint32_t)lane & 31u)) = x;
+        }
         uint32_t total = 0;
-        for (uint32_t off = 0; off < len; off += kSrvPass) {
+        auto pass = [&](uint32_t p, srv_u32x4 (&cur)[2]) {
+            const uint32_t off = p * (uint32_t)kSrvPass;
             const uint32_t plen = len - off < (uint32_t)kSrvPass ? len - off : (uint32_t)kSrvPass;
             // stream positions < 63 have no full window (chunker.rs:118-136): never reported
             const uint64_t pos0 = base + off;
             const uint32_t lo_ok = pos0 >= 63 ? 0u : (uint32_t)(63 - pos0);
-            // pass 0 stages the slot's history with the data; later passes keep the
-            // previous pass's last 64 bytes as theirs
-            const uint32_t src0 = off == 0 ? 0u : kServerHist + off;
-            const uint32_t dst0 = off == 0 ? 0u : kServerHist;
-            if (off > 0) {
-                uint8_t v = 0;
-                if (tid < 64) v = st[kSrvPass + tid];
+            const uint32_t d[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+            uint32_t q[32];
+            uint32_t h = 0;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                h = __builtin_amdgcn_alignbit(h, h, 31) ^ lookup(d[i >> 2], i & 3);
+                q[i] = h;
+            }
+            load(p + kSrvAhead, cur);  // the slot's registers are free again
+            if (probe && p == 0) t_loaded = wall_clock64();
+            // this lane's chain is row tid + 2 (the previous pass's readers are done: the
+            // barrier before the row copy below)
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                *reinterpret_cast<srv_u32x4*>(rows + srv_row_off((uint32_t)tid + 2u, (uint32_t)k)) =
+                    srv_u32x4{q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]};
+            __syncthreads();
+            uint32_t p2[32];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const srv_u32x4 v = *reinterpret_cast<const srv_u32x4*>(rows + srv_row_off((uint32_t)tid, (uint32_t)k));
+                p2[4 * k] = v.x;
+                p2[4 * k + 1] = v.y;
+                p2[4 * k + 2] = v.z;
+                p2[4 * k + 3] = v.w;
+            }
+            const uint32_t X = p2[31] ^ rd(srv_row_dw((uint32_t)tid + 1u, 31u));
+            uint32_t hp[32];
+            uint32_t mx = 0;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                hp[i] = q[i] ^ p2[i] ^ __builtin_amdgcn_alignbit(X, X, 31 - i);
+                mx = mx > hp[i] ? mx : hp[i];
+            }
+            // bit i = position off + 32 tid + i passes, within [lo_ok, plen)
+            uint32_t bits = 0;
+            if (mx >= thr) {
+                const int p0 = tid * kSrvLaneBytes;
+#pragma unroll
+                for (int i = 0; i < 32; ++i) bits |= (hp[i] >= thr ? 1u : 0u) << i;
+                const int lo = (int)lo_ok - p0, up = (int)plen - p0;
+                const uint32_t keep_lo = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
+                const uint32_t keep_hi = up >= 32 ? 0xFFFFFFFFu : (up <= 0 ? 0u : (0xFFFFFFFFu >> (32 - up)));
+                bits &= keep_lo & keep_hi;
+            }
+            if (probe && p == 0) t_hashed = wall_clock64();
+            // stream-order compaction (hits are rare: one barrier tells whether any)
+            const uint32_t c = __builtin_popcount(bits);
+            if (__syncthreads_or(c != 0)) {
+                uint32_t x = c;
+#pragma unroll
+                for (int dd = 1; dd < 64; dd <<= 1) {
+                    const uint32_t z = __shfl_up(x, dd, 64);
+                    if (lane >= dd) x += z;
+                }
+                if (lane == 63) wsum[wave] = x;
                 __syncthreads();
-                if (tid < 64) st[tid] = v;
-            }
-            const uint32_t nbytes = off == 0 ? kServerHist + plen : plen;
-            const uint32_t n16 = nbytes / 16;
-            const srv_u32x4* src = reinterpret_cast<const srv_u32x4*>(slot + src0);
-            for (uint32_t i0 = tid; i0 < n16; i0 += 8 * kSrvThreads) {  // 8 loads in flight
-                srv_u32x4 v[8];
+                uint32_t before = total, all = total;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t i = i0 + (uint32_t)u * kSrvThreads;
-                    if (i < n16) v[u] = __builtin_nontemporal_load(src + i);
+                for (int w2 = 0; w2 < kSrvThreads / 64; ++w2) {
+                    before += w2 < wave ? wsum[w2] : 0u;
+                    all += wsum[w2];
                 }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t i = i0 + (uint32_t)u * kSrvThreads;
-                    if (i < n16) *reinterpret_cast<srv_u32x4*>(st + dst0 + 16 * i) = v[u];
-                }
-            }
-            for (uint32_t i = n16 * 16 + tid; i < nbytes; i += kSrvThreads) st[dst0 + i] = slot[src0 + i];
-            __syncthreads();
-            if (probe && off == 0) t_staged = wall_clock64();
-            // the cut test at every position: thread t takes the S bytes at t * S (S = 32,
-            // 64 or 128: the shortest that covers the pass with the 256 threads)
-            const uint32_t S = plen <= 32 * kSrvThreads ? 32u : plen <= 64 * kSrvThreads ? 64u : 128u;
-            uint4 h = make_uint4(0, 0, 0, 0);
-            if (tid * S < plen) {
-                const uint8_t* const sd = st + kServerHist;
-                h = S == 32 ? lane_hits<32>(sd, (int)(tid * S), tab, mask, minimum)
-                    : S == 64 ? lane_hits<64>(sd, (int)(tid * S), tab, mask, minimum)
-                              : lane_hits<128>(sd, (int)(tid * S), tab, mask, minimum);
-                uint32_t hw[4] = {h.x, h.y, h.z, h.w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {  // reportable positions [lo_ok, plen)
-                    const int p0 = (int)(tid * S) + 32 * q;
-                    const int lo = (int)lo_ok - p0, up = (int)plen - p0;
-                    const uint32_t keep_lo = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
-                    const uint32_t keep_hi = up >= 32 ? 0xFFFFFFFFu : (up <= 0 ? 0u : (0xFFFFFFFFu >> (32 - up)));
-                    hw[q] &= q < (int)(S / 32) ? keep_lo & keep_hi : 0u;
-                }
-                h = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-            }
-            if (probe && off == 0) t_hashed = wall_clock64();
-            // stream-order compaction: thread t owns positions [t S, t S + S)
-            const uint32_t c = __builtin_popcount(h.x) + __builtin_popcount(h.y) +
-                               __builtin_popcount(h.z) + __builtin_popcount(h.w);
-            uint32_t x = c;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(x, d, 64);
-                if (lane >= d) x += y;
-            }
-            if (lane == 63) wsum[wave] = x;
-            __syncthreads();
-            uint32_t before = total, all = total;
-#pragma unroll
-            for (int w2 = 0; w2 < kSrvThreads / 64; ++w2) {
-                before += w2 < wave ? wsum[w2] : 0u;
-                all += wsum[w2];
-            }
-            uint32_t o = before + x - c;
-            const uint32_t w4[4] = {h.x, h.y, h.z, h.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint32_t m = w4[q];
+                uint32_t o = before + x - c;
+                uint32_t m = bits;
                 while (m) {
                     const int bit = __builtin_ctz(m);
                     m &= m - 1;
-                    if (o < kServerCand) mb->cand[o] = pos0 + (uint64_t)(tid * S + q * 32 + bit);
+                    if (o < kServerCand) mb->cand[o] = pos0 + (uint64_t)(tid * kSrvLaneBytes + bit);
                     ++o;
                 }
+                total = all;
+                __syncthreads();  // wsum reused
             }
-            total = all;
-            __syncthreads();  // st, hv, wsum reused by the next pass
+            // the next pass's rows 0 and 1 = this pass's last two rows (every reader of them
+            // is past the barrier above)
+            if (p + 1 < npass) {
+                if (tid < 64) {
+                    const uint32_t r = (uint32_t)tid >> 5, i = (uint32_t)tid & 31u;
+                    *reinterpret_cast<uint32_t*>(rows + srv_row_dw(r, i)) = rd(srv_row_dw(kSrvThreads + r, i));
+                }
+                __syncthreads();
+            }
+        };
+        for (uint32_t p0 = 0; p0 < npass; p0 += kSrvAhead) {
+#pragma unroll
+            for (int k = 0; k < kSrvAhead; ++k)
+                if (p0 + k < npass) pass(p0 + k, ring[k]);
         }
         // every wave's stores drained, then the acknowledgement (system scope)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -206,7 +249,7 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
         if (tid == 0) {
             if (probe) {
                 mb->probe[0] = t_seen;
-                mb->probe[1] = t_staged;
+                mb->probe[1] = t_loaded;
                 mb->probe[2] = t_hashed;
                 mb->probe[3] = wall_clock64();
             }

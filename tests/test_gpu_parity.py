@@ -241,7 +241,13 @@ def test_device_generator_matches_oracle(gpu, oracle, kind):
 
 @pytest.mark.parametrize("feed,avg,n", [(1, 1024, 24 * KiB), (7, 256, 64 * KiB),
                                         (65, 4096, 256 * KiB), (4096, 64 * KiB, 3 * MiB),
-                                        (256 * KiB, 64 * KiB, 12 * MiB)])
+                                        (256 * KiB, 64 * KiB, 12 * MiB),
+                                        # scan server passes (8 KiB): ragged multi-pass
+                                        # requests, dense hits, the largest request, and a
+                                        # request with more hits than the mailbox holds
+                                        (12345, 64, 1 * MiB), (8192, 2, 256 * KiB),
+                                        (1 * MiB, 2 * KiB, 5 * MiB + 17), (8192, 4 * MiB, 24 * MiB),
+                                        (64 * KiB, 2, 512 * KiB)])
 def test_scan_feed_granularity(gpu, oracle, feed, avg, n):
     """test_chunker1 (chunker.rs:202-271) style: same cuts for any feed size."""
     data = gen_np.gen_random(n, feed)
