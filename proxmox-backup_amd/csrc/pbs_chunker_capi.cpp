@@ -151,6 +151,7 @@ struct pbs_chunker {
     bool timing_pending = false;
     bool fused = true;        // PBS_FUSED=0: multi-launch path for every batch (A/B)
     bool fused_force = false; // PBS_FUSED=1: the fused pass for every batch it can serve (tests)
+    bool scan_pass = true;    // PBS_SCAN_PASS=0: small averages take scan_main + exact + sort (A/B)
     uint64_t fused_min_avg = 0;
     int balance = 1;           // PBS_BALANCE=0: no priority trading between SIMD partners (A/B)
     int scan_dyn_env = -1;         // PBS_SCAN_DYN=0/1: force the static / dynamic tile order
@@ -619,9 +620,9 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
     // slot: the history right-aligned in its first kServerHist bytes, then the data
     std::memcpy(sv.slot + kServerHist - c->carry_len, c->carry, c->carry_len);
     std::memcpy(sv.slot + kServerHist, hsrc, bl);
+    const uint32_t seq = (uint32_t)++sv.seq;
     sv.mb->req_base = pos;
     sv.mb->req_len = (uint32_t)bl;
-    const uint32_t seq = (uint32_t)++sv.seq;
     if (!sv.running) {
         int rc = server_launch(c, (uint32_t)(seq - 1));
         if (rc) return rc;
@@ -632,15 +633,16 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
     for (uint32_t spin = 0;; ++spin) {
         ack = __atomic_load_n(&sv.mb->ack_seq, __ATOMIC_ACQUIRE);
         if ((uint32_t)ack == seq) break;
-        if (__atomic_load_n(&sv.mb->exited, __ATOMIC_ACQUIRE) == (uint32_t)(seq - 1)) {
+        const bool late = (spin & 1023) == 1023 &&
+                          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kServerTimeoutS;
+        if (!late && __atomic_load_n(&sv.mb->exited, __ATOMIC_ACQUIRE) == (uint32_t)(seq - 1)) {
             // it went idle just before this request: relaunch, the request is still there
             HIP_TRY(c, hipStreamSynchronize(sv.stream));
             int rc = server_launch(c, (uint32_t)(seq - 1));
             if (rc) return rc;
             continue;
         }
-        if ((spin & 1023) == 1023 &&
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kServerTimeoutS) {
+        if (late) {
             sv.broken = true;
             server_stop(c);
             return fail(c, PBS_ERR_HIP);
@@ -910,6 +912,8 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     a.ntiles = ntiles;
     a.t_big = t_big;
     a.balance = (uint32_t)c->balance;
+    a.resolver = 1;
+    a.groups = 1;
     a.table_rot = c->d_table.as<uint32_t>();
     a.thr = p.thr;
     a.tile_ctr = reinterpret_cast<uint32_t*>(ctr + 2);
@@ -1003,6 +1007,125 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     return PBS_OK;
 }
 
+// Averages below the fused pass's (64 KiB: ~900 k candidates in 64 GiB, more than its resolver
+// walks in time): scan_fused_kernel without resolver waves -- the static tile order with SIMD
+// balancing, the flagged blocks evaluated at the tile ends (up to kFusedGroups records of 64
+// blocks per tile) -- then the records' candidates gathered in stream order (no sort) and the
+// multi-kernel resolve.  Replaces scan_main + scan_exact + radix sort.  *done = false (nothing
+// changed) when a record overflowed: the caller takes the multi-launch path.
+// (from 64 KiB: a 2.5 MiB tile of random bytes holds ~120 flagged blocks, far below the
+// 256 its records take; at 32 KiB ~240, and a batch with one overflowing tile is scanned twice)
+constexpr uint64_t kScanPassMinAvg = 64 * 1024;
+bool use_scan_pass(const pbs_chunker* c, uint64_t bl) {
+    return c->fused && c->scan_pass && c->prm.hash_cuts && c->prm.avg >= kScanPassMinAvg &&
+           c->prm.avg < c->fused_min_avg && bl > kFusedMaxBytes && c->cu >= 2;
+}
+
+int fused_scan_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_t pos, uint64_t bl,
+                    size_t np, uint64_t rend, uint64_t* out, size_t cap, size_t* n, bool* done) {
+    const Params& p = c->prm;
+    *done = false;
+    FusedPassArgs a{};
+    uint64_t ntiles = 0, t_big = 0, covered = 0;
+    bool dyn = false;
+    int seg = scan_main_plan(bl, c->cu, &ntiles, &dyn, &t_big);
+    dyn = dyn && c->scan_dyn_env == 1;  // static order unless PBS_SCAN_DYN=1
+    if (dyn) {
+        covered = scan_main_covered(ntiles, t_big, seg);
+    } else {
+        fused_static_plan(bl, (uint64_t)c->cu * kFusedWavesPerWG, &a);
+        ntiles = t_big = a.ntiles;
+        covered = ((a.t_small * a.seg_q + a.t_long) + (ntiles - a.t_small) * a.seg_qs + a.t_small_long) *
+                  64 * kBlockBytes;
+    }
+    const uint64_t ntail = ((bl - covered + kBlockBytes - 1) / kBlockBytes + kTailBlocks - 1) / kTailBlocks;
+    const uint64_t items = ntiles + ntail;
+    if (items == 0) return PBS_OK;
+    const uint64_t nrec = items * kFusedGroups;
+    const void* old_rec = c->d_rec.p;
+    const size_t old_cap = c->d_rec.cap;
+    HIP_TRY(c, c->d_rec.ensure(nrec * 8));
+    if (c->d_rec.p != old_rec || c->d_rec.cap != old_cap || ((c->rec_epoch + 1) & 0xFFFFu) == 0) {
+        HIP_TRY(c, hipMemsetAsync(c->d_rec.p, 0, c->d_rec.cap, c->stream));
+        c->rec_epoch = 0;
+    }
+    c->rec_epoch = (c->rec_epoch + 1) & 0xFFFFu;
+    const uint64_t expected = bl / p.avg * 3 / 2 + 1;
+    const uint64_t cand_cap = std::min<uint64_t>(std::min<uint64_t>(bl + 1, expected * 2 + 8192), kMaxBatchCand);
+    HIP_TRY(c, c->d_cand.ensure(cand_cap * 8));
+    HIP_TRY(c, c->d_counters.ensure(32));
+    HIP_TRY(c, hipMemsetAsync(c->d_counters.p, 0, 32, c->stream));
+    HIP_TRY(c, c->d_pre.ensure(64));
+    if (c->carry_len)
+        HIP_TRY(c, hipMemcpyAsync(c->d_pre.p, c->carry, c->carry_len, hipMemcpyHostToDevice, c->stream));
+    // d_C = [pending (np) | the batch's candidates in stream order]
+    HIP_TRY(c, c->d_C.ensure((np + cand_cap + 2) * 8));
+    if (np)
+        HIP_TRY(c, hipMemcpyAsync(c->d_C.p, c->pending.data() + c->pend_head, np * 8, hipMemcpyHostToDevice,
+                                  c->stream));
+    size_t tb = 0;
+    HIP_TRY(c, exclusive_sum_u64(nullptr, &tb, nullptr, nullptr, (uint32_t)(nrec + 1), c->stream));
+    HIP_TRY(c, c->d_scan_tmp.ensure(tb));
+    HIP_TRY(c, c->d_cnt.ensure((nrec + 1) * 8));
+    HIP_TRY(c, c->d_off.ensure((nrec + 1) * 8));
+    HIP_TRY(c, c->d_res.ensure(32));
+    HIP_TRY(c, hipMemsetAsync(c->d_res.p, 0, 16, c->stream));
+    unsigned long long* ctr = c->d_counters.as<unsigned long long>();
+    a.data = dsrc;
+    a.len = bl;
+    a.ntiles = ntiles;
+    a.t_big = t_big;
+    a.balance = (uint32_t)c->balance;
+    a.resolver = 0;
+    a.groups = kFusedGroups;
+    a.table_rot = c->d_table.as<uint32_t>();
+    a.thr = p.thr;
+    a.tile_ctr = reinterpret_cast<uint32_t*>(ctr + 2);
+    a.pre = c->d_pre.as<uint8_t>();
+    a.pre_len = c->carry_len;
+    a.covered = covered;
+    a.ntail = ntail;
+    a.base = pos;
+    a.rec = c->d_rec.as<unsigned long long>();
+    a.epoch = c->rec_epoch;
+    a.cand = c->d_cand.as<uint64_t>();
+    a.ncand = ctr + 1;
+    a.cand_cap = cand_cap;
+    a.nflag = ctr;
+    HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+    HIP_TRY(c, launch_scan_fused(a, seg, dyn, c->cu, c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
+    HIP_TRY(c, launch_fused_gather(a.rec, nrec, a.epoch, a.cand, c->d_C.as<uint64_t>() + np, c->d_cnt.as<uint64_t>(),
+                                   c->d_off.as<uint64_t>(), c->d_scan_tmp.p, c->d_scan_tmp.cap,
+                                   c->d_res.as<uint64_t>(), c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_res.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_small + 2, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream));
+    const uint64_t tl = std::min<uint64_t>(bl, kWindow - 1);
+    uint8_t* tail = reinterpret_cast<uint8_t*>(c->h_small + 24);
+    if (!hsrc) HIP_TRY(c, hipMemcpyAsync(tail, dsrc + bl - tl, tl, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const uint64_t nnew = c->h_small[0], overflow = c->h_small[1], nflag = c->h_small[2];
+    if (overflow || nnew > cand_cap) return PBS_OK;  // dense input: the multi-launch path
+    float ms = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    c->timing.scan_ms += ms;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+    c->timing.exact_ms += ms;  // the gather
+    c->timing.bytes += bl;
+    c->timing.fused += bl;
+    c->timing.suspects += nflag;
+    c->timing.candidates += nnew;
+    const uint64_t m = (uint64_t)np + nnew;
+    if (m > 0xFFFFFFF0ull) return fail(c, PBS_ERR_NOMEM);
+    int rc = run_resolve(c, (uint32_t)m, rend, out, cap, n);
+    if (rc) return rc;
+    update_carry(c, hsrc ? hsrc + bl - tl : tail, tl);
+    c->scanned_end = pos + bl;
+    *done = true;
+    return PBS_OK;
+}
+
 int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final, uint64_t* out,
                    size_t cap, size_t* n_out, bool device) {
     if (!c) return PBS_ERR_INVALID;
@@ -1053,6 +1176,15 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
         if (bl && use_fused(c, bl)) {
             bool done = false;
             int rc = fused_pass(c, dsrc, hsrc, pos, bl, np, rend, out, cap, &n, &done);
+            if (rc) return rc;
+            if (done) {
+                pos += bl;
+                continue;
+            }
+        }
+        if (bl && use_scan_pass(c, bl)) {
+            bool done = false;
+            int rc = fused_scan_pass(c, dsrc, hsrc, pos, bl, np, rend, out, cap, &n, &done);
             if (rc) return rc;
             if (done) {
                 pos += bl;
@@ -1216,6 +1348,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
         c->fused_force = e[0] == '1';
     }
     if (const char* e = std::getenv("PBS_SCAN_SERVER")) c->srv.enabled = e[0] != '0';
+    if (const char* e = std::getenv("PBS_SCAN_PASS")) c->scan_pass = e[0] != '0';
     if (const char* e = std::getenv("PBS_SERVER_POLL")) c->srv.flags = e[0] == '4' ? kSrvPollAll : 0u;
     if (const char* e = std::getenv("PBS_SERVER_PROBE"))
         if (e[0] == '1') c->srv.flags |= kSrvProbe;

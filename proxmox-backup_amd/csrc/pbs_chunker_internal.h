@@ -54,6 +54,9 @@ struct FusedPassArgs {
     uint32_t seg_q, seg_qs;
     uint64_t t_long, t_small, t_small_long;
     uint32_t balance;           // SIMD partners trade issue priority by progress (PBS_BALANCE)
+    uint32_t resolver;          // 1: waves 0..4 of workgroup 0 resolve (records: `groups` == 1);
+                                // 0: every wave scans, the host resolves the records (scan pass)
+    uint32_t groups;            // records per tile: up to 64 flagged blocks each (1 or kFusedGroups)
     uint32_t pool;              // static order: tiles [t_small, ntiles) are drawn from tile_ctr
     const uint32_t* table_rot;  // T' (256 words)
     uint32_t thr;
@@ -98,9 +101,17 @@ struct FusedPassArgs {
 };
 
 constexpr int kTailBlocks = 64;     // blocks per tail item of the fused pass
+constexpr int kFusedGroups = 4;     // scan pass (no resolver): records per tile, so a tile may
+                                    // hold 4 x 64 flagged blocks (small averages)
 constexpr int kFusedStaticSeg = 40960;  // static-order fused pass: longest segment (bitmap size)
 constexpr int kResolveBatch = 256;  // tile records per resolver step (4 per lane)
 hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid, hipStream_t stream);
+// Scan pass (FusedPassArgs::resolver == 0): the records' candidates, in record order (= stream
+// order), to out[0 ..); counts/offs: nrec + 1 u64 scratch each; res[0] = candidates,
+// res[1] = 1 when a record overflowed (the batch must take another path).
+hipError_t launch_fused_gather(const unsigned long long* rec, uint64_t nrec, uint32_t epoch,
+                               const uint64_t* cand, uint64_t* out, uint64_t* counts, uint64_t* offs,
+                               void* scan_tmp, size_t scan_tmp_bytes, uint64_t* res, hipStream_t stream);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
                              uint32_t pre_len, const uint64_t* susp,
                              const unsigned long long* nsusp, uint64_t susp_cap, uint64_t ext_first,

@@ -918,6 +918,55 @@ hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid
     return hipGetLastError();
 }
 
+// ---- scan pass (scan_fused_kernel without resolver waves): records -> candidates in order
+__global__ void fused_rec_counts_kernel(const unsigned long long* __restrict__ rec, uint64_t nrec, uint32_t epoch,
+                                        uint64_t* __restrict__ counts, uint64_t* __restrict__ res) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > nrec) return;
+    uint64_t c = 0;
+    if (i < nrec) {
+        const uint64_t r = rec[i];
+        // a record of an earlier launch (another epoch) is a group this launch left empty
+        if ((uint32_t)(r >> 48) == epoch) {
+            c = (r >> 32) & 0xFFFFu;
+            if (c == kRecOverflow) {
+                res[1] = 1;
+                c = 0;
+            }
+        }
+    }
+    counts[i] = c;
+}
+
+__global__ void fused_gather_kernel(const unsigned long long* __restrict__ rec, uint64_t nrec, uint32_t epoch,
+                                    const uint64_t* __restrict__ offs, const uint64_t* __restrict__ cand,
+                                    uint64_t* __restrict__ out, uint64_t* __restrict__ res) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); r < nrec; r += nwaves) {
+        const uint64_t v = rec[r];
+        if ((uint32_t)(v >> 48) != epoch) continue;
+        const uint32_t c = (uint32_t)(v >> 32) & 0xFFFFu;
+        if (c == kRecOverflow) continue;
+        const uint64_t idx = (uint32_t)v, o = offs[r];
+        for (uint32_t j = (uint32_t)lane; j < c; j += 64) out[o + j] = cand[idx + j];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) res[0] = offs[nrec];
+}
+
+hipError_t launch_fused_gather(const unsigned long long* rec, uint64_t nrec, uint32_t epoch, const uint64_t* cand,
+                               uint64_t* out, uint64_t* counts, uint64_t* offs, void* scan_tmp, size_t scan_tmp_bytes,
+                               uint64_t* res, hipStream_t stream) {
+    if (nrec + 1 > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(fused_rec_counts_kernel, dim3((unsigned)((nrec + 256) / 256)), dim3(256), 0, stream, rec, nrec,
+                       epoch, counts, res);
+    hipError_t e = exclusive_sum_u64(scan_tmp, &scan_tmp_bytes, counts, offs, (uint32_t)(nrec + 1), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fused_gather_kernel, dim3(1024), dim3(256), 0, stream, rec, nrec, epoch, offs, cand, out, res);
+    return hipGetLastError();
+}
+
 hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, const uint32_t* table_rot,
                               uint32_t thr, uint64_t last_seq, uint64_t idle_ticks,
                               uint32_t flags, hipStream_t stream) {

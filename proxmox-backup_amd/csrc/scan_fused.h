@@ -596,11 +596,14 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     const bool bal_sleep = a.balance == 2;
     uint8_t* stage = (uint8_t*)(s_lds + kTableDwords) + wave * kStagePerWave;
     PBS_FUSED_STAMP(0)
-    if (blockIdx.x == 0 && wave == 0) {
+    const bool resolver = __builtin_amdgcn_readfirstlane(a.resolver) != 0;
+    const uint32_t nres = resolver ? 1u + kFusedHelpers : 0u;  // resolver waves (workgroup 0)
+    const uint32_t G = __builtin_amdgcn_readfirstlane(a.groups);  // records per tile
+    if (resolver && blockIdx.x == 0 && wave == 0) {
         fused_main(a, reinterpret_cast<uint64_t*>(stage), lane);
         return;
     }
-    if (blockIdx.x == 0 && wave <= kFusedHelpers) {
+    if (resolver && blockIdx.x == 0 && wave <= kFusedHelpers) {
         fused_helper(a, reinterpret_cast<uint64_t*>(stage), wave - 1, kFusedHelpers, lane);
         return;
     }
@@ -625,8 +628,8 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     const uint32_t rd_base = (uint32_t)lane * 128u;
     const uint32_t rsw = ((uint32_t)lane >> 1) & 7u;
     // scanner waves: all but workgroup 0's resolver waves
-    const uint64_t nw = (uint64_t)gridDim.x * NW - (1 + kFusedHelpers);
-    uint64_t tile = (uint64_t)blockIdx.x * NW + wave - (1 + kFusedHelpers);
+    const uint64_t nw = (uint64_t)gridDim.x * NW - nres;
+    uint64_t tile = (uint64_t)blockIdx.x * NW + wave - nres;
     const uint64_t ntiles = a.ntiles, t_big = a.t_big;
     const uint8_t* data = a.data;
 
@@ -676,7 +679,8 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
             }
         }
     };
-    // the wave's flagged blocks of tile t (bitmap, lane order = stream order) -> publish
+    // the wave's flagged blocks of tile t (bitmap, lane order = stream order) -> publish,
+    // 64 blocks per record (records t * G .. t * G + G - 1; more blocks: overflow)
     auto tile_end = [&](uint64_t t, uint64_t toff, uint32_t seg_cur) {
         uint32_t w[NBW];
 #pragma unroll
@@ -685,8 +689,9 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
             bm[q] = 0;
         }
         if (t == 0 && lane == 0) w[0] |= 1u;  // the stream's first block: carry bytes
+        for (uint32_t g = 0;; ++g) {
         int nb = 0;
-        bool over = false;
+        bool over = false, more = false;
         int64_t myB = 0;
         for (;;) {
             bool has = false;
@@ -695,7 +700,8 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
             const unsigned long long m = __ballot(has);
             if (!m) break;
             if (nb == 64) {
-                over = true;
+                more = true;
+                over = g + 1 == G;
                 break;
             }
             const int L = __ffsll(m) - 1;
@@ -718,7 +724,9 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
             ++nb;
         }
         if (nb && lane == 0) atomicAdd(a.nflag, (unsigned long long)nb);
-        fused_publish(a, s_lds, t, myB, nb, over, lane);
+        fused_publish(a, s_lds, t * G + g, myB, nb, over, lane);
+        if (!more || over) break;
+        }
     };
 
     const bool pool = DYN == 0 && __builtin_amdgcn_readfirstlane(a.pool) != 0;
@@ -820,7 +828,7 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
     while (tile < ntiles + a.ntail) {
         const uint64_t b0 = a.covered / kIter + (tile - ntiles) * kTailBlocks;
         const int nb = (int)(nblk - b0 < (uint64_t)kTailBlocks ? nblk - b0 : (uint64_t)kTailBlocks);
-        fused_publish(a, s_lds, tile, (int64_t)((b0 + (uint64_t)lane) * kIter), nb, false, lane);
+        fused_publish(a, s_lds, tile * G, (int64_t)((b0 + (uint64_t)lane) * kIter), nb, false, lane);
         if (DYN != 0 || pool) {
             uint32_t v = 0;
             if (lane == 0) v = atomicAdd(a.tile_ctr, 1u);

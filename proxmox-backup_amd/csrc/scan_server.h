@@ -148,6 +148,7 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             *reinterpret_cast<uint32_t*>(rows + srv_row_dw((uint32_t)lane >> 5, (uint32_t)lane & 31u)) = x;
         }
         uint32_t total = 0;
+        bool stored = false;  // some pass stored candidates (block-uniform)
         auto pass = [&](uint32_t p, srv_u32x4 (&cur)[2]) {
             const uint32_t off = p * (uint32_t)kSrvPass;
             const uint32_t plen = len - off < (uint32_t)kSrvPass ? len - off : (uint32_t)kSrvPass;
@@ -203,6 +204,7 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             // stream-order compaction (hits are rare: one barrier tells whether any)
             const uint32_t c = __builtin_popcount(bits);
             if (__syncthreads_or(c != 0)) {
+                stored = true;
                 uint32_t x = c;
 #pragma unroll
                 for (int dd = 1; dd < 64; dd <<= 1) {
@@ -243,9 +245,12 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             for (int k = 0; k < kSrvAhead; ++k)
                 if (p0 + k < npass) pass(p0 + k, ring[k]);
         }
-        // every wave's stores drained, then the acknowledgement (system scope)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        // every wave's stores drained, then the acknowledgement (system scope); without
+        // candidates every wave is past the last pass's barrier already
+        if (stored) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         if (tid == 0) {
             if (probe) {
                 mb->probe[0] = t_seen;

@@ -210,6 +210,34 @@ def test_small_batches(gpu, oracle, avg, piece):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("kind,n,avg", [("vmimage", 192 * MiB + 5, 64 * KiB), ("random", 96 * MiB, 64 * KiB),
+                                        ("random", 40 * MiB + 3, 64 * KiB)])
+def test_scan_pass(gpu, oracle, kind, n, avg):
+    """64 KiB averages: scan_fused_kernel without resolver waves, the records' candidates
+    gathered in stream order, the multi-kernel resolve -- whole, and split into three calls
+    (pending candidates of the open chunk carried over), against the oracle."""
+    import torch
+    n8 = (n + 7) // 8 * 8  # (the generator fills whole 8-byte words; n itself is ragged)
+    dev = torch.empty(n8, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n8, gpu.GEN_VMIMAGE if kind == "vmimage" else gpu.GEN_RANDOM,
+                        0x5EED0003, 7 * GiB)
+    host = dev[:n].cpu().numpy()
+    ref = oracle.chunk_feed(avg, host)
+    with gpu.Chunker(avg) as c:
+        c.set_stream(torch.cuda.current_stream().cuda_stream)
+        got = c.find_cuts_device(dev.data_ptr(), n, is_final=True)
+        t = c.last_timing()
+    assert t["fused"] == t["bytes"] == n, t  # the scan pass served the whole stream
+    assert np.array_equal(got[:-1], ref) and int(got[-1]) == n
+    cuts = [n // 3 + 1, 2 * n // 3 + 4093]
+    parts = []
+    with gpu.Chunker(avg) as c:
+        c.set_stream(torch.cuda.current_stream().cuda_stream)
+        for a, b in zip([0] + cuts, cuts + [n]):
+            parts.append(c.find_cuts_device(dev.data_ptr() + a, b - a, is_final=b == n))
+    assert np.array_equal(np.concatenate(parts), got)
+
+
 def test_small_batches_device(gpu, oracle):
     import torch
     n, avg = 5 * MiB + 24, 256 * KiB
