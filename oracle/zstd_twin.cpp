@@ -51,7 +51,7 @@ namespace {
 constexpr uint32_t kBlock = 64 * 1024;
 constexpr uint32_t kSub = 8192;     // one GPU wave's sub-block
 constexpr uint32_t kHist = 16384;   // window before a sub-block (reaches into the previous block)
-constexpr uint32_t kRound = 256, kHistRound = 512, kMaxStep = 8, kHistMaxStep = 32;
+constexpr uint32_t kRound = 256, kHistRound = 512, kMaxStep = 8, kHistMaxStep = 32, kHistStep0 = 4;
 constexpr uint32_t kHashLog = 12, kCap = 32, kMinMatch = 5;
 constexpr uint32_t kHufStreams = 48 * 1024;  // largest Huffman stream bytes of a block
 
@@ -91,7 +91,7 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
         // history: the window before the sub-block enters the table in rounds like the
         // parse's (lookups before inserts; step 1 after a round in which some position's 5
         // bytes equal its table or run candidate's, doubling to kHistMaxStep without)
-        uint32_t hs = 1;
+        uint32_t hs = kHistStep0;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kHistRound * hs;
             uint32_t pos[kHistRound], cand[kHistRound], np = 0;

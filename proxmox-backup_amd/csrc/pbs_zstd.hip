@@ -65,7 +65,8 @@ constexpr int kZThreads = 512;
 constexpr int kZWaves = kZThreads / 64;
 constexpr uint32_t kZSub = 8192;     // one wave's sub-block
 constexpr uint32_t kZHist = 16384;   // window before a sub-block
-constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8, kZHistMaxStep = 32;
+constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8, kZHistMaxStep = 32,
+                   kZHistStep0 = 4;  // the history rounds start at step 4 (1: pxar 1.038 -> 1.042 x libzstd, text 1.074 -> 1.079)
 constexpr int kZPer = kZRound / 64;  // positions per lane and round
 constexpr uint32_t kZHistRound = 512;  // history rounds (no walk: wider, fewer)
 constexpr int kZPerH = kZHistRound / 64;
@@ -221,7 +222,21 @@ __device__ __forceinline__ void stage_to_global(uint8_t* dst, const Win& W, uint
     if (t < head) dst[t] = (uint8_t)W.byte(from + t);
     const uint32_t nwd = (cnt - head) >> 2;
     uint32_t* const dw = reinterpret_cast<uint32_t*>(dst + head);
-    for (uint32_t w = t; w < nwd; w += nt) dw[w] = W.word(from + head + 4 * w);
+    // four dwords per thread and step, their LDS reads issued together (one dword a step
+    // waited an LDS round trip per store: a VM block's ~40 KB of raw literals took 4.5 us)
+    for (uint32_t w0 = t; w0 < nwd; w0 += 4 * nt) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w = w0 + (uint32_t)k * nt;
+            v[k] = W.word(from + head + 4 * (w < nwd ? w : 0u));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w = w0 + (uint32_t)k * nt;
+            if (w < nwd) dw[w] = v[k];
+        }
+    }
     for (uint32_t i = head + 4 * nwd + t; i < cnt; i += nt) dst[i] = (uint8_t)W.byte(from + i);
 }
 
@@ -914,7 +929,7 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
 #pragma unroll
         for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<uint32_t*>(tw)[lane + 64 * i] = 0;
         // history: accelerated rounds over [wlo, s0)
-        uint32_t hs = 1;
+        uint32_t hs = kZHistStep0;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kZHistRound * hs;
             uint32_t h[kZPerH], t[kZPerH], wp[kZPerH], b4[kZPerH], lo[kZPerH], hi[kZPerH], o3[kZPerH];
@@ -2058,9 +2073,8 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
         __syncthreads();
         ZMARK(8);
-        if (!ctl.seq_ok) {  // raw block
-            const uint8_t* const sb = reinterpret_cast<const uint8_t*>(stage) + r + hist;
-            for (uint32_t i = tid; i < n; i += kZThreads) out[3 + i] = sb[i];
+        if (!ctl.seq_ok) {  // raw block (dword stores: byte stores cost a 64 KiB block 128 rounds)
+            stage_to_global(out + 3, W, hist, n, (uint32_t)tid, kZThreads);
             if (tid == 0) {
                 write_block_header(out, last, 0, n);
                 sizes[k] = 3 + (uint64_t)n;
