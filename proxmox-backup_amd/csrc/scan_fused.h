@@ -44,7 +44,7 @@ constexpr int kLaneProbes = 3;      // linear probes before the binary lane sear
 constexpr int kMainAhead = 8;       // resolver vectors the main wave has in flight
 constexpr int kStageCand = 512;     // candidates of one resolver step staged in LDS
 constexpr int kFusedHelpers = 4;    // resolver helper waves (workgroup 0, waves 1..4)
-constexpr int kPubDepth = 8;        // exact windows in flight per wave (fused_publish)
+constexpr int kPubDepth = 16;       // exact windows in flight per wave (fused_publish)
 
 constexpr uint32_t kRecOverflow = 0xFFFFu;
 static_assert(kFusedWavesPerWG == kWavesPerWG && kFusedResolverWaves == 1 + kFusedHelpers,
