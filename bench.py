@@ -240,7 +240,7 @@ def secondary_random(args, ch, buf, stream, steps: int = 3):
 
 def blob_stage(args, buf, cuts, stream, reps: int = 2):
     """SURVEY 8(f) rank 4: DataBlob::encode(chunk, None, compress = true) for every chunk of
-    the device-resident stream (pbs_blob_encode_chunks_device: zstd frames of 128 KiB
+    the device-resident stream (pbs_blob_encode_chunks_device: zstd frames of 64 KiB
     blocks, compressed-or-not per chunk, blob images + CRC), wall clock of the synchronous
     call; libzstd level 1 (the image's 1.4.8) + zlib.crc32 on the host cores over a bounded
     sample of the same chunks beside it, with both compressed sizes of that sample."""

@@ -53,8 +53,9 @@ size_t pbs_blob_encode_uncompressed(const uint8_t *data, size_t len, uint32_t cr
 
 /* DataBlob images of every chunk on the GPU (`DataBlob::encode(data, None, compress)`,
  * data_blob.rs:87-176, unencrypted path).  compress != 0: each chunk is compressed into a
- * zstd frame (independent 128 KiB blocks: RLE, compressed with raw literals and the
- * predefined FSE tables, or raw; decodable by any zstd decoder, the reference's
+ * zstd frame (64 KiB blocks: RLE, compressed -- Huffman, raw or RLE literals; sequences
+ * with repeat offsets and predefined, RLE or own FSE tables -- or raw; the match window
+ * reaches 16 KiB before each 8 KiB sub-block; decodable by any zstd decoder, the reference's
  * `zstd::stream::decode_all` :214 included -- but not byte-identical to libzstd level 1,
  * which is what the reference writes: "parity unpinned"); the blob
  * is {COMPRESSED_BLOB_MAGIC_1_0, CRC, frame} when the frame is shorter than the chunk
