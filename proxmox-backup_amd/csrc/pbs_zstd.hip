@@ -1151,16 +1151,34 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                     msrc = hsrc - e;
                     mlen += e;
                 }
-                // forwards to the end (within the sub-block): 4 bytes per lane a step
+                // forwards to the end (within the sub-block): 16 bytes per lane a step, their
+                // word reads issued together (4 bytes a step took 16 dependent LDS round trips
+                // per zero page of a VM image)
+                auto fwd_mis16 = [&](uint32_t src, uint32_t dst) {  // first mismatch of my 16 bytes (16: none)
+                    const uint32_t xf = dst + 16 * kk, xs = src + 16 * kk;
+                    uint32_t mis = 16;
+                    if (xf + 16 <= se) {
+                        uint32_t d[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) d[k] = W.word(xs + 4 * k) ^ W.word(xf + 4 * k);
+#pragma unroll
+                        for (int k = 3; k >= 0; --k)
+                            if (d[k]) mis = 4 * (uint32_t)k + ((uint32_t)__builtin_ctz(d[k]) >> 3);
+                    } else {
+                        mis = 0;
+                        while (xf + mis < se && W.byte(xs + mis) == W.byte(xf + mis)) ++mis;
+                    }
+                    return mis;
+                };
                 while (ext) {
-                    const uint32_t mis = fwd_mis(msrc + mlen, mpos + mlen);
-                    const unsigned long long bad = __ballot(mis < 4);
+                    const uint32_t mis = fwd_mis16(msrc + mlen, mpos + mlen);
+                    const unsigned long long bad = __ballot(mis < 16);
                     if (bad) {
                         const int f = __builtin_ctzll(bad);
-                        mlen += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
+                        mlen += 16 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
                         break;
                     }
-                    mlen += 256;
+                    mlen += 1024;
                 }
                 mpos = uni(mpos);
                 msrc = uni(msrc);
