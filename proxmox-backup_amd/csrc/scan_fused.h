@@ -24,6 +24,11 @@
 //                   last 63 bytes to the host.  It finishes a few microseconds after the
 //                   last tile, so the pass costs one launch and one host sync.
 //
+// Scan pass (FusedPassArgs::resolver == 0, small averages): no resolver waves -- every wave
+// scans, and a tile publishes up to `groups` records of 64 flagged blocks each; the host
+// gathers the records' candidates in record (= stream) order and resolves them
+// (pbs_chunker_capi.cpp fused_scan_pass).
+//
 // Stand-down: a tile with more than 64 flagged blocks, a full candidate list or more than
 // kFusedKeep open-chunk candidates (dense input) sets status 1 -- the host then runs the
 // batch through the multi-launch path (scan_main + scan_exact + resolve), which has no
@@ -690,42 +695,42 @@ __global__ __launch_bounds__(kWavesPerWG * 64) void scan_fused_kernel(FusedPassA
         }
         if (t == 0 && lane == 0) w[0] |= 1u;  // the stream's first block: carry bytes
         for (uint32_t g = 0;; ++g) {
-        int nb = 0;
-        bool over = false, more = false;
-        int64_t myB = 0;
-        for (;;) {
-            bool has = false;
+            int nb = 0;
+            bool over = false, more = false;
+            int64_t myB = 0;
+            for (;;) {
+                bool has = false;
 #pragma unroll
-            for (int q = 0; q < NBW; ++q) has |= w[q] != 0u;
-            const unsigned long long m = __ballot(has);
-            if (!m) break;
-            if (nb == 64) {
-                more = true;
-                over = g + 1 == G;
-                break;
-            }
-            const int L = __ffsll(m) - 1;
-            int bitpos = 0;
-            bool found = false;
-#pragma unroll
-            for (int q = 0; q < NBW; ++q) {
-                if (!found && w[q]) {
-                    bitpos = q * 32 + __builtin_ctz(w[q]);
-                    found = true;
+                for (int q = 0; q < NBW; ++q) has |= w[q] != 0u;
+                const unsigned long long m = __ballot(has);
+                if (!m) break;
+                if (nb == 64) {
+                    more = true;
+                    over = g + 1 == G;
+                    break;
                 }
-            }
-            bitpos = __builtin_amdgcn_readlane(bitpos, L);  // L is wave-uniform
-            if (lane == L) {
+                const int L = __ffsll(m) - 1;
+                int bitpos = 0;
+                bool found = false;
 #pragma unroll
-                for (int q = 0; q < NBW; ++q)
-                    if (q == (bitpos >> 5)) w[q] &= w[q] - 1;
+                for (int q = 0; q < NBW; ++q) {
+                    if (!found && w[q]) {
+                        bitpos = q * 32 + __builtin_ctz(w[q]);
+                        found = true;
+                    }
+                }
+                bitpos = __builtin_amdgcn_readlane(bitpos, L);  // L is wave-uniform
+                if (lane == L) {
+#pragma unroll
+                    for (int q = 0; q < NBW; ++q)
+                        if (q == (bitpos >> 5)) w[q] &= w[q] - 1;
+                }
+                if (lane == nb) myB = (int64_t)(toff + (uint64_t)L * seg_cur + (uint64_t)bitpos * kIter);
+                ++nb;
             }
-            if (lane == nb) myB = (int64_t)(toff + (uint64_t)L * seg_cur + (uint64_t)bitpos * kIter);
-            ++nb;
-        }
-        if (nb && lane == 0) atomicAdd(a.nflag, (unsigned long long)nb);
-        fused_publish(a, s_lds, t * G + g, myB, nb, over, lane);
-        if (!more || over) break;
+            if (nb && lane == 0) atomicAdd(a.nflag, (unsigned long long)nb);
+            fused_publish(a, s_lds, t * G + g, myB, nb, over, lane);
+            if (!more || over) break;
         }
     };
 
