@@ -259,10 +259,14 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                 mb->probe[3] = wall_clock64();
             }
             s_go = 0;
-            // ONE 8-byte store: seq, candidate count, overflow flag (the host reads them together)
+            // ONE 8-byte store: seq, candidate count, overflow flag (the host reads them together);
+            // a release (an L2 write-back first) only when candidates were stored before it
             const uint64_t ack = (uint64_t)seq | (uint64_t)(total < kServerCand ? total : kServerCand) << 32 |
                                  (total > kServerCand ? 1ull << 63 : 0ull);
-            __hip_atomic_store(&mb->ack_seq, ack, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (stored)
+                __hip_atomic_store(&mb->ack_seq, ack, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            else
+                __hip_atomic_store(&mb->ack_seq, ack, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
         last = seq;

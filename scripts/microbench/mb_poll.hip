@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void bw_kernel(const u32x4* host, uint32_t n16
     }
 }
 
-__global__ __launch_bounds__(256) void ping_kernel(const Rec* rec, uint64_t* ack, int pollers, int sleep) {
+__global__ __launch_bounds__(256) void ping_kernel(const Rec* rec, uint64_t* ack, int pollers, int sleep, int relaxed) {
     __shared__ uint32_t s_go, s_seq;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t last = 0;
@@ -102,7 +102,10 @@ __global__ __launch_bounds__(256) void ping_kernel(const Rec* rec, uint64_t* ack
         const uint32_t seq = s_seq;
         if (tid == 0) {
             s_go = 0;
-            __hip_atomic_store(ack, (uint64_t)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (relaxed)
+                __hip_atomic_store(ack, (uint64_t)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            else
+                __hip_atomic_store(ack, (uint64_t)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
         last = seq;
@@ -148,11 +151,12 @@ int main() {
     CK(hipHostGetDevicePointer((void**)&d_ack, h_ack, 0));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    for (int pollers : {1, 2, 4}) {
-        for (int sleep : {0, 1, 2}) {
+    for (int relaxed : {0, 1})
+    for (int pollers : {1, 4}) {
+        for (int sleep : {2}) {
             memset(h_rec, 0, 4 * sizeof(Rec));
             *h_ack = 0;
-            hipLaunchKernelGGL(ping_kernel, dim3(1), dim3(256), 0, st, d_rec, d_ack, pollers, sleep);
+            hipLaunchKernelGGL(ping_kernel, dim3(1), dim3(256), 0, st, d_rec, d_ack, pollers, sleep, relaxed);
             std::vector<double> rt;
             const int N = 20000;
             for (uint32_t s = 1; s <= N; ++s) {
@@ -166,7 +170,7 @@ int main() {
             std::sort(rt.begin(), rt.end());
             double m = 0;
             for (double x : rt) m += x / rt.size();
-            printf("ping: pollers %d sleep %d: mean %.2f us p10 %.2f p50 %.2f p90 %.2f\n", pollers, sleep, m,
+            printf("ping: %s ack, pollers %d sleep %d: mean %.2f us p10 %.2f p50 %.2f p90 %.2f\n", relaxed ? "relaxed" : "release", pollers, sleep, m,
                    rt[rt.size() / 10], rt[rt.size() / 2], rt[rt.size() * 9 / 10]);
         }
     }
