@@ -465,6 +465,27 @@ def test_periodic_dense_candidates(gpu, oracle):
     assert np.array_equal(got, ref)
 
 
+def test_scan_pass_dense_falls_back(gpu, oracle):
+    """At 64 KiB averages a period-7 stream whose window hash passes makes every 128-byte
+    block a flagged one: every tile of the scan pass overflows its four records, and the
+    batch goes through the multi-launch path instead -- same cuts as the oracle."""
+    import torch
+    pat = _passing_pattern(oracle, 7, 64 * KiB)
+    n = 48 * MiB + 5
+    host = np.tile(pat, n // 7 + 1)[:n]
+    dev = torch.from_numpy(host).to("cuda")
+    torch.cuda.synchronize()
+    with gpu.Chunker(64 * KiB) as c:
+        got = c.find_cuts_device(dev.data_ptr(), n, is_final=True)
+        t = c.last_timing()
+    del dev
+    ref = oracle.chunk_feed(64 * KiB, host)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    assert t["fused"] == 0, t  # the scan pass stood down
+    assert np.array_equal(got, ref)
+
+
 # ---------------------------------------------------------------- fused pass (scan_fused.h)
 
 FUSED_CASES = [
