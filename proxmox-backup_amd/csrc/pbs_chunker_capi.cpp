@@ -816,9 +816,16 @@ void fused_static_plan(uint64_t len, uint64_t nw, FusedPassArgs* a) {
     }
 }
 
-// Averages served by the fused pass: at >= 128 KiB a tile (1-2 MiB) of random data holds
-// ~12-24 candidates, far below the 64 flagged blocks one tile's exact step takes.
-constexpr uint64_t kFusedMinAvg = 128 * 1024;
+// Averages served by the fused pass: from 256 KiB.  Below, the scan pass (fused_scan_pass)
+// is faster: at 128 KiB the fused resolver's main wave, ~64 candidates per us, bounds the pass
+// (same process, profiles/r03/scanpass128k/: 8 GiB VM image 1.79-1.80 ms fused vs 1.53-1.57
+// scan pass, 8 GiB random 2.47-2.48 vs 1.60-1.64, 16 GiB VM image 3.16-3.17 vs 2.88-2.89,
+// 64 GiB random 12.7-13.2 vs 11.8-12.3, 64 GiB VM image 11.26-11.49 vs 11.18-11.42); at
+// 256 KiB (config 5) both are within noise of each other on the 64 GiB VM image.  With
+// PBS_FUSED=1 (tests) the fused pass serves from 128 KiB: a tile (1-2 MiB) of random data
+// then holds ~12-24 candidates, far below the 64 flagged blocks one tile's exact step takes.
+constexpr uint64_t kFusedMinAvg = 256 * 1024;
+constexpr uint64_t kFusedForceMinAvg = 128 * 1024;
 constexpr uint64_t kFusedMinBytes = 0;
 
 // Tile order of the fused pass: static with SIMD balancing (the wave behind its SIMD partner
@@ -843,7 +850,8 @@ bool fused_dynamic(const pbs_chunker* c, uint64_t bl) {
 // for every batch it can serve (its parity tests run small inputs), PBS_FUSED=0 never,
 // PBS_FUSED_MIN_BYTES raises the size threshold (A/B).
 bool use_fused(const pbs_chunker* c, uint64_t bl) {
-    if (!(c->fused && c->prm.hash_cuts && c->prm.avg >= c->fused_min_avg && bl > kFusedMaxBytes && c->cu >= 2))
+    const uint64_t min_avg = c->fused_force ? std::min(kFusedForceMinAvg, c->fused_min_avg) : c->fused_min_avg;
+    if (!(c->fused && c->prm.hash_cuts && c->prm.avg >= min_avg && bl > kFusedMaxBytes && c->cu >= 2))
         return false;
     return c->fused_force || bl >= c->fused_min_bytes;
 }
