@@ -24,6 +24,7 @@
 // chunk), scanned_end (bytes whose candidates are known).  Re-submitted bytes are
 // never rescanned.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdint>
@@ -107,13 +108,21 @@ inline uint32_t rotl32(uint32_t x, uint32_t r) {
 
 }  // namespace
 
-// Host side of the scan server (scan_server.h): mailbox + request slot in fine-grained
-// pinned host memory, the kernel on its own stream.
+// Host side of the scan server (scan_server.h): the mailbox (acknowledgement, candidates)
+// in fine-grained pinned host memory; the request record and slot in fine-grained VRAM
+// written through the BAR (dev_req), or in pinned host memory when the host has no
+// mapping of it; the kernel on its own stream.
 struct ScanServer {
     ServerMailbox* mb = nullptr;  // host view (mapped)
     ServerMailbox* mb_dev = nullptr;
-    uint8_t* slot = nullptr;
+    ServerReq* req = nullptr;  // host view of the request record (the mailbox's, or in VRAM)
+    ServerReq* req_dev = nullptr;
+    uint8_t* slot = nullptr;  // host view
     uint8_t* slot_dev = nullptr;
+    uint8_t* hslot = nullptr;  // pinned host slot (the slot itself without VRAM; else the
+    uint8_t* hslot_dev = nullptr;  // requests over kServerVramMax)
+    void* vram = nullptr;  // the VRAM allocation of record + slot (dev_req)
+    bool dev_req = true;   // PBS_SERVER_VRAM=0: record + slot in pinned host memory (A/B)
     hipStream_t stream = nullptr;
     uint64_t seq = 0;
     bool running = false;
@@ -586,19 +595,61 @@ constexpr double kServerTimeoutS = 10.0;
 void server_stop(pbs_chunker* c) {
     ScanServer& sv = c->srv;
     if (!sv.running) return;
-    __atomic_store_n(&sv.mb->req_len, kServerQuit, __ATOMIC_RELEASE);
+    __atomic_store_n(&sv.req->req_len, kServerQuit, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();  // write-combined BAR stores leave now
     (void)hipStreamSynchronize(sv.stream);
-    __atomic_store_n(&sv.mb->req_len, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&sv.req->req_len, 0u, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
     sv.running = false;
 }
 
 int server_launch(pbs_chunker* c, uint64_t last) {
     ScanServer& sv = c->srv;
     __atomic_store_n(&sv.mb->exited, ~0ull, __ATOMIC_RELEASE);
-    HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.slot_dev, c->d_table.as<uint32_t>(), c->prm.thr, last,
-                                  kServerIdleTicks, sv.flags, sv.stream));
+    const uint32_t flags = sv.flags | (sv.vram ? kSrvDevReq : 0u);
+    HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.req_dev, sv.slot_dev, sv.hslot_dev, c->d_table.as<uint32_t>(), c->prm.thr,
+                                  last, kServerIdleTicks, flags, sv.stream));
     sv.running = true;
     return PBS_OK;
+}
+
+// Request record + slot in fine-grained VRAM that this process can store to directly (the
+// GPU's BAR mapping at the allocation's own address; mb_bar.hip).  Whether the host has
+// that mapping is tested without touching it: write(2) of the record into a pipe fails
+// with EFAULT on an unmapped address.  Then a host store must read back through the
+// runtime.  Any failure leaves sv.vram null (pinned host memory instead).
+void server_map_vram(pbs_chunker* c) {
+    ScanServer& sv = c->srv;
+    DeviceGuard g(c->device);
+    if (!g.ok) return;
+    void* p = nullptr;
+    const size_t bytes = 256 + kServerHist + kServerMaxBytes;
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess || !p) return;
+    bool mapped = false;
+    int fds[2];
+    if (pipe(fds) == 0) {
+        mapped = write(fds[1], p, sizeof(ServerReq)) == (ssize_t)sizeof(ServerReq);
+        close(fds[0]);
+        close(fds[1]);
+    }
+    if (mapped) {
+        ServerReq* r = static_cast<ServerReq*>(p);
+        std::memset(r, 0, sizeof(ServerReq));
+        r->pad0[0] = 0x5CA17E57u;
+        __builtin_ia32_sfence();
+        ServerReq back{};
+        mapped = hipMemcpyAsync(&back, p, sizeof back, hipMemcpyDeviceToHost, sv.stream) == hipSuccess &&
+                 hipStreamSynchronize(sv.stream) == hipSuccess && back.pad0[0] == 0x5CA17E57u &&
+                 back.req_seq == 0 && back.req_len == 0;
+    }
+    if (!mapped) {
+        (void)hipFree(p);
+        (void)hipGetLastError();
+        return;
+    }
+    sv.vram = p;
+    sv.req = sv.req_dev = static_cast<ServerReq*>(p);
+    sv.slot = sv.slot_dev = static_cast<uint8_t*>(p) + 256;
 }
 
 // scan() of host bytes [pos, pos + bl) through the scan server: their candidates are
@@ -612,22 +663,36 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
         HIP_TRY(c, hipHostMalloc((void**)&sv.mb, sizeof(ServerMailbox), fl));
         std::memset(sv.mb, 0, sizeof(ServerMailbox));
-        HIP_TRY(c, hipHostMalloc((void**)&sv.slot, kServerHist + kServerMaxBytes, fl));
         HIP_TRY(c, hipHostGetDevicePointer((void**)&sv.mb_dev, sv.mb, 0));
-        HIP_TRY(c, hipHostGetDevicePointer((void**)&sv.slot_dev, sv.slot, 0));
         HIP_TRY(c, hipStreamCreateWithFlags(&sv.stream, hipStreamNonBlocking));
+        if (sv.dev_req) server_map_vram(c);
+        HIP_TRY(c, hipHostMalloc((void**)&sv.hslot, kServerHist + kServerMaxBytes, fl));
+        HIP_TRY(c, hipHostGetDevicePointer((void**)&sv.hslot_dev, sv.hslot, 0));
+        if (!sv.vram) {
+            sv.slot = sv.hslot;
+            sv.slot_dev = sv.hslot_dev;
+            sv.req = reinterpret_cast<ServerReq*>(sv.mb);
+            sv.req_dev = reinterpret_cast<ServerReq*>(sv.mb_dev);
+        }
     }
-    // slot: the history right-aligned in its first kServerHist bytes, then the data
-    std::memcpy(sv.slot + kServerHist - c->carry_len, c->carry, c->carry_len);
-    std::memcpy(sv.slot + kServerHist, hsrc, bl);
+    // slot: the history right-aligned in its first kServerHist bytes, then the data; long
+    // requests of a VRAM-mode server go to the pinned slot (kServerVramMax)
+    const bool host_slot = sv.vram && bl > kServerVramMax;
+    uint8_t* const slot = host_slot ? sv.hslot : sv.slot;
+    std::memcpy(slot + kServerHist - c->carry_len, c->carry, c->carry_len);
+    std::memcpy(slot + kServerHist, hsrc, bl);
     const uint32_t seq = (uint32_t)++sv.seq;
-    sv.mb->req_base = pos;
-    sv.mb->req_len = (uint32_t)bl;
+    sv.req->req_base = pos;
+    sv.req->req_len = (uint32_t)bl | (host_slot ? kServerHostSlot : 0u);
+    // write-combined BAR stores (slot, len, base) are not ordered by a release store: fence
+    // them out before the seq, and the seq itself after
+    __builtin_ia32_sfence();
     if (!sv.running) {
         int rc = server_launch(c, (uint32_t)(seq - 1));
         if (rc) return rc;
     }
-    __atomic_store_n(&sv.mb->req_seq, seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&sv.req->req_seq, seq, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t ack = 0;
     for (uint32_t spin = 0;; ++spin) {
@@ -1272,15 +1337,18 @@ void destroy(pbs_chunker* c) {
         const ScanServer& sv = c->srv;
         const double n = (double)sv.probe_n;
         std::fprintf(stderr,
-                     "scan server probe: %llu requests, host round trip %.2f us; kernel: loads + chains %.2f us, "
-                     "hash %.2f us, compaction + ack %.2f us (request seen -> acknowledged %.2f us)\n",
-                     (unsigned long long)sv.probe_n, sv.probe_rtt_us / n, sv.probe_ticks[0] / n / 100.0,
+                     "scan server probe (request + slot in %s): %llu requests, host round trip %.2f us; kernel: "
+                     "loads + chains %.2f us, hash %.2f us, compaction + ack %.2f us (request seen -> acknowledged "
+                     "%.2f us)\n",
+                     sv.vram ? "VRAM" : "pinned host memory", (unsigned long long)sv.probe_n,
+                     sv.probe_rtt_us / n, sv.probe_ticks[0] / n / 100.0,
                      sv.probe_ticks[1] / n / 100.0, sv.probe_ticks[2] / n / 100.0,
                      (sv.probe_ticks[0] + sv.probe_ticks[1] + sv.probe_ticks[2]) / n / 100.0);
     }
     if (c->srv.stream) (void)hipStreamDestroy(c->srv.stream);
     if (c->srv.mb) (void)hipHostFree(c->srv.mb);
-    if (c->srv.slot) (void)hipHostFree(c->srv.slot);
+    if (c->srv.vram) (void)hipFree(c->srv.vram);
+    if (c->srv.hslot) (void)hipHostFree(c->srv.hslot);
     DevBuf* bufs[] = {&c->d_table, &c->d_pre, &c->d_counters, &c->d_susp, &c->d_cand, &c->d_C,
                       &c->d_sort_tmp, &c->d_nxt, &c->d_jtmp, &c->d_nf, &c->d_on, &c->d_cnt,
                       &c->d_off, &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in, &c->d_rec,
@@ -1356,6 +1424,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
         c->fused_force = e[0] == '1';
     }
     if (const char* e = std::getenv("PBS_SCAN_SERVER")) c->srv.enabled = e[0] != '0';
+    if (const char* e = std::getenv("PBS_SERVER_VRAM")) c->srv.dev_req = e[0] != '0';
     if (const char* e = std::getenv("PBS_SCAN_PASS")) c->scan_pass = e[0] != '0';
     if (const char* e = std::getenv("PBS_SERVER_POLL")) c->srv.flags = e[0] == '4' ? kSrvPollAll : 0u;
     if (const char* e = std::getenv("PBS_SERVER_PROBE"))

@@ -199,6 +199,12 @@ constexpr uint32_t kServerMaxBytes = 1u << 20;  // request slot (bigger calls: b
 constexpr uint32_t kServerCand = 16384;         // candidates one request may return
 constexpr uint32_t kServerHist = 64;            // slot bytes before the data: the history
 constexpr uint32_t kServerQuit = 1u << 31;      // req_len flag
+constexpr uint32_t kServerHostSlot = 1u << 30;  // req_len flag: the data are in the pinned host slot
+// requests up to this size go to the VRAM slot when there is one: the host's write-combined
+// BAR stores (~47 GB/s) beat the kernel's PCIe reads of pinned memory for short requests
+// only (8 KiB 7.2 -> 4.9 us round trip, 256 KiB reads 3.8 -> 3.6 GB/s, mb_bar.hip and
+// profiles/r03/vram)
+constexpr uint32_t kServerVramMax = 128u << 10;
 struct alignas(64) ServerMailbox {
     // host -> device: ONE 16-byte record the kernel polls with one load (the host stores
     // len and base before seq, all in one cache line, so a record with the new seq has them)
@@ -216,9 +222,22 @@ struct alignas(64) ServerMailbox {
     uint64_t probe[4];             // kSrvProbe: wall_clock64 at request seen, chains done, hashed, acked
     uint64_t cand[kServerCand];
 };
+// The request record alone (the layout of ServerMailbox's first 64 bytes).  With the
+// request in device memory (kSrvDevReq) the host writes it and the slot through the GPU's
+// BAR mapping of a fine-grained VRAM allocation, so the kernel polls and reads its own HBM
+// instead of pinned host memory across PCIe; otherwise it points at the mailbox.
+struct alignas(64) ServerReq {
+    uint32_t req_seq;
+    uint32_t req_len;
+    uint64_t req_base;
+    uint32_t pad0[12];
+};
+static_assert(sizeof(ServerReq) == 64, "ServerReq is one cache line");
 constexpr uint32_t kSrvPollAll = 1;  // launch flag: every wave polls (staggered), not one lane
 constexpr uint32_t kSrvProbe = 2;    // launch flag: per-request phase stamps into probe[]
-hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, const uint32_t* table_rot,
+constexpr uint32_t kSrvDevReq = 4;   // launch flag: request + slot in fine-grained VRAM written by the host
+hipError_t launch_scan_server(ServerMailbox* mb_dev, const ServerReq* req_dev, const uint8_t* slot_dev,
+                              const uint8_t* hslot_dev, const uint32_t* table_rot,
                               uint32_t thr, uint64_t last_seq, uint64_t idle_ticks,
                               uint32_t flags, hipStream_t stream);
 

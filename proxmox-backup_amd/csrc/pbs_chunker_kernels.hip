@@ -967,12 +967,12 @@ hipError_t launch_fused_gather(const unsigned long long* rec, uint64_t nrec, uin
     return hipGetLastError();
 }
 
-hipError_t launch_scan_server(ServerMailbox* mb_dev, const uint8_t* slot_dev, const uint32_t* table_rot,
-                              uint32_t thr, uint64_t last_seq, uint64_t idle_ticks,
-                              uint32_t flags, hipStream_t stream) {
+hipError_t launch_scan_server(ServerMailbox* mb_dev, const ServerReq* req_dev, const uint8_t* slot_dev,
+                              const uint8_t* hslot_dev, const uint32_t* table_rot, uint32_t thr, uint64_t last_seq,
+                              uint64_t idle_ticks, uint32_t flags, hipStream_t stream) {
     (void)hipGetLastError();
-    hipLaunchKernelGGL(scan_server_kernel, dim3(1), dim3(kSrvThreads), 0, stream, mb_dev, slot_dev,
-                       table_rot, thr, last_seq, idle_ticks, flags);
+    hipLaunchKernelGGL(scan_server_kernel, dim3(1), dim3(kSrvThreads), 0, stream, mb_dev, req_dev, slot_dev,
+                       hslot_dev, table_rot, thr, last_seq, idle_ticks, flags);
     return hipGetLastError();
 }
 

@@ -1,12 +1,16 @@
 // scan_server_kernel: the low-latency path of pbs_chunker_scan (Chunker::scan,
 // chunker.rs:112-168, called by ChunkStream on every read, chunk_stream.rs:40-77).
 //
-// ONE persistent workgroup polls the mailbox (pbs_chunker_internal.h) in fine-grained
-// pinned host memory with 16-byte loads {seq, len | quit, base} (kSrvPollAll: lane 0 of
-// every wave, staggered).  A request then costs one more PCIe round trip: every lane loads
-// its 32 bytes of the slot straight into registers (8 KiB per pass over 256 lanes; the
-// next kSrvAhead passes' bytes in flight while one is hashed -- a dependent load of host
-// memory takes ~1.2 us, 8 KiB ~1.6 us, scripts/microbench/mb_poll.hip).
+// ONE persistent workgroup polls the request record (pbs_chunker_internal.h ServerReq)
+// with 16-byte loads {seq, len | quit, base} (kSrvPollAll: lane 0 of every wave,
+// staggered), then every lane loads its 32 bytes of the slot straight into registers (8 KiB
+// per pass over 256 lanes; the next kSrvAhead passes' bytes in flight while one is hashed).
+// kSrvDevReq (the default since round 3): record and slot live in fine-grained VRAM that the
+// host writes through the BAR (posted write-combined stores), so polling and the slot
+// reads stay in this GPU's HBM -- 8 KiB round trip 7.2 -> 4.9 us in
+// scripts/microbench/mb_bar.hip.  Otherwise both sit in the mailbox's pinned host memory
+// and cost PCIe round trips (a dependent load of host memory ~1.2 us, 8 KiB ~1.6 us,
+// mb_poll.hip).  Acknowledgement and candidates always go to pinned host memory.
 //
 // The hash at every position without the 64-step warm-up per lane: with the chain
 // Q(j) = rotl(Q(j-1), 1) ^ T[b_j] over the whole slot, h(j) = Q(j) ^ Q(j-64) (rotations are
@@ -60,7 +64,9 @@ __device__ __forceinline__ uint32_t srv_row_dw(uint32_t r, uint32_t i) {  // dwo
 }
 
 __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox* mb,
-                                                                  const uint8_t* __restrict__ slot,
+                                                                  const ServerReq* req,
+                                                                  const uint8_t* __restrict__ slot_main,
+                                                                  const uint8_t* __restrict__ slot_host,
                                                                   const uint32_t* __restrict__ table_rot,
                                                                   uint32_t thr, uint64_t last_seq,
                                                                   uint64_t idle_ticks, uint32_t flags) {
@@ -91,7 +97,7 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                 for (int d = 0; d < wave; ++d) __builtin_amdgcn_s_sleep(8);
             for (;;) {
                 if (__hip_atomic_load(&s_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-                const srv_u32x4 r = *reinterpret_cast<volatile srv_u32x4*>(&mb->req_seq);
+                const srv_u32x4 r = *reinterpret_cast<const volatile srv_u32x4*>(&req->req_seq);
                 uint32_t go = 0;
                 if (r.y & kServerQuit) {
                     go = 2;
@@ -110,7 +116,12 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             }
         }
         __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the slot is read after the record
+        // the slot is read after the record; a slot in VRAM written over the BAR is reused by
+        // every request, so no stale line of it may survive in the caches (system scope)
+        if (flags & kSrvDevReq)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        else
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (s_go != 1) {
             if (tid == 0)
                 __hip_atomic_store(&mb->exited, (uint64_t)last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -118,7 +129,9 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
         }
         const uint64_t t_seen = probe ? wall_clock64() : 0;
         uint64_t t_loaded = 0, t_hashed = 0;
-        const uint32_t seq = (uint32_t)ctl[0], len = (uint32_t)(ctl[0] >> 32);
+        const uint32_t seq = (uint32_t)ctl[0], len = (uint32_t)(ctl[0] >> 32) & ~kServerHostSlot;
+        // long requests of a VRAM-mode server come in the pinned host slot (kServerHostSlot)
+        const uint8_t* const slot = (ctl[0] >> 32) & kServerHostSlot ? slot_host : slot_main;
         const uint64_t base = ctl[1];
         const srv_u32x4* const src = reinterpret_cast<const srv_u32x4*>(slot + kServerHist);
         // this lane's 32 bytes of pass p (lanes wholly past the data load nothing)

@@ -296,6 +296,31 @@ def test_scan_feed_granularity(gpu, oracle, feed, avg, n):
     assert np.array_equal(np.array(got, dtype=np.uint64), ref)
 
 
+@pytest.mark.parametrize("vram", ["1", "0"])
+@pytest.mark.parametrize("feed", [8192, 256 * KiB + 3])
+def test_scan_server_request_placement(gpu, oracle, monkeypatch, vram, feed):
+    """scan() per read with the server's request record + slot in BAR-written VRAM (default;
+    requests over 128 KiB in the pinned slot) and in pinned host memory
+    (PBS_SERVER_VRAM=0): the oracle's cuts either way, over many requests that reuse the
+    same slots (stale lines would show here)."""
+    monkeypatch.setenv("PBS_SERVER_VRAM", vram)
+    n, avg = 6 * MiB + 333, 64 * KiB
+    data = gen_np.gen_random(n, 0x5EED0011)
+    ref = oracle.chunk_feed(avg, data, 0)
+    got = []
+    with gpu.Chunker(avg) as c:
+        for piece in range(0, n, feed):
+            p = data[piece:piece + feed]
+            off = 0
+            while off < p.size:
+                k = c.scan(p[off:])
+                if k == 0:
+                    break
+                off += k
+                got.append(piece + off)
+    assert np.array_equal(np.array(got, dtype=np.uint64), ref)
+
+
 def test_chunker1_whole_buffer(gpu):
     """test_chunker1's test2 loop on its own 1 MiB counter buffer (chunker.rs:246-257)."""
     buf = gen_np.gen_counter(1 * MiB)
