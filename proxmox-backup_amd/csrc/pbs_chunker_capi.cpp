@@ -618,10 +618,8 @@ int server_launch(pbs_chunker* c, uint64_t last) {
 // that mapping is tested without touching it: write(2) of the record into a pipe fails
 // with EFAULT on an unmapped address.  Then a host store must read back through the
 // runtime.  Any failure leaves sv.vram null (pinned host memory instead).
-void server_map_vram(pbs_chunker* c) {
+void server_map_vram(pbs_chunker* c) {  // on the handle's device (server_scan's guard)
     ScanServer& sv = c->srv;
-    DeviceGuard g(c->device);
-    if (!g.ok) return;
     void* p = nullptr;
     const size_t bytes = 256 + kServerHist + kServerMaxBytes;
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess || !p) return;
@@ -660,6 +658,10 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
     *served = false;
     if (!sv.enabled || sv.broken || bl == 0 || bl > kServerMaxBytes || !c->prm.hash_cuts) return PBS_OK;
     if (!sv.mb) {
+        // the handle's device, whatever the calling thread's current one is: the stream,
+        // the VRAM record and the kernel must sit with the handle's table
+        DeviceGuard g(c->device);
+        if (!g.ok) return fail(c, PBS_ERR_HIP);
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
         HIP_TRY(c, hipHostMalloc((void**)&sv.mb, sizeof(ServerMailbox), fl));
         std::memset(sv.mb, 0, sizeof(ServerMailbox));
