@@ -61,6 +61,9 @@ def parse():
                          "launcher and aggregation without a GPU)")
     ap.add_argument("--host-inclusive-gib", type=float, default=4.0,
                     help="also time the host-buffer path (H2D + kernels + D2H) on this many GiB; 0 = skip")
+    ap.add_argument("--pinned-out", type=int, default=1,
+                    help="1: the timed passes write the cut list into a pinned host array allocated "
+                         "once; 0: a pageable array per call (the Python default, A/B)")
     ap.add_argument("--secondary-random", type=int, default=1,
                     help="after the headline, regenerate the same buffer as random data and "
                          "time the pass over it too (a secondary line: no zero extents)")
@@ -726,9 +729,16 @@ def main():
                                  stream.cuda_stream)
         torch.cuda.synchronize()
         ptr = buf.data_ptr()
+        # the cut list lands in a pinned host array allocated once (DMA straight into it; a
+        # pageable one is staged through a bounce buffer and then copied: ~6 MB per pass
+        # at 64 KiB averages)
+        cut_out = None
+        if args.pinned_out:
+            cut_out = torch.empty(ch.cuts_bound(size), dtype=torch.int64,
+                                  pin_memory=True).numpy().view(np.uint64)
 
         def step():
-            return ch.find_cuts_device(ptr, size, is_final=True)
+            return ch.find_cuts_device(ptr, size, is_final=True, out=cut_out)
         work_bytes = size
 
     scan_ms, last, fused = [], {}, []

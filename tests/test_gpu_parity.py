@@ -147,6 +147,28 @@ def test_find_cuts_device(gpu, oracle):
     assert t["bytes"] == n - half and t["total_ms"] > 0
 
 
+def test_find_cuts_device_into_pinned_out(gpu, oracle):
+    """find_cuts_device(out=...) as bench.py times it: the cut list DMA'd into a pinned
+    host array (64 KiB averages: a long list), the oracle's cuts, and a too-small or
+    wrongly typed array refused."""
+    import torch
+    n = 40 * MiB + 3
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n, gpu.GEN_RANDOM, 0x5EED0002, 0)
+    host = dev.cpu().numpy()
+    ref = oracle.chunk_feed(64 * KiB, host)
+    with gpu.Chunker(64 * KiB) as c:
+        c.set_stream(torch.cuda.current_stream().cuda_stream)
+        out = torch.empty(c.cuts_bound(n), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+        for _ in range(2):  # the same array reused
+            got = c.find_cuts_device(dev.data_ptr(), n, is_final=True, out=out)
+            assert np.array_equal(got[:-1], ref) and int(got[-1]) == n
+        with pytest.raises(ValueError):
+            c.find_cuts_device(dev.data_ptr(), n, is_final=True, out=out[:8])
+        with pytest.raises(ValueError):
+            c.find_cuts_device(dev.data_ptr(), n, is_final=True, out=out.view(np.int64))
+
+
 def _zebra(n_runs: int, zero_run: int, rand_run: int, seed: int) -> np.ndarray:
     """Zero runs (no candidates -> long forced-cut runs) between random runs."""
     r = gen_np.gen_random(n_runs * rand_run, seed)
