@@ -152,7 +152,7 @@ def test_find_cuts_device_into_pinned_out(gpu, oracle):
     host array (64 KiB averages: a long list), the oracle's cuts, and a too-small or
     wrongly typed array refused."""
     import torch
-    n = 40 * MiB + 3
+    n = 40 * MiB + 8  # the generator writes whole 8-byte words
     dev = torch.empty(n, dtype=torch.uint8, device="cuda")
     gpu.generate_device(dev.data_ptr(), n, gpu.GEN_RANDOM, 0x5EED0002, 0)
     host = dev.cpu().numpy()
