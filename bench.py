@@ -77,6 +77,10 @@ def parse():
                     help="also time the host-stream pipeline (copy -> chunk -> SHA-256 per chunk, "
                          "pbs_pipeline_host) over this many GiB of a pageable host copy of the "
                          "stream, with the oracle + hashlib on the host cores beside it")
+    ap.add_argument("--verify", type=int, default=1,
+                    help="1: after the timed region compare every rank's cut list (and the "
+                         "secondary line's) with tests/golden/bench_cuts.json (oracle-made) and "
+                         "exit 3 unless all match; 0: skip (streams without a golden entry)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per scan launch (written by profiles/collect_traffic.py)")
     return ap.parse_args()
@@ -227,18 +231,20 @@ def secondary_random(args, ch, buf, stream, steps: int = 3):
         wall.append(time.perf_counter() - t0)
         t = ch.last_timing()
         scan.append(t["scan_ms"])
-        fused.append(t["fused"] == t["bytes"])
+        fused.append(pass_path(t))
         n = int(cuts.size)
     ms = float(np.mean(wall)) * 1e3
     sk = float(np.mean(scan))
     achieved = size / (sk / 1e3) / 1e9
+    rec = {"chunks": n, **cut_record(cuts, keep=0)}
+    if args.verify:
+        verify_record(rec, "random", size, args.avg, SEEDS["random"])
     return {"workload": f"random-{args.size_gib:g}GiB-avg{args.avg}", "seed": hex(SEEDS["random"]),
             "value": round(size / (1 << 30) / (ms / 1e3), 3), "unit": "GiB/s", "steps": steps,
-            "ms_per_step": round(ms, 3), "chunks": n,
+            "ms_per_step": round(ms, 3), **rec,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "kernel": "scan_fused_kernel" if all(fused) else "scan_main_kernel",
-                         "avg_launch_ms": round(sk, 4)}}
+                         "kernel": kernel_name(fused), "avg_launch_ms": round(sk, 4)}}
 
 
 def blob_stage(args, buf, cuts, stream, reps: int = 2):
@@ -577,6 +583,26 @@ def launch_ranks(args) -> int:
     return rc
 
 
+def pass_path(t: dict) -> str:
+    """Which path a pass took (last_timing): the one-launch fused pass, the scan pass
+    (scan_fused_kernel without resolver waves + gather + multi-kernel resolve) or the
+    multi-launch path (scan_main_kernel + scan_exact + sort + resolve)."""
+    if t["bytes"] > 0 and t["scan_pass"] == t["bytes"]:
+        return "scan_pass"
+    if t["bytes"] > 0 and t["fused"] == t["bytes"]:
+        return "fused"
+    return "multi"
+
+
+def kernel_name(paths) -> str:
+    """The dominant kernel of the timed passes (the roofline's kernel)."""
+    if paths and all(p == "fused" for p in paths):
+        return "scan_fused_kernel"
+    if paths and all(p == "scan_pass" for p in paths):
+        return "scan_fused_kernel (scan pass)"
+    return "scan_main_kernel"
+
+
 def timed_steps(step, args, dist, sync, after=None):
     """W untimed warm-up steps, then exactly K steps bracketed by a barrier + device sync
     on both sides.  Returns (this rank's elapsed seconds, last step's result)."""
@@ -613,6 +639,44 @@ def cut_record(cuts, keep: int = 8192) -> dict:
     return out
 
 
+# PBS_BENCH_GOLDEN: another golden file (tests: a corrupted copy must fail verification)
+GOLDEN = os.environ.get("PBS_BENCH_GOLDEN", os.path.join(ROOT, "tests", "golden", "bench_cuts.json"))
+_golden = None
+
+
+def golden_entry(workload: str, size: int, avg: int, seed: int):
+    """The oracle-made record of this stream (tests/golden/make_bench_golden.py), or None."""
+    global _golden
+    if _golden is None:
+        try:
+            with open(GOLDEN) as f:
+                _golden = json.load(f)["streams"]
+        except (OSError, ValueError, KeyError):
+            _golden = {}
+    return _golden.get(f"{workload}:{size}:{avg}:{seed:#x}")
+
+
+def verify_record(rec: dict, workload: str, size: int, avg: int, seed: int) -> dict:
+    """Compares a timed cut list's record (cut_record) with the golden one: adds
+    "verified" True / False, or None with "verify_note" when no golden entry exists."""
+    g = golden_entry(workload, size, avg, seed)
+    if g is None:
+        rec["verified"] = None
+        rec["verify_note"] = (f"no golden entry for {workload}:{size}:{avg}:{seed:#x} in "
+                              f"tests/golden/bench_cuts.json")
+    else:
+        rec["verified"] = bool(g["cuts_sha256"] == rec["cuts_sha256"] and g["chunks"] == rec["chunks"])
+        if not rec["verified"]:
+            rec["verify_note"] = (f"cut list differs from the oracle's: {rec['chunks']} chunks, sha "
+                                  f"{rec['cuts_sha256'][:16]} vs {g['chunks']}, {g['cuts_sha256'][:16]}")
+    return rec
+
+
+def verdict(recs, extra=()) -> bool:
+    """True when every rank's (and every extra line's) cut list equals its golden one."""
+    return all(r.get("verified") is True for r in list(recs) + list(extra))
+
+
 def per_rank_records(rec: dict, dist, world: int):
     if dist is None:
         return [rec]
@@ -643,9 +707,17 @@ def standin_main(args, world: int, rank: int):
     buf = {"counter": lambda: oracle.gen_counter(size, 0),
            "random": lambda: oracle.gen_random(size, seed, 0),
            "vmimage": lambda: oracle.gen_vmimage(size, seed, 0)}[args.workload]()
-    elapsed, cuts = timed_steps(lambda: oracle.chunk_feed(args.avg, buf), args, dist, lambda: None)
-    recs = per_rank_records({"rank": rank, "seed": seed, "elapsed_s": elapsed, "bytes": size,
-                             "chunks": int(cuts.size), **cut_record(cuts)}, dist, world)
+    import numpy as np
+
+    def step():  # find_cuts(..., is_final=True)'s list: the stream end when the tail is non-empty
+        c = oracle.chunk_feed(args.avg, buf)
+        return np.append(c, np.uint64(size)) if size and (c.size == 0 or int(c[-1]) != size) else c
+    elapsed, cuts = timed_steps(step, args, dist, lambda: None)
+    rec = {"rank": rank, "seed": seed, "elapsed_s": elapsed, "bytes": size,
+           "chunks": int(cuts.size), **cut_record(cuts)}
+    if args.verify:
+        verify_record(rec, args.workload, size, args.avg, seed)
+    recs = per_rank_records(rec, dist, world)
     mx, total = aggregate(elapsed, size, dist, torch.device("cpu"))
     if rank == 0:
         out = base_line(args, "STAND-IN (CPU oracle over gloo, not a GPU measurement): GiB/s chunked",
@@ -655,9 +727,13 @@ def standin_main(args, world: int, rank: int):
                          "stream_bytes_per_rank": size})
         out["stand_in"] = True
         out["per_rank"] = recs
+        if args.verify:
+            out["verified"] = verdict(recs)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    if args.verify and not verdict(recs):
+        sys.exit(3)
 
 
 def main():
@@ -746,13 +822,17 @@ def main():
     def after(cuts):
         t = ch.last_timing()
         scan_ms.append(t["scan_ms"])
-        fused.append(t["fused"] == t["bytes"] and t["bytes"] > 0)
+        fused.append(pass_path(t))
         last.update(t, ncuts=int(cuts.size))
 
     elapsed, cuts = timed_steps(step, args, dist, torch.cuda.synchronize, after)
-    recs = per_rank_records({"rank": rank, "seed": seed, "elapsed_s": round(elapsed, 6),
-                             "bytes": work_bytes, "chunks": last.get("ncuts", 0),
-                             **cut_record(cuts)}, dist, world)
+    # after the timed region: this rank's last timed cut list against the oracle's golden
+    # record of the same stream (tests/golden/bench_cuts.json)
+    rec = {"rank": rank, "seed": seed, "elapsed_s": round(elapsed, 6), "bytes": work_bytes,
+           "chunks": int(cuts.size), **cut_record(cuts)}
+    if args.verify:
+        verify_record(rec, args.workload, size, args.avg, seed)
+    recs = per_rank_records(rec, dist, world)
     elapsed, total_bytes = aggregate(elapsed, work_bytes, dist, red_dev)
 
     value = total_bytes * args.steps / (1 << 30) / elapsed
@@ -789,6 +869,8 @@ def main():
     if rank != 0:
         if dist:
             dist.destroy_process_group()
+        if args.verify and not verdict(recs):
+            sys.exit(3)
         return
     default_cfg = (args.size_gib == 64.0 and args.avg == 4 * 1024 * 1024
                    and args.workload == "vmimage" and args.mode == "streams")
@@ -808,13 +890,13 @@ def main():
     out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                        "traffic_note": traffic_note,
-                       "kernel": "scan_fused_kernel" if fused and all(fused) else "scan_main_kernel",
+                       "kernel": kernel_name(fused),
                        "avg_launch_ms": round(avg_scan_s * 1e3, 4)}
     out["build_id"] = pbschunk.build_id()
     if share:
         out["rehearsal"] = "TEST ONLY: all ranks on GPU 0 over gloo; not a scaling measurement"
+    out["per_rank"] = recs
     if dist is not None:
-        out["per_rank"] = recs
         out["backend"] = dist.get_backend()
     if host_incl is not None:
         out["host_inclusive_gib_s"] = round(host_incl, 3)
@@ -831,9 +913,18 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)
         if args.cpu_config1:
             out["cpu_config1"] = cpu_config1(args)
+    extra = [out["secondary_random"]] if "secondary_random" in out else []
+    if args.verify:
+        # every timed cut list (each rank's, the secondary line's) equals the oracle's
+        out["verified"] = verdict(recs, extra)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    if args.verify and not out["verified"]:
+        print("bench.py: a timed cut list is not verified against tests/golden/bench_cuts.json "
+              "(see per_rank / secondary_random verify_note; --verify 0 for streams without a "
+              "golden entry)", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

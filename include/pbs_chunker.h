@@ -114,7 +114,9 @@ typedef struct {
     uint64_t suspects;  /* 128-byte blocks flagged by the main kernel */
     uint64_t candidates;
     uint64_t cuts;
-    uint64_t fused;     /* bytes chunked by the one-launch pass (scan_fused_kernel) */
+    uint64_t fused;     /* bytes chunked by scan_fused_kernel: the one-launch pass or the scan pass */
+    uint64_t scan_pass; /* of those, bytes through the scan pass (no resolver waves; gather +
+                         * multi-kernel resolve after it: 64/128 KiB averages) */
 } pbs_timing;
 int pbs_chunker_last_timing(const pbs_chunker *c, pbs_timing *t);
 

@@ -26,6 +26,7 @@
  */
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 #include <math.h>
 
@@ -247,4 +248,79 @@ static inline uint8_t vm_byte(uint64_t seed, uint64_t x) {
 
 void ora_gen_vmimage(uint8_t *buf, uint64_t len, uint64_t seed, uint64_t offset) {
     for (uint64_t k = 0; k < len; k++) buf[k] = vm_byte(seed, offset + k);
+}
+
+/* The same bytes as ora_gen_{counter,random,vmimage} (kind 0/1/2), a word at a time
+ * where the range is 8-byte aligned (one splitmix64 per word instead of per byte;
+ * tests/test_oracle.py checks the two agree), for the long streams of
+ * tests/golden/make_bench_golden.py. */
+static void gen_block(int kind, uint64_t seed, uint8_t *buf, uint64_t len, uint64_t off) {
+    if (kind == 0) { ora_gen_counter(buf, len, off); return; }
+    uint64_t k = 0;
+    for (; k < len && ((off + k) & 7u); k++)
+        buf[k] = kind == 1 ? (uint8_t)(splitmix64(seed ^ ((off + k) >> 3)) >> (((off + k) & 7) * 8))
+                           : vm_byte(seed, off + k);
+    uint64_t page = ~0ull;  /* VM image: the zero decision is made once per 4 KiB page */
+    int zero = 0;
+    for (; k + 8 <= len; k += 8) {
+        uint64_t x = off + k, w;
+        if (kind == 1) {
+            w = splitmix64(seed ^ (x >> 3));
+        } else {
+            if ((x >> 12) != page) {
+                page = x >> 12;
+                uint64_t g = x >> 30, ext = (splitmix64(seed ^ VM_SEED_EXT ^ g) & 15u) << 26;
+                uint64_t in_g = x & ((1ull << 30) - 1);
+                zero = (in_g >= ext && in_g < ext + (1ull << 26)) ||
+                       splitmix64(seed ^ VM_SEED_PAGE ^ page) % 100u < 40u;
+            }
+            w = zero ? 0 : splitmix64(seed ^ VM_SEED_WORD ^ (x >> 3));
+        }
+        memcpy(buf + k, &w, 8);  /* little-endian host */
+    }
+    for (; k < len; k++)
+        buf[k] = kind == 1 ? (uint8_t)(splitmix64(seed ^ ((off + k) >> 3)) >> (((off + k) & 7) * 8))
+                           : vm_byte(seed, off + k);
+}
+
+void ora_gen_block(int kind, uint64_t seed, uint8_t *buf, uint64_t len, uint64_t off) {
+    gen_block(kind, seed, buf, len, off);
+}
+
+/*
+ * The cut list of a whole generated stream (kind 0 counter, 1 random, 2 VM image; `len`
+ * bytes from offset 0) as the reference computes it: the stream is generated `piece`
+ * bytes at a time and fed through the caller loop of ChunkStream::poll_next
+ * (chunk_stream.rs:40-77) around ora_scan (chunker.rs:112-168), so no stream has to
+ * fit in memory.  Writes the absolute chunk END offsets, and at EOF the stream end when
+ * the tail is non-empty (chunk_stream.rs:64-68) -- the list find_cuts(..., is_final)
+ * returns.  Returns the count, -1 for a bad average, -2 if `cap` is too small, -3 when
+ * out of memory.
+ */
+int64_t ora_chunk_generated(int kind, uint64_t seed, uint64_t avg, uint64_t len, uint64_t piece,
+                            uint64_t *out, uint64_t cap) {
+    ora_chunker c;
+    if (ora_new(&c, avg) != 0) return -1;
+    if (piece == 0) piece = 16ull << 20;
+    uint8_t *buf = (uint8_t *)malloc(piece);
+    if (!buf) return -3;
+    uint64_t n = 0;
+    for (uint64_t base = 0; base < len; base += piece) {
+        uint64_t plen = len - base < piece ? len - base : piece;
+        gen_block(kind, seed, buf, plen, base);
+        uint64_t off = 0;
+        while (off < plen) {
+            uint64_t k = ora_scan(&c, buf + off, plen - off);
+            if (k == 0) break;
+            off += k;
+            if (n >= cap) { free(buf); return -2; }
+            out[n++] = base + off;
+        }
+    }
+    free(buf);
+    if (len > 0 && (n == 0 || out[n - 1] != len)) {
+        if (n >= cap) return -2;
+        out[n++] = len;
+    }
+    return (int64_t)n;
 }

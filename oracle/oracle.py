@@ -54,6 +54,10 @@ def lib():
             getattr(L, name).restype = None
         L.ora_gen_counter.argtypes = [p, u64, u64]
         L.ora_gen_counter.restype = None
+        L.ora_gen_block.argtypes = [ctypes.c_int, u64, p, u64, u64]
+        L.ora_gen_block.restype = None
+        L.ora_chunk_generated.argtypes = [ctypes.c_int, u64, u64, u64, u64, p, u64]
+        L.ora_chunk_generated.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -131,6 +135,31 @@ def gen_vmimage(length: int, seed: int, offset: int = 0) -> np.ndarray:
     a = np.empty(length, dtype=np.uint8)
     lib().ora_gen_vmimage(_ptr(a), length, seed, offset)
     return a
+
+
+GEN_KINDS = {"counter": 0, "random": 1, "vmimage": 2}
+
+
+def gen_block(kind: str, length: int, seed: int, offset: int = 0) -> np.ndarray:
+    """The word-at-a-time generator (same bytes as gen_counter/gen_random/gen_vmimage)."""
+    a = np.empty(length, dtype=np.uint8)
+    lib().ora_gen_block(GEN_KINDS[kind], seed, _ptr(a), length, offset)
+    return a
+
+
+def chunk_generated(kind: str, seed: int, avg: int, length: int, piece: int = 16 << 20) -> np.ndarray:
+    """Cut list (chunk END offsets, the stream end appended when the tail is non-empty:
+    find_cuts(..., is_final=True)'s list) of a whole generated stream, generated and
+    scanned `piece` bytes at a time by the streaming restatement of Chunker::scan --
+    streams of any length in bounded memory.  Releases the GIL (ctypes)."""
+    min_eff = max(avg // 4, 65)
+    cap = length // min_eff + 2
+    out = np.empty(cap, dtype=np.uint64)
+    n = lib().ora_chunk_generated(GEN_KINDS[kind], seed, int(avg), int(length), int(piece),
+                                  _ptr(out), cap)
+    if n < 0:
+        raise ValueError(f"oracle chunk_generated failed ({n})")
+    return out[:n].copy()
 
 
 def splitmix64(x: int) -> int:

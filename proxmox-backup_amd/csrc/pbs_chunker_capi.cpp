@@ -1189,6 +1189,7 @@ int fused_scan_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, ui
     c->timing.exact_ms += ms;  // the gather
     c->timing.bytes += bl;
     c->timing.fused += bl;
+    c->timing.scan_pass += bl;
     c->timing.suspects += nflag;
     c->timing.candidates += nnew;
     const uint64_t m = (uint64_t)np + nnew;

@@ -76,7 +76,7 @@ class Timing(ctypes.Structure):
         ("resolve_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
         ("bytes", ctypes.c_uint64), ("suspects", ctypes.c_uint64),
         ("candidates", ctypes.c_uint64), ("cuts", ctypes.c_uint64),
-        ("fused", ctypes.c_uint64),
+        ("fused", ctypes.c_uint64), ("scan_pass", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

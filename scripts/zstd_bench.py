@@ -2,7 +2,9 @@
 on text-like and pxar-like data (tests/corpus_gen.py): a seeded 32 MiB corpus tiled to
 --gib GiB in HBM (a chunk's window never reaches a neighbouring tile), cut by the GPU
 chunker at --avg, encoded --reps times (best wall clock), with libzstd level 1 on the
-host over the first 64 MiB for the ratio.
+host over the first 64 MiB for the ratio, and libzstd level 1 (+ zlib.crc32, the blob's
+CRC) over every chunk of the corpus on --threads host threads (default: the CPUs this
+process may use, capped by the cgroup quota: 16 on the GPU box) for the host rate.
 
     python scripts/zstd_bench.py [--corpus text|pxar|vm|both|text,vm,...] [--gib 1] [--avg 4194304]
 """
@@ -22,7 +24,14 @@ def main():
     ap.add_argument("--gib", type=float, default=1.0)
     ap.add_argument("--avg", type=int, default=4 << 20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=0)
     a = ap.parse_args()
+    import threading
+    import zlib
+
+    sys.path.insert(0, ROOT)
+    import bench
+    threads = a.threads or bench.cpu_threads(argparse.Namespace(cpu_threads=0))
     import numpy as np
     import torch
 
@@ -60,12 +69,34 @@ def main():
             ch = np.ascontiguousarray(host[int(bounds[i]):int(bounds[i + 1])])
             dst = np.empty(L.ZSTD_compressBound(ch.size), np.uint8)
             ref += L.ZSTD_compress(dst.ctypes.data, dst.size, ch.ctypes.data, ch.size, 1)
+        # host rate: libzstd level 1 + crc32 over every chunk, `threads` threads
+        nb = int(bounds.size - 1)
+
+        def work(ix):
+            dst = np.empty(L.ZSTD_compressBound(int(np.diff(bounds.astype(np.int64)).max())), np.uint8)
+            for i in ix:
+                a0, b0 = int(bounds[i]), int(bounds[i + 1])
+                r = L.ZSTD_compress(dst.ctypes.data, dst.size, host.ctypes.data + a0, b0 - a0, 1)
+                zlib.crc32(memoryview(dst)[:r])
+
+        host_best = None
+        for _ in range(2):
+            ths = [threading.Thread(target=work, args=(list(range(k, nb, threads)),)) for k in range(threads)]
+            h0 = time.perf_counter()
+            [x.start() for x in ths]
+            [x.join() for x in ths]
+            dt = time.perf_counter() - h0
+            host_best = dt if host_best is None else min(host_best, dt)
         print(json.dumps({"corpus": name, "bytes": n, "chunks": int(bounds.size - 1), "gen_s": round(gen_s, 1),
                           "GiB/s": round(n / (1 << 30) / (best["total_ms"] / 1e3), 2),
                           "ms": {k: round(best[k], 2) for k in ("total_ms", "compress_ms", "assemble_ms", "crc_ms")},
                           "out_in": round(best["bytes_out"] / n, 4),
                           "sample_payload": {"ours": ours, "libzstd_level1": ref, "ratio": round(ours / ref, 4),
-                                             "chunks": take}}), flush=True)
+                                             "chunks": take},
+                          "host_libzstd_level1": {"GiB/s": round(n / (1 << 30) / host_best, 2), "threads": threads,
+                                                  "version": int(L.ZSTD_versionNumber()),
+                                                  "sample": f"all {nb} chunks, best of 2, + zlib.crc32"}}),
+              flush=True)
         del dev, out
         pbschunk.blob_encode_release()
 

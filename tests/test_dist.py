@@ -146,14 +146,66 @@ def test_kfd_gpu_count_without_hip():
 
 def test_standin_records_cut_lists(oracle):
     """Every rank's record carries its cut list (and its SHA-256), so the multi-rank runs
-    can be diffed against the oracle rank by rank."""
+    can be diffed against the oracle rank by rank; each is verified against the golden
+    record (tests/golden/bench_cuts.json)."""
     size = int(0.01 * (1 << 30)) // 8 * 8
     rc, out, err = _run_bench(["--gpus", "2", "--cpu-standin", "--size-gib", "0.01", "--avg", "65536",
                                "--steps", "1", "--warmup", "0"])
     assert rc == 0, err[-2000:]
-    for r in out["per_rank"]:  # (the stand-in's list is the oracle's: no tail entry)
-        ref = oracle.chunk_feed(65536, oracle.gen_vmimage(size, r["seed"], 0))
-        assert r["cuts"] == [int(x) for x in ref] and r["chunks"] == ref.size
+    assert out["verified"] is True
+    for r in out["per_rank"]:  # (find_cuts(is_final)'s list: the stream end appended)
+        ref = _oracle_cuts(oracle, "vmimage", r["seed"], size, 65536)
+        assert r["cuts"] == ref and r["chunks"] == len(ref) and r["verified"] is True
+
+
+def test_bench_verification_fails_loudly(tmp_path):
+    """A cut list that differs from the golden record, or a stream without one, makes
+    bench.py print verified false / null and exit 3 (the line still printed)."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = json.load(open(os.path.join(root, "tests", "golden", "bench_cuts.json")))
+    size = int(0.01 * (1 << 30)) // 8 * 8
+    k = f"vmimage:{size}:{4 << 20}:{0x5EED0004:#x}"  # rank 1's entry
+    doc["streams"][k]["cuts_sha256"] = "0" * 64
+    bad = tmp_path / "golden.json"
+    bad.write_text(json.dumps(doc))
+    rc, out, err = _run_bench(["--gpus", "2", "--cpu-standin", "--size-gib", "0.01", "--steps", "1",
+                               "--warmup", "0"], env={"PBS_BENCH_GOLDEN": str(bad)})
+    assert rc == 3 and out["verified"] is False
+    recs = sorted(out["per_rank"], key=lambda r: r["rank"])
+    assert recs[0]["verified"] is True and recs[1]["verified"] is False
+    rc, out, err = _run_bench(["--gpus", "2", "--cpu-standin", "--size-gib", "0.02", "--steps", "1",
+                               "--warmup", "0"])
+    assert rc == 3 and out["verified"] is False
+    assert all(r["verified"] is None and "no golden entry" in r["verify_note"] for r in out["per_rank"])
+    rc, out, err = _run_bench(["--gpus", "2", "--cpu-standin", "--size-gib", "0.02", "--steps", "1",
+                               "--warmup", "0", "--verify", "0"])
+    assert rc == 0 and "verified" not in out
+
+
+def test_bench_golden_script_pinned(oracle):
+    """tests/golden/make_bench_golden.py reproduces its committed small entries, and its
+    streaming oracle (ora_chunk_generated, the stream generated 16 MiB at a time) equals
+    chunk_feed over the whole generated buffer with the tail appended."""
+    import json
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    import make_bench_golden as mbg
+    have = json.load(open(mbg.OUT))["streams"]
+    todo = [s for s in mbg.streams() if s[1] < (64 << 20)]
+    assert len(todo) == 4
+    for s in todo:
+        assert mbg.record(*s) == have[mbg.key(*s)]
+    # every bench stream has an entry: config 3 ranks 0-7, config 5, config 2, all averages
+    assert all(mbg.key(*s) in have for s in mbg.streams())
+    n = (40 << 20) + 13
+    for kind, seed in (("vmimage", 0x5EED0003), ("random", 0x5EED0002), ("counter", 0)):
+        buf = oracle.gen_block(kind, n, seed)
+        ref = oracle.chunk_feed(65536, buf)
+        ref = np.append(ref, np.uint64(n)) if ref.size == 0 or int(ref[-1]) != n else ref
+        assert np.array_equal(oracle.chunk_generated(kind, seed, 65536, n, piece=(3 << 20) + 5), ref)
 
 
 @pytest.mark.gpu

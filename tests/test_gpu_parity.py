@@ -250,7 +250,7 @@ def test_scan_pass(gpu, oracle, kind, n, avg):
         c.set_stream(torch.cuda.current_stream().cuda_stream)
         got = c.find_cuts_device(dev.data_ptr(), n, is_final=True)
         t = c.last_timing()
-    assert t["fused"] == t["bytes"] == n, t  # the scan pass served the whole stream
+    assert t["scan_pass"] == t["fused"] == t["bytes"] == n, t  # the scan pass served the whole stream
     assert np.array_equal(got[:-1], ref) and int(got[-1]) == n
     cuts = [n // 3 + 1, 2 * n // 3 + 4093]
     parts = []
@@ -530,7 +530,7 @@ def test_scan_pass_dense_falls_back(gpu, oracle):
     ref = oracle.chunk_feed(64 * KiB, host)
     if ref.size == 0 or int(ref[-1]) != n:
         ref = np.append(ref, np.uint64(n))
-    assert t["fused"] == 0, t  # the scan pass stood down
+    assert t["fused"] == 0 and t["scan_pass"] == 0, t  # the scan pass stood down
     assert np.array_equal(got, ref)
 
 
@@ -614,5 +614,5 @@ def test_fused_pass_pool(gpu, oracle, monkeypatch, gib, kind, avg, div, rnd):
     host = dev[:n].cpu().numpy()
     del dev
     cand, ref = _oracle_two_phase_parallel(oracle, host, avg)
-    assert t["fused"] == n and t["candidates"] == cand.size
+    assert t["fused"] == n and t["scan_pass"] == 0 and t["candidates"] == cand.size
     assert np.array_equal(got, ref)

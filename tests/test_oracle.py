@@ -80,6 +80,13 @@ def test_generators_match_numpy(oracle, gen):
         else:
             a, b = oracle.gen_vmimage(n, 0x5EED0003, off), gen_np.gen_vmimage(n, 0x5EED0003, off)
         assert np.array_equal(a, b), (gen, off, n)
+        # the word-at-a-time generator of the long golden streams writes the same bytes
+        seed = {"counter": 0, "random": 0x5EED0002, "vmimage": 0x5EED0003}[gen]
+        assert np.array_equal(a, oracle.gen_block(gen, n, seed, off)), (gen, off, n)
+    # page and extent edges of the VM image in word steps
+    for off, n in (((1 << 30) - 5 * 4096 - 3, 11 * 4096 + 7), (512 * MiB - 4096 - 5, 3 * 4096 + 11)):
+        assert np.array_equal(oracle.gen_vmimage(n, 0x5EED0003, off),
+                              oracle.gen_block("vmimage", n, 0x5EED0003, off))
 
 
 def test_vmimage_has_zero_pages_and_extent(oracle):
