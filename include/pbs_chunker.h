@@ -169,6 +169,11 @@ int pbs_table_copy(uint32_t *out256);
  * same build. */
 const char *pbs_build_id(void);
 
+/* Device buffers the library's per-device work areas have allocated so far (blob
+ * encoding, digests, CRCs, the known-chunk test reuse theirs across calls: a repeated call
+ * of the same size allocates nothing). */
+uint64_t pbs_debug_arena_allocs(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -36,6 +36,8 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+
+#include "dev_arena.h"
 #include <numeric>
 #include <thread>
 #include <vector>
@@ -142,9 +144,36 @@ CtrKey ctr_key(hipStream_t st, int dev) {
     return CtrKey{dev, st, shared ? std::this_thread::get_id() : std::thread::id()};
 }
 
-unsigned long long* stream_counter(hipStream_t st, int dev) {
+// A thread's counters of the shared stream handles (null stream, hipStreamPerThread) are
+// freed when the thread exits (or by release_thread_counters), so threads that come and
+// go leave no device allocations behind.
+void free_thread_counters(std::thread::id th) {
     std::lock_guard<std::mutex> g(g_ctr_mu);
+    for (auto it = g_ctrs.begin(); it != g_ctrs.end();) {
+        if (it->first.th == th && th != std::thread::id()) {
+            int cur = -1;
+            const bool have = hipGetDevice(&cur) == hipSuccess;
+            if (hipSetDevice(it->first.dev) == hipSuccess) (void)hipFree(it->second);
+            if (have) (void)hipSetDevice(cur);
+            it = g_ctrs.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+struct ThreadCounters {
+    bool armed = false;
+    ~ThreadCounters() {
+        if (armed) free_thread_counters(std::this_thread::get_id());
+    }
+};
+thread_local ThreadCounters t_counters;
+void arm_thread_counters() { t_counters.armed = true; }
+
+unsigned long long* stream_counter(hipStream_t st, int dev) {
     const CtrKey key = ctr_key(st, dev);
+    if (key.th != std::thread::id()) arm_thread_counters();
+    std::lock_guard<std::mutex> g(g_ctr_mu);
     auto it = g_ctrs.find(key);
     if (it != g_ctrs.end()) return it->second;
     int cur = -1;
@@ -158,7 +187,14 @@ unsigned long long* stream_counter(hipStream_t st, int dev) {
     return d;
 }
 
+ArenaPool& crc_pool() {
+    static ArenaPool* p = new ArenaPool;  // never destroyed (HIP may be torn down first at exit)
+    return *p;
+}
+
 }  // namespace
+
+void release_thread_counters() { free_thread_counters(std::this_thread::get_id()); }
 
 void release_stream_counter(hipStream_t st) {
     int dev = 0;
@@ -366,27 +402,30 @@ extern "C" int pbs_crc32_chunks_device(const uint8_t* dev_data, size_t data_len,
         return bounds[a + 1] - bounds[a] > bounds[b + 1] - bounds[b];
     });
     hipStream_t st = (hipStream_t)hip_stream;
-    uint64_t* d_bounds = nullptr;
-    uint32_t* d_order = nullptr;
-    uint32_t* d_crc = nullptr;
+    int sdev = 0;
+    if (hipStreamGetDevice(st, &sdev) != hipSuccess) return PBS_ERR_NO_DEVICE;
+    DeviceGuard dg(sdev);  // the work area belongs on the stream's device
+    if (!dg.ok) return PBS_ERR_NO_DEVICE;
+    ArenaLease ar(crc_pool(), sdev);
+    uint64_t* d_bounds = ar->get<uint64_t>(0, (n + 1) * 8);
+    uint32_t* d_order = ar->get<uint32_t>(1, n * 4);
+    uint32_t* d_crc = ar->get<uint32_t>(2, n * 4);
     int rc = PBS_OK;
-    if (hipMalloc(&d_bounds, (n + 1) * 8) != hipSuccess || hipMalloc(&d_order, n * 4) != hipSuccess ||
-        hipMalloc(&d_crc, n * 4) != hipSuccess) {
+    if (!d_bounds || !d_order || !d_crc) {
         rc = PBS_ERR_NOMEM;
     } else if (hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
                hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
         rc = PBS_ERR_HIP;
     } else {
         rc = pbs_crc32_chunks_async(dev_data, data_len, base, d_bounds, d_order, n, d_crc, hip_stream);
-        if (rc == PBS_OK && (hipMemcpyAsync(crcs, d_crc, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                             hipStreamSynchronize(st) != hipSuccess))
+        if (rc == PBS_OK && hipMemcpyAsync(crcs, d_crc, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
             rc = PBS_ERR_HIP;
     }
-    if (d_bounds) (void)hipFree(d_bounds);
-    if (d_order) (void)hipFree(d_order);
-    if (d_crc) (void)hipFree(d_crc);
+    if (hipStreamSynchronize(st) != hipSuccess && rc == PBS_OK) rc = PBS_ERR_HIP;  // (before the arena goes back)
     return rc;
 }
+
+extern "C" uint64_t pbs_debug_arena_allocs(void) { return g_arena_allocs.load(); }
 
 extern "C" uint32_t pbs_crc32(uint32_t crc, const uint8_t* data, size_t len) {
     static CrcTables tb;

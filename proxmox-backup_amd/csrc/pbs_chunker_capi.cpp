@@ -883,15 +883,21 @@ void fused_static_plan(uint64_t len, uint64_t nw, FusedPassArgs* a) {
     }
 }
 
-// Averages served by the fused pass: from 256 KiB.  Below, the scan pass (fused_scan_pass)
-// is faster: at 128 KiB the fused resolver's main wave, ~64 candidates per us, bounds the pass
+// Averages served by the fused pass: from 512 KiB (round 4; 256 KiB before).  Below, the scan
+// pass (fused_scan_pass) is faster.  At 256 KiB, same process, alternating handles
+// (scripts/ab_handles.py, profiles/r04/): 64 GiB random 11.78 fused vs 11.57 ms scan pass, 64 GiB
+// VM image 10.74 vs 10.68, 16 GiB VM image 2.85 vs 2.80, 8 GiB random 1.76 vs 1.58 -- the
+// fused kernel itself runs 0.2-0.3 ms longer there (its resolver's waits); at 512 KiB random
+// 11.25 vs 11.26 (equal), at 4 MiB random 11.32 vs 11.55 (the scan pass's gather + resolve after
+// the kernel, ~0.23 ms, then costs more than the fused kernel saves).  Round 3:
+// at 128 KiB the fused resolver's main wave, ~64 candidates per us, bounds the pass
 // (same process, profiles/r03/scanpass128k/: 8 GiB VM image 1.79-1.80 ms fused vs 1.53-1.57
 // scan pass, 8 GiB random 2.47-2.48 vs 1.60-1.64, 16 GiB VM image 3.16-3.17 vs 2.88-2.89,
 // 64 GiB random 12.7-13.2 vs 11.8-12.3, 64 GiB VM image 11.26-11.49 vs 11.18-11.42); at
 // 256 KiB (config 5) both are within noise of each other on the 64 GiB VM image.  With
 // PBS_FUSED=1 (tests) the fused pass serves from 128 KiB: a tile (1-2 MiB) of random data
 // then holds ~12-24 candidates, far below the 64 flagged blocks one tile's exact step takes.
-constexpr uint64_t kFusedMinAvg = 256 * 1024;
+constexpr uint64_t kFusedMinAvg = 512 * 1024;
 constexpr uint64_t kFusedForceMinAvg = 128 * 1024;
 constexpr uint64_t kFusedMinBytes = 0;
 

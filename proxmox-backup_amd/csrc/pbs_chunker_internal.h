@@ -264,6 +264,8 @@ struct DeviceGuard {
 
 // pbs_blob.hip: free the blob-CRC chunk counter kept for `st` (call before destroying it)
 void release_stream_counter(hipStream_t st);
+// frees the calling thread's counters of the shared stream handles (pbs_blob.hip)
+void release_thread_counters();
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,
                       int kind, hipStream_t stream);
 

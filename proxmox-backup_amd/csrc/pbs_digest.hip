@@ -24,6 +24,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+
+#include "dev_arena.h"
 #include <numeric>
 #include <thread>
 #include <vector>
@@ -514,6 +516,18 @@ __global__ __launch_bounds__(256) void zero_flags_kernel(const uint8_t* __restri
 
 using namespace pbs;
 
+namespace {
+// work areas of the synchronous digest / known-chunk entry points (dev_arena.h)
+pbs::ArenaPool& digest_pool() {
+    static pbs::ArenaPool* p = new pbs::ArenaPool;  // never destroyed (HIP may be torn down first)
+    return *p;
+}
+pbs::ArenaPool& known_pool() {
+    static pbs::ArenaPool* p = new pbs::ArenaPool;
+    return *p;
+}
+}  // namespace
+
 extern "C" int pbs_digest_chunks_async(const uint8_t* dev_data, size_t data_len, uint64_t base,
                                        const uint64_t* bounds_dev, const uint32_t* order_dev,
                                        size_t n, const uint8_t* key, size_t key_len,
@@ -556,12 +570,16 @@ extern "C" int pbs_digest_chunks_device(const uint8_t* dev_data, size_t data_len
         return bounds[a + 1] - bounds[a] > bounds[b + 1] - bounds[b];
     });
     hipStream_t st = (hipStream_t)hip_stream;
-    uint64_t* d_bounds = nullptr;
-    uint32_t* d_order = nullptr;
-    uint8_t* d_dig = nullptr;
+    int sdev = 0;
+    if (hipStreamGetDevice(st, &sdev) != hipSuccess) return PBS_ERR_NO_DEVICE;
+    pbs::DeviceGuard dg(sdev);  // the work area belongs on the stream's device
+    if (!dg.ok) return PBS_ERR_NO_DEVICE;
+    pbs::ArenaLease ar(digest_pool(), sdev);
+    uint64_t* d_bounds = ar->get<uint64_t>(0, (n + 1) * 8);
+    uint32_t* d_order = ar->get<uint32_t>(1, n * 4);
+    uint8_t* d_dig = ar->get<uint8_t>(2, n * 32);
     int rc = PBS_OK;
-    if (hipMalloc(&d_bounds, (n + 1) * 8) != hipSuccess || hipMalloc(&d_order, n * 4) != hipSuccess ||
-        hipMalloc(&d_dig, n * 32) != hipSuccess) {
+    if (!d_bounds || !d_order || !d_dig) {
         rc = PBS_ERR_NOMEM;
     } else if (hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
                hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
@@ -570,13 +588,10 @@ extern "C" int pbs_digest_chunks_device(const uint8_t* dev_data, size_t data_len
         rc = pbs_digest_chunks_async(dev_data, data_len, base, d_bounds, d_order, n, key, key_len,
                                      d_dig, hip_stream);
         if (rc == PBS_OK &&
-            (hipMemcpyAsync(digests, d_dig, n * 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
-             hipStreamSynchronize(st) != hipSuccess))
+            (hipMemcpyAsync(digests, d_dig, n * 32, hipMemcpyDeviceToHost, st) != hipSuccess))
             rc = PBS_ERR_HIP;
     }
-    if (d_bounds) (void)hipFree(d_bounds);
-    if (d_order) (void)hipFree(d_order);
-    if (d_dig) (void)hipFree(d_dig);
+    if (hipStreamSynchronize(st) != hipSuccess && rc == PBS_OK) rc = PBS_ERR_HIP;  // (before the arena goes back)
     return rc;
 }
 
@@ -587,23 +602,29 @@ extern "C" int pbs_known_chunks_device(const uint8_t* digests_dev, size_t n, con
     if (n == 0) return PBS_OK;
     if (!digests_dev || !is_known_dev || (k && !known_dev) || n > 0xFFFFFFF0u) return PBS_ERR_INVALID;
     hipStream_t st = (hipStream_t)hip_stream;
-    uint64_t *key = nullptr, *skey = nullptr;
-    uint32_t *idx = nullptr, *sidx = nullptr, *head = nullptr, *rstart = nullptr;
-    unsigned int* cnt = nullptr;
+    int sdev = 0;
+    if (hipStreamGetDevice(st, &sdev) != hipSuccess) return PBS_ERR_NO_DEVICE;
+    pbs::DeviceGuard dg(sdev);
+    if (!dg.ok) return PBS_ERR_NO_DEVICE;
+    pbs::ArenaLease ar(known_pool(), sdev);
+    uint64_t* key = ar->get<uint64_t>(0, n * 8);
+    uint64_t* skey = ar->get<uint64_t>(1, n * 8);
+    uint32_t* idx = ar->get<uint32_t>(2, n * 4);
+    uint32_t* sidx = ar->get<uint32_t>(3, n * 4);
+    uint32_t* head = ar->get<uint32_t>(4, n * 4);
+    uint32_t* rstart = ar->get<uint32_t>(5, n * 4);
+    unsigned int* cnt = ar->get<unsigned int>(6, 4);
     void* tmp = nullptr;
     int rc = PBS_OK;
     size_t tb_sort = 0, tb_scan = 0;
     const unsigned grid = (unsigned)((n + 255) / 256);
-    if (hipMalloc(&key, n * 8) != hipSuccess || hipMalloc(&skey, n * 8) != hipSuccess ||
-        hipMalloc(&idx, n * 4) != hipSuccess || hipMalloc(&sidx, n * 4) != hipSuccess ||
-        hipMalloc(&head, n * 4) != hipSuccess || hipMalloc(&rstart, n * 4) != hipSuccess ||
-        hipMalloc(&cnt, 4) != hipSuccess) {
+    if (!key || !skey || !idx || !sidx || !head || !rstart || !cnt) {
         rc = PBS_ERR_NOMEM;
         goto done;
     }
     if (radix_sort(nullptr, &tb_sort, key, skey, idx, sidx, n, 0, 64, st) != hipSuccess ||
         inclusive_max_u32(nullptr, &tb_scan, head, rstart, n, st) != hipSuccess ||
-        hipMalloc(&tmp, std::max(tb_sort, tb_scan)) != hipSuccess) {
+        !(tmp = ar->get<void>(7, std::max(tb_sort, tb_scan)))) {
         rc = PBS_ERR_NOMEM;
         goto done;
     }
@@ -637,8 +658,7 @@ extern "C" int pbs_known_chunks_device(const uint8_t* digests_dev, size_t n, con
         if (n_known) *n_known = h;
     }
 done:
-    for (void* q : {(void*)key, (void*)skey, (void*)idx, (void*)sidx, (void*)head, (void*)rstart, (void*)cnt, tmp})
-        if (q) (void)hipFree(q);
+    if (rc != PBS_OK) (void)hipStreamSynchronize(st);  // (before the arena goes back)
     return rc;
 }
 
@@ -751,6 +771,8 @@ extern "C" void pbs_digest_hybrid_release(void) {
     std::lock_guard<std::mutex> lk(hs.mu);
     hs.release();
     hs.dev = -1;
+    digest_pool().clear();
+    known_pool().clear();
 }
 
 extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* host_data, size_t data_len,
@@ -789,26 +811,23 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
     if (threads > 0)
         while (m < n && clen(order[m]) >= kZeroMin) ++m;
 
-    uint64_t* d_bounds = nullptr;
-    uint32_t* d_order = nullptr;
-    uint8_t* d_dig = nullptr;
-    uint8_t* d_flags = nullptr;
+    pbs::ArenaLease ar(digest_pool(), sdev);
+    uint64_t* d_bounds = ar->get<uint64_t>(0, (n + 1) * 8);
+    uint32_t* d_order = ar->get<uint32_t>(1, n * 4);
+    uint8_t* d_dig = ar->get<uint8_t>(2, n * 32);
+    uint8_t* d_flags = m ? ar->get<uint8_t>(3, m) : nullptr;
     int rc = PBS_OK;
     auto fail = [&](int r) {
         if (rc == PBS_OK) rc = r;
     };
-    if (hipMalloc(&d_bounds, (n + 1) * 8) != hipSuccess || hipMalloc(&d_order, n * 4) != hipSuccess ||
-        hipMalloc(&d_dig, n * 32) != hipSuccess || (m && hipMalloc(&d_flags, m) != hipSuccess))
-        fail(PBS_ERR_NOMEM);
+    if (!d_bounds || !d_order || !d_dig || (m && !d_flags)) fail(PBS_ERR_NOMEM);
     std::vector<uint8_t> zf(m, 0);
     // the host share's D2H copies run on the HostStage streams, which do not wait for the
     // caller's stream: this event marks the point on `st` after the caller's producer
     // work (recorded before anything of ours, so the copies do not also wait for the GPU
     // digest launch)
     hipEvent_t ready = nullptr;
-    if (rc == PBS_OK && !host_data && threads > 0 &&
-        (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess ||
-         hipEventRecord(ready, st) != hipSuccess))
+    if (rc == PBS_OK && !host_data && threads > 0 && (!(ready = ar->event(2)) || hipEventRecord(ready, st) != hipSuccess))
         fail(PBS_ERR_HIP);
     if (rc == PBS_OK && (hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
                          hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess))
@@ -864,7 +883,7 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
     const size_t g = work.size() - h;
     hipEvent_t ev[2] = {nullptr, nullptr};
     if (rc == PBS_OK && g) {
-        if (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess ||
+        if (!(ev[0] = ar->event(0)) || !(ev[1] = ar->event(1)) ||
             hipMemcpyAsync(d_order, work.data() + h, g * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipEventRecord(ev[0], st) != hipSuccess)
             fail(PBS_ERR_HIP);
@@ -931,11 +950,7 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
     if (rc == PBS_OK)
         for (const auto& d : dup)
             if (d.first != d.second) std::memcpy(digests + 32 * (size_t)d.first, digests + 32 * (size_t)d.second, 32);
-    for (auto e : ev)
-        if (e) (void)hipEventDestroy(e);
-    if (ready) (void)hipEventDestroy(ready);
-    for (void* p : {(void*)d_bounds, (void*)d_order, (void*)d_dig, (void*)d_flags})
-        if (p) (void)hipFree(p);
+    (void)hipStreamSynchronize(st);  // nothing of ours in flight when the arena goes back
     if (timing) {
         const HClock::time_point t1 = HClock::now();
         timing->total_ms = hms(t0, t1);

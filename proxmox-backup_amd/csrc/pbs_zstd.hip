@@ -54,6 +54,7 @@
 #include "pbs_blob.h"
 #include "pbs_chunker.h"
 #include "pbs_chunker_internal.h"
+#include "dev_arena.h"
 #include "zstd_enc.h"
 
 namespace pbs {
@@ -2166,35 +2167,16 @@ __global__ void blob_crc_header_kernel(const uint64_t* __restrict__ boff, const 
     h[3] = (uint8_t)(v >> 24);
 }
 
-// Per-device scratch kept for the process: the block slots (~ the input size) and the
-// sequence lists of the resident workgroups.
-struct ZScratch {
-    std::mutex mu;
-    int dev = -1;
-    uint8_t* slots = nullptr;
-    size_t slots_cap = 0;
-    Seq* seqs = nullptr;
-    size_t seqs_cap = 0;
-    Coded* coded = nullptr;
-    size_t coded_cap = 0;
-    uint32_t* chains = nullptr;
-    size_t chains_cap = 0;
-};
-ZScratch& zscratch() {
-    static ZScratch* z = new ZScratch;  // never destroyed (HIP may be torn down first at exit)
-    return *z;
+// Work areas of pbs_blob_encode_chunks_device, per device (dev_arena.h): the block slots
+// (~ the input size), the sequence lists of the resident workgroups and the per-call
+// arrays.  Concurrent calls on one device lease different arenas; a call in steady state
+// allocates and frees nothing.
+ArenaPool& zpool() {
+    static ArenaPool* p = new ArenaPool;  // never destroyed (HIP may be torn down first at exit)
+    return *p;
 }
-
-template <typename T>
-bool grow(T** p, size_t* cap, size_t need) {
-    if (*cap >= need) return true;
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    if (hipMalloc(p, need * sizeof(T)) != hipSuccess) return false;
-    *cap = need;
-    return true;
-}
+enum ZSlot : unsigned { kZsBounds, kZsItems, kZsFirst, kZsSizes, kZsIpre, kZsBsz, kZsBoff, kZsComp, kZsCrc, kZsTmp,
+                        kZsSlots, kZsSeqs, kZsCoded, kZsChains };
 
 }  // namespace
 }  // namespace pbs
@@ -2203,21 +2185,11 @@ using namespace pbs;
 
 extern "C" size_t pbs_zstd_frame_bound(size_t len) { return (size_t)zstd::frame_bound(len); }
 
-// Frees the blob encoder's cached device scratch (~ the bytes of the largest call).
+// Frees the blob encoder's idle device work areas (~ the bytes of the largest call each)
+// and the calling thread's CRC counters of the shared streams.
 extern "C" void pbs_blob_encode_release(void) {
-    ZScratch& z = zscratch();
-    std::lock_guard<std::mutex> lk(z.mu);
-    if (z.dev >= 0) {
-        DeviceGuard dg(z.dev);
-        for (void* p : {(void*)z.slots, (void*)z.seqs, (void*)z.coded, (void*)z.chains})
-            if (p) (void)hipFree(p);
-    }
-    z.slots = nullptr;
-    z.seqs = nullptr;
-    z.coded = nullptr;
-    z.chains = nullptr;
-    z.slots_cap = z.seqs_cap = z.coded_cap = z.chains_cap = 0;
-    z.dev = -1;
+    zpool().clear();
+    release_thread_counters();
 }
 
 extern "C" size_t pbs_blob_stream_bound(const uint64_t* bounds, size_t n) {
@@ -2263,12 +2235,6 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     first[n] = items.size();
     const uint64_t ni = items.size();
 
-    uint64_t *d_bounds = nullptr, *d_items = nullptr, *d_first = nullptr, *d_sizes = nullptr, *d_ipre = nullptr,
-             *d_bsz = nullptr, *d_boff = nullptr;
-    uint8_t* d_comp = nullptr;
-    uint32_t* d_crc = nullptr;
-    void* d_tmp = nullptr;
-    hipEvent_t ev[4] = {};
     int rc = PBS_OK;
     auto fail = [&](int r) {
         if (rc == PBS_OK) rc = r;
@@ -2279,37 +2245,34 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     (void)exclusive_sum_u64(nullptr, &t1b, nullptr, nullptr, (uint32_t)(n + 1), st);
     (void)exclusive_sum_u64(nullptr, &t2b, nullptr, nullptr, (uint32_t)(ni + 1), st);
     size_t tmpb = std::max(t1b, t2b);
-    if (hipMalloc(&d_bounds, (n + 1) * 8) != hipSuccess || hipMalloc(&d_items, ni * 8) != hipSuccess ||
-        hipMalloc(&d_first, (n + 1) * 8) != hipSuccess || hipMalloc(&d_sizes, (ni + 1) * 8) != hipSuccess ||
-        hipMalloc(&d_ipre, (ni + 1) * 8) != hipSuccess || hipMalloc(&d_bsz, (n + 1) * 8) != hipSuccess ||
-        hipMalloc(&d_boff, (n + 1) * 8) != hipSuccess || hipMalloc(&d_comp, n) != hipSuccess ||
-        hipMalloc(&d_crc, n * 4) != hipSuccess || hipMalloc(&d_tmp, std::max<size_t>(tmpb, 256)) != hipSuccess)
-        fail(PBS_ERR_NOMEM);
-    for (auto& e : ev)
-        if (rc == PBS_OK) ok(hipEventCreate(&e));
-    ZScratch& zs = zscratch();
-    std::lock_guard<std::mutex> lk(zs.mu);
     const unsigned grid = (unsigned)std::min<uint64_t>(ni, (uint64_t)ncu);  // one 512-thread workgroup per CU
-    if (rc == PBS_OK && compress) {
-        if (zs.dev != dev) {  // first use, or another device: free the old scratch there
-            if (zs.dev >= 0) {
-                DeviceGuard og(zs.dev);
-                for (void* p : {(void*)zs.slots, (void*)zs.seqs, (void*)zs.coded, (void*)zs.chains})
-                    if (p) (void)hipFree(p);
-            }
-            zs.slots = nullptr;
-            zs.seqs = nullptr;
-            zs.coded = nullptr;
-            zs.chains = nullptr;
-            zs.slots_cap = zs.seqs_cap = zs.coded_cap = zs.chains_cap = 0;
-            zs.dev = dev;
-        }
-        if (!grow(&zs.slots, &zs.slots_cap, ni * kSlot) ||
-            !grow(&zs.seqs, &zs.seqs_cap, (size_t)grid * kZBlockSeq) ||
-            !grow(&zs.coded, &zs.coded_cap, (size_t)grid * kZBlockSeq) ||
-            !grow(&zs.chains, &zs.chains_cap, (size_t)grid * 6 * kZBlockSeq))
-            fail(PBS_ERR_NOMEM);
+    ArenaLease ar(zpool(), dev);
+    uint64_t* d_bounds = ar->get<uint64_t>(kZsBounds, (n + 1) * 8);
+    uint64_t* d_items = ar->get<uint64_t>(kZsItems, ni * 8);
+    uint64_t* d_first = ar->get<uint64_t>(kZsFirst, (n + 1) * 8);
+    uint64_t* d_sizes = ar->get<uint64_t>(kZsSizes, (ni + 1) * 8);
+    uint64_t* d_ipre = ar->get<uint64_t>(kZsIpre, (ni + 1) * 8);
+    uint64_t* d_bsz = ar->get<uint64_t>(kZsBsz, (n + 1) * 8);
+    uint64_t* d_boff = ar->get<uint64_t>(kZsBoff, (n + 1) * 8);
+    uint8_t* d_comp = ar->get<uint8_t>(kZsComp, n);
+    uint32_t* d_crc = ar->get<uint32_t>(kZsCrc, n * 4);
+    void* d_tmp = ar->get<void>(kZsTmp, std::max<size_t>(tmpb, 256));
+    uint8_t* z_slots = nullptr;
+    Seq* z_seqs = nullptr;
+    Coded* z_coded = nullptr;
+    uint32_t* z_chains = nullptr;
+    if (compress) {
+        z_slots = ar->get<uint8_t>(kZsSlots, ni * kSlot);
+        z_seqs = ar->get<Seq>(kZsSeqs, (size_t)grid * kZBlockSeq * sizeof(Seq));
+        z_coded = ar->get<Coded>(kZsCoded, (size_t)grid * kZBlockSeq * sizeof(Coded));
+        z_chains = ar->get<uint32_t>(kZsChains, (size_t)grid * 6 * kZBlockSeq * sizeof(uint32_t));
+        if (!z_slots || !z_seqs || !z_coded || !z_chains) fail(PBS_ERR_NOMEM);
     }
+    if (!d_bounds || !d_items || !d_first || !d_sizes || !d_ipre || !d_bsz || !d_boff || !d_comp || !d_crc || !d_tmp)
+        fail(PBS_ERR_NOMEM);
+    hipEvent_t ev[4] = {};
+    for (unsigned i = 0; i < 4 && rc == PBS_OK; ++i)
+        if (!(ev[i] = ar->event(i))) fail(PBS_ERR_HIP);
     if (rc == PBS_OK)
         ok(hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st)) &&
             ok(hipMemcpyAsync(d_items, items.data(), ni * 8, hipMemcpyHostToDevice, st)) &&
@@ -2328,7 +2291,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
         }
         if (compress)
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
-                               ni, zs.slots, d_sizes, zs.seqs, zs.coded, zs.chains, zprobe ? 1 : 0);
+                               ni, z_slots, d_sizes, z_seqs, z_coded, z_chains, zprobe ? 1 : 0);
         if (compress && zprobe) {
             unsigned long long h[48] = {};
             (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
@@ -2364,7 +2327,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     if (rc == PBS_OK && blob_offsets[n] > blobs_cap) fail(PBS_ERR_CAPACITY);
     if (rc == PBS_OK) {
         hipLaunchKernelGGL(zstd_assemble_kernel, dim3((unsigned)std::min<uint64_t>(ni, (uint64_t)ncu * 8)),
-                           dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items, ni, d_first, zs.slots,
+                           dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items, ni, d_first, z_slots,
                            d_sizes, d_ipre, d_boff, d_comp, blobs_dev);
         ok(hipGetLastError()) && ok(hipEventRecord(ev[2], st));
     }
@@ -2394,11 +2357,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
         if (compressed)
             for (size_t i = 0; i < n; ++i) timing->compressed_chunks += compressed[i];
     }
-    for (auto e : ev)
-        if (e) (void)hipEventDestroy(e);
-    for (void* p : {(void*)d_bounds, (void*)d_items, (void*)d_first, (void*)d_sizes, (void*)d_ipre, (void*)d_bsz,
-                    (void*)d_boff, (void*)d_comp, (void*)d_crc, d_tmp})
-        if (p) (void)hipFree(p);
+    if (rc != PBS_OK) (void)hipStreamSynchronize(st);  // the arena goes back idle
     if (timing) timing->total_ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
     return rc;
 }

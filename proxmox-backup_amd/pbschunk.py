@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = (
     # include/pbs_blob.h (blob CRC)
     "pbs_crc32_chunks_device", "pbs_crc32_chunks_async", "pbs_crc32", "pbs_blob_encode_uncompressed",
     "pbs_blob_encode_chunks_device", "pbs_blob_stream_bound", "pbs_zstd_frame_bound",
-    "pbs_blob_encode_release", "pbs_digest_hybrid_release",
+    "pbs_blob_encode_release", "pbs_digest_hybrid_release", "pbs_debug_arena_allocs",
 )
 
 
@@ -168,6 +168,7 @@ def lib():
         "pbs_device_count": ([], i),
         "pbs_table_copy": ([p], i),
         "pbs_build_id": ([], ctypes.c_char_p),
+        "pbs_debug_arena_allocs": ([], u64),
         "pbs_chunker_candidates_device": ([p, p, sz, p, sz, u64, p, sz, ctypes.POINTER(sz)], i),
         "pbs_chunker_resolve_device": ([p, p, sz, u64, i, p, sz, ctypes.POINTER(sz)], i),
         "pbs_digest_chunks_device": ([p, sz, u64, p, sz, p, sz, p, p], i),
@@ -641,6 +642,11 @@ def blob_encode_chunks_device(dev_ptr: int, data_len: int, bounds, blobs_dev: in
     if rc != PBS_OK:
         raise ChunkerError(rc, "pbs_blob_encode_chunks_device")
     return offs, crcs, comp, t.as_dict()
+
+
+def debug_arena_allocs() -> int:
+    """Device buffers the per-device work areas have allocated so far (tests)."""
+    return int(lib().pbs_debug_arena_allocs())
 
 
 def blob_encode_release() -> None:

@@ -131,3 +131,57 @@ def test_two_fused_passes_at_once(gpu, oracle, monkeypatch):
         assert len(outs[k]) >= 3
         for i, got in enumerate(outs[k]):
             assert np.array_equal(got, refs[k]), f"handle {k} pass {i}"
+
+
+def test_blob_and_digest_threads_reuse_work_areas(gpu, oracle):
+    """Two threads, two streams: blob encoding (zstd frames + CRC) of one stream and
+    SHA-256 + CRC-32 of another's chunks at the same time, three rounds each.  Every
+    result equals the twin's / hashlib's / zlib's, and after one warm-up call of each the
+    repeated calls allocate no device memory (per-device work areas, csrc/dev_arena.h:
+    no hipMalloc / hipFree on the hot call)."""
+    import zlib
+
+    import torch
+
+    import corpus_gen
+    torch.cuda.set_device(0)
+    ta = np.concatenate([corpus_gen.text(6 * MiB, 31), corpus_gen.pxar(6 * MiB, 32),
+                         gen_np.gen_vmimage(4 * MiB, 0x5EED0003, 0)])
+    tb = gen_np.gen_vmimage(96 * MiB, 0x5EED0004, 5 * GiB)
+    bounds = []
+    for d in (ta, tb):
+        c = oracle.chunk_feed(256 * KiB, d)
+        bounds.append(np.concatenate([[0], _with_end(c, d.size)]).astype(np.uint64))
+    da, db = (torch.from_numpy(x).to("cuda") for x in (ta, tb))
+    torch.cuda.synchronize()
+    cap = gpu.blob_stream_bound(bounds[0])
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    exp_blobs = [oracle.blob_compressed(ta[int(a):int(b)].tobytes()) for a, b in zip(bounds[0][:-1], bounds[0][1:])]
+    exp_dig = oracle.chunk_digests(tb, bounds[1])
+    exp_crc = oracle.chunk_crcs(tb, bounds[1])
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def blobs():
+        offs, crcs, comp, tm = gpu.blob_encode_chunks_device(da.data_ptr(), ta.size, bounds[0], out.data_ptr(), cap,
+                                                             hip_stream=sa.cuda_stream)
+        img = out[: int(offs[-1])].cpu().numpy().tobytes()
+        for i, e in enumerate(exp_blobs):
+            b = img[int(offs[i]):int(offs[i + 1])]
+            assert b == e, f"blob {i}"
+            assert int(crcs[i]) == zlib.crc32(b[12:])
+
+    def digests():
+        dg = gpu.digest_chunks_device(db.data_ptr(), tb.size, bounds[1], hip_stream=sb.cuda_stream)
+        assert np.array_equal(dg, exp_dig)
+        cr = gpu.crc32_chunks_device(db.data_ptr(), tb.size, bounds[1], hip_stream=sb.cuda_stream)
+        assert np.array_equal(cr, exp_crc)
+
+    blobs()
+    digests()
+    a0 = gpu.debug_arena_allocs()
+
+    def loop(f):
+        return lambda: [f() for _ in range(3)]
+
+    _run_threads(loop(blobs), loop(digests))
+    assert gpu.debug_arena_allocs() == a0, "a repeated call allocated device memory"

@@ -234,9 +234,10 @@ def test_small_batches(gpu, oracle, avg, piece):
 
 @pytest.mark.parametrize("kind,n,avg", [("vmimage", 192 * MiB + 5, 64 * KiB), ("random", 96 * MiB, 64 * KiB),
                                         ("random", 40 * MiB + 3, 64 * KiB), ("vmimage", 160 * MiB + 3, 128 * KiB),
-                                        ("random", 72 * MiB, 128 * KiB)])
+                                        ("random", 72 * MiB, 128 * KiB), ("random", 200 * MiB + 7, 256 * KiB),
+                                        ("vmimage", 256 * MiB, 256 * KiB)])
 def test_scan_pass(gpu, oracle, kind, n, avg):
-    """64 and 128 KiB averages: scan_fused_kernel without resolver waves, the records' candidates
+    """64, 128 and 256 KiB averages: scan_fused_kernel without resolver waves, the records' candidates
     gathered in stream order, the multi-kernel resolve -- whole, and split into three calls
     (pending candidates of the open chunk carried over), against the oracle."""
     import torch
