@@ -621,7 +621,9 @@ int server_launch(pbs_chunker* c, uint64_t last) {
 void server_map_vram(pbs_chunker* c) {  // on the handle's device (server_scan's guard)
     ScanServer& sv = c->srv;
     void* p = nullptr;
-    const size_t bytes = 256 + kServerHist + kServerMaxBytes;
+    // the request record, then the slot: only requests up to kServerVramMax use it (longer
+    // ones go to the pinned host slot)
+    const size_t bytes = 256 + kServerHist + kServerVramMax;
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess || !p) return;
     bool mapped = false;
     int fds[2];

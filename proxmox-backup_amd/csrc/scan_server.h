@@ -273,10 +273,11 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             }
             s_go = 0;
             // ONE 8-byte store: seq, candidate count, overflow flag (the host reads them together);
-            // a release (an L2 write-back first) only when candidates were stored before it
+            // a release (an L2 write-back first) only when candidates -- or the probe stamps --
+            // were stored before it
             const uint64_t ack = (uint64_t)seq | (uint64_t)(total < kServerCand ? total : kServerCand) << 32 |
                                  (total > kServerCand ? 1ull << 63 : 0ull);
-            if (stored)
+            if (stored || probe)
                 __hip_atomic_store(&mb->ack_seq, ack, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             else
                 __hip_atomic_store(&mb->ack_seq, ack, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -306,15 +306,17 @@ class Chunker:
     def find_cuts_device(self, dev_ptr: int, length: int, is_final: bool = False,
                          out: Optional[np.ndarray] = None) -> np.ndarray:
         """Same over a device (HBM) buffer, e.g. ``tensor.data_ptr()``.  With ``out`` (a
-        contiguous uint64 array of at least ``cuts_bound(length)`` entries, ideally pinned
-        host memory so the cut list is DMA'd straight into it) the cuts are written there
-        and a view of it is returned; otherwise a fresh array."""
+        writeable contiguous uint64 array of at least ``cuts_bound(length)`` entries, ideally
+        pinned host memory so the cut list is DMA'd straight into it) the cuts are written
+        there and a view of it is returned -- the next call with the same array overwrites
+        that view; otherwise a fresh array."""
         cap = self.cuts_bound(length)
         if out is None:
             buf = self._out(cap)
         else:
-            if out.dtype != np.uint64 or not out.flags.c_contiguous or out.size < cap:
-                raise ValueError(f"out must be a contiguous uint64 array of >= {cap} entries")
+            if (out.dtype != np.uint64 or not out.flags.c_contiguous or not out.flags.writeable
+                    or out.size < cap):
+                raise ValueError(f"out must be a writeable contiguous uint64 array of >= {cap} entries")
             buf = out
         n = ctypes.c_size_t(0)
         rc = lib().pbs_chunker_find_cuts_device(self._h, ctypes.c_void_p(dev_ptr), length,

@@ -48,11 +48,21 @@ def collective_device(dist, device):
     return device
 
 
+def _live(dist) -> bool:
+    """A process group to run collectives in (the torch.distributed module passed without
+    an initialised group, or None, means one rank: nothing to exchange)."""
+    return dist is not None and dist.is_initialized()
+
+
 def exchange_halo(tail: "torch.Tensor", dist, rank: int, world: int) -> bytes:
     """All-gather every rank's last <= 63 bytes and return the left neighbour's (b"" on
     rank 0)."""
     import torch
 
+    if not _live(dist):
+        if int(tail.numel()) > HALO:
+            raise ValueError("tail longer than the halo")
+        return b""
     tail = tail.to(collective_device(dist, tail.device))
     buf = torch.zeros(HALO + 1, dtype=torch.uint8, device=tail.device)
     n = int(tail.numel())
@@ -60,8 +70,6 @@ def exchange_halo(tail: "torch.Tensor", dist, rank: int, world: int) -> bytes:
         raise ValueError("tail longer than the halo")
     buf[:n] = tail
     buf[HALO] = n
-    if dist is None:
-        return b""
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)
     if rank == 0:
@@ -75,7 +83,7 @@ def gather_candidates(cand: "torch.Tensor", dist, world: int) -> "torch.Tensor":
     (the result on ``cand``'s device)."""
     import torch
 
-    if dist is None:
+    if not _live(dist):
         return cand
     home = cand.device
     cand = cand.to(collective_device(dist, home))

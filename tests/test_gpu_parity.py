@@ -167,6 +167,9 @@ def test_find_cuts_device_into_pinned_out(gpu, oracle):
             c.find_cuts_device(dev.data_ptr(), n, is_final=True, out=out[:8])
         with pytest.raises(ValueError):
             c.find_cuts_device(dev.data_ptr(), n, is_final=True, out=out.view(np.int64))
+        ro = np.frombuffer(bytes(8 * c.cuts_bound(n)), dtype=np.uint64)  # read-only
+        with pytest.raises(ValueError):
+            c.find_cuts_device(dev.data_ptr(), n, is_final=True, out=ro)
 
 
 def _zebra(n_runs: int, zero_run: int, rand_run: int, seed: int) -> np.ndarray:

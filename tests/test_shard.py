@@ -103,6 +103,23 @@ def test_sharded_stream_gloo(oracle, world):
         assert cuts == ref, rank
 
 
+def test_collectives_without_a_group():
+    """One rank: the torch.distributed module passed with no initialised process group
+    (or None) means nothing to exchange -- no collective is called."""
+    import torch
+    import torch.distributed as dist
+
+    import shard
+    assert not dist.is_initialized()
+    tail = torch.arange(63, dtype=torch.uint8)
+    cand = torch.tensor([70, 900], dtype=torch.int64)
+    for d in (dist, None):
+        assert shard.exchange_halo(tail, d, 0, 1) == b""
+        assert shard.gather_candidates(cand, d, 1) is cand
+    with pytest.raises(ValueError):
+        shard.exchange_halo(torch.zeros(64, dtype=torch.uint8), dist, 0, 1)
+
+
 def test_shard_ranges():
     import shard
     for total, world in [(64 << 30, 8), (1000, 3), (8 * 7 + 5, 7)]:
