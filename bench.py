@@ -533,7 +533,12 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
                                                      if k.endswith("_ms")},
             "host_share": {"chunks": t["host_chunks"], "gib": round(t["host_bytes"] / (1 << 30), 3),
                            "threads": t["host_threads"],
-                           "min_len": int(str(os.environ.get("PBS_PIPE_HOST_MIN", 8 << 20)), 0)},
+                           "routing": (f"fixed: chunks >= {os.environ['PBS_PIPE_HOST_MIN']} B"
+                                       if "PBS_PIPE_HOST_MIN" in os.environ else
+                                       "deadline: the GPU when its SHA-256 chain ends before the copy does")},
+            "digest_queue": {"gpu_jobs": t["gpu_jobs"], "claimed": t["gpu_claimed"],
+                             "launches": t["queue_launches"], "gpu_done_ms": round(t["gpu_done_ms"], 2),
+                             "host_work_ms": round(t["host_work_ms"], 2)},
             "cpu_baseline": {"value": round(cpu, 3), "unit": "GiB/s", "cores": nth,
                              "kind": "port (oracle chunker) + hashlib + zlib.crc32",
                              "sample": f"{nth} x 256 MiB slices: chunk_feed then sha256 + crc32 per chunk"}}

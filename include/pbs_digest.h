@@ -127,6 +127,12 @@ typedef struct {
     uint64_t host_chunks, host_bytes; /* digests computed on the host threads */
     double host_done_ms;              /* host threads joined (ms after the first copy) */
     int host_threads;
+    uint64_t gpu_jobs;                /* chunks routed to the GPU's digest queue */
+    uint64_t gpu_claimed;             /* of those, taken by the queue's workgroups (the rest:
+                                       * hashed on the host at the end) */
+    uint64_t queue_launches;          /* launches of the queue grid (it exits when idle) */
+    double gpu_done_ms;               /* the digest queue and the CRC launches finished */
+    double host_work_ms;              /* the host threads' last digest finished */
 } pbs_pipeline_timing;
 int pbs_pipeline_host(size_t avg, const uint8_t *host, size_t len, size_t piece,
                       const uint8_t *key, size_t key_len, int digest_cus, uint64_t *ends,

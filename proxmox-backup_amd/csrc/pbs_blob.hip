@@ -105,13 +105,17 @@ const CrcTables* device_tables(int dev) {
     if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     CrcTables* d = nullptr;
     bool ok = hipMalloc(&d, sizeof(CrcTables)) == hipSuccess;
-    // landed before any launch on a non-blocking stream (which does not wait for the
-    // null stream the copy runs on)
-    if (ok && (hipMemcpy(d, &host, sizeof(CrcTables), hipMemcpyHostToDevice) != hipSuccess ||
-               hipStreamSynchronize(nullptr) != hipSuccess)) {
+    // landed before any launch on another stream: copied on a private non-blocking stream
+    // and waited for there (the null stream would also wait for every blocking stream's
+    // work -- e.g. the pipeline's persistent digest queue, pbs_pipeline.cpp)
+    hipStream_t cs = nullptr;
+    if (ok && (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess ||
+               hipMemcpyAsync(d, &host, sizeof(CrcTables), hipMemcpyHostToDevice, cs) != hipSuccess ||
+               hipStreamSynchronize(cs) != hipSuccess)) {
         (void)hipFree(d);
         ok = false;
     }
+    if (cs) (void)hipStreamDestroy(cs);
     if (cur != dev) (void)hipSetDevice(cur);
     if (!ok) return nullptr;
     tabs[dev] = d;

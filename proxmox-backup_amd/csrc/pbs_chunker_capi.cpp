@@ -43,20 +43,30 @@ using namespace pbs;
 
 namespace {
 
+// A device buffer that grows on demand.  The buffer it outgrows is retired, not freed:
+// hipFree waits for the whole device (every stream of the process, e.g. the host
+// pipeline's persistent digest queue), so buffers are freed only with the handle; growth
+// at least doubles, so the retired ones sum to less than the live one.
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    std::vector<void*> retired;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
-        if (p) (void)hipFree(p);
+        size_t want = bytes + bytes / 4 + 256;
+        if (p) {
+            retired.push_back(p);
+            want = std::max(want, 2 * cap);
+        }
         p = nullptr;
         cap = 0;
-        size_t want = bytes + bytes / 4 + 256;
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
         return e;
     }
     void release() {
+        for (void* r : retired) (void)hipFree(r);
+        retired.clear();
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;

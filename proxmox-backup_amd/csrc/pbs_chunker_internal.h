@@ -264,6 +264,32 @@ struct DeviceGuard {
 
 // pbs_blob.hip: free the blob-CRC chunk counter kept for `st` (call before destroying it)
 void release_stream_counter(hipStream_t st);
+
+// ---- digest queue (pbs_digest.hip sha256_queue_kernel; used by pbs_pipeline.cpp) -------
+struct DigestJob {   // in pinned host memory, written by the host before the count
+    uint64_t start;  // chunk start, bytes from the device buffer's start
+    uint64_t len;
+    uint64_t idx;    // output slot (the chunk's index): digests + 32 * idx
+    uint64_t pad;
+};
+struct DigestQueueDev {  // device memory, zeroed before the launch
+    unsigned long long next;       // jobs claimed
+    unsigned long long mirror;     // last control word seen: count | final << 63
+    unsigned long long last_poll;  // wall_clock64 of the last read of the host word
+    unsigned long long polls;      // reads of the host word (statistics)
+    unsigned long long last_h;     // the last value read
+    unsigned long long nseen;      // debug: distinct values read, and when (wall_clock64)
+    unsigned long long seen[16];
+    unsigned long long seen_t[16];
+};
+constexpr uint64_t kDigestQueueFinal = 1ull << 63;
+// Persistent grid of `grid` two-wave workgroups on `st` hashing the published jobs into
+// digests (device, 32 bytes per slot) until the final bit is set and every job is taken,
+// or idle_ticks (100 MHz) pass without a new job (launch it again for later jobs: the
+// queue state in `q` carries over).  key: <= PBS_DIGEST_MAX_KEY bytes.
+hipError_t launch_sha256_queue(const uint8_t* data, const uint8_t* key, size_t key_len, const DigestJob* jobs_dev,
+                               const uint64_t* ctl_dev, DigestQueueDev* q, uint8_t* digests, int grid,
+                               uint64_t idle_ticks, hipStream_t st);
 // frees the calling thread's counters of the shared stream handles (pbs_blob.hip)
 void release_thread_counters();
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,

@@ -203,16 +203,12 @@ constexpr int kShaWaves = 2;
 #ifdef PBS_SHA_PROBE
 __device__ uint64_t g_sha_probe[5];
 #endif
-__global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
-    const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
-    const uint32_t* __restrict__ order, uint64_t n, DigestKey key, uint8_t* __restrict__ digests) {
-    __shared__ uint4 sw[3][16][64];  // [slot][t / 4][lane]: W[t] + K[t] for 4 t (b128 per lane)
-    __shared__ uint32_t s_blocks;
+// The two waves of one workgroup hash 64 chunks, lane l's chunk [s, e) of `data` (live
+// lanes only) into dig (32 bytes; wave 0 writes).  sw / s_blocks: the workgroup's LDS.
+__device__ __forceinline__ void sha_batch(const uint8_t* __restrict__ data, uint64_t s, uint64_t e, bool live,
+                                          const DigestKey& key, uint8_t* __restrict__ dig, uint4 (&sw)[3][16][64],
+                                          uint32_t& s_blocks) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t k = (uint64_t)blockIdx.x * 64 + lane;
-    const bool live = k < n;
-    const uint64_t i = live ? (order ? order[k] : k) : 0;
-    const uint64_t s = live ? bounds[i] - base : 0, e = live ? bounds[i + 1] - base : 0;
     const uint64_t len = e - s;
     const uint64_t nfull = len >> 6;
     const uint32_t rem = (uint32_t)(len & 63);
@@ -391,9 +387,107 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
     }
 #endif
     if (wave == 0 && live) {
-        uint32_t* out = reinterpret_cast<uint32_t*>(digests + 32 * i);
+        uint32_t* out = reinterpret_cast<uint32_t*>(dig);
 #pragma unroll
         for (int q = 0; q < 8; ++q) out[q] = __builtin_bswap32(st[q]);
+    }
+}
+
+__global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
+    const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
+    const uint32_t* __restrict__ order, uint64_t n, DigestKey key, uint8_t* __restrict__ digests) {
+    __shared__ uint4 sw[3][16][64];  // [slot][t / 4][lane]: W[t] + K[t] for 4 t (b128 per lane)
+    __shared__ uint32_t s_blocks;
+    const int lane = threadIdx.x & 63;
+    const uint64_t k = (uint64_t)blockIdx.x * 64 + lane;
+    const bool live = k < n;
+    const uint64_t i = live ? (order ? order[k] : k) : 0;
+    const uint64_t s = live ? bounds[i] - base : 0, e = live ? bounds[i + 1] - base : 0;
+    sha_batch(data, s, e, live, key, digests + 32 * i, sw, s_blocks);
+}
+
+// ---------------------------------------------------------------------------------
+// Digest queue (the host-stream pipeline, pbs_pipeline.cpp): a persistent grid of the
+// two-wave workgroups above takes chunk jobs as the host publishes them, so a chunk's
+// serial SHA-256 chain starts as soon as its end is known instead of at the next
+// launch.  The host appends jobs {start, len, out index} to a pinned (coherent, mapped)
+// array and then stores the count (bit 63: no more jobs) into the pinned control word.
+// An idle workgroup claims up to 64 published jobs with one CAS on the device counter
+// `next`; the control word is read over PCIe by at most one workgroup every ~2 us
+// (`last_poll`) and mirrored in device memory, where the others see it.  A workgroup
+// exits when every job is claimed and the final bit is set, or after idle_ticks (wall
+// clock, 100 MHz) without a new job -- the host relaunches the grid when it publishes
+// jobs after that.  Exiting when idle matters: a resident grid holds up whatever waits
+// for the whole device or for its stream (hipFree, null-stream copies).
+__global__ __launch_bounds__(64 * kShaWaves) void sha256_queue_kernel(
+    const uint8_t* __restrict__ data, DigestKey key, const volatile DigestJob* __restrict__ jobs,
+    const volatile uint64_t* __restrict__ ctl_host, DigestQueueDev* __restrict__ q, uint8_t* __restrict__ digests,
+    uint64_t idle_ticks) {
+    __shared__ uint4 sw[3][16][64];
+    __shared__ uint32_t s_blocks;
+    __shared__ uint64_t s_j0, s_k;
+    const int lane = threadIdx.x & 63;
+    uint64_t t_job = wall_clock64();
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint64_t j0 = 0, k = 0;
+            for (;;) {
+                const uint64_t m = __hip_atomic_load(&q->mirror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t avail = m & 0xFFFFFFFFull, nx = __hip_atomic_load(&q->next, __ATOMIC_RELAXED,
+                                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                if (avail > nx) {
+                    const uint64_t want = avail - nx < 64 ? avail - nx : 64;
+                    unsigned long long exp = nx;
+                    if (__hip_atomic_compare_exchange_strong(&q->next, &exp, nx + want, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        j0 = nx;
+                        k = want;
+                        break;
+                    }
+                    continue;
+                }
+                if (m >> 63) break;  // every job claimed, no more coming
+                const uint64_t now = wall_clock64();
+                if (now - t_job > idle_ticks) break;  // nothing new for a while: exit (relaunched on demand)
+                unsigned long long lp = __hip_atomic_load(&q->last_poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (now - lp > 200 && __hip_atomic_compare_exchange_strong(&q->last_poll, &lp, now, __ATOMIC_RELAXED,
+                                                                           __ATOMIC_RELAXED,
+                                                                           __HIP_MEMORY_SCOPE_AGENT)) {
+                    const uint64_t h = __hip_atomic_load(ctl_host, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_fetch_max(&q->mirror, (unsigned long long)h, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&q->polls, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long prev =
+                        __hip_atomic_exchange(&q->last_h, (unsigned long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (prev != h) {
+                        const unsigned long long ix =
+                            __hip_atomic_fetch_add(&q->nseen, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (ix < 16) {
+                            q->seen[ix] = h;
+                            q->seen_t[ix] = now;
+                        }
+                    }
+                } else {
+                    __builtin_amdgcn_s_sleep(8);
+                }
+            }
+            s_j0 = j0;
+            s_k = k;
+        }
+        __syncthreads();
+        const uint64_t j0 = s_j0, k = s_k;
+        if (k == 0) return;  // uniform
+        t_job = wall_clock64();
+        const bool live = (uint64_t)lane < k;
+        uint64_t st0 = 0, len = 0, idx = 0;
+        if (live) {
+            st0 = jobs[j0 + lane].start;
+            len = jobs[j0 + lane].len;
+            idx = jobs[j0 + lane].idx;
+        }
+        sha_batch(data, st0, st0 + len, live, key, digests + 32 * idx, sw, s_blocks);
+        t_job = wall_clock64();  // idle from here: look for new jobs for idle_ticks
+        __syncthreads();         // s_j0 / s_k and the LDS are reused
     }
 }
 
@@ -512,6 +606,20 @@ __global__ __launch_bounds__(256) void zero_flags_kernel(const uint8_t* __restri
 }
 
 }  // namespace
+
+hipError_t launch_sha256_queue(const uint8_t* data, const uint8_t* key, size_t key_len, const DigestJob* jobs_dev,
+                               const uint64_t* ctl_dev, DigestQueueDev* q, uint8_t* digests, int grid,
+                               uint64_t idle_ticks, hipStream_t st) {
+    if (key_len > PBS_DIGEST_MAX_KEY || grid <= 0) return hipErrorInvalidValue;
+    DigestKey k{};
+    k.len = (uint32_t)key_len;
+    if (key_len) std::memcpy(k.bytes, key, key_len);
+    hipLaunchKernelGGL(sha256_queue_kernel, dim3((unsigned)grid), dim3(64 * kShaWaves), 0, st, data, k,
+                       (const volatile DigestJob*)jobs_dev, (const volatile uint64_t*)ctl_dev, q, digests,
+                       idle_ticks);
+    return hipGetLastError();
+}
+
 }  // namespace pbs
 
 using namespace pbs;

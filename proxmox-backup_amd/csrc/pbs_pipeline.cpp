@@ -5,21 +5,29 @@
 //   copy thread   pageable host pieces -> HBM (hipMemcpyAsync on its own stream; the DMA
 //                 engines, no CUs)
 //   main thread   chunker over each resident piece (find_cuts_device on a stream
-//                 CU-masked to CUs [digest_cus, n)); the completed chunks go to per-chunk
-//                 SHA-256 launches on four digest streams CU-masked to CUs [0, digest_cus)
+//                 CU-masked to CUs [digest_cus, n)); every completed chunk is routed at
+//                 once: to the GPU's digest queue -- a persistent grid on CUs
+//                 [0, digest_cus) that takes jobs as they are published
+//                 (pbs_digest.hip sha256_queue_kernel) -- or to the host threads
 //
 // The CU split keeps the persistent scan kernel and the long-running digest workgroups
 // apart: a scan workgroup (130 KiB LDS, 2 x 208 VGPRs per SIMD) cannot share a CU with a
 // digest workgroup, and a digest launch lasts as long as its longest chunk's serial
 // hash (~0.6 s for a 16 MiB chunk), so without the split a scan launch would wait for it.
-// The chunks are digested in a few large launches (a quarter of the stream, at most
-// 16 GiB each), which overlap on the four digest streams and with the later copies.
-//   host threads  the LONG chunks (>= PBS_PIPE_HOST_MIN, default 8 MiB) are hashed on the
-//                 host cores straight from the caller's buffer (SHA extensions,
-//                 pbs_sha_host.cpp; all-zero chunks once per length), because one GPU
-//                 lane walks a chunk's serial chain at ~30 MB/s: a 16 MiB chunk in the
-//                 last launch kept the GPU busy ~0.6 s after the last copy.  The GPU keeps
-//                 the short chunks (and every chunk's CRC).
+//   routing       one GPU lane walks a chunk's serial SHA-256 chain at ~25-35 MB/s, a host
+//                 thread (SHA extensions, pbs_sha_host.cpp) at ~2.2 GB/s but there are only
+//                 ~14 of them.  A chunk goes to the GPU when its chain ends before the copy
+//                 does (now + len / 25 MB/s <= the copy's projected end + slack), else to
+//                 the host threads (straight from the caller's buffer; all-zero chunks once
+//                 per length).  So early chunks of any length hash on the GPU under the
+//                 copy, and only the long chunks found near the end load the host
+//                 (round 3 sent every chunk >= 8 MiB to the host and digested the rest in
+//                 four quarter-stream launches: the last launch's 8 MiB chains and the
+//                 host's quarter-sized bursts ran ~240 ms past the last copy;
+//                 scripts/pipe_sim.py models both).  PBS_PIPE_HOST_MIN=<bytes> restores the
+//                 fixed length threshold.
+// The blob CRC-32 of every chunk (HBM-bound, milliseconds) still runs as a few large
+// launches on the other digest streams.
 // C ABI: include/pbs_digest.h.
 #include <hip/hip_runtime.h>
 
@@ -28,6 +36,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <deque>
 #include <cstring>
@@ -116,8 +125,61 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     ok = ok && pbs_chunker_set_stream(c, s_scan) == PBS_OK &&
          pbs_chunker_set_cu_count(c, ncu - dig) == PBS_OK;
     if (!ok && rc == PBS_OK) rc = PBS_ERR_HIP;
+    // the digest queue: control word + jobs in pinned coherent host memory (the GPU reads
+    // them over PCIe), its claim counter and mirror in device memory
+    uint8_t* hqmem = nullptr;
+    uint64_t* q_ctl = nullptr;
+    pbs::DigestJob* q_jobs = nullptr;
+    pbs::DigestQueueDev* d_q = nullptr;
+    bool q_running = false;
+    if (ok && (hipHostMalloc((void**)&hqmem, 64 + std::max<size_t>(cap, 1) * sizeof(pbs::DigestJob),
+                             hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+               hipMalloc(&d_q, sizeof(pbs::DigestQueueDev)) != hipSuccess)) {
+        ok = false;
+        rc = PBS_ERR_NOMEM;
+    }
+    uint64_t* q_ctl_dev = nullptr;
+    pbs::DigestJob* q_jobs_dev = nullptr;
+    if (ok) {
+        q_ctl = reinterpret_cast<uint64_t*>(hqmem);
+        q_jobs = reinterpret_cast<pbs::DigestJob*>(hqmem + 64);
+        __atomic_store_n(q_ctl, 0ull, __ATOMIC_RELEASE);
+        ok = hip_ok(hipHostGetDevicePointer((void**)&q_ctl_dev, q_ctl, 0)) &&
+             hip_ok(hipHostGetDevicePointer((void**)&q_jobs_dev, q_jobs, 0)) &&
+             hip_ok(hipMemsetAsync(d_q, 0, sizeof(pbs::DigestQueueDev), s_dig[0]));
+        q_running = ok;
+    }
+    // two workgroups (48 KiB LDS each) per digest CU.  The grid stays resident until the final
+    // count -- nothing on this path may wait for the whole device meanwhile (the chunker's
+    // buffers retire instead of hipFree, the CRC tables load on their own stream) -- or until
+    // PBS_PIPE_IDLE_MS (10 s) pass without a new job; it is launched again when jobs come
+    // after such an exit, and jobs it never took are hashed on the host at the end
+    const int q_wgs = (int)env_u64("PBS_PIPE_QUEUE_WGS", (uint64_t)dig * 2);
+    const uint64_t q_idle = env_u64("PBS_PIPE_IDLE_MS", 10000) * 100000ull;  // wall_clock64: 100 MHz
+    uint64_t q_launches = 0;
+    auto q_launch = [&]() {
+        if (!q_running) return;
+        if (q_launches && hipStreamQuery(s_dig[0]) == hipErrorNotReady) return;  // still resident
+        if (pbs::launch_sha256_queue(d_data, key, key_len, q_jobs_dev, q_ctl_dev, d_q, d_dig, q_wgs, q_idle,
+                                     s_dig[0]) == hipSuccess)
+            ++q_launches;
+        else
+            q_running = false;  // the host hashes what the queue did not take
+    };
+    uint64_t nj = 0;  // jobs published
 
     const Clock::time_point t0 = Clock::now();
+    const bool dbg = std::getenv("PBS_PIPE_DEBUG") != nullptr;
+    std::vector<std::pair<uint64_t, double>> pubs;  // debug (PBS_PIPE_DEBUG)
+    auto publish = [&](bool final) {
+        pubs.emplace_back(nj | (final ? pbs::kDigestQueueFinal : 0ull), ms_since(t0));
+        // the job records before the count, and the count out of the store buffers at once
+        // (without the fences the GPU's polls saw a count published ms earlier for the rest
+        // of the run)
+        __builtin_ia32_sfence();
+        __atomic_store_n(q_ctl, nj | (final ? pbs::kDigestQueueFinal : 0ull), __ATOMIC_SEQ_CST);
+        __builtin_ia32_sfence();
+    };
     std::atomic<size_t> copied{0};
     std::atomic<bool> copy_failed{false};
     std::mutex mu;
@@ -147,8 +209,18 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         });
     }
 
-    // host share: long chunks, hashed from `host` by a pool fed in stream order
-    const uint64_t host_min = env_u64("PBS_PIPE_HOST_MIN", 8ull << 20);
+    // host share: the chunks routed to the host threads, hashed from `host` by a pool fed
+    // in stream order.  Routing (see the top): PBS_PIPE_HOST_MIN = a fixed length threshold
+    // instead (0: no host share); PBS_PIPE_GPU_MBS = one GPU lane's SHA-256 rate while the
+    // scan and the copies run beside it (25: 36 MB/s alone, but the board is at its power
+    // cap here); PBS_PIPE_SLACK_MS = how far past the copy's projected end a GPU chain may
+    // run (20).  Same-process sweep over the 64 GiB stream (scripts/pipe_sweep.py,
+    // profiles/r04/pipeline/): 25/20 -> 1329 ms, 30/20 -> 1385, 35/40 -> 1490, 20/0 -> 1353,
+    // the fixed 8 MiB threshold 1528
+    const uint64_t host_min = env_u64("PBS_PIPE_HOST_MIN", ~0ull);
+    const bool deadline = host_min == ~0ull;
+    const double gpu_bpms = (double)env_u64("PBS_PIPE_GPU_MBS", 25) * 1e3;  // bytes per ms
+    const double slack_ms = (double)env_u64("PBS_PIPE_SLACK_MS", 20);
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     const int hthreads = host_min ? (int)env_u64("PBS_PIPE_HOST_THREADS", (uint64_t)std::max(1, std::min(hw, 16) - 2)) : 0;
     std::deque<uint64_t> hq;  // chunk indices
@@ -157,11 +229,12 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     bool hdone = false;
     std::atomic<uint64_t> host_chunks{0}, host_bytes{0};
     double host_done_at = 0;
+    std::atomic<uint64_t> host_work_us{0};  // the host threads' last digest done (us after t0)
     std::vector<uint8_t> hmask;  // 1 = digest computed on the host
     std::map<uint64_t, std::array<uint8_t, 32>> zero_dig;  // digest of an all-zero chunk per length
     std::vector<std::thread> hpool;
+    hmask.assign(ok ? cap : 0, 0);
     if (ok && hthreads > 0) {
-        hmask.assign(cap, 0);
         for (int j = 0; j < hthreads; ++j)
             hpool.emplace_back([&] {
                 for (;;) {
@@ -198,6 +271,9 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
                     }
                     host_chunks += 1;
                     host_bytes += e0 - s0;
+                    const uint64_t us = (uint64_t)(ms_since(t0) * 1000.0);
+                    for (uint64_t cur = host_work_us.load(); us > cur && !host_work_us.compare_exchange_weak(cur, us);) {
+                    }
                 }
             });
     }
@@ -225,6 +301,13 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         const int r = pbs_chunker_find_cuts_device(c, d_data + off, pn, k + 1 == npieces, tmp.data(),
                                                    tmp.size(), &m);
         chunk_ms += ms_since(tk);
+        if (dbg && ms_since(tk) > 20.0) {
+            pbs_timing tt{};
+            pbs_chunker_last_timing(c, &tt);
+            std::fprintf(stderr, "piece %zu: find_cuts_device %.3f ms (at %.3f ms; scan %.3f fused %llu scan_pass %llu)\n",
+                         k, ms_since(tk), ms_since(t0), tt.scan_ms, (unsigned long long)tt.fused,
+                         (unsigned long long)tt.scan_pass);
+        }
         if (r != PBS_OK) {
             rc = r;
             break;
@@ -233,16 +316,49 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
             rc = PBS_ERR_CAPACITY;
             break;
         }
+        const size_t n0 = n;
         if (m) {
             std::memcpy(ends + n, tmp.data(), m * 8);
             n += m;
         }
-        // digest the chunks completed since the last launch once they cover dbatch bytes
-        // (or at the end): a launch lasts as long as its longest chunk's serial hash, so
-        // few large launches, overlapping on the digest streams, keep the CUs busy
+        // route the chunks completed in this piece: the GPU's digest queue when the chain
+        // ends before the copy's projected end (+ slack), else the host threads
+        if (n > n0) {
+            const double now = ms_since(t0);
+            // projected end of the copy: the rate at which pieces have become resident so
+            // far (this loop waits for each piece's copy), ~55 GB/s before two pieces
+            const double rate = k >= 1 && now > 0 ? (double)(off + pn) / now : 55e6;  // bytes per ms
+            const double t_end = (double)len / rate + slack_ms;
+            size_t nh = 0;
+            for (size_t i = n0; i < n; ++i) {
+                const uint64_t s0 = i ? ends[i - 1] : 0, cl = ends[i] - s0;
+                const bool to_host = hthreads > 0 && (deadline ? now + (double)cl / gpu_bpms > t_end : cl >= host_min);
+                if (to_host) {
+                    hmask[i] = 1;
+                    ++nh;
+                } else {
+                    q_jobs[nj].start = s0;
+                    q_jobs[nj].len = cl;
+                    q_jobs[nj].idx = i;
+                    ++nj;
+                }
+            }
+            publish(false);  // the jobs above were written before the count (release)
+            if (nj) q_launch();  // (again, if the grid went idle and exited)
+            if (nh) {
+                {
+                    std::lock_guard<std::mutex> g(hmu);
+                    for (size_t i = n0; i < n; ++i)
+                        if (hmask[i]) hq.push_back(i);
+                }
+                hcv.notify_all();
+            }
+        }
+        // the blob CRC of the chunks completed since the last launch once they cover dbatch
+        // bytes (or at the end), on the digest streams other than the queue's
         const uint64_t done_to = n ? ends[n - 1] : 0;
         const bool last = k + 1 == npieces;
-        if (n > launched && (done_to - start >= dbatch || last)) {
+        if (crcs && n > launched && (done_to - start >= dbatch || last)) {
             const size_t mm = n - launched;
             hb.emplace_back(mm + 1);
             ho.emplace_back(mm);
@@ -254,42 +370,15 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
             std::stable_sort(o.begin(), o.end(), [&](uint32_t x, uint32_t y) {
                 return b[x + 1] - b[x] > b[y + 1] - b[y];
             });
-            // the longest chunks (a prefix of o) go to the host threads
-            size_t nh = 0;
-            if (hthreads > 0) {
-                while (nh < mm && b[o[nh] + 1] - b[o[nh]] >= host_min) ++nh;
-                if (nh) {
-                    {
-                        std::lock_guard<std::mutex> g(hmu);
-                        for (size_t q = 0; q < nh; ++q) {
-                            hq.push_back(launched + o[q]);
-                            hmask[launched + o[q]] = 1;
-                        }
-                    }
-                    hcv.notify_all();
-                }
-            }
-            hipStream_t sd = s_dig[launches % kDigestStreams];
-            // o sorted longest first: the CRC launch takes all of it, the digest launch
-            // the suffix after the host's prefix
+            hipStream_t sd = s_dig[1 + launches % (kDigestStreams - 1)];
             if (!hip_ok(hipMemcpyAsync(d_bounds + nb, b.data(), (mm + 1) * 8, hipMemcpyHostToDevice, sd)) ||
                 !hip_ok(hipMemcpyAsync(d_order + launched, o.data(), mm * 4, hipMemcpyHostToDevice, sd)))
                 break;
-            if (mm > nh) {
-                const int dr = pbs_digest_chunks_async(d_data, len, 0, d_bounds + nb, d_order + launched + nh,
-                                                       mm - nh, key, key_len, d_dig + 32 * launched, sd);
-                if (dr != PBS_OK) {
-                    rc = dr;
-                    break;
-                }
-            }
-            if (crcs) {  // the blob CRC of the same chunks, behind the digests on that stream
-                const int cr = pbs_crc32_chunks_async(d_data, len, 0, d_bounds + nb, d_order + launched, mm,
-                                                      d_crc + launched, sd);
-                if (cr != PBS_OK) {
-                    rc = cr;
-                    break;
-                }
+            const int cr = pbs_crc32_chunks_async(d_data, len, 0, d_bounds + nb, d_order + launched, mm,
+                                                  d_crc + launched, sd);
+            if (cr != PBS_OK) {
+                rc = cr;
+                break;
             }
             ++launches;
             nb += mm + 1;
@@ -298,6 +387,8 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         }
         last_chunk_at = ms_since(t0);
     }
+    if (q_running) publish(true);  // every path: the queue grid drains
+    if (q_launches && rc != PBS_OK) (void)hipStreamSynchronize(s_dig[0]);  // before its memory goes
     if (copier.joinable()) copier.join();
     {
         std::lock_guard<std::mutex> g(hmu);
@@ -305,8 +396,10 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     }
     hcv.notify_all();
     std::vector<uint8_t> gdig;
+    double gpu_done_at = 0;
     if (rc == PBS_OK && ok) {
         for (auto& s : s_dig) hip_ok(hipStreamSynchronize(s));
+        gpu_done_at = ms_since(t0);
         if (rc == PBS_OK && n) {
             if (hpool.empty()) {
                 hip_ok(hipMemcpy(digests, d_dig, n * 32, hipMemcpyDeviceToHost));
@@ -325,6 +418,21 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     }
     for (auto& th : hpool) th.join();  // error paths
     if (!host_done_at && host_chunks) host_done_at = ms_since(t0);
+    pbs::DigestQueueDev qd{};
+    if (q_launches) (void)hipMemcpy(&qd, d_q, sizeof qd, hipMemcpyDeviceToHost);
+    // jobs the queue grid never took (it drains after stall_ticks without a new job, e.g.
+    // a caller stalled between pieces for that long): hashed here, so no digest is lost
+    if (rc == PBS_OK && qd.next < nj) {
+        std::atomic<uint64_t> nx{qd.next};
+        auto work = [&] {
+            for (uint64_t j; (j = nx.fetch_add(1)) < nj;)
+                pbs::sha256_host_one(host + q_jobs[j].start, q_jobs[j].len, key, key_len, digests + 32 * q_jobs[j].idx);
+        };
+        std::vector<std::thread> fb;
+        for (int t = 1; t < std::max(1, hthreads); ++t) fb.emplace_back(work);
+        work();
+        for (auto& th : fb) th.join();
+    }
     const double total = ms_since(t0);
     if (timing) {
         timing->total_ms = total;
@@ -338,12 +446,28 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         timing->host_bytes = host_bytes;
         timing->host_done_ms = host_done_at;
         timing->host_threads = hthreads;
+        timing->gpu_jobs = nj;
+        timing->gpu_claimed = qd.next;
+        timing->queue_launches = q_launches;
+        timing->gpu_done_ms = gpu_done_at;
+        timing->host_work_ms = host_work_us.load() / 1000.0;
+        if (std::getenv("PBS_PIPE_DEBUG")) {
+            std::fprintf(stderr, "digest queue: jobs %llu claimed %llu launches %llu mirror %llx polls %llu last_h %llx; seen:",
+                         (unsigned long long)nj, qd.next, (unsigned long long)q_launches, qd.mirror, qd.polls,
+                         qd.last_h);
+            for (unsigned long long i = 0; i < qd.nseen && i < 16; ++i)
+                std::fprintf(stderr, " %llx@%.3fms", qd.seen[i], (qd.seen_t[i] - qd.seen_t[0]) / 1e5);
+            std::fprintf(stderr, " | host publishes:");
+            for (auto& pr : pubs) std::fprintf(stderr, " %llx@%.3fms", (unsigned long long)pr.first, pr.second);
+            std::fprintf(stderr, " | last chunk at %.3f ms\n", last_chunk_at);
+        }
     }
     *n_out = n;
     for (auto& e : ev_copied)
         if (e) (void)hipEventDestroy(e);
-    for (void* p : {(void*)d_data, (void*)d_dig, (void*)d_bounds, (void*)d_order, (void*)d_crc})
+    for (void* p : {(void*)d_data, (void*)d_dig, (void*)d_bounds, (void*)d_order, (void*)d_crc, (void*)d_q})
         if (p) (void)hipFree(p);
+    if (hqmem) (void)hipHostFree(hqmem);
     pbs_chunker_free(c);  // before its stream goes away
     if (s_copy) (void)hipStreamDestroy(s_copy);
     if (s_scan) (void)hipStreamDestroy(s_scan);

@@ -90,6 +90,8 @@ class PipelineTiming(ctypes.Structure):
         ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64), ("pieces", ctypes.c_uint64),
         ("host_chunks", ctypes.c_uint64), ("host_bytes", ctypes.c_uint64),
         ("host_done_ms", ctypes.c_double), ("host_threads", ctypes.c_int),
+        ("gpu_jobs", ctypes.c_uint64), ("gpu_claimed", ctypes.c_uint64), ("queue_launches", ctypes.c_uint64),
+        ("gpu_done_ms", ctypes.c_double), ("host_work_ms", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:

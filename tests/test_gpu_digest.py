@@ -168,7 +168,8 @@ def test_known_chunks(gpu, oracle, torch_dev, n, k, clash):
 
 
 @pytest.mark.parametrize("kind,avg,piece,key,host_min", [
-    ("vmimage", 1 << 20, 8 << 20, None, None),          # chunks shorter than a piece
+    ("vmimage", 1 << 20, 8 << 20, None, None),          # chunks shorter than a piece (deadline routing)
+    ("vmimage", 1 << 20, 8 << 20, None, "slack"),       # deadline far away: every digest on the GPU queue
     ("vmimage", 4 << 20, 5 << 20 | 3, b"k" * 32, None),  # 16 MiB chunks spanning pieces, keyed
     ("random", 64 << 10, 1 << 20, None, None),           # many chunks per piece
     ("vmimage", 4 << 20, 8 << 20, b"k" * 32, "0"),       # GPU digests only
@@ -178,9 +179,12 @@ def test_known_chunks(gpu, oracle, torch_dev, n, k, clash):
 def test_pipeline_host(gpu, oracle, monkeypatch, kind, avg, piece, key, host_min):
     """Overlapped copy -> chunk -> digest over a pageable host buffer (pbs_pipeline_host)
     equals the oracle chunker + hashlib, with chunks straddling the copy pieces, and the
-    digests split between the GPU and the host threads (PBS_PIPE_HOST_MIN) or all on one
-    side; all-zero chunks hashed once per length on the host."""
-    if host_min is not None:
+    digests split between the GPU's digest queue and the host threads (by the copy-end
+    deadline, or PBS_PIPE_HOST_MIN) or all on one side; all-zero chunks hashed once per
+    length on the host."""
+    if host_min == "slack":
+        monkeypatch.setenv("PBS_PIPE_SLACK_MS", "100000")
+    elif host_min is not None:
         monkeypatch.setenv("PBS_PIPE_HOST_MIN", host_min)
     n = 100 * MiB + 77
     data = gen_np.gen_vmimage(n, 0x5EED0003, 0) if kind == "vmimage" else gen_np.gen_random(n, 21)
@@ -193,7 +197,7 @@ def test_pipeline_host(gpu, oracle, monkeypatch, kind, avg, piece, key, host_min
     assert np.array_equal(dig, oracle.chunk_digests(data, bounds, key or b""))
     assert np.array_equal(crcs, oracle.chunk_crcs(data, bounds))  # the blob CRCs
     assert t["chunks"] == ref.size and t["bytes"] == n
-    if host_min == "0":
+    if host_min in ("0", "slack"):
         assert t["host_chunks"] == 0
     elif host_min == "1":
         assert t["host_chunks"] == ref.size
