@@ -114,10 +114,13 @@ int pbs_known_chunks_device(const uint8_t *digests_dev, size_t n, const uint8_t 
  * in chunk order, and with `crcs` != NULL each chunk's CRC-32 (the uncompressed blob's
  * DataBlob::compute_crc, include/pbs_blob.h; computed right after each digest launch on
  * the same stream); cap >= pbs_chunker_cuts_bound for the average.  Needs `len` bytes of
- * device memory.  Chunks of at least PBS_PIPE_HOST_MIN bytes (environment, default
- * 8 MiB; 0 = none) are digested on PBS_PIPE_HOST_THREADS host threads (default
- * min(hardware threads, 16) - 2) straight from `host`, the rest on the GPU.
- * Synchronous. */
+ * device memory, kept in the device's pipeline work area between calls (freed by
+ * pbs_pipeline_release).  Each chunk is routed when the chunker completes it: to a
+ * persistent GPU digest grid when its serial hash (len / PBS_PIPE_GPU_MBS, default 25 MB/s)
+ * ends before the copy's projected end + PBS_PIPE_SLACK_MS (default 20), else to
+ * PBS_PIPE_HOST_THREADS host threads (default min(hardware threads, 16) - 2) straight from
+ * `host`; PBS_PIPE_HOST_MIN=<bytes> instead sends chunks of at least that length to the
+ * host and the rest to the GPU.  Synchronous. */
 typedef struct {
     double total_ms; /* first copy issued .. digests on the host */
     double h2d_ms;   /* copy thread: all pieces issued and landed */
@@ -138,6 +141,9 @@ int pbs_pipeline_host(size_t avg, const uint8_t *host, size_t len, size_t piece,
                       const uint8_t *key, size_t key_len, int digest_cus, uint64_t *ends,
                       uint8_t *digests, uint32_t *crcs, size_t cap, size_t *n_out,
                       pbs_pipeline_timing *timing);
+
+/* Frees the idle pipeline work areas (device memory of the last stream lengths). */
+void pbs_pipeline_release(void);
 
 /* Host SHA-256 (FIPS 180-4), used for the index checksum (the reference's
  * openssl::sha::Sha256 over 40-byte entries; a few hundred KiB per index). */

@@ -28,8 +28,9 @@ public:
     int dev() const { return dev_; }
     // slot `i`'s buffer of at least `bytes` (the calling thread's current device must be
     // dev()); grows by 1/8 headroom so slowly growing calls do not reallocate every time
+    // (`headroom` false: exactly `bytes`, for stream-sized slots of tens of GiB)
     template <typename T>
-    T* get(unsigned i, size_t bytes) {
+    T* get(unsigned i, size_t bytes, bool headroom = true) {
         if (bytes == 0) bytes = 1;
         if (bufs_.size() <= i) bufs_.resize(i + 1);
         Buf& b = bufs_[i];
@@ -37,7 +38,7 @@ public:
             if (b.p) (void)hipFree(b.p);
             b.p = nullptr;
             b.cap = 0;
-            const size_t want = bytes + bytes / 8;
+            const size_t want = headroom ? bytes + bytes / 8 : bytes;
             if (hipMalloc(&b.p, want) != hipSuccess) {
                 (void)hipGetLastError();
                 return nullptr;

@@ -49,6 +49,7 @@
 #include "pbs_blob.h"
 #include "pbs_chunker.h"
 #include "pbs_chunker_internal.h"
+#include "dev_arena.h"
 #include "pbs_digest.h"
 #include "sha_host.h"
 
@@ -73,7 +74,14 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
     return e && *e ? std::strtoull(e, nullptr, 0) : dflt;
 }
 
+pbs::ArenaPool& pipe_pool() {
+    static pbs::ArenaPool* p = new pbs::ArenaPool();  // never destroyed: no hipFree at exit
+    return *p;
+}
+
 }  // namespace
+
+extern "C" void pbs_pipeline_release(void) { pipe_pool().clear(); }
 
 extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, size_t piece,
                                  const uint8_t* key, size_t key_len, int digest_cus,
@@ -114,13 +122,21 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
               hip_ok(masked_stream(&s_scan, dig, ncu - dig, ncu));
     for (auto& s : s_dig) ok = ok && hip_ok(masked_stream(&s, 0, dig, ncu));
     for (auto& e : ev_copied) ok = ok && hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    // device: the stream, the digests, and per-launch bounds/order (<= cap + npieces + 1)
-    if (ok && (hipMalloc(&d_data, len) != hipSuccess || hipMalloc(&d_dig, cap * 32) != hipSuccess ||
-               hipMalloc(&d_bounds, (cap + npieces + 1) * 8) != hipSuccess ||
-               hipMalloc(&d_order, std::max<size_t>(cap, 1) * 4) != hipSuccess ||
-               (crcs && hipMalloc(&d_crc, std::max<size_t>(cap, 1) * 4) != hipSuccess))) {
-        ok = false;
-        rc = PBS_ERR_NOMEM;
+    // device: the stream, the digests, and per-launch bounds/order (<= cap + npieces + 1),
+    // from the device's pipeline work area: kept between calls (pbs_pipeline_release), so a
+    // repeated call neither allocates nor frees -- allocating a stream-sized buffer right
+    // after freeing one cost 2.5 s for 64 GiB (profiles/r04/pipeline/sweep_r04j.log)
+    pbs::ArenaLease area(pipe_pool(), dev);
+    if (ok) {
+        d_data = area->get<uint8_t>(0, len, false);
+        d_dig = area->get<uint8_t>(1, cap * 32);
+        d_bounds = area->get<uint64_t>(2, (cap + npieces + 1) * 8);
+        d_order = area->get<uint32_t>(3, std::max<size_t>(cap, 1) * 4);
+        if (crcs) d_crc = area->get<uint32_t>(4, std::max<size_t>(cap, 1) * 4);
+        if (!d_data || !d_dig || !d_bounds || !d_order || (crcs && !d_crc)) {
+            ok = false;
+            rc = PBS_ERR_NOMEM;
+        }
     }
     ok = ok && pbs_chunker_set_stream(c, s_scan) == PBS_OK &&
          pbs_chunker_set_cu_count(c, ncu - dig) == PBS_OK;
@@ -134,7 +150,7 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     bool q_running = false;
     if (ok && (hipHostMalloc((void**)&hqmem, 64 + std::max<size_t>(cap, 1) * sizeof(pbs::DigestJob),
                              hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-               hipMalloc(&d_q, sizeof(pbs::DigestQueueDev)) != hipSuccess)) {
+               !(d_q = area->get<pbs::DigestQueueDev>(5, sizeof(pbs::DigestQueueDev))))) {
         ok = false;
         rc = PBS_ERR_NOMEM;
     }
@@ -417,6 +433,10 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         if (rc == PBS_OK && n && crcs) hip_ok(hipMemcpy(crcs, d_crc, n * 4, hipMemcpyDeviceToHost));
     }
     for (auto& th : hpool) th.join();  // error paths
+    // error paths too: nothing of this call may still run when the work area returns to
+    // the pool (no hipFree any more to wait for it)
+    for (hipStream_t s : {s_copy, s_scan, s_dig[0], s_dig[1], s_dig[2], s_dig[3]})
+        if (s) (void)hipStreamSynchronize(s);
     if (!host_done_at && host_chunks) host_done_at = ms_since(t0);
     pbs::DigestQueueDev qd{};
     if (q_launches) (void)hipMemcpy(&qd, d_q, sizeof qd, hipMemcpyDeviceToHost);
@@ -465,8 +485,6 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     *n_out = n;
     for (auto& e : ev_copied)
         if (e) (void)hipEventDestroy(e);
-    for (void* p : {(void*)d_data, (void*)d_dig, (void*)d_bounds, (void*)d_order, (void*)d_crc, (void*)d_q})
-        if (p) (void)hipFree(p);
     if (hqmem) (void)hipHostFree(hqmem);
     pbs_chunker_free(c);  // before its stream goes away
     if (s_copy) (void)hipStreamDestroy(s_copy);

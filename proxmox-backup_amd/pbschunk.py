@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "pbs_crc32_chunks_device", "pbs_crc32_chunks_async", "pbs_crc32", "pbs_blob_encode_uncompressed",
     "pbs_blob_encode_chunks_device", "pbs_blob_stream_bound", "pbs_zstd_frame_bound",
     "pbs_blob_encode_release", "pbs_digest_hybrid_release", "pbs_debug_arena_allocs",
+    "pbs_pipeline_release",
 )
 
 
@@ -196,6 +197,7 @@ def lib():
         "pbs_zstd_frame_bound": ([sz], sz),
         "pbs_blob_encode_release": ([], None),
         "pbs_digest_hybrid_release": ([], None),
+        "pbs_pipeline_release": ([], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -661,6 +663,12 @@ def blob_encode_release() -> None:
 def digest_hybrid_release() -> None:
     """Free the hybrid digest's cached pinned host slices."""
     lib().pbs_digest_hybrid_release()
+
+
+def pipeline_release() -> None:
+    """Free the idle pipeline work areas (pipeline_host keeps the stream-sized device
+    buffer between calls)."""
+    lib().pbs_pipeline_release()
 
 
 def blob_stream_bound(bounds) -> int:

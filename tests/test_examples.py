@@ -55,6 +55,9 @@ def test_chunk_speed2_example(examples, gpu, oracle, n, piece, avg):
     assert sizes == [b - a for a, b in zip(bounds, bounds[1:])]
     assert f"Uploaded {len(sizes)} chunks" in r.stdout
     assert f"Average chunk size was {n // len(sizes)} bytes." in r.stdout
+    # the default is the unchanged caller (one scan() per read); the gathering mode's
+    # rate is printed beside it, over the same chunks
+    assert f"beside: min_scan 4194304 (4 MiB gathered per scan): {len(sizes)} chunks" in r.stdout
 
 
 @pytest.mark.gpu

@@ -201,9 +201,26 @@ def test_pipeline_host(gpu, oracle, monkeypatch, kind, avg, piece, key, host_min
         assert t["host_chunks"] == 0
     elif host_min == "1":
         assert t["host_chunks"] == ref.size
-    # without the CRC output: same cut list and digests
+    # without the CRC output: same cut list and digests, from the same device work area
+    a0 = gpu.debug_arena_allocs()
     ends2, dig2, _ = gpu.pipeline_host(data, avg, piece=piece, key=key, digest_cus=32)
     assert np.array_equal(ends2, ends) and np.array_equal(dig2, dig)
+    assert gpu.debug_arena_allocs() == a0
+
+
+def test_pipeline_release(gpu, oracle):
+    """pbs_pipeline_release frees the idle work area; the next call allocates a new one
+    and gives the same result."""
+    n = 20 * MiB + 3
+    data = gen_np.gen_vmimage(n, 0x5EED0003, 0)
+    ends, dig, _ = gpu.pipeline_host(data, 1 << 20, piece=4 << 20)
+    gpu.pipeline_release()
+    a0 = gpu.debug_arena_allocs()
+    ends2, dig2, _ = gpu.pipeline_host(data, 1 << 20, piece=4 << 20)
+    assert gpu.debug_arena_allocs() > a0
+    assert np.array_equal(ends2, ends) and np.array_equal(dig2, dig)
+    bounds = np.concatenate([[0], ends]).astype(np.uint64)
+    assert np.array_equal(dig, oracle.chunk_digests(data, bounds))
 
 
 @pytest.mark.parametrize("prev", [0, 5, 40])
