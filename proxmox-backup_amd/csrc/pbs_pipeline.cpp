@@ -74,14 +74,95 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
     return e && *e ? std::strtoull(e, nullptr, 0) : dflt;
 }
 
-pbs::ArenaPool& pipe_pool() {
-    static pbs::ArenaPool* p = new pbs::ArenaPool();  // never destroyed: no hipFree at exit
+// Everything a call sets up, kept per device between calls (pbs_pipeline_release frees the
+// idle ones): the device buffers (a stream-sized one among them -- allocating 64 GiB right
+// after freeing 64 GiB cost 2.5 s, profiles/r04/pipeline/sweep_r04j.log), the chunker
+// handle, the CU-masked streams, the copy events and the pinned job array.  Setting these
+// up and tearing them down cost ~75 ms per 64 GiB call beside its 1.4 s (r04k bench.log:
+// wall 1471 ms, total_ms 1395).
+struct PipeArea {
+    explicit PipeArea(int d) : dev(d), mem(d) {}
+    ~PipeArea() {
+        if (c) pbs_chunker_free(c);  // before its stream goes away
+        drop_streams();
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (hq) (void)hipHostFree(hq);
+    }
+    void drop_streams() {
+        if (s_copy) (void)hipStreamDestroy(s_copy);
+        if (s_scan) (void)hipStreamDestroy(s_scan);
+        for (auto& s : s_dig)
+            if (s) {
+                pbs::release_stream_counter(s);
+                (void)hipStreamDestroy(s);
+            }
+        s_copy = s_scan = nullptr;
+        for (auto& s : s_dig) s = nullptr;
+        dig = -1;
+    }
+    int dev;
+    pbs::DevArena mem;  // slots: 0 stream, 1 digests, 2 bounds, 3 order, 4 CRCs, 5 queue state
+    pbs_chunker* c = nullptr;
+    size_t avg = 0;
+    int dig = -1;  // digest CUs the streams are masked for
+    hipStream_t s_copy = nullptr, s_scan = nullptr, s_dig[kDigestStreams] = {};
+    std::vector<hipEvent_t> ev;
+    uint8_t* hq = nullptr;
+    size_t hq_bytes = 0;
+};
+
+struct PipePool {
+    std::mutex mu;
+    std::map<int, std::vector<PipeArea*>> idle;
+};
+
+PipePool& pipe_pool() {
+    static PipePool* p = new PipePool();  // never destroyed: no HIP calls at exit
     return *p;
+}
+
+PipeArea* pipe_acquire(int dev) {
+    PipePool& p = pipe_pool();
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        std::vector<PipeArea*>& v = p.idle[dev];
+        if (!v.empty()) {
+            PipeArea* a = v.back();
+            v.pop_back();
+            return a;
+        }
+    }
+    return new PipeArea(dev);
+}
+
+// back to the pool after a good call; after a failed one (state unknown) it is freed
+void pipe_release(PipeArea* a, bool good) {
+    if (!good) {
+        delete a;
+        return;
+    }
+    PipePool& p = pipe_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    p.idle[a->dev].push_back(a);
 }
 
 }  // namespace
 
-extern "C" void pbs_pipeline_release(void) { pipe_pool().clear(); }
+extern "C" void pbs_pipeline_release(void) {
+    PipePool& p = pipe_pool();
+    std::map<int, std::vector<PipeArea*>> v;
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        v.swap(p.idle);
+    }
+    int cur = -1;
+    const bool have = hipGetDevice(&cur) == hipSuccess;
+    for (auto& kv : v)
+        for (PipeArea* a : kv.second)
+            if (hipSetDevice(kv.first) == hipSuccess) delete a;
+    if (have) (void)hipSetDevice(cur);
+}
 
 extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, size_t piece,
                                  const uint8_t* key, size_t key_len, int digest_cus,
@@ -98,35 +179,55 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 16)
         return PBS_ERR_HIP;
     const int dig = std::min(std::max(digest_cus, 4), ncu - 8);
-    int err = PBS_OK;
-    pbs_chunker* c = pbs_chunker_new(avg, &err);
-    if (!c) return err;
-    if (cap < pbs_chunker_cuts_bound(c, len)) {
-        pbs_chunker_free(c);
-        return PBS_ERR_CAPACITY;
-    }
+    if (__builtin_popcountll(avg) != 1) return PBS_ERR_NOT_POW2;  // as pbs_chunker_new
+    if (cap < len / std::max<size_t>(avg >> 2, 65) + 3) return PBS_ERR_CAPACITY;  // pbs_chunker_cuts_bound
     const size_t npieces = (len + piece - 1) / piece;
-    hipStream_t s_copy = nullptr, s_scan = nullptr, s_dig[kDigestStreams] = {};
-    uint8_t* d_data = nullptr;
-    uint8_t* d_dig = nullptr;
-    uint64_t* d_bounds = nullptr;
-    uint32_t* d_order = nullptr;
-    uint32_t* d_crc = nullptr;
-    std::vector<hipEvent_t> ev_copied(npieces, nullptr);
     int rc = PBS_OK;
     auto hip_ok = [&](hipError_t e) {
         if (e != hipSuccess && rc == PBS_OK) rc = PBS_ERR_HIP;
         return e == hipSuccess;
     };
-    bool ok = hip_ok(hipStreamCreateWithFlags(&s_copy, hipStreamNonBlocking)) &&
-              hip_ok(masked_stream(&s_scan, dig, ncu - dig, ncu));
-    for (auto& s : s_dig) ok = ok && hip_ok(masked_stream(&s, 0, dig, ncu));
-    for (auto& e : ev_copied) ok = ok && hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    // device: the stream, the digests, and per-launch bounds/order (<= cap + npieces + 1),
-    // from the device's pipeline work area: kept between calls (pbs_pipeline_release), so a
-    // repeated call neither allocates nor frees -- allocating a stream-sized buffer right
-    // after freeing one cost 2.5 s for 64 GiB (profiles/r04/pipeline/sweep_r04j.log)
-    pbs::ArenaLease area(pipe_pool(), dev);
+    // the device's work area (the first call on a device, or after pbs_pipeline_release,
+    // creates it); returned to the pool when this call ends
+    PipeArea* A = pipe_acquire(dev);
+    struct Return {
+        PipeArea* a;
+        const int& rc;
+        ~Return() { pipe_release(a, rc == PBS_OK); }
+    } give_back{A, rc};
+    if (!A->c || A->avg != avg) {
+        if (A->c) pbs_chunker_free(A->c);
+        int err = PBS_OK;
+        A->c = pbs_chunker_new(avg, &err);
+        A->avg = A->c ? avg : 0;
+        if (!A->c) return rc = err;
+    } else if (pbs_chunker_reset(A->c) != PBS_OK) {
+        return rc = PBS_ERR_HIP;
+    }
+    pbs_chunker* const c = A->c;
+    bool ok = true;
+    if (A->dig != dig) {  // CU masks for this split
+        A->drop_streams();
+        ok = hip_ok(hipStreamCreateWithFlags(&A->s_copy, hipStreamNonBlocking)) &&
+             hip_ok(masked_stream(&A->s_scan, dig, ncu - dig, ncu));
+        for (auto& s : A->s_dig) ok = ok && hip_ok(masked_stream(&s, 0, dig, ncu));
+        if (ok) A->dig = dig;
+    }
+    while (ok && A->ev.size() < npieces) {
+        hipEvent_t e = nullptr;
+        ok = hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (ok) A->ev.push_back(e);
+    }
+    hipStream_t const s_copy = A->s_copy, s_scan = A->s_scan;
+    hipStream_t* const s_dig = A->s_dig;
+    const std::vector<hipEvent_t>& ev_copied = A->ev;
+    // device: the stream, the digests, and per-launch bounds/order (<= cap + npieces + 1)
+    pbs::DevArena* const area = &A->mem;
+    uint8_t* d_data = nullptr;
+    uint8_t* d_dig = nullptr;
+    uint64_t* d_bounds = nullptr;
+    uint32_t* d_order = nullptr;
+    uint32_t* d_crc = nullptr;
     if (ok) {
         d_data = area->get<uint8_t>(0, len, false);
         d_dig = area->get<uint8_t>(1, cap * 32);
@@ -143,14 +244,22 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     if (!ok && rc == PBS_OK) rc = PBS_ERR_HIP;
     // the digest queue: control word + jobs in pinned coherent host memory (the GPU reads
     // them over PCIe), its claim counter and mirror in device memory
-    uint8_t* hqmem = nullptr;
     uint64_t* q_ctl = nullptr;
     pbs::DigestJob* q_jobs = nullptr;
     pbs::DigestQueueDev* d_q = nullptr;
     bool q_running = false;
-    if (ok && (hipHostMalloc((void**)&hqmem, 64 + std::max<size_t>(cap, 1) * sizeof(pbs::DigestJob),
-                             hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-               !(d_q = area->get<pbs::DigestQueueDev>(5, sizeof(pbs::DigestQueueDev))))) {
+    const size_t hq_need = 64 + std::max<size_t>(cap, 1) * sizeof(pbs::DigestJob);
+    if (ok && A->hq_bytes < hq_need) {
+        if (A->hq) (void)hipHostFree(A->hq);
+        A->hq = nullptr;
+        A->hq_bytes = 0;
+        if (hipHostMalloc((void**)&A->hq, hq_need, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess)
+            A->hq_bytes = hq_need;
+        else
+            A->hq = nullptr;
+    }
+    uint8_t* const hqmem = A->hq;
+    if (ok && (!hqmem || !(d_q = area->get<pbs::DigestQueueDev>(5, sizeof(pbs::DigestQueueDev))))) {
         ok = false;
         rc = PBS_ERR_NOMEM;
     }
@@ -201,30 +310,6 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     std::mutex mu;
     std::condition_variable cv;
     double h2d_ms = 0;
-    std::thread copier;
-    if (ok) {
-        copier = std::thread([&] {
-            const Clock::time_point tc = Clock::now();
-            for (size_t k = 0; k < npieces; ++k) {
-                const size_t off = k * piece, n = std::min(piece, len - off);
-                if (hipMemcpyAsync(d_data + off, host + off, n, hipMemcpyHostToDevice, s_copy) !=
-                        hipSuccess ||
-                    hipEventRecord(ev_copied[k], s_copy) != hipSuccess) {
-                    copy_failed = true;
-                    break;
-                }
-                {
-                    std::lock_guard<std::mutex> g(mu);
-                    copied = k + 1;
-                }
-                cv.notify_one();
-            }
-            (void)hipStreamSynchronize(s_copy);
-            h2d_ms = ms_since(tc);
-            cv.notify_one();
-        });
-    }
-
     // host share: the chunks routed to the host threads, hashed from `host` by a pool fed
     // in stream order.  Routing (see the top): PBS_PIPE_HOST_MIN = a fixed length threshold
     // instead (0: no host share); PBS_PIPE_GPU_MBS = one GPU lane's SHA-256 rate while the
@@ -250,9 +335,8 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     std::map<uint64_t, std::array<uint8_t, 32>> zero_dig;  // digest of an all-zero chunk per length
     std::vector<std::thread> hpool;
     hmask.assign(ok ? cap : 0, 0);
-    if (ok && hthreads > 0) {
-        for (int j = 0; j < hthreads; ++j)
-            hpool.emplace_back([&] {
+    // one host worker: takes routed chunks until the queue is empty and the routing done
+    auto host_work = [&] {
                 for (;;) {
                     uint64_t i;
                     {
@@ -291,8 +375,35 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
                     for (uint64_t cur = host_work_us.load(); us > cur && !host_work_us.compare_exchange_weak(cur, us);) {
                     }
                 }
-            });
+    };
+    if (ok && hthreads > 0)
+        for (int j = 0; j < hthreads; ++j) hpool.emplace_back(host_work);
+    std::thread copier;
+    if (ok) {
+        copier = std::thread([&] {
+            const Clock::time_point tc = Clock::now();
+            for (size_t k = 0; k < npieces; ++k) {
+                const size_t off = k * piece, n = std::min(piece, len - off);
+                if (hipMemcpyAsync(d_data + off, host + off, n, hipMemcpyHostToDevice, s_copy) !=
+                        hipSuccess ||
+                    hipEventRecord(ev_copied[k], s_copy) != hipSuccess) {
+                    copy_failed = true;
+                    break;
+                }
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    copied = k + 1;
+                }
+                cv.notify_one();
+            }
+            (void)hipStreamSynchronize(s_copy);
+            h2d_ms = ms_since(tc);
+            cv.notify_one();
+            // the copies have landed: this thread hashes host-routed chunks too
+            if (hthreads > 0) host_work();
+        });
     }
+
     double chunk_ms = 0, last_chunk_at = 0;
     size_t n = 0, nb = 0, launches = 0, launched = 0;
     uint64_t start = 0;  // start of the first chunk not yet digested
@@ -405,16 +516,19 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     }
     if (q_running) publish(true);  // every path: the queue grid drains
     if (q_launches && rc != PBS_OK) (void)hipStreamSynchronize(s_dig[0]);  // before its memory goes
-    if (copier.joinable()) copier.join();
     {
         std::lock_guard<std::mutex> g(hmu);
         hdone = true;
     }
     hcv.notify_all();
+    // the routing is done: this thread hashes what is left of the host share, beside the
+    // pool and the copy thread (16 threads in the drain instead of 14)
+    if (hthreads > 0 && rc == PBS_OK) host_work();
+    if (copier.joinable()) copier.join();
     std::vector<uint8_t> gdig;
     double gpu_done_at = 0;
     if (rc == PBS_OK && ok) {
-        for (auto& s : s_dig) hip_ok(hipStreamSynchronize(s));
+        for (int i = 0; i < kDigestStreams; ++i) hip_ok(hipStreamSynchronize(s_dig[i]));
         gpu_done_at = ms_since(t0);
         if (rc == PBS_OK && n) {
             if (hpool.empty()) {
@@ -483,16 +597,5 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         }
     }
     *n_out = n;
-    for (auto& e : ev_copied)
-        if (e) (void)hipEventDestroy(e);
-    if (hqmem) (void)hipHostFree(hqmem);
-    pbs_chunker_free(c);  // before its stream goes away
-    if (s_copy) (void)hipStreamDestroy(s_copy);
-    if (s_scan) (void)hipStreamDestroy(s_scan);
-    for (auto& s : s_dig)
-        if (s) {
-            pbs::release_stream_counter(s);
-            (void)hipStreamDestroy(s);
-        }
-    return rc;
+    return rc;  // the work area goes back to the pool (give_back)
 }

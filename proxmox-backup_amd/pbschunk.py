@@ -836,8 +836,9 @@ def pipeline_host(data, avg: int, piece: int = 1 << 30, key=None, digest_cus: in
     overlapped copy -> chunk -> digest path over a host buffer; with crc=True also the
     per-chunk blob CRC-32s: (ends, digests, crcs, timing)."""
     a = _as_u8(data)
-    with Chunker(avg) as c:
-        cap = c.cuts_bound(a.size) + 1
+    # pbs_chunker_cuts_bound without a handle (min_eff = max(avg / 4, 65)); an average
+    # that is not a power of two fails in the call below
+    cap = a.size // max(int(avg) >> 2, 65) + 4
     ends = np.empty(cap, dtype=np.uint64)
     dig = np.empty((cap, 32), dtype=np.uint8)
     crcs = np.empty(cap, dtype=np.uint32) if crc else None

@@ -23,6 +23,10 @@ def simulate(ends, zero, piece, copy_bps, r_gpu, r_host, threads, policy, slack_
     deadline = t_copy_end + slack_ms
     gpu_done, host_jobs = 0.0, []
     seen_zero = set()
+    # "eft": deadline first, else whichever side finishes the chunk first -- the host side
+    # modelled as the workers' free times, FIFO (the pool is fed in stream order)
+    model = [0.0] * threads
+    heapq.heapify(model)
     for c in range(n):
         L = int(lens[c])
         if zero[c]:
@@ -35,8 +39,16 @@ def simulate(ends, zero, piece, copy_bps, r_gpu, r_host, threads, policy, slack_
             t_launch = (q + 1) * total / 4 / copy_bps * 1e3 + 0.3
         else:  # a persistent kernel takes the chunk as soon as it is known
             t_launch = t_known[c]
-        to_gpu = {"fixed8": L < (8 << 20), "deadline": t_launch + g <= deadline,
-                  "gpu": True}[policy]
+        if policy == "eft":
+            to_gpu = t_launch + g <= deadline
+            if not to_gpu:
+                h_end = max(model[0], t_known[c]) + L / r_host * 1e3
+                to_gpu = t_launch + g < h_end
+                if not to_gpu:
+                    heapq.heapreplace(model, h_end)
+        else:
+            to_gpu = {"fixed8": L < (8 << 20), "deadline": t_launch + g <= deadline,
+                      "gpu": True}[policy]
         if to_gpu:
             gpu_done = max(gpu_done, t_launch + g)
         else:
@@ -88,7 +100,8 @@ def main():
     print(f"{ends.size} chunks, {zero.sum()} zero (in the extents)")
     for piece in (a.piece_mib, 256, 64):
         for launch in ("quarter", "persistent"):
-            for policy, slack in (("fixed8", 0), ("gpu", 0), ("deadline", 0), ("deadline", 30), ("deadline", 60)):
+            for policy, slack in (("fixed8", 0), ("gpu", 0), ("deadline", 0), ("deadline", 20), ("deadline", 60),
+                                  ("eft", 0), ("eft", 20)):
                 r = simulate(ends, zero, piece << 20, a.copy_gbs * 1e9, a.r_gpu_mbs * 1e6, a.r_host_mbs * 1e6,
                              a.threads, policy, slack, launch)
                 print(f"piece {piece:5d} MiB {launch:10s} {policy:8s} slack {slack:3d}: {r}")

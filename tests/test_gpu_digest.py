@@ -223,6 +223,24 @@ def test_pipeline_release(gpu, oracle):
     assert np.array_equal(dig, oracle.chunk_digests(data, bounds))
 
 
+def test_pipeline_area_changes(gpu, oracle):
+    """The kept work area across calls that change what it holds: another average (a new
+    chunker handle), another CU split (new streams), a longer stream (larger buffers), a
+    failed call (invalid average: the call raises, the next one is unaffected)."""
+    n = 24 * MiB + 11
+    data = gen_np.gen_vmimage(2 * n, 0x5EED0003, 0)
+    for avg, cus, ln in [(1 << 20, 32, n), (256 << 10, 32, n), (256 << 10, 16, n), (1 << 20, 16, 2 * n)]:
+        ends, dig, t = gpu.pipeline_host(data[:ln], avg, piece=5 << 20, digest_cus=cus)
+        ref = oracle.chunk_feed(avg, data[:ln])
+        if ref.size == 0 or int(ref[-1]) != ln:
+            ref = np.append(ref, np.uint64(ln))
+        assert np.array_equal(ends, ref), (avg, cus, ln)
+        assert np.array_equal(dig, oracle.chunk_digests(data[:ln], np.concatenate([[0], ref]).astype(np.uint64)))
+        if avg == 1 << 20 and cus == 32:
+            with pytest.raises(gpu.ChunkerError):
+                gpu.pipeline_host(data[:ln], 3 << 19, piece=5 << 20)
+
+
 @pytest.mark.parametrize("prev", [0, 5, 40])
 def test_upload_stream_host(gpu, oracle, prev):
     """backup_writer.rs:638-700 end to end from a host buffer: cut list, digests, blob
