@@ -173,6 +173,7 @@ struct pbs_chunker {
     bool scan_pass = true;    // PBS_SCAN_PASS=0: small averages take scan_main + exact + sort (A/B)
     uint64_t fused_min_avg = 0;
     int balance = 1;           // PBS_BALANCE=0: no priority trading between SIMD partners (A/B)
+    bool direct_out = true;    // PBS_DIRECT_OUT=0: the multi-kernel resolve always copies its cuts (A/B)
     int scan_dyn_env = -1;         // PBS_SCAN_DYN=0/1: force the static / dynamic tile order
     uint64_t fused_min_bytes = 0;  // smallest batch for the fused pass (PBS_FUSED_MIN_BYTES)  // smallest average served by the fused pass (PBS_FUSED_MIN_AVG: A/B)
     uint64_t susp_cap = 0, cand_cap = 0;
@@ -393,8 +394,24 @@ int finish_resolve(pbs_chunker* c, uint64_t s_open, uint64_t end, std::vector<ui
 // Resolve the min/max rule over c->d_C[0..m) (sorted, absolute) from chunk_start with
 // bytes known up to `end`.  Appends cut END offsets to host `out` at *n, moves
 // chunk_start to the open chunk and keeps the open chunk's candidates pending.
-int run_resolve(pbs_chunker* c, uint32_t m, uint64_t end, uint64_t* out, size_t cap, size_t* n) {
-    const Params& p = c->prm;
+int ensure_small_host_bufs(pbs_chunker* c);
+template <class T>
+int mapped(pbs_chunker* c, T* host, T** dev);
+
+// The device address of a host cut array the GPU can write (pinned / registered memory),
+// or nullptr (pageable: the cuts go through a device buffer and a copy).  Asked every call
+// (a cached answer would outlive the caller's buffer).
+uint64_t* out_device_view(uint64_t* out) {
+    if (!out) return nullptr;
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
+        return static_cast<uint64_t*>(at.devicePointer);
+    (void)hipGetLastError();  // pageable memory: not an error here
+    return nullptr;
+}
+
+// Device buffers of a multi-kernel resolve over up to m nodes.
+int resolve_buffers(pbs_chunker* c, uint32_t m) {
     const uint32_t nodes = m + 2;
     HIP_TRY(c, c->d_C.ensure((size_t)nodes * 8));  // no-op: d_C already holds m entries
     HIP_TRY(c, c->d_nxt.ensure((size_t)nodes * 4));
@@ -405,13 +422,70 @@ int run_resolve(pbs_chunker* c, uint32_t m, uint64_t end, uint64_t* out, size_t 
     HIP_TRY(c, c->d_off.ensure((size_t)nodes * 8));
     HIP_TRY(c, c->d_res.ensure(32));
     size_t tb = 0;
-    HIP_TRY(c, exclusive_sum_u64(nullptr, &tb, c->d_cnt.as<uint64_t>(), c->d_off.as<uint64_t>(),
-                                 m + 1, c->stream));
+    HIP_TRY(c, exclusive_sum_u64(nullptr, &tb, c->d_cnt.as<uint64_t>(), c->d_off.as<uint64_t>(), m + 1, c->stream));
     HIP_TRY(c, c->d_scan_tmp.ensure(tb));
+    return PBS_OK;
+}
+
+// The multi-kernel resolve into a cut array the GPU can write (out_dev: pinned host memory):
+// the emit kernel writes the cuts there, the results and the open chunk's candidates go to
+// mapped host memory, and the host syncs once (the copying path: device buffers, a sync,
+// copies, a second sync).  m_dev != nullptr: the node count is m_base + *m_dev on the device
+// (m its upper bound) and m_base + *m_host after the sync -- the scan pass launches this
+// right behind its gather, whose overflow flag (*overflow, h_small[1]) is read after the
+// sync: set, nothing changed and the caller takes another path.
+int resolve_direct(pbs_chunker* c, uint32_t m, const uint64_t* m_dev, uint32_t m_base,
+                   const volatile uint64_t* m_host, uint64_t end, uint64_t* out_dev, size_t cap, size_t* n,
+                   bool* overflow) {
+    const Params& p = c->prm;
+    int rc = resolve_buffers(c, m);
+    if (rc) return rc;
+    uint64_t *small_dev = nullptr, *keep_dev = nullptr;
+    if ((rc = ensure_small_host_bufs(c)) || (rc = mapped(c, c->h_small, &small_dev)) ||
+        (rc = mapped(c, c->h_keep, &keep_dev)))
+        return rc;
+    const uint64_t room = std::min<uint64_t>(cut_bound(c, m, end), cap - *n);
+    ResolveParams rp{p.min_eff, p.max_eff, end, c->chunk_start};
+    volatile uint64_t* r = c->h_small + 4;
+    r[0] = r[1] = r[2] = r[3] = 0;
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    HIP_TRY(c, launch_resolve(c->d_C.as<uint64_t>(), m, rp, c->d_nxt.as<uint32_t>(), c->d_jtmp.as<uint32_t>(),
+                              c->d_nf.as<uint64_t>(), c->d_on.as<uint32_t>(), c->d_cnt.as<uint64_t>(),
+                              c->d_off.as<uint64_t>(), c->d_scan_tmp.p, c->d_scan_tmp.cap, out_dev + *n, room,
+                              small_dev + 4, c->stream, m_dev, m_base));
+    HIP_TRY(c, launch_resolve_keep(c->d_C.as<uint64_t>(), m, small_dev + 4, keep_dev, kHostKeep, m_dev, m_base,
+                                   c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (overflow && (*overflow = c->h_small[1] != 0)) return PBS_OK;
+    const uint64_t mm = m_dev ? m_base + *m_host : m;
+    const uint64_t ncut = r[0], s_open = r[1], idx = r[2], keep_over = r[3];
+    if (ncut > room) return fail(c, PBS_ERR_CAPACITY);
+    std::vector<uint64_t> keep(mm > idx ? mm - idx : 0);
+    if (!keep.empty()) {
+        if (!keep_over) {
+            std::memcpy(keep.data(), c->h_keep, keep.size() * 8);
+        } else {
+            HIP_TRY(c, hipMemcpyAsync(keep.data(), c->d_C.as<uint64_t>() + idx, keep.size() * 8,
+                                      hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+        }
+    }
+    *n += ncut;
+    return finish_resolve(c, s_open, end, keep, ncut);
+}
+
+int run_resolve(pbs_chunker* c, uint32_t m, uint64_t end, uint64_t* out, size_t cap, size_t* n) {
+    const Params& p = c->prm;
+    // a cut array the GPU can write (pinned, as bench.py hands it): resolve_direct
+    uint64_t* const out_dev = c->direct_out ? out_device_view(out) : nullptr;
+    if (out_dev && cap > *n) return resolve_direct(c, m, nullptr, 0, nullptr, end, out_dev, cap, n, nullptr);
+    int rc = resolve_buffers(c, m);
+    if (rc) return rc;
     const uint64_t out_cap = cut_bound(c, m, end);
+    ResolveParams rp{p.min_eff, p.max_eff, end, c->chunk_start};
     HIP_TRY(c, c->d_cuts.ensure(out_cap * 8));
     HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
-    ResolveParams rp{p.min_eff, p.max_eff, end, c->chunk_start};
     HIP_TRY(c, launch_resolve(c->d_C.as<uint64_t>(), m, rp, c->d_nxt.as<uint32_t>(),
                               c->d_jtmp.as<uint32_t>(), c->d_nf.as<uint64_t>(),
                               c->d_on.as<uint32_t>(), c->d_cnt.as<uint64_t>(),
@@ -1161,8 +1235,6 @@ int fused_scan_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, ui
     HIP_TRY(c, c->d_scan_tmp.ensure(tb));
     HIP_TRY(c, c->d_cnt.ensure((nrec + 1) * 8));
     HIP_TRY(c, c->d_off.ensure((nrec + 1) * 8));
-    HIP_TRY(c, c->d_res.ensure(32));
-    HIP_TRY(c, hipMemsetAsync(c->d_res.p, 0, 16, c->stream));
     unsigned long long* ctr = c->d_counters.as<unsigned long long>();
     a.data = dsrc;
     a.len = bl;
@@ -1188,15 +1260,45 @@ int fused_scan_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, ui
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, launch_scan_fused(a, seg, dyn, c->cu, c->stream));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
-    HIP_TRY(c, launch_fused_gather(a.rec, nrec, a.epoch, a.cand, c->d_C.as<uint64_t>() + np, c->d_cnt.as<uint64_t>(),
-                                   c->d_off.as<uint64_t>(), c->d_scan_tmp.p, c->d_scan_tmp.cap,
-                                   c->d_res.as<uint64_t>(), c->stream));
-    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->h_small, c->d_res.p, 16, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->h_small + 2, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream));
+    // the gather writes its count, the overflow flag, the kernel's counters and the batch's
+    // last bytes straight to mapped host memory: one sync, no copies after it
     const uint64_t tl = std::min<uint64_t>(bl, kWindow - 1);
     uint8_t* tail = reinterpret_cast<uint8_t*>(c->h_small + 24);
-    if (!hsrc) HIP_TRY(c, hipMemcpyAsync(tail, dsrc + bl - tl, tl, hipMemcpyDeviceToHost, c->stream));
+    int rc0 = ensure_small_host_bufs(c);
+    if (rc0) return rc0;
+    uint64_t* small_dev = nullptr;
+    if ((rc0 = mapped(c, c->h_small, &small_dev))) return rc0;
+    c->h_small[0] = c->h_small[1] = 0;
+    HIP_TRY(c, c->d_res.ensure(32));
+    HIP_TRY(c, launch_fused_gather(a.rec, nrec, a.epoch, a.cand, c->d_C.as<uint64_t>() + np, c->d_cnt.as<uint64_t>(),
+                                   c->d_off.as<uint64_t>(), c->d_scan_tmp.p, c->d_scan_tmp.cap, small_dev,
+                                   c->d_counters.as<unsigned long long>(), dsrc + bl - tl, (uint32_t)tl,
+                                   reinterpret_cast<uint8_t*>(small_dev + 24), c->d_res.as<uint64_t>(), c->stream));
+    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    // into a pinned cut array: the resolve goes right behind the gather, the candidate count
+    // read on the device, and the host syncs once for the whole pass
+    uint64_t* const out_dev = c->direct_out ? out_device_view(out) : nullptr;
+    if (out_dev && cap > *n && np + cand_cap + 2 <= 0xFFFFFFF0ull) {
+        bool overflow = false;
+        const int rc = resolve_direct(c, (uint32_t)(np + cand_cap), c->d_res.as<uint64_t>(), (uint32_t)np,
+                                      c->h_small, rend, out_dev, cap, n, &overflow);
+        if (rc || overflow) return rc;  // overflow: nothing changed, *done stays false
+        const uint64_t nnew = c->h_small[0], nflag = c->h_small[2];
+        float ms = 0;
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        c->timing.scan_ms += ms;
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+        c->timing.exact_ms += ms;  // the gather
+        c->timing.bytes += bl;
+        c->timing.fused += bl;
+        c->timing.scan_pass += bl;
+        c->timing.suspects += nflag;
+        c->timing.candidates += nnew;
+        update_carry(c, hsrc ? hsrc + bl - tl : tail, tl);
+        c->scanned_end = pos + bl;
+        *done = true;
+        return PBS_OK;
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const uint64_t nnew = c->h_small[0], overflow = c->h_small[1], nflag = c->h_small[2];
     if (overflow || nnew > cand_cap) return PBS_OK;  // dense input: the multi-launch path
@@ -1452,6 +1554,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
         if (e[0] == '1') c->srv.flags |= kSrvProbe;
     c->fused_min_avg = kFusedMinAvg;
     if (const char* e = std::getenv("PBS_BALANCE")) c->balance = std::atoi(e);
+    if (const char* e = std::getenv("PBS_DIRECT_OUT")) c->direct_out = e[0] != '0';
     if (const char* e = std::getenv("PBS_SCAN_DYN")) c->scan_dyn_env = e[0] == '1' ? 1 : 0;
     c->fused_min_bytes = kFusedMinBytes;
     if (const char* e = std::getenv("PBS_FUSED_MIN_BYTES")) c->fused_min_bytes = std::strtoull(e, nullptr, 0);

@@ -107,11 +107,19 @@ constexpr int kFusedStaticSeg = 40960;  // static-order fused pass: longest segm
 constexpr int kResolveBatch = 256;  // tile records per resolver step (4 per lane)
 hipError_t launch_scan_fused(const FusedPassArgs& a, int seg, bool dyn, int grid, hipStream_t stream);
 // Scan pass (FusedPassArgs::resolver == 0): the records' candidates, in record order (= stream
-// order), to out[0 ..); counts/offs: nrec + 1 u64 scratch each; res[0] = candidates,
-// res[1] = 1 when a record overflowed (the batch must take another path).
+// order), to out[0 ..); counts/offs: nrec + 1 u64 scratch each; res (mapped host memory,
+// res[1] zeroed by the caller): [0] candidates, [1] = 1 when a record overflowed (the batch
+// must take another path), [2] / [3] the counters (flagged blocks, candidates listed); the
+// batch's last tl <= 256 bytes to tail_dst; the candidate count also to count_dev (device).
 hipError_t launch_fused_gather(const unsigned long long* rec, uint64_t nrec, uint32_t epoch,
                                const uint64_t* cand, uint64_t* out, uint64_t* counts, uint64_t* offs,
-                               void* scan_tmp, size_t scan_tmp_bytes, uint64_t* res, hipStream_t stream);
+                               void* scan_tmp, size_t scan_tmp_bytes, uint64_t* res,
+                               const unsigned long long* counters, const uint8_t* tail_src, uint32_t tl,
+                               uint8_t* tail_dst, uint64_t* count_dev, hipStream_t stream);
+// The open chunk's candidates C[res[2], m) -> keep (mapped host memory, keep_cap entries);
+// res[3] = 1 when they do not fit.
+hipError_t launch_resolve_keep(const uint64_t* C, uint32_t m, uint64_t* res, uint64_t* keep, uint64_t keep_cap,
+                               const uint64_t* m_dev, uint32_t m_base, hipStream_t stream);
 hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* pre,
                              uint32_t pre_len, const uint64_t* susp,
                              const unsigned long long* nsusp, uint64_t susp_cap, uint64_t ext_first,
@@ -133,10 +141,13 @@ hipError_t launch_crc32_skip(const uint8_t* data, const uint64_t* bounds_dev, ui
                              uint32_t* out, hipStream_t st);
 hipError_t inclusive_max_u32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint32_t* out,
                              uint64_t n, hipStream_t stream);
+// m_dev != nullptr: the node count is m_base + *m_dev, on the device only; m is then its upper
+// bound (grids, the scan); the host needs no sync between the producer of m and this.
 hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p, uint32_t* nxt,
                           uint32_t* jtmp, uint64_t* nforced, uint32_t* on, uint64_t* cnt,
                           uint64_t* off, void* scan_tmp, size_t scan_tmp_bytes, uint64_t* out,
-                          uint64_t out_cap, uint64_t* res, hipStream_t stream);
+                          uint64_t out_cap, uint64_t* res, hipStream_t stream,
+                          const uint64_t* m_dev = nullptr, uint32_t m_base = 0);
 // Single-workgroup sort + resolve + emit for batches with np + nnew + 2 <= kSmallResolveMax
 // candidates (keys sorted in LDS).  C[0..np) holds the pending (sorted) candidates on
 // entry and C[0..m) all sorted candidates on exit.  Cuts go to out[] and, while they

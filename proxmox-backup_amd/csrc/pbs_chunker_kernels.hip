@@ -201,16 +201,27 @@ __device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t* __restrict__
     return a;
 }
 
+// m_dev != nullptr: the node count is m_base + *m_dev, known on the device only (the host
+// launched with an upper bound; threads past it exit).  jcopy: a second copy of nxt (the
+// pointer doubling's input)
+__device__ __forceinline__ uint32_t node_count(uint32_t m, const uint64_t* m_dev, uint32_t m_base) {
+    return m_dev ? m_base + (uint32_t)*m_dev : m;
+}
+
 __global__ __launch_bounds__(256) void resolve_next_kernel(const uint64_t* __restrict__ C,
-                                                           uint32_t m, ResolveParams p,
+                                                           uint32_t m_arg, ResolveParams p,
                                                            uint32_t* __restrict__ nxt,
                                                            uint64_t* __restrict__ nforced,
-                                                           uint32_t* __restrict__ on) {
+                                                           uint32_t* __restrict__ on,
+                                                           const uint64_t* __restrict__ m_dev, uint32_t m_base,
+                                                           uint32_t* __restrict__ jcopy) {
+    const uint32_t m = node_count(m_arg, m_dev, m_base);
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t none = m + 1;
     if (j > m + 1) return;
     if (j == m + 1) {
         nxt[j] = none;
+        jcopy[j] = none;
         nforced[j] = 0;
         on[j] = 0;
         return;
@@ -240,6 +251,7 @@ __global__ __launch_bounds__(256) void resolve_next_kernel(const uint64_t* __res
         s += k * p.max_eff;
     }
     nxt[j] = res;
+    jcopy[j] = res;
     nforced[j] = nf;
     on[j] = (j == m) ? 1u : 0u;
 }
@@ -250,9 +262,11 @@ __global__ __launch_bounds__(256) void resolve_next_kernel(const uint64_t* __res
 // marks its i * 2^t-th successors (i = 1..7, gathered along J_t) and J_{t+3} = J_t^8:
 // the same result as three rounds with a third of the launches.  Races on `on` are
 // benign: marks only go 0 -> 1, and any node marked is on the chain.
-__global__ __launch_bounds__(256) void resolve_double3_kernel(uint32_t n, const uint32_t* __restrict__ jin,
+__global__ __launch_bounds__(256) void resolve_double3_kernel(uint32_t n_arg, const uint32_t* __restrict__ jin,
                                                               uint32_t* __restrict__ jout,
-                                                              uint32_t* on) {
+                                                              uint32_t* on, const uint64_t* __restrict__ m_dev,
+                                                              uint32_t m_base) {
+    const uint32_t n = m_dev ? node_count(0, m_dev, m_base) + 2 : n_arg;
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const bool mk = on[j] != 0u;
@@ -267,12 +281,17 @@ __global__ __launch_bounds__(256) void resolve_double3_kernel(uint32_t n, const 
 
 __device__ __forceinline__ uint32_t slot_of(uint32_t j, uint32_t m) { return j == m ? 0u : j + 1u; }
 
-__global__ __launch_bounds__(256) void resolve_count_kernel(uint32_t m, const uint32_t* __restrict__ nxt,
+__global__ __launch_bounds__(256) void resolve_count_kernel(uint32_t m_arg, const uint32_t* __restrict__ nxt,
                                                             const uint64_t* __restrict__ nforced,
                                                             const uint32_t* __restrict__ on,
-                                                            uint64_t* __restrict__ cnt) {
+                                                            uint64_t* __restrict__ cnt,
+                                                            const uint64_t* __restrict__ m_dev, uint32_t m_base) {
+    const uint32_t m = node_count(m_arg, m_dev, m_base);
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j > m) return;  // nodes 0..m
+    if (j > m) {  // nodes 0..m; slots past them (an upper-bound launch) count nothing
+        if (j <= m_arg) cnt[j] = 0;
+        return;
+    }
     // slot 0 = the start node m (its cuts come first), slot j+1 = candidate node j
     cnt[slot_of(j, m)] = on[j] ? nforced[j] + (nxt[j] != m + 1 ? 1u : 0u) : 0u;
 }
@@ -281,10 +300,11 @@ __global__ __launch_bounds__(256) void resolve_count_kernel(uint32_t m, const ui
 // res[1] = start of the open (undecided) chunk, res[2] = index of the first
 // candidate >= res[1].
 __global__ __launch_bounds__(256) void resolve_emit_kernel(
-    const uint64_t* __restrict__ C, uint32_t m, ResolveParams p, const uint32_t* __restrict__ nxt,
+    const uint64_t* __restrict__ C, uint32_t m_arg, ResolveParams p, const uint32_t* __restrict__ nxt,
     const uint64_t* __restrict__ nforced, const uint32_t* __restrict__ on,
     const uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off, uint64_t* __restrict__ out,
-    uint64_t out_cap, uint64_t* __restrict__ res) {
+    uint64_t out_cap, uint64_t* __restrict__ res, const uint64_t* __restrict__ m_dev, uint32_t m_base) {
+    const uint32_t m = node_count(m_arg, m_dev, m_base);
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > m || !on[j]) return;
     const uint64_t s = (j == m) ? p.s0 : C[j] + 1;
@@ -938,9 +958,14 @@ __global__ void fused_rec_counts_kernel(const unsigned long long* __restrict__ r
     counts[i] = c;
 }
 
+// res (mapped host memory): [0] candidates gathered, [1] overflow (counts kernel), [2] flagged
+// blocks, [3] candidates listed (the scan kernel's counters); the batch's last tl bytes go to
+// tail_dst (mapped) -- the host reads all of it after one sync, no copies
 __global__ void fused_gather_kernel(const unsigned long long* __restrict__ rec, uint64_t nrec, uint32_t epoch,
                                     const uint64_t* __restrict__ offs, const uint64_t* __restrict__ cand,
-                                    uint64_t* __restrict__ out, uint64_t* __restrict__ res) {
+                                    uint64_t* __restrict__ out, uint64_t* __restrict__ res,
+                                    const unsigned long long* __restrict__ counters, const uint8_t* __restrict__ tail_src,
+                                    uint32_t tl, uint8_t* __restrict__ tail_dst, uint64_t* __restrict__ count_dev) {
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
     for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); r < nrec; r += nwaves) {
@@ -951,19 +976,55 @@ __global__ void fused_gather_kernel(const unsigned long long* __restrict__ rec, 
         const uint64_t idx = (uint32_t)v, o = offs[r];
         for (uint32_t j = (uint32_t)lane; j < c; j += 64) out[o + j] = cand[idx + j];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) res[0] = offs[nrec];
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            res[0] = offs[nrec];
+            count_dev[0] = offs[nrec];  // (device memory: what the resolve kernels read)
+            res[2] = counters[0];
+            res[3] = counters[1];
+        }
+        if (threadIdx.x < tl) tail_dst[threadIdx.x] = tail_src[threadIdx.x];
+    }
+}
+
+// The open chunk's candidates C[idx, m) (idx = res[2], written by resolve_emit_kernel) to
+// mapped host memory when they fit keep_cap, else res[3] = 1 (the host copies them)
+__global__ void resolve_keep_kernel(const uint64_t* __restrict__ C, uint32_t m_arg, uint64_t* res, uint64_t* __restrict__ keep,
+                                    uint64_t keep_cap, const uint64_t* __restrict__ m_dev, uint32_t m_base) {
+    const uint32_t m = node_count(m_arg, m_dev, m_base);
+    const uint64_t idx = res[2];
+    const uint64_t nk = m > idx ? m - idx : 0;
+    if (nk > keep_cap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) res[3] = 1;
+        return;
+    }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nk; i += (uint64_t)gridDim.x * blockDim.x)
+        keep[i] = C[idx + i];
+}
+
+hipError_t launch_resolve_keep(const uint64_t* C, uint32_t m, uint64_t* res, uint64_t* keep, uint64_t keep_cap,
+                               const uint64_t* m_dev, uint32_t m_base, hipStream_t stream) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(resolve_keep_kernel, dim3(16), dim3(256), 0, stream, C, m, res, keep, keep_cap, m_dev, m_base);
+    return hipGetLastError();
 }
 
 hipError_t launch_fused_gather(const unsigned long long* rec, uint64_t nrec, uint32_t epoch, const uint64_t* cand,
                                uint64_t* out, uint64_t* counts, uint64_t* offs, void* scan_tmp, size_t scan_tmp_bytes,
-                               uint64_t* res, hipStream_t stream) {
+                               uint64_t* res, const unsigned long long* counters, const uint8_t* tail_src, uint32_t tl,
+                               uint8_t* tail_dst, uint64_t* count_dev, hipStream_t stream) {
+    if (tl > 256) return hipErrorInvalidValue;
     if (nrec + 1 > 0xFFFFFFFFull) return hipErrorInvalidValue;
     (void)hipGetLastError();
     hipLaunchKernelGGL(fused_rec_counts_kernel, dim3((unsigned)((nrec + 256) / 256)), dim3(256), 0, stream, rec, nrec,
                        epoch, counts, res);
     hipError_t e = exclusive_sum_u64(scan_tmp, &scan_tmp_bytes, counts, offs, (uint32_t)(nrec + 1), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fused_gather_kernel, dim3(1024), dim3(256), 0, stream, rec, nrec, epoch, offs, cand, out, res);
+    // a wave per record, every record at once (a grid-stride loop of 25 records per wave
+    // chained three memory round trips per record: 37 us at 64 KiB averages)
+    const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>((nrec + 3) / 4, 1), 1u << 20);
+    hipLaunchKernelGGL(fused_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, rec, nrec, epoch, offs, cand,
+                       out, res, counters, tail_src, tl, tail_dst, count_dev);
     return hipGetLastError();
 }
 
@@ -996,30 +1057,30 @@ hipError_t launch_scan_exact(const uint8_t* data, uint64_t len, const uint8_t* p
 hipError_t launch_resolve(const uint64_t* C, uint32_t m, const ResolveParams& p, uint32_t* nxt,
                           uint32_t* jtmp, uint64_t* nforced, uint32_t* on, uint64_t* cnt,
                           uint64_t* off, void* scan_tmp, size_t scan_tmp_bytes, uint64_t* out,
-                          uint64_t out_cap, uint64_t* res, hipStream_t stream) {
+                          uint64_t out_cap, uint64_t* res, hipStream_t stream, const uint64_t* m_dev,
+                          uint32_t m_base) {
+    // m_dev: the node count lives on the device (m is its upper bound, grids sized by it)
     const uint32_t n = m + 2;
     const unsigned blocks = (n + 255) / 256;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(resolve_next_kernel, dim3(blocks), dim3(256), 0, stream, C, m, p, nxt,
-                       nforced, on);
-    // pointer doubling over copies of nxt (nxt itself is kept for emission)
-    hipError_t e = hipMemcpyAsync(jtmp, nxt, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, stream);
-    if (e != hipSuccess) return e;
+    // nxt, and its copy in jtmp that the pointer doubling consumes (nxt is kept for emission)
     uint32_t* ja = jtmp;
     uint32_t* jb = jtmp + n;
+    hipLaunchKernelGGL(resolve_next_kernel, dim3(blocks), dim3(256), 0, stream, C, m, p, nxt,
+                       nforced, on, m_dev, m_base, ja);
     for (uint64_t span = 1; span < n; span <<= 3) {  // three rounds per launch
-        hipLaunchKernelGGL(resolve_double3_kernel, dim3(blocks), dim3(256), 0, stream, n, ja, jb, on);
+        hipLaunchKernelGGL(resolve_double3_kernel, dim3(blocks), dim3(256), 0, stream, n, ja, jb, on, m_dev, m_base);
         uint32_t* t = ja;
         ja = jb;
         jb = t;
     }
     hipLaunchKernelGGL(resolve_count_kernel, dim3(blocks), dim3(256), 0, stream, m, nxt, nforced,
-                       on, cnt);
+                       on, cnt, m_dev, m_base);
     size_t tb = scan_tmp_bytes;
-    e = exclusive_sum_u64(scan_tmp, &tb, cnt, off, m + 1, stream);
+    hipError_t e = exclusive_sum_u64(scan_tmp, &tb, cnt, off, m + 1, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(resolve_emit_kernel, dim3(blocks), dim3(256), 0, stream, C, m, p, nxt,
-                       nforced, on, cnt, off, out, out_cap, res);
+                       nforced, on, cnt, off, out, out_cap, res, m_dev, m_base);
     return hipGetLastError();
 }
 

@@ -1620,6 +1620,7 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
     __shared__ uint4 stage[kZStageWords];
     __shared__ __attribute__((aligned(16))) uint8_t work[64 * 1024];
     __shared__ FseT fse[3];  // LL, OF, ML
+    __shared__ FseT fse_huf;  // the Huffman description's scratch (beside the sequence tables)
     __shared__ PreT pre[3];  // the predefined tables, same order
     __shared__ Ctl ctl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1852,7 +1853,11 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
         ZMARK(2);
 
-        // ---- literal mode (wave 0) and repeat-offset coding (wave 1, one lane per sub-block)
+        // ---- repeat-offset coding (every wave its sub-block), then two independent halves at
+        // once: the literal mode (Huffman code, wave 0) and the sequence side -- per stream (LL
+        // on wave 1, OF on 2, ML on 3) its code histogram, its table and its FSE state chain.
+        // (Round 3 ran them one after the other: the chains waited for the literal mode and the
+        // literal section for the chains -- ~80 us of a ~1.25 ms text block.)
         const bool role_probe = probe_on && blockIdx.x == 0;
         uint64_t zt = role_probe ? wall_clock64() : 0;
         auto role_end = [&](int idx) {
@@ -1864,22 +1869,67 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         };
         rep_code_wave(ctl, wseq_all, coded, (uint32_t)wave, lane);
         __threadfence_block();
-        if (wave == 1) role_end(18);
-        if (wave == 0) {
-            if (ctl.need_full) literal_mode_wave(E, ctl, fse[0], nlit, lane, role_probe ? g_zprobe : nullptr);
-            role_end(17);
+        {
+            // this sub-block's code histograms (LL | ML | OF, 121 bins) into the wave's own copy
+            // in the stream buffer (free until the literal section); the stream's wave sums them
+            uint32_t* const wc = E.streams + wave * 128;
+            for (uint32_t i = (uint32_t)lane; i < 128; i += 64) wc[i] = 0;
+            __builtin_amdgcn_wave_barrier();
+            uint32_t first = 0;
+            for (int w2 = 0; w2 < wave; ++w2) first += min(ctl.nseq[w2], kZSubSeq);
+            const uint32_t cnt = min(ctl.nseq[wave], kZSubSeq);
+            for (uint32_t q0 = 0; q0 < cnt; q0 += 64 * 4) {
+                uint32_t cv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t q = q0 + 64 * (uint32_t)u + (uint32_t)lane;
+                    cv[u] = q < cnt ? coded[first + q].codes : 0xFFFFFFFFu;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (cv[u] != 0xFFFFFFFFu) {
+                        atomicAdd(&wc[cv[u] & 0xFF], 1u);
+                        atomicAdd(&wc[36 + ((cv[u] >> 8) & 0xFF)], 1u);
+                        atomicAdd(&wc[36 + 53 + (cv[u] >> 16)], 1u);
+                    }
+            }
         }
-        for (uint32_t i = tid; i < 36 + 53 + 32; i += kZThreads) E.shist[i] = 0;
+        if (wave == 1) role_end(18);
         __syncthreads();
         ZMARK(3);
         uint32_t nseq = 0;
         for (int w2 = 0; w2 < kZWaves; ++w2) nseq += min(ctl.nseq[w2], kZSubSeq);
-        for (uint32_t q = tid; q < nseq; q += kZThreads) {
-            const uint32_t cc = coded[q].codes;
-            atomicAdd(&E.shist[cc & 0xFF], 1u);
-            atomicAdd(&E.shist[36 + ((cc >> 8) & 0xFF)], 1u);
-            atomicAdd(&E.shist[36 + 53 + (cc >> 16)], 1u);
+        if (wave == 0) {
+            if (ctl.need_full) literal_mode_wave(E, ctl, fse_huf, nlit, lane, role_probe ? g_zprobe : nullptr);
+            role_end(17);
+        } else if (wave <= 3) {
+            const int k = wave - 1;  // 0 LL, 1 OF, 2 ML
+            const uint32_t sh = k == 0 ? 0u : k == 1 ? 16u : 8u;
+            uint32_t* const hk = E.shist + (k == 0 ? 0 : k == 1 ? 36 + 53 : 36);  // (the histogram layout: LL, ML, OF)
+            const uint32_t nbin = k == 0 ? 36u : k == 1 ? 32u : 53u;
+            const uint32_t boff = k == 0 ? 0u : k == 1 ? 36u + 53u : 36u;
+            uint32_t tot = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < kZWaves; ++w2) tot += (uint32_t)lane < nbin ? E.streams[w2 * 128 + boff + lane] : 0u;
+            if ((uint32_t)lane < nbin) hk[lane] = tot;
+            __builtin_amdgcn_wave_barrier();
+            if (nseq > 0) {
+                if (k == 0) seq_table_wave(fse[0], hk, 36, nseq, kLLNorm, kLLLog, kLLMaxLog, lane);
+                if (k == 1) seq_table_wave(fse[1], hk, 29, nseq, kOFNorm, kOFLog, kOFMaxLog, lane);
+                if (k == 2) seq_table_wave(fse[2], hk, 53, nseq, kMLNorm, kMLLog, kMLMaxLog, lane);
+            }
+            if (wave == 1) role_end(19);
+            if (nseq >= 2 && fse[k].mode != 1) {
+                const FseView tv = fse[k].mode == 2 ? view(fse[k]) : view(pre[k]);
+                seq_chain_wave(tv, coded, nseq, sh, chains + (uint64_t)k * kZBlockSeq,
+                               reinterpret_cast<uint16_t*>(chains + 3ull * kZBlockSeq) + (uint64_t)k * kZBlockSeq,
+                               &ctl.seq_last[k], lane, role_probe && k == 0 ? g_zprobe : nullptr);
+                __threadfence_block();
+            }
+            if (wave == 1) role_end(20);
         }
+        __syncthreads();
+        ZMARK(5);
         // literal runs (few sequences: the raw literals are copied run by run, coalesced)
         if (wave == 0 && nseq < kZRuns) {
             const Coded x = (uint32_t)lane < nseq ? coded[lane] : Coded{0, 0, 0, 0};
@@ -1928,16 +1978,7 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                     }
             }
         }
-        // sequence tables: LL on wave 1, OF on wave 2, ML on wave 3 (lane 0 each)
         __syncthreads();
-        ZMARK(5);
-        if (role_probe) zt = wall_clock64();
-        if (wave >= 1 && wave <= 3 && nseq > 0) {
-            if (wave == 1) seq_table_wave(fse[0], E.shist, 36, nseq, kLLNorm, kLLLog, kLLMaxLog, lane);
-            if (wave == 2) seq_table_wave(fse[1], E.shist + 36 + 53, 29, nseq, kOFNorm, kOFLog, kOFMaxLog, lane);
-            if (wave == 3) seq_table_wave(fse[2], E.shist + 36, 53, nseq, kMLNorm, kMLLog, kMLMaxLog, lane);
-            if (wave == 1) role_end(19);
-        }
         // literal section: size decision (thread 0)
         if (tid == 0) {
             uint32_t lm = lit_mode, sz = 0;
@@ -1971,17 +2012,7 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             g_zprobe[11] += nseq;
             g_zprobe[12] += nlit;
         }
-        // ---- sequences: the three FSE state chains (lane 0 of waves 1-3), the section
-        // header (count, modes, table descriptions; wave 0 lane 0)
-        if (wave >= 1 && wave <= 3 && nseq >= 2 && fse[wave - 1].mode != 1) {
-            const int k = wave - 1;  // 0 LL, 1 OF, 2 ML
-            const FseView tv = fse[k].mode == 2 ? view(fse[k]) : view(pre[k]);
-            seq_chain_wave(tv, coded, nseq, k == 0 ? 0u : k == 1 ? 16u : 8u, chains + (uint64_t)k * kZBlockSeq,
-                           reinterpret_cast<uint16_t*>(chains + 3ull * kZBlockSeq) + (uint64_t)k * kZBlockSeq,
-                           &ctl.seq_last[k], lane, role_probe && k == 0 ? g_zprobe : nullptr);
-            __threadfence_block();
-        }
-        if (wave == 1) role_end(20);
+        // ---- the sequence section header (count, modes, table descriptions; thread 0)
         if (wave == 0 && role_probe) zt = wall_clock64();
         if (tid == 0) {
             uint8_t* o = lit_out + lsz;
@@ -2299,7 +2330,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
             const double nb = h[10] ? (double)h[10] : 1.0;
             std::fprintf(stderr,
                          "zstd probe (workgroup 0, us per block over %llu blocks, %.0f sequences, %.0f literals per "
-                         "block): stage %.1f parse %.1f litmap %.1f litmode %.1f codehist %.1f tables %.1f chains %.1f "
+                         "block): stage %.1f parse %.1f litmap %.1f repcode %.1f sizes %.1f litmode||seqside %.1f decision %.1f "
                          "literals %.1f seqstream %.1f end %.1f | wave 0: history %.1f rounds+walk %.1f | litmap: bitmap %.1f "
                          "sampled %.1f | roles: litmode %.1f repcode %.1f LLtable %.1f LLchain %.1f litsection %.1f | long LL "
                          "chains %llu: pass 1 %.1f rounds %.1f (%.2f rounds) | Huffman: rank %.1f merge %.1f lengths %.1f codes "

@@ -263,6 +263,17 @@ def test_scan_pass(gpu, oracle, kind, n, avg):
         for a, b in zip([0] + cuts, cuts + [n]):
             parts.append(c.find_cuts_device(dev.data_ptr() + a, b - a, is_final=b == n))
     assert np.array_equal(np.concatenate(parts), got)
+    # into a pinned cut array, as bench.py times it: the resolve writes the cuts there
+    # itself (and the open chunk's candidates to mapped memory), whole and split
+    with gpu.Chunker(avg) as c:
+        c.set_stream(torch.cuda.current_stream().cuda_stream)
+        out = torch.empty(c.cuts_bound(n), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+        out[:] = 7
+        assert np.array_equal(c.find_cuts_device(dev.data_ptr(), n, is_final=True, out=out), got)
+        parts = [c.find_cuts_device(dev.data_ptr(), cuts[0], out=out).copy()]
+        parts.append(c.find_cuts_device(dev.data_ptr() + cuts[0], cuts[1] - cuts[0], out=out).copy())
+        parts.append(c.find_cuts_device(dev.data_ptr() + cuts[1], n - cuts[1], is_final=True, out=out).copy())
+    assert np.array_equal(np.concatenate(parts), got)
 
 
 def test_small_batches_device(gpu, oracle):
