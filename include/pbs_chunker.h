@@ -70,7 +70,9 @@ int pbs_chunker_find_cuts(pbs_chunker *c, const uint8_t *data, size_t len, int i
                           uint64_t *out, size_t cap, size_t *n_out);
 
 /* Same as pbs_chunker_find_cuts with `dev_data` a device pointer (HBM-resident
- * input, e.g. a torch tensor's data_ptr()); `out` is a host array. */
+ * input, e.g. a torch tensor's data_ptr()); `out` is a host array.  When `out` is pinned
+ * or registered host memory the GPU writes long cut lists into it directly (no staging
+ * copy, one sync per call); any host array works.  Entries past *n_out are unspecified. */
 int pbs_chunker_find_cuts_device(pbs_chunker *c, const uint8_t *dev_data, size_t len,
                                  int is_final, uint64_t *out, size_t cap, size_t *n_out);
 
