@@ -1,9 +1,10 @@
-"""A/B of the scan pass's tile ends (PBS_FUSED_DBG, FusedPassArgs::dbg): 0 = as built,
-1 = no exact hash at the tile ends (no candidates: cut lists wrong, timing only), 2 = no
-wait for the candidate stores before the record, 3 = both.  One process, settings
-alternated, 64 GiB: median scan-kernel ms and wall ms per pass.
+"""A/B of an environment knob read when a chunker handle is created, one process, settings
+alternated, 64 GiB per stream: median scan-kernel ms and wall ms per pass, and whether each
+setting's cut list still equals the golden record.  Round 4 ran it with PBS_FUSED_DBG (a
+temporary switch of the scan pass's tile ends, since removed; `profiles/r04/scanpass/
+tileend.log`) and with PBS_FUSED_MIN_AVG (the scan pass forced up to 4 MiB, `r04p_*.log`).
 
-    python scripts/tile_end_ab.py [--kinds vmimage,random] [--avgs 65536,131072] [--dbg 0,1,2,3]
+    python scripts/tile_end_ab.py --env PBS_FUSED_MIN_AVG --dbg 262144,8388608 [--kinds vmimage] [--avgs ...]
 """
 import argparse
 import json
@@ -22,8 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kinds", default="vmimage,random")
     ap.add_argument("--avgs", default="65536,131072")
-    ap.add_argument("--dbg", default="0,1,2,3")
-    ap.add_argument("--env", default="PBS_FUSED_DBG")
+    ap.add_argument("--dbg", default="262144,8388608", help="the knob's values, comma-separated")
+    ap.add_argument("--env", default="PBS_FUSED_MIN_AVG")
     ap.add_argument("--size-gib", type=float, default=64.0)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--reps", type=int, default=2)
