@@ -116,10 +116,10 @@ int pbs_known_chunks_device(const uint8_t *digests_dev, size_t n, const uint8_t 
  * the same stream); cap >= pbs_chunker_cuts_bound for the average.  Needs `len` bytes of
  * device memory, kept in the device's pipeline work area between calls (freed by
  * pbs_pipeline_release).  Each chunk is routed when the chunker completes it: to a
- * persistent GPU digest grid when its serial hash (len / PBS_PIPE_GPU_MBS, default 25 MB/s)
- * ends before the copy's projected end + PBS_PIPE_SLACK_MS (default 20), else to
- * PBS_PIPE_HOST_THREADS host threads (default min(hardware threads, 16) - 2) straight from
- * `host`; PBS_PIPE_HOST_MIN=<bytes> instead sends chunks of at least that length to the
+ * persistent GPU digest grid when its serial hash (len / PBS_PIPE_GPU_MBS, default 15 MB/s)
+ * ends before the copy's projected end + PBS_PIPE_SLACK_MS (default 10), else to
+ * PBS_PIPE_HOST_THREADS host threads (default min(hardware threads, 16) - 2, up to four
+ * chunks in step each) straight from `host`; PBS_PIPE_HOST_MIN=<bytes> instead sends chunks of at least that length to the
  * host and the rest to the GPU.  Synchronous. */
 typedef struct {
     double total_ms; /* first copy issued .. digests on the host */

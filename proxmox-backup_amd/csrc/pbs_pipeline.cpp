@@ -15,9 +15,11 @@
 // digest workgroup, and a digest launch lasts as long as its longest chunk's serial
 // hash (~0.6 s for a 16 MiB chunk), so without the split a scan launch would wait for it.
 //   routing       one GPU lane walks a chunk's serial SHA-256 chain at ~25-35 MB/s, a host
-//                 thread (SHA extensions, pbs_sha_host.cpp) at ~2.2 GB/s but there are only
-//                 ~14 of them.  A chunk goes to the GPU when its chain ends before the copy
-//                 does (now + len / 25 MB/s <= the copy's projected end + slack), else to
+//                 thread (SHA extensions, pbs_sha_host.cpp) at ~2.5 GB/s per chunk, ~4.4
+//                 with four chunks in step, but there are only ~14 of them.  A chunk goes to
+//                 the GPU when its chain ends before the copy does (now + len / 15 MB/s <=
+//                 the copy's projected end + slack; the assumed rate is below the lane's so
+//                 the host takes more of the late chunks), else to
 //                 the host threads (straight from the caller's buffer; all-zero chunks once
 //                 per length).  So early chunks of any length hash on the GPU under the
 //                 copy, and only the long chunks found near the end load the host
@@ -312,16 +314,19 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     double h2d_ms = 0;
     // host share: the chunks routed to the host threads, hashed from `host` by a pool fed
     // in stream order.  Routing (see the top): PBS_PIPE_HOST_MIN = a fixed length threshold
-    // instead (0: no host share); PBS_PIPE_GPU_MBS = one GPU lane's SHA-256 rate while the
-    // scan and the copies run beside it (25: 36 MB/s alone, but the board is at its power
-    // cap here); PBS_PIPE_SLACK_MS = how far past the copy's projected end a GPU chain may
-    // run (20).  Same-process sweep over the 64 GiB stream (scripts/pipe_sweep.py,
-    // profiles/r04/pipeline/): 25/20 -> 1329 ms, 30/20 -> 1385, 35/40 -> 1490, 20/0 -> 1353,
-    // the fixed 8 MiB threshold 1528
+    // instead (0: no host share); PBS_PIPE_GPU_MBS = the GPU lane rate the routing assumes
+    // (15; a lane runs ~25 MB/s beside the scan and the copies, 36 alone: the lower figure
+    // hands the host more of the late chunks, which it hashes four in step per thread);
+    // PBS_PIPE_SLACK_MS = how far past the copy's projected end a GPU chain may run (10).
+    // Same-process sweeps over the 64 GiB stream (scripts/pipe_sweep.py): with one chunk at a
+    // time per host thread (profiles/r04/pipeline/) 25/20 -> 1329 ms, 30/20 -> 1385, 35/40 ->
+    // 1490, 20/0 -> 1353, the fixed 8 MiB threshold 1528; with four in step
+    // (profiles/r04/sha_lanes/) 25/20 -> 1321-1326, 20/0 -> 1279, 10-17 MB/s with 0-10 ms ->
+    // 1240-1256
     const uint64_t host_min = env_u64("PBS_PIPE_HOST_MIN", ~0ull);
     const bool deadline = host_min == ~0ull;
-    const double gpu_bpms = (double)env_u64("PBS_PIPE_GPU_MBS", 25) * 1e3;  // bytes per ms
-    const double slack_ms = (double)env_u64("PBS_PIPE_SLACK_MS", 20);
+    const double gpu_bpms = (double)env_u64("PBS_PIPE_GPU_MBS", 15) * 1e3;  // bytes per ms
+    const double slack_ms = (double)env_u64("PBS_PIPE_SLACK_MS", 10);
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     const int hthreads = host_min ? (int)env_u64("PBS_PIPE_HOST_THREADS", (uint64_t)std::max(1, std::min(hw, 16) - 2)) : 0;
     std::deque<uint64_t> hq;  // chunk indices
@@ -335,46 +340,47 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     std::map<uint64_t, std::array<uint8_t, 32>> zero_dig;  // digest of an all-zero chunk per length
     std::vector<std::thread> hpool;
     hmask.assign(ok ? cap : 0, 0);
-    // one host worker: takes routed chunks until the queue is empty and the routing done
+    // one host worker: takes routed chunks until the queue is empty and the routing done,
+    // up to four in step (pbs::sha256_host_lanes); an all-zero chunk is hashed once per length
     auto host_work = [&] {
-                for (;;) {
-                    uint64_t i;
-                    {
-                        std::unique_lock<std::mutex> g(hmu);
-                        hcv.wait(g, [&] { return hdone || !hq.empty(); });
-                        if (hq.empty()) return;
-                        i = hq.front();
-                        hq.pop_front();
-                    }
-                    const uint64_t s0 = i ? ends[i - 1] : 0, e0 = ends[i], cl = e0 - s0;
-                    uint8_t* out = digests + 32 * i;
-                    const bool zero = pbs::all_zero(host + s0, cl);
-                    if (zero) {  // zero extents: one hash per length
-                        bool hit = false;
-                        {
-                            std::lock_guard<std::mutex> g(hmu);
-                            auto it = zero_dig.find(cl);
-                            if (it != zero_dig.end()) {
-                                std::memcpy(out, it->second.data(), 32);
-                                hit = true;
-                            }
-                        }
-                        if (hit) {
-                            host_chunks += 1;
-                            continue;
-                        }
-                    }
-                    pbs::sha256_host_one(host + s0, cl, key, key_len, out);
-                    if (zero) {
-                        std::lock_guard<std::mutex> g(hmu);
-                        std::memcpy(zero_dig[cl].data(), out, 32);
-                    }
-                    host_chunks += 1;
-                    host_bytes += e0 - s0;
-                    const uint64_t us = (uint64_t)(ms_since(t0) * 1000.0);
-                    for (uint64_t cur = host_work_us.load(); us > cur && !host_work_us.compare_exchange_weak(cur, us);) {
+        auto next = [&](pbs::ShaJob& j, bool block) {
+            for (;;) {
+                uint64_t i;
+                {
+                    std::unique_lock<std::mutex> g(hmu);
+                    if (block) hcv.wait(g, [&] { return hdone || !hq.empty(); });
+                    if (hq.empty()) return false;
+                    i = hq.front();
+                    hq.pop_front();
+                }
+                const uint64_t s0 = i ? ends[i - 1] : 0, cl = ends[i] - s0;
+                uint8_t* out = digests + 32 * i;
+                const bool zero = pbs::all_zero(host + s0, cl);
+                if (zero) {
+                    std::lock_guard<std::mutex> g(hmu);
+                    auto it = zero_dig.find(cl);
+                    if (it != zero_dig.end()) {
+                        std::memcpy(out, it->second.data(), 32);
+                        host_chunks += 1;
+                        continue;
                     }
                 }
+                j = pbs::ShaJob{host + s0, cl, out, zero ? 1ull : 0ull};
+                return true;
+            }
+        };
+        auto done = [&](const pbs::ShaJob& j) {
+            if (j.tag) {
+                std::lock_guard<std::mutex> g(hmu);
+                std::memcpy(zero_dig[j.len].data(), j.out, 32);
+            }
+            host_chunks += 1;
+            host_bytes += j.len;
+            const uint64_t us = (uint64_t)(ms_since(t0) * 1000.0);
+            for (uint64_t cur = host_work_us.load(); us > cur && !host_work_us.compare_exchange_weak(cur, us);) {
+            }
+        };
+        pbs::sha256_host_lanes(next, done, key, key_len);
     };
     if (ok && hthreads > 0)
         for (int j = 0; j < hthreads; ++j) hpool.emplace_back(host_work);

@@ -8,6 +8,9 @@
 // hybrid digest (pbs_digest.hip) therefore gives the longest chunks to host threads
 // running this code and the rest to the GPU.
 //
+// A thread hashes up to four chunks in step (sha256_host_lanes): one message's rounds wait
+// on each sha256rnds2's latency, four messages' rounds overlap.
+//
 // Block function: the SHA-NI form (sha256rnds2 does two rounds on the ABEF/CDGH state
 // halves; sha256msg1/msg2 + one alignr extend the schedule four words at a time), with a
 // runtime CPUID check and the portable FIPS 180-4 rounds as the fallback.  Padding and
@@ -20,6 +23,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -73,41 +77,78 @@ void blocks_portable(uint32_t h[8], const uint8_t* p, size_t nb) {
     }
 }
 
-// Four schedule words per step: quad q = W[4q .. 4q+3] (+K) feeds two sha256rnds2.
-__attribute__((target("sha,sse4.1,ssse3"))) void blocks_ni(uint32_t h[8], const uint8_t* p, size_t nb) {
+// Four schedule words per step: quad q = W[4q .. 4q+3] (+K) feeds two sha256rnds2.  N
+// independent messages advance together: one message's chain waits on each sha256rnds2's
+// latency, N of them overlap (sha256_host_lanes below).
+template <int N>
+__attribute__((target("sha,sse4.1,ssse3"), always_inline)) inline void blocks_ni_n(uint32_t* const* h,
+                                                                                 const uint8_t* const* pin,
+                                                                                 size_t nb) {
     const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bll, 0x0405060700010203ll);
-    // state words {a,b,c,d},{e,f,g,h} -> ABEF / CDGH lane order of sha256rnds2
-    __m128i t = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)h), 0xB1);        // C D A B
-    __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)(h + 4)), 0x1B);  // E F G H
-    __m128i s0 = _mm_alignr_epi8(t, s1, 8);                                          // A B E F
-    s1 = _mm_blend_epi16(s1, t, 0xF0);                                                // C D G H
-    for (; nb; --nb, p += 64) {
-        const __m128i save0 = s0, save1 = s1;
-        __m128i m[4];
+    __m128i s0[N], s1[N];
+    const uint8_t* p[N];
+#pragma GCC unroll 4
+    for (int j = 0; j < N; ++j) {
+        // state words {a,b,c,d},{e,f,g,h} -> ABEF / CDGH lane order of sha256rnds2
+        const __m128i t = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)h[j]), 0xB1);  // C D A B
+        const __m128i e = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)(h[j] + 4)), 0x1B);  // E F G H
+        s0[j] = _mm_alignr_epi8(t, e, 8);   // A B E F
+        s1[j] = _mm_blend_epi16(e, t, 0xF0);  // C D G H
+        p[j] = pin[j];
+    }
+    for (; nb; --nb) {
+        __m128i save0[N], save1[N], m[N][4];
+#pragma GCC unroll 4
+        for (int j = 0; j < N; ++j) save0[j] = s0[j], save1[j] = s1[j];
 #pragma GCC unroll 16
         for (int q = 0; q < 16; ++q) {
-            __m128i& x = m[q & 3];
-            if (q < 4) {
-                x = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(p + 16 * q)), bswap);
-            } else {
-                // W[t] = W[t-16] + s0(W[t-15]) + W[t-7] + s1(W[t-2])
-                const __m128i w7 = _mm_alignr_epi8(m[(q - 1) & 3], m[(q - 2) & 3], 4);
-                x = _mm_sha256msg2_epu32(_mm_add_epi32(_mm_sha256msg1_epu32(x, m[(q - 3) & 3]), w7),
-                                         m[(q - 1) & 3]);
+#pragma GCC unroll 4
+            for (int j = 0; j < N; ++j) {
+                __m128i& x = m[j][q & 3];
+                if (q < 4) {
+                    x = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(p[j] + 16 * q)), bswap);
+                } else {
+                    // W[t] = W[t-16] + s0(W[t-15]) + W[t-7] + s1(W[t-2])
+                    const __m128i w7 = _mm_alignr_epi8(m[j][(q - 1) & 3], m[j][(q - 2) & 3], 4);
+                    x = _mm_sha256msg2_epu32(_mm_add_epi32(_mm_sha256msg1_epu32(x, m[j][(q - 3) & 3]), w7),
+                                             m[j][(q - 1) & 3]);
+                }
+                const __m128i wk = _mm_add_epi32(x, _mm_load_si128((const __m128i*)(kK + 4 * q)));
+                s1[j] = _mm_sha256rnds2_epu32(s1[j], s0[j], wk);
+                s0[j] = _mm_sha256rnds2_epu32(s0[j], s1[j], _mm_shuffle_epi32(wk, 0x0E));
             }
-            __m128i wk = _mm_add_epi32(x, _mm_load_si128((const __m128i*)(kK + 4 * q)));
-            s1 = _mm_sha256rnds2_epu32(s1, s0, wk);
-            s0 = _mm_sha256rnds2_epu32(s0, s1, _mm_shuffle_epi32(wk, 0x0E));
         }
-        s0 = _mm_add_epi32(s0, save0);
-        s1 = _mm_add_epi32(s1, save1);
+#pragma GCC unroll 4
+        for (int j = 0; j < N; ++j) {
+            s0[j] = _mm_add_epi32(s0[j], save0[j]);
+            s1[j] = _mm_add_epi32(s1[j], save1[j]);
+            p[j] += 64;
+        }
     }
-    t = _mm_shuffle_epi32(s0, 0x1B);             // F E B A
-    s1 = _mm_shuffle_epi32(s1, 0xB1);            // D C H G
-    s0 = _mm_blend_epi16(t, s1, 0xF0);           // D C B A
-    s1 = _mm_alignr_epi8(s1, t, 8);              // H G F E
-    _mm_storeu_si128((__m128i*)h, s0);
-    _mm_storeu_si128((__m128i*)(h + 4), s1);
+#pragma GCC unroll 4
+    for (int j = 0; j < N; ++j) {
+        const __m128i t = _mm_shuffle_epi32(s0[j], 0x1B);  // F E B A
+        const __m128i u = _mm_shuffle_epi32(s1[j], 0xB1);  // D C H G
+        _mm_storeu_si128((__m128i*)h[j], _mm_blend_epi16(t, u, 0xF0));     // D C B A
+        _mm_storeu_si128((__m128i*)(h[j] + 4), _mm_alignr_epi8(u, t, 8));  // H G F E
+    }
+}
+
+__attribute__((target("sha,sse4.1,ssse3"))) void blocks_ni(uint32_t h[8], const uint8_t* p, size_t nb) {
+    uint32_t* const hh[1] = {h};
+    const uint8_t* const pp[1] = {p};
+    blocks_ni_n<1>(hh, pp, nb);
+}
+
+// `lanes` (1-4) messages in step, `nb` blocks each
+__attribute__((target("sha,sse4.1,ssse3"))) void blocks_ni_lanes(int lanes, uint32_t* const* h, const uint8_t* const* p,
+                                                                  size_t nb) {
+    switch (lanes) {
+        case 1: blocks_ni_n<1>(h, p, nb); break;
+        case 2: blocks_ni_n<2>(h, p, nb); break;
+        case 3: blocks_ni_n<3>(h, p, nb); break;
+        default: blocks_ni_n<4>(h, p, nb); break;
+    }
 }
 
 using BlockFn = void (*)(uint32_t*, const uint8_t*, size_t);
@@ -169,6 +210,62 @@ void sha256_host_one(const uint8_t* msg, size_t len, const uint8_t* key, size_t 
     sha256_host_final(s, msg + len / 64 * 64, len % 64, key, key_len, out);
 }
 
+// Up to kShaLanes messages in step per thread: on the EPYC 9575F hosts one message runs at
+// 2.47 GB/s (each sha256rnds2 waits for the previous one), two in step at 3.55, four at
+// 4.36 (scripts/sha_host_lanes_bench.cpp, profiles/r04/sha_lanes/).  While fewer than four
+// are open, the lanes advance kShaStep blocks at a time and then ask for more work.
+constexpr int kShaLanes = 4;
+constexpr uint64_t kShaStep = 2048;  // 128 KiB
+
+void sha256_host_lanes(const std::function<bool(ShaJob&, bool)>& next, const std::function<void(const ShaJob&)>& done,
+                       const uint8_t* key, size_t key_len) {
+    struct Lane {
+        ShaJob j;
+        HostSha s;
+        const uint8_t* p;
+        uint64_t nb;  // whole blocks left
+    };
+    Lane L[kShaLanes];
+    int act = 0;
+    const bool ni = blocks() == blocks_ni;
+    const char* e = std::getenv("PBS_SHA_HOST_LANES");  // A/B runs: 1 = one message at a time
+    const int lanes = e && *e ? std::max(1, std::min(kShaLanes, std::atoi(e))) : kShaLanes;
+    for (;;) {
+        while (act < lanes && next(L[act].j, act == 0)) {
+            Lane& l = L[act++];
+            sha256_host_init(l.s);
+            l.p = l.j.p;
+            l.nb = l.j.len / 64;
+        }
+        if (act == 0) return;
+        uint64_t k = act < lanes ? kShaStep : ~0ull;
+        for (int i = 0; i < act; ++i) k = std::min(k, L[i].nb);
+        if (k) {
+            uint32_t* h[kShaLanes];
+            const uint8_t* p[kShaLanes];
+            for (int i = 0; i < act; ++i) h[i] = L[i].s.h, p[i] = L[i].p;
+            if (ni)
+                blocks_ni_lanes(act, h, p, k);
+            else
+                for (int i = 0; i < act; ++i) blocks()(h[i], p[i], k);
+            for (int i = 0; i < act; ++i) {
+                L[i].p += 64 * k;
+                L[i].nb -= k;
+                L[i].s.total += 64 * k;
+            }
+        }
+        for (int i = 0; i < act;) {  // lanes without a whole block left: tail, key, padding
+            if (L[i].nb) {
+                ++i;
+                continue;
+            }
+            sha256_host_final(L[i].s, L[i].p, L[i].j.len % 64, key, key_len, L[i].j.out);
+            done(L[i].j);
+            L[i] = L[--act];
+        }
+    }
+}
+
 // Hashes chunks items[0..n) (indices into bounds) of a host buffer holding stream bytes
 // [base, ...) on `threads` threads; items are taken in the given order (longest first
 // keeps the threads' finishing times close).
@@ -176,11 +273,15 @@ void sha256_host_items(const uint8_t* host, uint64_t base, const uint64_t* bound
                        size_t n, const uint8_t* key, size_t key_len, uint8_t* digests, int threads) {
     std::atomic<size_t> next{0};
     auto work = [&] {
-        for (size_t k; (k = next.fetch_add(1, std::memory_order_relaxed)) < n;) {
-            const uint32_t i = items ? items[k] : (uint32_t)k;
-            sha256_host_one(host + (bounds[i] - base), bounds[i + 1] - bounds[i], key, key_len,
-                            digests + 32 * (size_t)i);
-        }
+        sha256_host_lanes(
+            [&](ShaJob& j, bool) {
+                const size_t k = next.fetch_add(1, std::memory_order_relaxed);
+                if (k >= n) return false;
+                const uint32_t i = items ? items[k] : (uint32_t)k;
+                j = ShaJob{host + (bounds[i] - base), bounds[i + 1] - bounds[i], digests + 32 * (size_t)i, i};
+                return true;
+            },
+            [](const ShaJob&) {}, key, key_len);
     };
     const int t = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), n));
     std::vector<std::thread> pool;

@@ -4,6 +4,8 @@ total, drain after the last piece, host share, digest-queue jobs; digests checke
 first run's (and the cut list against the golden record).
 
     python scripts/pipe_sweep.py [--gib 64] "SLACK_MS=40" "SLACK_MS=120,HOST_THREADS=15" ...
+
+(a name starting with PBS_ is taken as it is, e.g. "PBS_SHA_HOST_LANES=1")
 """
 import argparse
 import os
@@ -38,10 +40,11 @@ def main():
     pbschunk.pipeline_host(host[: 64 << 20], 4 << 20, piece=16 << 20, crc=True)  # warm-up
     ref = None
     for st in a.settings:
-        keys = [f"PBS_PIPE_{kv.split('=')[0]}" for kv in st.split(",") if kv]
+        name = lambda k: k if k.startswith("PBS_") else f"PBS_PIPE_{k}"  # noqa: E731
+        keys = [name(kv.split("=")[0]) for kv in st.split(",") if kv]
         for kv in filter(None, st.split(",")):
             k, v = kv.split("=", 1)
-            os.environ[f"PBS_PIPE_{k}"] = v
+            os.environ[name(k)] = v
         t0 = time.perf_counter()
         ends, dig, crcs, t = pbschunk.pipeline_host(host, 4 << 20, piece=a.piece_mib << 20, crc=True)
         wall = time.perf_counter() - t0

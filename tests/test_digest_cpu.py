@@ -111,6 +111,20 @@ def test_host_chunk_digests(pbschunk, oracle, klen):
     assert np.array_equal(got, oracle.chunk_digests(data, bounds, key or b""))
 
 
+@pytest.mark.parametrize("threads", [1, 3])
+def test_host_chunk_digests_lanes(pbschunk, oracle, threads):
+    """The host threads hash up to four chunks in step (sha256_host_lanes): lanes that end
+    at different blocks, refill from the list and run alone in 128 KiB steps; short and
+    long chunks interleaved, one and three threads."""
+    rng = np.random.default_rng(12)
+    lens = [int(v) for v in rng.integers(0, 300_000, 40)] + [0, 1, 63, 64, 65, 2 << 20, (3 << 20) + 5]
+    rng.shuffle(lens)
+    bounds = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    data = rng.integers(0, 256, int(bounds[-1]), dtype=np.uint8)
+    got = pbschunk.digest_chunks_host(data, bounds, key=b"lane-key", threads=threads)
+    assert np.array_equal(got, oracle.chunk_digests(data, bounds, b"lane-key"))
+
+
 def test_host_chunk_digests_base_and_range(pbschunk, oracle):
     data, bounds = _host_digest_cases()
     base = 1000
