@@ -54,9 +54,11 @@ int pbs_digest_chunks_async(const uint8_t *dev_data, size_t data_len, uint64_t b
 /* Hybrid per-chunk SHA-256: same digests as pbs_digest_chunks_device, with the work
  * split between the GPU and host threads.  A GPU lane walks one chunk's serial chain
  * (~35 MB/s), so the longest chunks set the GPU's makespan; a host core with the SHA
- * extensions walks one ~40x faster.  The longest chunks go to host threads until the
- * host's estimated time (their bytes / (threads x host_mb_s), at most 14 GB/s when
- * they are copied from HBM) meets the GPU's (the longest remaining chunk / gpu_mb_s);
+ * extensions walks one ~70x faster (~120x with four chunks in step per thread).  The
+ * longest chunks go to host threads until the host's estimated time (their bytes /
+ * (threads x host_mb_s), at most 45 GB/s when they are copied from HBM: whole chunks, back
+ * to back on one stream, into a pinned ring kept between calls) meets the GPU's (the
+ * longest remaining chunk / gpu_mb_s);
  * long chunks (>= 1 MiB) that are all zero bytes are hashed once per distinct length.
  * `dev_data` (device) holds stream bytes [base, base + data_len); `host_data` (NULL or a
  * host copy of the same bytes) lets the host threads read the bytes directly instead of
@@ -65,7 +67,8 @@ int pbs_digest_chunks_async(const uint8_t *dev_data, size_t data_len, uint64_t b
 typedef struct {
     int host_threads;      /* 0: min(hardware threads, 16); < 0: GPU only */
     uint64_t host_min_len; /* 0: cost model; else chunks at least this long go to the host */
-    double host_mb_s;      /* per-thread host SHA-256 rate for the model (0: 1400) */
+    double host_mb_s;      /* per-thread host SHA-256 rate for the model (0: 4000 with the SHA
+                            * extensions, 250 without) */
     double gpu_mb_s;       /* one GPU lane's chain rate for the model (0: 35) */
 } pbs_digest_hybrid_opts;
 typedef struct {
@@ -82,7 +85,7 @@ int pbs_digest_chunks_hybrid(const uint8_t *dev_data, const uint8_t *host_data, 
                              size_t key_len, uint8_t *digests, const pbs_digest_hybrid_opts *opts,
                              pbs_digest_hybrid_timing *timing, void *hip_stream);
 
-/* Frees the pinned host slices the hybrid digest keeps between calls. */
+/* Frees the pinned host memory (ring, slices) the hybrid digest keeps between calls. */
 void pbs_digest_hybrid_release(void);
 
 /* SHA-256(chunk || key) of every chunk of a host buffer on `threads` host threads (0:

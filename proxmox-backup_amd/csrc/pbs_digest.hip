@@ -21,6 +21,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -780,17 +782,52 @@ double hms(HClock::time_point a, HClock::time_point b) {
     return std::chrono::duration<double, std::milli>(b - a).count();
 }
 
-constexpr size_t kSlice = 4u << 20;         // D2H slice of a host-hashed chunk
+constexpr size_t kSlice = 4u << 20;         // D2H slice of a host-hashed chunk (chunks over the ring's slot)
 constexpr uint64_t kZeroMin = 1u << 20;      // chunks tested for all-zero content
+constexpr uint64_t kRingMax = 1ull << 30;    // pinned ring of whole-chunk slots, at most 1 GiB
+// D2H rate of whole chunks copied back to back on one stream into pinned slots (the cost
+// model's cap on the host share's rate when its bytes come from HBM)
+constexpr double kD2HRate = 45e9;
 
-// Per-thread pinned double buffers and copy streams for the host share, kept for the
-// process (pinning 8 MiB per thread on every call would cost more than it hides).
+// Pinned host memory and copy streams for the host share, kept for the process (pinning
+// on every call would cost more than it hides): a ring of whole-chunk slots filled by one
+// copy stream, and per-thread double buffers for chunks longer than a slot.
 struct HostStage {
     std::mutex mu;
     int dev = -1;
+    uint8_t* ring = nullptr;
+    size_t ring_bytes = 0;
+    hipStream_t cst = nullptr;   // the ring's copy stream
+    std::vector<hipEvent_t> rev; // one per slot
     std::vector<uint8_t*> buf;  // 2 * kSlice each
     std::vector<hipStream_t> st;
     std::vector<hipEvent_t> ev;  // 2 per thread
+    // a ring of `slots` slots of `sb` bytes (on device dv, like the streams below)
+    bool ring_grow(int dv, size_t slots, size_t sb) {
+        if (dev != dv) {
+            release();
+            dev = dv;
+        }
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess) return false;
+        if (cur != dv && hipSetDevice(dv) != hipSuccess) return false;
+        bool ok = true;
+        if (!cst) ok = hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) == hipSuccess;
+        if (ok && ring_bytes < slots * sb) {
+            if (ring) (void)hipHostFree(ring);
+            ring = nullptr;
+            ring_bytes = 0;
+            ok = hipHostMalloc((void**)&ring, slots * sb, hipHostMallocDefault) == hipSuccess;
+            if (ok) ring_bytes = slots * sb;
+        }
+        while (ok && rev.size() < slots) {
+            hipEvent_t e = nullptr;
+            ok = hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+            if (ok) rev.push_back(e);
+        }
+        if (cur != dv) (void)hipSetDevice(cur);
+        return ok;
+    }
     // streams and events are created on device dv (the caller's stream's device), not
     // on whatever device the calling thread has current
     bool grow(int dv, int t) {
@@ -826,6 +863,13 @@ struct HostStage {
         return ok;
     }
     void release() {
+        if (ring) (void)hipHostFree(ring);
+        if (cst) (void)hipStreamDestroy(cst);
+        for (auto e : rev) (void)hipEventDestroy(e);
+        ring = nullptr;
+        ring_bytes = 0;
+        cst = nullptr;
+        rev.clear();
         for (auto b : buf) (void)hipHostFree(b);
         for (auto s : st) (void)hipStreamDestroy(s);
         for (auto e : ev) (void)hipEventDestroy(e);
@@ -871,6 +915,88 @@ bool hash_from_device(const uint8_t* src, uint64_t len, const uint8_t* key, size
     return true;
 }
 
+// The host share items[0..h) from HBM through the ring: one copier (this thread) copies
+// whole chunks into free slots back to back on hs.cst; `t` threads hash them as they land,
+// up to four in step each (pbs::sha256_host_lanes), and free their slots.  Every chunk must
+// fit a slot (sb bytes).  False on a HIP error (no copy in flight on return).
+bool hash_ring(HostStage& hs, size_t slots, size_t sb, const uint8_t* dev_data, uint64_t base,
+               const uint64_t* bounds, const uint32_t* items, size_t h, const uint8_t* key, size_t key_len,
+               uint8_t* digests, int t) {
+    std::mutex qm;
+    std::condition_variable qcv;
+    std::deque<size_t> freeq;
+    std::deque<std::pair<uint32_t, size_t>> landed;  // (chunk, slot) in copy order
+    bool copies_done = false;
+    std::atomic<bool> bad{false};
+    for (size_t j = 0; j < slots; ++j) freeq.push_back(j);
+    auto next = [&](pbs::ShaJob& job, bool block) {
+        std::unique_lock<std::mutex> g(qm);
+        for (;;) {
+            if (bad) return false;
+            if (!landed.empty()) {
+                const auto [i, slot] = landed.front();
+                const hipError_t q = hipEventQuery(hs.rev[slot]);
+                if (q == hipSuccess) {
+                    landed.pop_front();
+                    job = pbs::ShaJob{hs.ring + slot * sb, bounds[i + 1] - bounds[i], digests + 32 * (size_t)i, slot};
+                    return true;
+                }
+                if (q != hipErrorNotReady) {
+                    bad = true;
+                    qcv.notify_all();
+                    return false;
+                }
+                if (!block) return false;
+                g.unlock();
+                if (hipEventSynchronize(hs.rev[slot]) != hipSuccess) bad = true;
+                g.lock();
+                continue;
+            }
+            if (copies_done || !block) return false;
+            qcv.wait(g);
+        }
+    };
+    auto done = [&](const pbs::ShaJob& job) {
+        {
+            std::lock_guard<std::mutex> g(qm);
+            freeq.push_back((size_t)job.tag);
+        }
+        qcv.notify_all();
+    };
+    std::vector<std::thread> pool;
+    for (int j = 0; j < t; ++j) pool.emplace_back([&] { pbs::sha256_host_lanes(next, done, key, key_len); });
+    for (size_t k = 0; k < h && !bad; ++k) {
+        size_t slot;
+        {
+            std::unique_lock<std::mutex> g(qm);
+            qcv.wait(g, [&] { return !freeq.empty() || bad; });
+            if (bad) break;
+            slot = freeq.front();
+            freeq.pop_front();
+        }
+        const uint32_t i = items[k];
+        if (hipMemcpyAsync(hs.ring + slot * sb, dev_data + (bounds[i] - base), bounds[i + 1] - bounds[i],
+                           hipMemcpyDeviceToHost, hs.cst) != hipSuccess ||
+            hipEventRecord(hs.rev[slot], hs.cst) != hipSuccess) {
+            bad = true;
+            break;
+        }
+        {
+            std::lock_guard<std::mutex> g(qm);
+            landed.emplace_back(i, slot);
+        }
+        qcv.notify_all();
+    }
+    {
+        std::lock_guard<std::mutex> g(qm);
+        copies_done = true;
+    }
+    qcv.notify_all();
+    for (auto& th : pool) th.join();
+    if (hipStreamSynchronize(hs.cst) != hipSuccess) bad = true;
+    return !bad;
+}
+
 }  // namespace
 
 // Frees the hybrid digest's pinned host slices and their streams.
@@ -900,11 +1026,13 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
     if (opts) o = *opts;
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     const int threads = o.host_threads < 0 ? 0 : o.host_threads == 0 ? std::min(hw, 16) : o.host_threads;
-    const double host_rate = (o.host_mb_s > 0 ? o.host_mb_s : 1400.0) * 1e6;  // bytes/s per thread
+    // per thread: ~4.3 GB/s with the SHA extensions and four chunks in step (EPYC 9575F,
+    // profiles/r04/sha_lanes/), far less with the portable rounds
+    const double host_rate = (o.host_mb_s > 0 ? o.host_mb_s : pbs::sha256_host_has_ni() ? 4000.0 : 250.0) * 1e6;
     const double gpu_rate = (o.gpu_mb_s > 0 ? o.gpu_mb_s : 35.0) * 1e6;        // bytes/s per chain
-    // from HBM the host share moves through 4 MiB pinned slices: ~14 GB/s measured over
-    // 16 threads on the MI355X box (profiles/r02/digest), below the threads' SHA rate
-    const double agg = std::min(threads * host_rate, host_data ? 1e12 : 14e9);
+    // from HBM the host share is copied whole chunk by whole chunk into a pinned ring
+    // (round 2's per-thread 4 MiB slices moved only ~14 GB/s over 16 threads)
+    const double agg = std::min(threads * host_rate, host_data ? 1e12 : kD2HRate);
     hipStream_t st = (hipStream_t)hip_stream;
     auto clen = [&](uint32_t i) { return bounds[i + 1] - bounds[i]; };
     int sdev = 0;
@@ -1016,15 +1144,30 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
             std::lock_guard<std::mutex> lk(hs.mu);
             int dv = 0;
             const int t = (int)std::min<size_t>((size_t)threads, h);
+            // whole chunks through the ring when a slot can hold the longest (always for the
+            // reference's chunk sizes, <= 16 MiB); slots for four open chunks per thread + 8
+            // in flight, within kRingMax
+            const uint64_t sb = (clen(work[0]) + 4095) / 4096 * 4096;
+            const size_t slots = std::min<size_t>(std::min<size_t>(h, 4 * (size_t)t + 8),
+                                                  sb ? (size_t)(kRingMax / sb) : 0);
+            const char* re = std::getenv("PBS_DIGEST_RING");  // 0: per-thread slices (tests, A/B)
+            const bool use_ring = sb && slots >= 2 && !(re && re[0] == '0');
             bool waits = true;
-            if (hipStreamGetDevice(st, &dv) != hipSuccess || !hs.grow(dv, t)) {
+            if (hipStreamGetDevice(st, &dv) != hipSuccess ||
+                (use_ring ? !hs.ring_grow(dv, slots, sb) : !hs.grow(dv, t))) {
                 fail(PBS_ERR_NOMEM);
+            } else if (use_ring) {
+                waits = hipStreamWaitEvent(hs.cst, ready, 0) == hipSuccess;
+                if (!waits) fail(PBS_ERR_HIP);
             } else {
                 for (int j = 0; j < t; ++j)
                     waits = waits && hipStreamWaitEvent(hs.st[j], ready, 0) == hipSuccess;
                 if (!waits) fail(PBS_ERR_HIP);
             }
-            if (rc == PBS_OK) {
+            if (rc == PBS_OK && use_ring) {
+                if (!hash_ring(hs, slots, sb, dev_data, base, bounds, work.data(), h, key, key_len, digests, t))
+                    fail(PBS_ERR_HIP);
+            } else if (rc == PBS_OK) {
                 std::atomic<size_t> next{0};
                 std::atomic<bool> bad{false};
                 auto run = [&](int j) {

@@ -319,19 +319,26 @@ def _hybrid_case():
     return data, bounds
 
 
-@pytest.mark.parametrize("mode", ["auto", "host_from_hbm", "host_from_copy", "gpu_only", "one_thread"])
+@pytest.mark.parametrize("mode", ["auto", "host_from_hbm", "host_from_hbm_slices", "host_from_copy", "gpu_only",
+                                  "one_thread", "one_thread_all"])
 @pytest.mark.parametrize("key", [None, bytes(range(32))])
-def test_hybrid_digest(gpu, oracle, torch_dev, mode, key):
+def test_hybrid_digest(gpu, oracle, torch_dev, mode, key, monkeypatch):
     """pbs_digest_chunks_hybrid against the oracle: the host share reading from HBM
-    (pinned 4 MiB slices) or from a host copy, the GPU share, and the all-zero long
-    chunks hashed once per length and copied to the rest."""
+    (whole chunks through the pinned ring -- with one thread and every chunk on the host
+    its 12 slots are reused -- or, PBS_DIGEST_RING=0, 4 MiB slices per thread) or from a
+    host copy, the GPU share, and the all-zero long chunks hashed once per length and
+    copied to the rest."""
     data, bounds = _hybrid_case()
     t, ptr = _dev(torch_dev, data, 3)
     kw = {"auto": dict(threads=4),
           "host_from_hbm": dict(threads=4, host_min_len=1),
+          "host_from_hbm_slices": dict(threads=4, host_min_len=1),
           "host_from_copy": dict(threads=4, host_min_len=1, host=data),
           "gpu_only": dict(threads=-1),
-          "one_thread": dict(threads=1, host_min_len=MiB)}[mode]
+          "one_thread": dict(threads=1, host_min_len=MiB),
+          "one_thread_all": dict(threads=1, host_min_len=1)}[mode]
+    if mode == "host_from_hbm_slices":
+        monkeypatch.setenv("PBS_DIGEST_RING", "0")
     got, tm = gpu.digest_chunks_hybrid(ptr, data.size, bounds, key=key, **kw)
     assert np.array_equal(got, oracle.chunk_digests(data, bounds, key or b""))
     n = bounds.size - 1
@@ -340,7 +347,7 @@ def test_hybrid_digest(gpu, oracle, torch_dev, mode, key):
     else:
         assert tm["zero_chunks"] == 5 and tm["zero_lengths"] == 2
         assert tm["host_chunks"] + tm["gpu_chunks"] == n - 3
-    if mode.startswith("host_from"):
+    if mode.startswith("host_from") or mode == "one_thread_all":
         assert tm["gpu_chunks"] == 2  # the empty chunks (length 0 < host_min_len)
 
 
@@ -355,6 +362,13 @@ def test_hybrid_digest_vm_stream(gpu, oracle, torch_dev):
     if ends.size == 0 or int(ends[-1]) != n:
         ends = np.append(ends, np.uint64(n))
     bounds = np.concatenate([[0], ends]).astype(np.uint64)
+    want = oracle.chunk_digests(data, bounds)
     got, tm = gpu.digest_chunks_hybrid(ptr, n, bounds, threads=8)
-    assert np.array_equal(got, oracle.chunk_digests(data, bounds))
+    assert np.array_equal(got, want)
+    # (at this size the model hands the host every chunk: 8 threads clear 512 MiB before
+    # one GPU lane finishes a 4 MiB chunk)
+    assert tm["host_chunks"] > 0
+    # a slow host rate in the model: a real split
+    got, tm = gpu.digest_chunks_hybrid(ptr, n, bounds, threads=8, host_mb_s=100)
+    assert np.array_equal(got, want)
     assert tm["host_chunks"] > 0 and tm["gpu_chunks"] > 0
