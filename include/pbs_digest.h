@@ -56,8 +56,8 @@ int pbs_digest_chunks_async(const uint8_t *dev_data, size_t data_len, uint64_t b
  * (~35 MB/s), so the longest chunks set the GPU's makespan; a host core with the SHA
  * extensions walks one ~70x faster (~120x with four chunks in step per thread).  The
  * longest chunks go to host threads until the host's estimated time (their bytes /
- * (threads x host_mb_s), at most 45 GB/s when they are copied from HBM: whole chunks, back
- * to back on one stream, into a pinned ring kept between calls) meets the GPU's (the
+ * (threads x host_mb_s), at most 50 GB/s when they are copied from HBM: whole chunks, back
+ * to back on two streams, into a pinned ring kept between calls) meets the GPU's (the
  * longest remaining chunk / gpu_mb_s);
  * long chunks (>= 1 MiB) that are all zero bytes are hashed once per distinct length.
  * `dev_data` (device) holds stream bytes [base, base + data_len); `host_data` (NULL or a

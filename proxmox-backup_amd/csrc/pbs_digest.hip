@@ -785,9 +785,11 @@ double hms(HClock::time_point a, HClock::time_point b) {
 constexpr size_t kSlice = 4u << 20;         // D2H slice of a host-hashed chunk (chunks over the ring's slot)
 constexpr uint64_t kZeroMin = 1u << 20;      // chunks tested for all-zero content
 constexpr uint64_t kRingMax = 1ull << 30;    // pinned ring of whole-chunk slots, at most 1 GiB
-// D2H rate of whole chunks copied back to back on one stream into pinned slots (the cost
-// model's cap on the host share's rate when its bytes come from HBM)
-constexpr double kD2HRate = 45e9;
+// D2H rate of whole chunks copied back to back on two streams into pinned slots (the cost
+// model's cap on the host share's rate when its bytes come from HBM): 16 GB of the 64 GiB
+// VM image's longest chunks in 310-316 ms on two streams, 327-337 on one
+// (profiles/r04/digest_ring/)
+constexpr double kD2HRate = 50e9;
 
 // Pinned host memory and copy streams for the host share, kept for the process (pinning
 // on every call would cost more than it hides): a ring of whole-chunk slots filled by one
@@ -797,7 +799,7 @@ struct HostStage {
     int dev = -1;
     uint8_t* ring = nullptr;
     size_t ring_bytes = 0;
-    hipStream_t cst = nullptr;   // the ring's copy stream
+    hipStream_t cst[2] = {nullptr, nullptr};  // the ring's copy streams
     std::vector<hipEvent_t> rev; // one per slot
     std::vector<uint8_t*> buf;  // 2 * kSlice each
     std::vector<hipStream_t> st;
@@ -812,7 +814,8 @@ struct HostStage {
         if (hipGetDevice(&cur) != hipSuccess) return false;
         if (cur != dv && hipSetDevice(dv) != hipSuccess) return false;
         bool ok = true;
-        if (!cst) ok = hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) == hipSuccess;
+        for (auto& c : cst)
+            if (ok && !c) ok = hipStreamCreateWithFlags(&c, hipStreamNonBlocking) == hipSuccess;
         if (ok && ring_bytes < slots * sb) {
             if (ring) (void)hipHostFree(ring);
             ring = nullptr;
@@ -864,11 +867,13 @@ struct HostStage {
     }
     void release() {
         if (ring) (void)hipHostFree(ring);
-        if (cst) (void)hipStreamDestroy(cst);
+        for (auto& c : cst) {
+            if (c) (void)hipStreamDestroy(c);
+            c = nullptr;
+        }
         for (auto e : rev) (void)hipEventDestroy(e);
         ring = nullptr;
         ring_bytes = 0;
-        cst = nullptr;
         rev.clear();
         for (auto b : buf) (void)hipHostFree(b);
         for (auto s : st) (void)hipStreamDestroy(s);
@@ -916,12 +921,12 @@ bool hash_from_device(const uint8_t* src, uint64_t len, const uint8_t* key, size
 }
 
 // The host share items[0..h) from HBM through the ring: one copier (this thread) copies
-// whole chunks into free slots back to back on hs.cst; `t` threads hash them as they land,
+// whole chunks into free slots back to back on `ncs` (1-2) copy streams in turn; `t` threads hash them as they land,
 // up to four in step each (pbs::sha256_host_lanes), and free their slots.  Every chunk must
 // fit a slot (sb bytes).  False on a HIP error (no copy in flight on return).
 bool hash_ring(HostStage& hs, size_t slots, size_t sb, const uint8_t* dev_data, uint64_t base,
                const uint64_t* bounds, const uint32_t* items, size_t h, const uint8_t* key, size_t key_len,
-               uint8_t* digests, int t) {
+               uint8_t* digests, int t, int ncs) {
     std::mutex qm;
     std::condition_variable qcv;
     std::deque<size_t> freeq;
@@ -976,8 +981,8 @@ bool hash_ring(HostStage& hs, size_t slots, size_t sb, const uint8_t* dev_data, 
         }
         const uint32_t i = items[k];
         if (hipMemcpyAsync(hs.ring + slot * sb, dev_data + (bounds[i] - base), bounds[i + 1] - bounds[i],
-                           hipMemcpyDeviceToHost, hs.cst) != hipSuccess ||
-            hipEventRecord(hs.rev[slot], hs.cst) != hipSuccess) {
+                           hipMemcpyDeviceToHost, hs.cst[k % ncs]) != hipSuccess ||
+            hipEventRecord(hs.rev[slot], hs.cst[k % ncs]) != hipSuccess) {
             bad = true;
             break;
         }
@@ -993,7 +998,8 @@ bool hash_ring(HostStage& hs, size_t slots, size_t sb, const uint8_t* dev_data, 
     }
     qcv.notify_all();
     for (auto& th : pool) th.join();
-    if (hipStreamSynchronize(hs.cst) != hipSuccess) bad = true;
+    for (int j = 0; j < ncs; ++j)
+        if (hipStreamSynchronize(hs.cst[j]) != hipSuccess) bad = true;
     return !bad;
 }
 
@@ -1157,7 +1163,8 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
                 (use_ring ? !hs.ring_grow(dv, slots, sb) : !hs.grow(dv, t))) {
                 fail(PBS_ERR_NOMEM);
             } else if (use_ring) {
-                waits = hipStreamWaitEvent(hs.cst, ready, 0) == hipSuccess;
+                waits = hipStreamWaitEvent(hs.cst[0], ready, 0) == hipSuccess &&
+                        hipStreamWaitEvent(hs.cst[1], ready, 0) == hipSuccess;
                 if (!waits) fail(PBS_ERR_HIP);
             } else {
                 for (int j = 0; j < t; ++j)
@@ -1165,7 +1172,9 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
                 if (!waits) fail(PBS_ERR_HIP);
             }
             if (rc == PBS_OK && use_ring) {
-                if (!hash_ring(hs, slots, sb, dev_data, base, bounds, work.data(), h, key, key_len, digests, t))
+                const char* ce = std::getenv("PBS_DIGEST_RING_STREAMS");  // copy streams, 1-2 (A/B)
+                const int ncs = ce && ce[0] == '1' ? 1 : 2;
+                if (!hash_ring(hs, slots, sb, dev_data, base, bounds, work.data(), h, key, key_len, digests, t, ncs))
                     fail(PBS_ERR_HIP);
             } else if (rc == PBS_OK) {
                 std::atomic<size_t> next{0};
