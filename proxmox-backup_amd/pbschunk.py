@@ -789,12 +789,13 @@ def read_didx(image: bytes):
 def index_stream_device(chunker: "Chunker", dev_ptr: int, length: int, key=None,
                         hip_stream: int = 0, uuid: bytes = bytes(16), ctime: int = 0):
     """The client's per-stream path on a device-resident stream: chunk boundaries
-    (GPU chunker), chunk digests (GPU SHA-256), then the .didx image and index_csum
-    (host).  Returns (ends, digests, csum, didx_bytes)."""
+    (GPU chunker), chunk digests (the hybrid SHA-256: GPU lanes, the longest chunks on
+    host cores), then the .didx image and index_csum (host).  Returns (ends, digests,
+    csum, didx_bytes)."""
     start = chunker.stream_offset
     ends = chunker.find_cuts_device(dev_ptr, length, is_final=True)
     bounds = np.concatenate([np.array([start], dtype=np.uint64), ends.astype(np.uint64)])
-    dig = digest_chunks_device(dev_ptr, length, bounds, base=start, key=key, hip_stream=hip_stream)
+    dig, _ = digest_chunks_hybrid(dev_ptr, length, bounds, base=start, key=key, hip_stream=hip_stream)
     image, csum = didx_build(ends, dig, uuid, ctime)
     return ends, dig, csum, image
 
