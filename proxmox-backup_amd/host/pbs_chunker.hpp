@@ -9,6 +9,9 @@
 //   pbs::sha256             openssl::sha::sha256 (host; index checksum)
 //   pbs::crc32_chunks_device DataBlob::compute_crc (data_blob.rs:70-75) per chunk, GPU
 //   pbs::crc32 / pbs::blob_encode_uncompressed  crc32fast::Hasher, DataBlob::encode(.., false)
+//   pbs::digest_chunks_host  the per-chunk digest on host cores (SHA extensions)
+//   pbs::pipeline_host      ChunkStream + the upload stream's per-chunk digest
+//                           (chunk_stream.rs:40-77, backup_writer.rs:671-678) over a host buffer
 //
 // Same names, argument meaning and error behaviour as the reference: a non-power-of-two
 // average throws std::invalid_argument with the reference's panic text; `scan` is
@@ -266,6 +269,49 @@ inline std::vector<uint8_t> blob_encode_uncompressed(const uint8_t* data, size_t
     if (pbs_blob_encode_uncompressed(data, len, crc, out.data(), out.size()) != out.size())
         throw std::invalid_argument("data blob too large (" + std::to_string(len) + " bytes).");
     return out;
+}
+
+// SHA-256 of every chunk [bounds[i], bounds[i+1]) of a host buffer (stream bytes
+// [base, base + len)) on `threads` host threads (0: all), optionally keyed.
+inline std::vector<Digest> digest_chunks_host(const uint8_t* data, size_t len, uint64_t base,
+                                              const std::vector<uint64_t>& bounds,
+                                              const std::vector<uint8_t>& key = {}, int threads = 0) {
+    const size_t n = bounds.size() > 1 ? bounds.size() - 1 : 0;
+    std::vector<Digest> out(n);
+    if (!n) return out;
+    const int rc = pbs_digest_chunks_host(data, len, base, bounds.data(), n, key.empty() ? nullptr : key.data(),
+                                          key.size(), out[0].data(), threads);
+    if (rc != PBS_OK) throw std::runtime_error(std::string("pbs_digest_chunks_host: ") + pbs_strerror(rc));
+    return out;
+}
+
+// The client's upload path over a whole host buffer (pbs_pipeline_host): chunk END
+// offsets (the tail included), the per-chunk digests and, with crc, the uncompressed
+// blobs' CRC-32s; copies to HBM, chunking and digests overlapped on the GPU and host cores.
+struct PipelineResult {
+    std::vector<uint64_t> ends;
+    std::vector<Digest> digests;
+    std::vector<uint32_t> crcs;
+    pbs_pipeline_timing timing;
+};
+inline PipelineResult pipeline_host(const uint8_t* data, size_t len, size_t avg, size_t piece = (size_t)1 << 30,
+                                    const std::vector<uint8_t>& key = {}, bool crc = true, int digest_cus = 64) {
+    // pbs_chunker_cuts_bound without a handle: every chunk but the tail >= max(avg / 4, 65)
+    const size_t cap = len / std::max<size_t>(avg >> 2, 65) + 4;
+    PipelineResult r;
+    r.ends.resize(cap);
+    r.digests.resize(cap);
+    if (crc) r.crcs.resize(cap);
+    size_t n = 0;
+    const int rc = pbs_pipeline_host(avg, data, len, piece, key.empty() ? nullptr : key.data(), key.size(),
+                                     digest_cus, r.ends.data(), r.digests[0].data(),
+                                     crc ? r.crcs.data() : nullptr, cap, &n, &r.timing);
+    if (rc == PBS_ERR_NOT_POW2) throw std::invalid_argument("chunk size is not a power of two");
+    if (rc != PBS_OK) throw std::runtime_error(std::string("pbs_pipeline_host: ") + pbs_strerror(rc));
+    r.ends.resize(n);
+    r.digests.resize(n);
+    if (crc) r.crcs.resize(n);
+    return r;
 }
 
 // DynamicIndexWriter (dynamic_index.rs:297-391): add_chunk(end offset, digest) per chunk,

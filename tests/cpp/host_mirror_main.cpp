@@ -9,6 +9,9 @@
 //   blob0 <hex>         first 16 bytes of the first chunk's uncompressed blob
 //   index <csum hex>    DynamicIndexWriter over the writer's chunks (host SHA-256
 //                       digests), written to $HOST_MIRROR_DIDX when set
+//   pipe <ends...>      pipeline_host over the buffer in `piece`-byte pieces
+//   pipedig <hex>       SHA-256 over the pipeline's digests in chunk order (and its crcs:
+//   pipecrc <crcs...>   the blob CRC-32s); hostdig <hex>: the same over digest_chunks_host
 // usage: host_mirror <avg> <len> <seed> <piece>   (input: splitmix64 random stream)
 #include <cstdio>
 #include <cstdlib>
@@ -101,6 +104,27 @@ int main(int argc, char** argv) {
         {
             pbs::Chunker c(avg);
             print("batch", c.find_cuts(data.data(), len, true));
+        }
+        {
+            const pbs::PipelineResult r = pbs::pipeline_host(data.data(), len, avg, piece);
+            print("pipe", r.ends);
+            std::vector<uint64_t> crcs(r.crcs.begin(), r.crcs.end());
+            print("pipecrc", crcs);
+            std::vector<uint8_t> all;
+            for (const auto& d : r.digests) all.insert(all.end(), d.begin(), d.end());
+            const pbs::Digest h = pbs::sha256(all.data(), all.size());
+            std::printf("pipedig ");
+            for (uint8_t b : h) std::printf("%02x", b);
+            std::printf("\n");
+            std::vector<uint64_t> bounds{0};
+            bounds.insert(bounds.end(), r.ends.begin(), r.ends.end());
+            const std::vector<pbs::Digest> hd = pbs::digest_chunks_host(data.data(), len, 0, bounds, {}, 3);
+            std::vector<uint8_t> all2;
+            for (const auto& d : hd) all2.insert(all2.end(), d.begin(), d.end());
+            const pbs::Digest h2 = pbs::sha256(all2.data(), all2.size());
+            std::printf("hostdig ");
+            for (uint8_t b : h2) std::printf("%02x", b);
+            std::printf("\n");
         }
         try {
             pbs::Chunker bad(avg + 1 == 2 ? 3 : avg + 1);

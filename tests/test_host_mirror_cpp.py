@@ -1,6 +1,7 @@
 """The C++ host mirror (proxmox-backup_amd/host/pbs_chunker.hpp): compiles against the
 C ABI on CPU; on the GPU its ChunkStream / DynamicChunkWriter / scan loop / find_cuts
 give the oracle's cut list."""
+import hashlib
 import os
 import subprocess
 
@@ -53,3 +54,10 @@ def test_host_mirror_matches_oracle(tmp_path, gpu, oracle, avg, n, piece):
     first = data[:int(wends[0])].tobytes()
     assert lines["blob0"][0] == oracle.blob_uncompressed(first)[:16].hex()
     assert open(didx, "rb").read() == ref_img
+    # pipeline_host (copy -> chunk -> digest + CRC) and digest_chunks_host over the buffer
+    pends = [int(x) for x in lines["pipe"]]
+    assert pends[:-1] == ref and pends[-1] == n
+    pb = np.concatenate([[0], np.array(pends, dtype=np.uint64)]).astype(np.uint64)
+    want = hashlib.sha256(oracle.chunk_digests(data, pb).tobytes()).hexdigest()
+    assert lines["pipedig"][0] == want and lines["hostdig"][0] == want
+    assert [int(x) for x in lines["pipecrc"]] == oracle.chunk_crcs(data, pb).tolist()
