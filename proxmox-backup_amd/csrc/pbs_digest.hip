@@ -883,9 +883,17 @@ struct HostStage {
         ev.clear();
     }
 };
-HostStage& host_stage() {
-    static HostStage* hs = new HostStage;  // never destroyed: HIP may be torn down first at exit
-    return *hs;
+// One stage per device (its streams and events belong to that device; calls on different
+// devices neither share a lock nor re-create each other's ring), created on first use and
+// never destroyed: HIP may be torn down first at exit.
+constexpr int kMaxStageDevices = 64;
+std::mutex g_stage_mu;
+HostStage* g_stages[kMaxStageDevices] = {};
+HostStage* host_stage(int dev) {
+    if (dev < 0 || dev >= kMaxStageDevices) return nullptr;
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    if (!g_stages[dev]) g_stages[dev] = new HostStage;
+    return g_stages[dev];
 }
 
 // SHA-256 of one device-resident chunk on this host thread: 4 MiB slices copied into the
@@ -1007,10 +1015,17 @@ bool hash_ring(HostStage& hs, size_t slots, size_t sb, const uint8_t* dev_data, 
 
 // Frees the hybrid digest's pinned host slices and their streams.
 extern "C" void pbs_digest_hybrid_release(void) {
-    HostStage& hs = host_stage();
-    std::lock_guard<std::mutex> lk(hs.mu);
-    hs.release();
-    hs.dev = -1;
+    for (int d = 0; d < kMaxStageDevices; ++d) {
+        HostStage* hs;
+        {
+            std::lock_guard<std::mutex> lk(g_stage_mu);
+            hs = g_stages[d];
+        }
+        if (!hs) continue;
+        std::lock_guard<std::mutex> lk(hs->mu);
+        hs->release();
+        hs->dev = -1;
+    }
     digest_pool().clear();
     known_pool().clear();
 }
@@ -1145,10 +1160,10 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
     if (rc == PBS_OK && h) {
         if (host_data) {
             pbs::sha256_host_items(host_data, base, bounds, work.data(), h, key, key_len, digests, threads);
-        } else {
-            HostStage& hs = host_stage();
+        } else if (HostStage* const hsp = host_stage(sdev)) {
+            HostStage& hs = *hsp;
             std::lock_guard<std::mutex> lk(hs.mu);
-            int dv = 0;
+            const int dv = sdev;
             const int t = (int)std::min<size_t>((size_t)threads, h);
             // whole chunks through the ring when a slot can hold the longest (always for the
             // reference's chunk sizes, <= 16 MiB); slots for four open chunks per thread + 8
@@ -1159,8 +1174,7 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
             const char* re = std::getenv("PBS_DIGEST_RING");  // 0: per-thread slices (tests, A/B)
             const bool use_ring = sb && slots >= 2 && !(re && re[0] == '0');
             bool waits = true;
-            if (hipStreamGetDevice(st, &dv) != hipSuccess ||
-                (use_ring ? !hs.ring_grow(dv, slots, sb) : !hs.grow(dv, t))) {
+            if (use_ring ? !hs.ring_grow(dv, slots, sb) : !hs.grow(dv, t)) {
                 fail(PBS_ERR_NOMEM);
             } else if (use_ring) {
                 waits = hipStreamWaitEvent(hs.cst[0], ready, 0) == hipSuccess &&
@@ -1193,6 +1207,8 @@ extern "C" int pbs_digest_chunks_hybrid(const uint8_t* dev_data, const uint8_t* 
                 for (auto& th : pool) th.join();
                 if (bad) fail(PBS_ERR_HIP);
             }
+        } else {
+            fail(PBS_ERR_NO_DEVICE);
         }
     }
     const HClock::time_point t_host1 = HClock::now();

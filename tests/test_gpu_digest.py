@@ -372,3 +372,39 @@ def test_hybrid_digest_vm_stream(gpu, oracle, torch_dev):
     got, tm = gpu.digest_chunks_hybrid(ptr, n, bounds, threads=8, host_mb_s=100)
     assert np.array_equal(got, want)
     assert tm["host_chunks"] > 0 and tm["gpu_chunks"] > 0
+
+
+def test_hybrid_digest_threads(gpu, oracle, torch_dev):
+    """Two threads run the hybrid digest at once on their own streams (the device's host
+    stage -- ring, copy streams -- is shared under its lock): every digest equal to the
+    oracle's."""
+    import threading
+
+    import torch
+
+    cases = []
+    for k in range(2):
+        data, bounds = _hybrid_case()
+        data = data.copy()
+        data[::4097] ^= np.uint8(k + 1)  # different bytes per thread
+        t, ptr = _dev(torch_dev, data)
+        cases.append((data, bounds, t, ptr, torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    got, errs = [None, None], []
+
+    def run(k):
+        data, bounds, t, ptr, s = cases[k]
+        try:
+            for _ in range(3):
+                got[k], _ = gpu.digest_chunks_hybrid(ptr, data.size, bounds, threads=2, host_min_len=1,
+                                                     hip_stream=s.cuda_stream)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(e)
+
+    ths = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    assert not errs, errs
+    for k in range(2):
+        data, bounds = cases[k][0], cases[k][1]
+        assert np.array_equal(got[k], oracle.chunk_digests(data, bounds))
