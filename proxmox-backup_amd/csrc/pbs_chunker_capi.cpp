@@ -174,6 +174,10 @@ struct pbs_chunker {
     uint64_t fused_min_avg = 0;
     int balance = 1;           // PBS_BALANCE=0: no priority trading between SIMD partners (A/B)
     bool direct_out = true;    // PBS_DIRECT_OUT=0: the multi-kernel resolve always copies its cuts (A/B)
+    // the direct resolve's one host sync: 1 = on the event behind its last kernel, 0 = the
+    // stream (PBS_SYNC_MODE, A/B: the event wait returned 10-20 us sooner per 64 GiB pass at
+    // 64 / 128 KiB, profiles/r04/scanpass/sync_ab.log)
+    int sync_mode = 1;
     int scan_dyn_env = -1;         // PBS_SCAN_DYN=0/1: force the static / dynamic tile order
     uint64_t fused_min_bytes = 0;  // smallest batch for the fused pass (PBS_FUSED_MIN_BYTES)  // smallest average served by the fused pass (PBS_FUSED_MIN_AVG: A/B)
     uint64_t susp_cap = 0, cand_cap = 0;
@@ -456,7 +460,10 @@ int resolve_direct(pbs_chunker* c, uint32_t m, const uint64_t* m_dev, uint32_t m
     HIP_TRY(c, launch_resolve_keep(c->d_C.as<uint64_t>(), m, small_dev + 4, keep_dev, kHostKeep, m_dev, m_base,
                                    c->stream));
     HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->sync_mode == 1)
+        HIP_TRY(c, hipEventSynchronize(c->ev[4]));
+    else
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (overflow && (*overflow = c->h_small[1] != 0)) return PBS_OK;
     const uint64_t mm = m_dev ? m_base + *m_host : m;
     const uint64_t ncut = r[0], s_open = r[1], idx = r[2], keep_over = r[3];
@@ -1555,6 +1562,7 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     c->fused_min_avg = kFusedMinAvg;
     if (const char* e = std::getenv("PBS_BALANCE")) c->balance = std::atoi(e);
     if (const char* e = std::getenv("PBS_DIRECT_OUT")) c->direct_out = e[0] != '0';
+    if (const char* e = std::getenv("PBS_SYNC_MODE")) c->sync_mode = std::atoi(e);
     if (const char* e = std::getenv("PBS_SCAN_DYN")) c->scan_dyn_env = e[0] == '1' ? 1 : 0;
     c->fused_min_bytes = kFusedMinBytes;
     if (const char* e = std::getenv("PBS_FUSED_MIN_BYTES")) c->fused_min_bytes = std::strtoull(e, nullptr, 0);
