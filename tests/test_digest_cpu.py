@@ -111,11 +111,13 @@ def test_host_chunk_digests(pbschunk, oracle, klen):
     assert np.array_equal(got, oracle.chunk_digests(data, bounds, key or b""))
 
 
+@pytest.mark.parametrize("lanes", ["1", "2", "3", "4"])
 @pytest.mark.parametrize("threads", [1, 3])
-def test_host_chunk_digests_lanes(pbschunk, oracle, threads):
-    """The host threads hash up to four chunks in step (sha256_host_lanes): lanes that end
-    at different blocks, refill from the list and run alone in 128 KiB steps; short and
-    long chunks interleaved, one and three threads."""
+def test_host_chunk_digests_lanes(pbschunk, oracle, threads, lanes, monkeypatch):
+    """The host threads hash up to four chunks in step (sha256_host_lanes; PBS_SHA_HOST_LANES
+    caps it, read per call): lanes that end at different blocks, refill from the list and
+    run alone in 128 KiB steps; short and long chunks interleaved, one and three threads."""
+    monkeypatch.setenv("PBS_SHA_HOST_LANES", lanes)
     rng = np.random.default_rng(12)
     lens = [int(v) for v in rng.integers(0, 300_000, 40)] + [0, 1, 63, 64, 65, 2 << 20, (3 << 20) + 5]
     rng.shuffle(lens)
