@@ -929,9 +929,10 @@ bool hash_from_device(const uint8_t* src, uint64_t len, const uint8_t* key, size
 }
 
 // The host share items[0..h) from HBM through the ring: one copier (this thread) copies
-// whole chunks into free slots back to back on `ncs` (1-2) copy streams in turn; `t` threads hash them as they land,
-// up to four in step each (pbs::sha256_host_lanes), and free their slots.  Every chunk must
-// fit a slot (sb bytes).  False on a HIP error (no copy in flight on return).
+// whole chunks into free slots back to back on `ncs` (1-2) copy streams in turn; `t`
+// threads hash them as they land, up to four in step each (pbs::sha256_host_lanes), and
+// free their slots.  Every chunk must fit a slot (sb bytes).  `bad` changes under qm, so no
+// wait misses it.  False on a HIP error (no copy in flight on return).
 bool hash_ring(HostStage& hs, size_t slots, size_t sb, const uint8_t* dev_data, uint64_t base,
                const uint64_t* bounds, const uint32_t* items, size_t h, const uint8_t* key, size_t key_len,
                uint8_t* digests, int t, int ncs) {
@@ -961,8 +962,13 @@ bool hash_ring(HostStage& hs, size_t slots, size_t sb, const uint8_t* dev_data, 
                 }
                 if (!block) return false;
                 g.unlock();
-                if (hipEventSynchronize(hs.rev[slot]) != hipSuccess) bad = true;
+                const bool ok = hipEventSynchronize(hs.rev[slot]) == hipSuccess;
                 g.lock();
+                if (!ok) {
+                    bad = true;  // (under the lock, then a wake-up: the copier may wait for a slot)
+                    qcv.notify_all();
+                    return false;
+                }
                 continue;
             }
             if (copies_done || !block) return false;
@@ -991,6 +997,7 @@ bool hash_ring(HostStage& hs, size_t slots, size_t sb, const uint8_t* dev_data, 
         if (hipMemcpyAsync(hs.ring + slot * sb, dev_data + (bounds[i] - base), bounds[i + 1] - bounds[i],
                            hipMemcpyDeviceToHost, hs.cst[k % ncs]) != hipSuccess ||
             hipEventRecord(hs.rev[slot], hs.cst[k % ncs]) != hipSuccess) {
+            std::lock_guard<std::mutex> g(qm);
             bad = true;
             break;
         }
