@@ -26,7 +26,8 @@
 //            (the blocks are encoded independently, so the decoder's repeat offsets at a
 //            block start are unknown to the encoder), else offset + 3.
 //
-// Parse (per 64 KiB block; 16 KiB sub-blocks = one GPU wave each, own hash table):
+// Parse (per 64 KiB block; eight ~8 KiB sub-blocks -- kSubA bytes for the first four,
+// kSubB for the last four -- one GPU wave each, own hash table):
 //   rounds of kRound positions sampled every `step` bytes (step 1 after a round with a
 //   match, doubling to kMaxStep without -- kHistMaxStep in the history before the
 //   sub-block, in rounds of kHistRound, whose last step the sub-block's first round keeps,
@@ -49,7 +50,14 @@
 namespace {
 
 constexpr uint32_t kBlock = 64 * 1024;
-constexpr uint32_t kSub = 8192;     // one GPU wave's sub-block
+// one GPU wave's sub-block: the first four 8 KiB + 384 bytes, the last four 8 KiB - 384
+constexpr uint32_t kSubA = 8192 + 384, kSubB = 8192 - 384;
+constexpr uint32_t sub_start(uint32_t w) { return w <= 4 ? w * kSubA : 4 * kSubA + (w - 4) * kSubB; }
+uint32_t sub_of(uint32_t pos) {  // the sub-block holding block position pos
+    uint32_t w = 0;
+    while (w < 7 && pos >= sub_start(w + 1)) ++w;
+    return w;
+}
 constexpr uint32_t kHist = 16384;   // window before a sub-block (reaches into the previous block)
 constexpr uint32_t kRound = 256, kHistRound = 512, kMaxStep = 8, kHistMaxStep = 32, kHistStep0 = 4;
 constexpr uint32_t kHashLog = 12, kCap = 32, kMinMatch = 5;
@@ -84,8 +92,8 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
     const uint8_t* const b = src - avail;  // positions P = p + avail
     const uint32_t N = avail + n;
     std::vector<uint32_t> table(1u << kHashLog);
-    for (uint32_t s0 = avail; s0 < N; s0 += kSub) {
-        const uint32_t se = std::min(s0 + kSub, N);
+    for (uint32_t w = 0; w < 8 && avail + sub_start(w) < N; ++w) {
+        const uint32_t s0 = avail + sub_start(w), se = std::min(avail + sub_start(w + 1), N);
         std::fill(table.begin(), table.end(), 0u);
         const uint32_t wlo = s0 - std::min(s0, kHist);  // the sub-block's window start
         // history: the window before the sub-block enters the table in rounds like the
@@ -807,8 +815,8 @@ std::vector<Coded> code_sequences(const std::vector<Seq>& s) {
     uint32_t rep[3] = {0, 0, 0};  // 0 = not known in this block
     uint32_t lit_end = 0, sub = 0;
     for (const Seq& e : s) {
-        if (e.pos / kSub != sub) {  // repeat offsets tracked per sub-block (one GPU lane each)
-            sub = e.pos / kSub;
+        if (sub_of(e.pos) != sub) {  // repeat offsets tracked per sub-block (one GPU lane each)
+            sub = sub_of(e.pos);
             rep[0] = rep[1] = rep[2] = 0;
         }
         Coded c;

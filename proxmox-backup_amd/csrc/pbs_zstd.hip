@@ -10,7 +10,8 @@
 //   stage   the block and up to 16 KiB of the chunk before it (the match window of its
 //           first sub-blocks) in LDS -- every later byte read is LDS;
 //   RLE     every byte equal: a 4-byte RLE block (the zero pages of a VM image);
-//   parse   each of the 8 waves parses one 8 KiB sub-block with its own 4096-entry table
+//   parse   each of the 8 waves parses one ~8 KiB sub-block (8 KiB + 384 bytes for waves
+//           0-3, - 384 for waves 4-7: see kZSubA) with its own 4096-entry table
 //           of 16-bit window positions: the 16 KiB before the sub-block first enter the
 //           table in accelerated rounds, then rounds of 256 sampled positions (step 1
 //           after a round with a match, doubling to 8 without): candidates = the table
@@ -64,7 +65,14 @@ using namespace zstd;
 
 constexpr int kZThreads = 512;
 constexpr int kZWaves = kZThreads / 64;
-constexpr uint32_t kZSub = 8192;     // one wave's sub-block
+// One wave's sub-block: waves 0-3 take 8 KiB + 384, waves 4-7 8 KiB - 384.  Waves w and
+// w + 4 share a SIMD and the issue arbiter favours the older one: with equal sub-blocks
+// waves 4-7 parsed ~9 % longer (text: 692 vs 756 us per block) whichever sub-blocks they
+// got (profiles/r04/zstd_swap/), and then ran alone on their SIMDs.
+constexpr uint32_t kZSubA = 8192 + 384, kZSubB = 8192 - 384;
+__device__ __host__ constexpr uint32_t zsub_start(int w) {  // block position of sub-block w (0..8)
+    return w <= 4 ? (uint32_t)w * kZSubA : 4 * kZSubA + (uint32_t)(w - 4) * kZSubB;
+}
 constexpr uint32_t kZHist = 16384;   // window before a sub-block
 constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8, kZHistMaxStep = 32,
                    kZHistStep0 = 4;  // the history rounds start at step 4 (1: pxar 1.038 -> 1.042 x libzstd, text 1.074 -> 1.079)
@@ -73,13 +81,13 @@ constexpr uint32_t kZHistRound = 512;  // history rounds (no walk: wider, fewer)
 constexpr int kZPerH = kZHistRound / 64;
 constexpr uint32_t kZTab = 1u << kZHashLog;
 constexpr uint32_t kZStageWords = (kZHist + kEncBlock) / 16 + 3;  // 16-byte words at any alignment + 2 zero words
-constexpr uint32_t kZSubSeq = kZSub / kZMin + 2;                  // sequences one sub-block can emit
+constexpr uint32_t kZSubSeq = kZSubA / kZMin + 2;                 // sequences one sub-block can emit
 constexpr uint32_t kZBlockSeq = kZWaves * kZSubSeq;
 constexpr uint64_t kSlot = kEncBlock + 1024;  // block header + up to 64 KiB + slack (section headers, flushes)
 constexpr uint32_t kHufStreams = 48 * 1024;  // Huffman streams staged in LDS (longer: raw literals)
 constexpr uint32_t kHufMax = 11;
 constexpr uint32_t kZRuns = 64;  // blocks with fewer sequences copy raw literals run by run
-static_assert(kEncBlock / kZSub == (uint32_t)kZWaves, "one sub-block per wave");
+static_assert(zsub_start(kZWaves) == kEncBlock && kZWaves == 8, "eight sub-blocks cover the block");
 static_assert(kZTab * 2 * kZWaves == 64 * 1024, "the tables fill the work area");
 
 // pbs-datastore/src/file_formats.rs:9, :12
@@ -921,10 +929,10 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
     PBS_GLOBAL uint32_t* const wseq_w = (PBS_GLOBAL uint32_t*)(wseq_g + (uint64_t)wave * kZSubSeq);
     const uint64_t t_in = probe ? wall_clock64() : 0;
     uint64_t t_hist = t_in;
-    const uint32_t s0 = hist + (uint32_t)wave * kZSub;
+    const uint32_t s0 = hist + zsub_start(wave);
     uint32_t ns = 0, lastend = 0;
     if (s0 < N) {
-        const uint32_t se = min(s0 + kZSub, N);
+        const uint32_t se = min(hist + zsub_start(wave + 1), N);
         const uint32_t wlo = s0 - min(s0, kZHist);
         uint16_t* const tw = tabs + wave * kZTab;
 #pragma unroll
