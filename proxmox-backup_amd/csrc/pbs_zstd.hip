@@ -800,27 +800,45 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
     const uint32_t seg = (m + 63) / 64;
     const uint32_t a = min(m, (uint32_t)lane * seg), b = min(m, a + seg);
     const uint32_t x0 = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
+    // kB steps a batch; the next batch's codes (and recorded states) are loaded before this
+    // batch's stores: loads and stores share one in-order counter, so loads issued after the
+    // stores would wait for them.  Loads past the segment read its last step (unused), so
+    // the loads are unconditional and the counter waits exact.
+    constexpr uint32_t kB = 8;
     auto run = [&](uint32_t x, bool stop_on_meet) -> uint32_t {  // returns the end state, ~0u: met
-        for (uint32_t j = a; j < b;) {
-            uint32_t c8[16], s8[16];
-            const uint32_t nj = min(16u, b - j);
+        if (a >= b) return x;
+        auto load = [&](uint32_t j, uint32_t (&c)[kB], uint32_t (&sv)[kB]) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u)  // 16 loads in flight (and the recorded states)
-                if ((uint32_t)u < nj) {
-                    c8[u] = (coded[ns - 2 - (j + u)].codes >> shift) & 0xFF;
-                    s8[u] = stop_on_meet ? states[j + u] : 0u;
-                }
+            for (int u = 0; u < (int)kB; ++u) {
+                const uint32_t jj = min(j + (uint32_t)u, b - 1);
+                c[u] = (coded[ns - 2 - jj].codes >> shift) & 0xFF;
+                sv[u] = stop_on_meet ? (uint32_t)states[jj] : 0u;
+            }
+        };
+        uint32_t cA[kB], sA[kB];
+        load(a, cA, sA);
+        for (uint32_t j = a;;) {
+            uint32_t cB[kB], sB[kB];
+            const uint32_t jn = j + kB;
+            const bool more = jn < b;
+            if (more) load(jn, cB, sB);
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-                if ((uint32_t)u < nj) {
-                    if (stop_on_meet && s8[u] == x) return ~0u;
+            for (int u = 0; u < (int)kB; ++u)
+                if (j + (uint32_t)u < b) {
+                    if (stop_on_meet && sA[u] == x) return ~0u;
                     states[j + u] = (uint16_t)x;
-                    const uint32_t sym = c8[u];
+                    const uint32_t sym = cA[u];
                     const uint32_t nb = (x + (uint32_t)t.dnb[sym]) >> 16;
                     chain[ns - 2 - (j + u)] = (x & ((1u << nb) - 1u)) | nb << 16;
                     x = t.next[(x >> nb) + t.dfs[sym]];
                 }
-            j += nj;
+            if (!more) break;
+#pragma unroll
+            for (int u = 0; u < (int)kB; ++u) {
+                cA[u] = cB[u];
+                sA[u] = sB[u];
+            }
+            j = jn;
         }
         return x;
     };
