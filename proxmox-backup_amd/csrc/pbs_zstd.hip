@@ -917,6 +917,34 @@ struct OrBits {
     }
 };
 
+// The same into words staged in LDS (ds_or: no global atomics, whose completion later loads
+// of the thread would wait for on the in-order memory counter)
+struct OrBitsL {
+    uint32_t* w;  // LDS
+    uint32_t wi;
+    uint64_t acc;
+    uint32_t n;
+    __device__ void init(uint32_t* words, uint32_t bit) {
+        w = words;
+        wi = bit >> 5;
+        n = bit & 31;
+        acc = 0;
+    }
+    __device__ void put(uint64_t v, uint32_t nb) {
+        acc |= (v & ((1ull << nb) - 1ull)) << n;  // nb <= 31
+        n += nb;
+        if (n >= 32) {
+            if ((uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
+            ++wi;
+            acc >>= 32;
+            n -= 32;
+        }
+    }
+    __device__ void done() {
+        if (n && (uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
+    }
+};
+
 // Two-queue Huffman merge (one lane): leaves 0..m-1 = the symbols sorted by (count,
 // symbol) (E.tw holds their sorted keys on entry), internal nodes m.. in creation order,
 // ties taking the leaf; parents in E.par, the root in ctl.root.
@@ -2098,7 +2126,54 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             const uint32_t sbytes = ns ? (T + flushb + 1 + 7) / 8 : 0u;
             const uint32_t body = lsz + hdr + sbytes;
             const bool ok = body < n;
-            if (ok && ns) {
+            const uint32_t lastw_l = ns ? (8u * (uint32_t)((uintptr_t)(lit_out + lsz + hdr) & 3u) + T + flushb) >> 5 : 0u;
+            if (ok && ns && lastw_l + 1 <= (uint32_t)(sizeof(E.streams) / 4)) {
+                // staged in LDS (the Huffman streams' buffer, free since the literal section was
+                // written), then stored as whole words; word 0 keeps the bytes before S0
+                uint8_t* const S0 = lit_out + lsz + hdr;
+                uint32_t* const A = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(S0) & ~(uintptr_t)3);
+                const uint32_t off0 = 8u * (uint32_t)(S0 - reinterpret_cast<uint8_t*>(A));
+                const uint32_t lastw = lastw_l;
+                uint32_t* const L = E.streams;
+                for (uint32_t wdx = tid; wdx <= lastw; wdx += kZThreads) L[wdx] = 0;
+                __syncthreads();
+                OrBitsL ob;
+                ob.init(L, off0 + (T - pt - st));
+                for (uint32_t q = q1; q-- > q0;) {
+                    const Coded x = coded[q];
+                    const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
+                    if (q + 1 < ns) {
+                        if (mode[1] != 1) {
+                            const uint32_t c = chains[kZBlockSeq + q];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                        if (mode[2] != 1) {
+                            const uint32_t c = chains[2 * kZBlockSeq + q];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                        if (mode[0] != 1) {
+                            const uint32_t c = chains[q];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                    }
+                    ob.put(x.ll - kLLBase[llc], kLLBits[llc]);
+                    ob.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
+                    ob.put(x.ofv - (1u << ofc), ofc);
+                }
+                ob.done();
+                if (tid == kZThreads - 1) {  // the final states (ML, OF, LL) and the end mark
+                    OrBitsL fb;
+                    fb.init(L, off0 + T);
+                    if (mode[2] != 1) fb.put(ctl.seq_last[2], (uint32_t)(mode[2] == 2 ? fse[2].log : pre[2].log));
+                    if (mode[1] != 1) fb.put(ctl.seq_last[1], (uint32_t)(mode[1] == 2 ? fse[1].log : pre[1].log));
+                    if (mode[0] != 1) fb.put(ctl.seq_last[0], (uint32_t)(mode[0] == 2 ? fse[0].log : pre[0].log));
+                    fb.put(1, 1);
+                    fb.done();
+                }
+                __syncthreads();
+                for (uint32_t wdx = tid; wdx <= lastw; wdx += kZThreads)
+                    A[wdx] = wdx ? L[wdx] : (off0 ? A[0] & ((1u << off0) - 1u) : 0u) | L[0];
+            } else if (ok && ns) {
                 uint8_t* const S0 = lit_out + lsz + hdr;
                 uint32_t* const A = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(S0) & ~(uintptr_t)3);
                 const uint32_t off0 = 8u * (uint32_t)(S0 - reinterpret_cast<uint8_t*>(A));
