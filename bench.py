@@ -136,14 +136,66 @@ def cpu_threads(args) -> int:
     return max(1, min(n, int(-(-quota // 1)))) if quota else n
 
 
+def cpu_mhz():
+    """Mean / min / max of the 'cpu MHz' lines of /proc/cpuinfo over the CPUs this process
+    may run on (None where the file has none)."""
+    try:
+        allowed = os.sched_getaffinity(0)
+        vals, cpu = [], None
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("processor"):
+                    cpu = int(ln.split(":")[1])
+                elif ln.startswith("cpu MHz") and cpu in allowed:
+                    vals.append(float(ln.split(":")[1]))
+        if vals:
+            return {"mean": round(sum(vals) / len(vals)), "min": round(min(vals)), "max": round(max(vals)),
+                    "cpus": len(vals)}
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
+class MhzSampler:
+    """cpu_mhz() sampled every 0.25 s on a thread while a CPU timing runs (the host's clock
+    under that load: a core sharing its SMT sibling, or held below turbo, shows here)."""
+
+    def __init__(self):
+        self.samples, self._stop = [], threading.Event()
+        self._th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.is_set():
+            m = cpu_mhz()
+            if m:
+                self.samples.append(m["mean"])
+            self._stop.wait(0.25)
+
+    def __enter__(self):
+        self._th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._th.join()
+
+    def summary(self):
+        v = self.samples
+        return {"mean": round(sum(v) / len(v)), "min": round(min(v)), "max": round(max(v)),
+                "samples": len(v)} if v else None
+
+
 def time_oracle(oracle, avg: int, sample, per: int, threads: int):
     """The oracle (gcc -O2 restatement of chunker.rs) on the host cores: one thread over
     sample[:per], then `threads` threads each over its own `per`-byte window of the
     shared read-only sample (windows start at different offsets: independent streams,
-    bounded memory).  Returns (1-thread GiB/s, aggregate GiB/s)."""
-    t0 = time.perf_counter()
+    bounded memory).  Returns (1-thread GiB/s, aggregate GiB/s, 1-thread CPU time / wall
+    time: below 1 when the thread was preempted or waited)."""
+    t0, c0 = time.perf_counter(), time.thread_time()
     oracle.chunk_feed(avg, sample[:per])
-    single = per / (1 << 30) / (time.perf_counter() - t0)
+    wall = time.perf_counter() - t0
+    single = per / (1 << 30) / wall
+    cpu_frac = (time.thread_time() - c0) / wall
     span = sample.size - per
     offs = [(t * span // max(1, threads)) // 4096 * 4096 for t in range(threads)]
     ths = [threading.Thread(target=oracle.chunk_feed, args=(avg, sample[o:o + per])) for o in offs]
@@ -151,7 +203,7 @@ def time_oracle(oracle, avg: int, sample, per: int, threads: int):
     [t.start() for t in ths]
     [t.join() for t in ths]  # ctypes releases the GIL
     agg = threads * per / (1 << 30) / (time.perf_counter() - t0)
-    return single, agg
+    return single, agg, cpu_frac
 
 
 def _oracle():
@@ -170,7 +222,8 @@ def cpu_baseline(args, workload, seed, avg):
            "vmimage": lambda n: oracle.gen_vmimage(n, seed, 0)}[workload]
     sample = gen(2 * per)
     threads = cpu_threads(args)
-    single, agg = time_oracle(oracle, avg, sample, per, threads)
+    with MhzSampler() as mhz:
+        single, agg, cpu_frac = time_oracle(oracle, avg, sample, per, threads)
     n, quota, model = cpu_info()
     out = {"value": round(agg, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
            "sample": f"{threads} threads x {args.cpu_sample_mib} MiB windows of one "
@@ -178,9 +231,14 @@ def cpu_baseline(args, workload, seed, avg):
                      f"whole-buffer scan loop (oracle/chunker_oracle.c, gcc -O2); 1 thread: "
                      f"{single:.3f} GiB/s; nproc {n}, os.cpu_count {os.cpu_count()}, cgroup "
                      f"quota {quota if quota is not None else 'none'} CPUs; host CPU: {model}",
-           "single_thread_gib_s": round(single, 3), "nproc": n, "cgroup_quota_cpus": quota}
+           "single_thread_gib_s": round(single, 3), "nproc": n, "cgroup_quota_cpus": quota,
+           # what makes two runs' baselines comparable (the single-thread rate
+           # moved 0.98 -> 1.61 GiB/s between round-end boxes with the same loop): the build,
+           # the host's clock during the timing, and whether the timed thread had its CPU
+           "oracle_build": oracle.build_info(), "cpu_mhz_during": mhz.summary(),
+           "single_thread_cpu_over_wall": round(cpu_frac, 3)}
     if threads != n and args.cpu_threads <= 0:  # the same at nproc threads, for the record
-        _, agg_n = time_oracle(oracle, avg, sample, 64 << 20, n)
+        _, agg_n, _ = time_oracle(oracle, avg, sample, 64 << 20, n)
         out["nproc_threads"] = {"threads": n, "value": round(agg_n, 3),
                                 "sample": f"{n} threads x 64 MiB windows of the same sample"}
     del sample
@@ -203,7 +261,7 @@ def cpu_config1(args):
         t0 = time.perf_counter()
         cuts = oracle.chunk_feed(avg, buf)
         one = buf.size / (1 << 30) / (time.perf_counter() - t0)
-        _, agg = time_oracle(oracle, avg, buf, 512 << 20, threads)
+        _, agg, _ = time_oracle(oracle, avg, buf, 512 << 20, threads)
         out[name] = {"1_thread": round(one, 3), "aggregate": round(agg, 3), "chunks": int(cuts.size)}
         del buf
     return out
@@ -732,6 +790,18 @@ def verdict(recs, extra=()) -> bool:
     return all(r.get("verified") is True for r in list(recs) + list(extra))
 
 
+def device_identity(torch, dev) -> dict:
+    """The GPU a rank ran on, as the runtime names it: PCI domain:bus:device, UUID, name --
+    an 8-rank line shows on its own that 8 distinct devices did the work."""
+    p = torch.cuda.get_device_properties(dev)
+    out = {"index": dev.index, "name": p.name, "arch": getattr(p, "gcnArchName", None)}
+    if hasattr(p, "pci_bus_id"):
+        out["pci"] = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{getattr(p, 'pci_device_id', 0):02x}"
+    if hasattr(p, "uuid"):
+        out["uuid"] = str(p.uuid)
+    return out
+
+
 def per_rank_records(rec: dict, dist, world: int):
     if dist is None:
         return [rec]
@@ -768,7 +838,10 @@ def standin_main(args, world: int, rank: int):
         c = oracle.chunk_feed(args.avg, buf)
         return np.append(c, np.uint64(size)) if size and (c.size == 0 or int(c[-1]) != size) else c
     elapsed, cuts = timed_steps(step, args, dist, lambda: None)
-    rec = {"rank": rank, "seed": seed, "elapsed_s": elapsed, "bytes": size,
+    import socket
+    rec = {"rank": rank, "seed": seed, "elapsed_s": elapsed, "bytes": size, "world_size": world,
+           "device": {"kind": "cpu-standin", "host": socket.gethostname(), "pid": os.getpid()},
+           "avg_launch_ms": round(elapsed / max(1, args.steps) * 1e3, 4),  # (an oracle pass)
            "chunks": int(cuts.size), **cut_record(cuts)}
     if args.verify:
         verify_record(rec, args.workload, size, args.avg, seed)
@@ -884,6 +957,11 @@ def main():
     # after the timed region: this rank's last timed cut list against the oracle's golden
     # record of the same stream (tests/golden/bench_cuts.json)
     rec = {"rank": rank, "seed": seed, "elapsed_s": round(elapsed, 6), "bytes": work_bytes,
+           "world_size": dist.get_world_size() if dist is not None else 1,
+           "device": device_identity(torch, dev),
+           # this rank's own kernel time (HIP events around the pass's launch), beside the
+           # line's roofline, which is rank 0's
+           "avg_launch_ms": round(float(np.mean(scan_ms)), 4) if scan_ms else None,
            "chunks": int(cuts.size), **cut_record(cuts)}
     if args.verify:
         verify_record(rec, args.workload, size, args.avg, seed)
@@ -963,7 +1041,7 @@ def main():
         out["blobs"] = blob_stage(args, buf, cuts, stream)
     if args.secondary_random and args.mode == "streams" and world == 1 and args.workload != "random":
         out["secondary_random"] = secondary_random(args, ch, buf, stream)
-    if args.cpu_baseline and world == 1:
+    if args.cpu_baseline:  # (rank 0 only: the other ranks have returned; after every timed region)
         del buf
         out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)
         if args.cpu_config1:

@@ -324,3 +324,10 @@ int64_t ora_chunk_generated(int kind, uint64_t seed, uint64_t avg, uint64_t len,
     }
     return (int64_t)n;
 }
+
+/* The compiler and flags this library was built with (bench.py's cpu_baseline records them
+ * beside its rates: a CPU baseline is only comparable across runs with the same build). */
+#ifndef ORA_CFLAGS
+#define ORA_CFLAGS "(unknown)"
+#endif
+const char *ora_build_info(void) { return "cc " __VERSION__ "; flags " ORA_CFLAGS; }

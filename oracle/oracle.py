@@ -81,6 +81,16 @@ class Chunker:
         return int(lib().ora_scan(self._buf, _ptr(a), a.size))
 
 
+def build_info() -> dict:
+    """The oracle library's compiler and flags (ora_build_info) and the SHA-256 of the .so."""
+    import hashlib
+    L = lib()
+    L.ora_build_info.restype = ctypes.c_char_p
+    with open(_LIB_PATH, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    return {"compiler_flags": L.ora_build_info().decode(), "so_sha256": sha[:16]}
+
+
 def chunk_feed(avg: int, data: np.ndarray, feed: int = 0) -> np.ndarray:
     """Chunk END offsets (exclusive) of every cut when the stream arrives in pieces of
     ``feed`` bytes (0 = whole buffer).  The tail is not included."""

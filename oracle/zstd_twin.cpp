@@ -27,20 +27,26 @@
 //            block start are unknown to the encoder), else offset + 3.
 //
 // Parse (per 64 KiB block; eight ~8 KiB sub-blocks -- kSubA bytes for the first four,
-// kSubB for the last four -- one GPU wave each, own hash table):
-//   rounds of kRound positions sampled every `step` bytes (step 1 after a round with a
-//   match, doubling to kMaxStep without -- kHistMaxStep in the history before the
-//   sub-block, in rounds of kHistRound, whose last step the sub-block's first round keeps,
-//   up to kMaxStep; a round starts at the end of a match that ran past the previous one, the
-//   positions inside it are not searched); per position the candidates are (a) the table
-//   (1 + the last position of an EARLIER round with the same hash of kHashBytes bytes),
-//   (b) the run candidate p - 1; lengths = common prefix capped at kCap (and the
-//   sub-block end), a candidate counts from kMinMatch bytes; the longer wins (ties: the
-//   table's).  The greedy walk from the current position takes the first position with a
-//   match; before it, the positions [cur, min(p, cur + 64)) are checked for a match at
-//   the sub-block's last offset (rep, >= kMinMatch), which wins when it starts earlier.
-//   A taken table match is extended backwards over the literals (at most 64 bytes); a
-//   capped match is extended forwards to its end (within the sub-block).
+// kSubB for the last four -- one GPU wave each, own hash table; round 5):
+//   history  every position of the kHist bytes before the sub-block enters the table (the
+//            table keeps 1 + the LAST position per hash of kHashBytes bytes);
+//   rounds   of kRound positions sampled every `step` bytes (step 1 after a round in which
+//            the walk took a match, doubling to kMaxStep without; a round starts at the end
+//            of a match that ran past the previous one, the positions inside it are not
+//            searched).  Per position p at or after the walk's position at the round start
+//            (`cur`), from state fixed at the round start only: the candidates are (a) the
+//            round-start repeat offset (the last match's offset; p - rep), (b) the table
+//            (the last position of an EARLIER round with the same hash), (c) the run
+//            candidate p - 1; a candidate counts from kMinMatch equal bytes.  The repeat
+//            candidate wins when it counts; else the longer of (b) and (c) within kCap (ties:
+//            the table's).  Its length is the common prefix capped at kCap (and the sub-block
+//            end); for (b) / (c) also how far the match extends backwards (at most kBack
+//            bytes, not before the window).
+//   walk     from `cur`, the first position with a match is taken: it starts up to its
+//            backward extension earlier (never before `cur`), a capped length is extended
+//            forwards to the match's end (within the sub-block), and `cur` moves to the
+//            match's end.  Nothing the walk does feeds back into the round's per-position
+//            data, so the GPU computes that data lane-parallel and walks with scalar steps.
 #include <stdint.h>
 
 #include <algorithm>
@@ -59,8 +65,8 @@ uint32_t sub_of(uint32_t pos) {  // the sub-block holding block position pos
     return w;
 }
 constexpr uint32_t kHist = 16384;   // window before a sub-block (reaches into the previous block)
-constexpr uint32_t kRound = 256, kHistRound = 512, kMaxStep = 8, kHistMaxStep = 32, kHistStep0 = 4;
-constexpr uint32_t kHashLog = 12, kCap = 32, kMinMatch = 5;
+constexpr uint32_t kRound = 256, kMaxStep = 8, kHistRound = 512, kHistMaxStep = 8, kHistStep0 = 1;
+constexpr uint32_t kHashLog = 12, kCap = 32, kMinMatch = 5, kBack = 8;
 constexpr uint32_t kHufStreams = 48 * 1024;  // largest Huffman stream bytes of a block
 
 // ------------------------------------------------------------------------ parse
@@ -88,7 +94,7 @@ inline uint32_t prefix(const uint8_t* s, uint32_t a, uint32_t b, uint32_t lim) {
 // src = the block (n bytes); src[-avail .. -1] = the chunk bytes before it
 uint64_t g_hist_inserts = 0;
 void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seqs) {
-    const uint32_t hb = 5;
+    const uint32_t hb = kMinMatch;
     const uint8_t* const b = src - avail;  // positions P = p + avail
     const uint32_t N = avail + n;
     std::vector<uint32_t> table(1u << kHashLog);
@@ -96,95 +102,89 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
         const uint32_t s0 = avail + sub_start(w), se = std::min(avail + sub_start(w + 1), N);
         std::fill(table.begin(), table.end(), 0u);
         const uint32_t wlo = s0 - std::min(s0, kHist);  // the sub-block's window start
-        // history: the window before the sub-block enters the table in rounds like the
-        // parse's (lookups before inserts; step 1 after a round in which some position's 5
-        // bytes equal its table or run candidate's, doubling to kHistMaxStep without)
+        // history: the window before the sub-block in rounds of kHistRound positions every
+        // `hs` bytes (inserts only; the table keeps the last position per hash); a round's
+        // first 64 positions look up their candidates before its inserts, and when one of
+        // them matches kMinMatch bytes (not a run of one byte) the next round steps 1, else
+        // the step doubles up to kHistMaxStep
         uint32_t hs = kHistStep0;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kHistRound * hs;
-            uint32_t pos[kHistRound], cand[kHistRound], np = 0;
-            for (uint32_t j = 0; j < kHistRound && r0 + j * hs < s0; ++j) pos[np++] = r0 + j * hs;
-            for (uint32_t k = 0; k < np; ++k) cand[k] = pos[k] + hb <= N ? table[hash5(b + pos[k])] : 0;
-            bool hit = false;
-            for (uint32_t k = 0; k < np; ++k) {
-                const uint32_t p = pos[k];
-                if (p + hb > N) continue;
-                uint32_t& t = table[hash5(b + p)];
-                if (p + 1 > t) t = p + 1;
-                // (5 equal bytes -- a run -- never count: runs need no dense history)
-                const bool run = rd32(b + p) == b[p] * 0x01010101u && b[p + 4] == b[p];
-                hit |= !run && cand[k] && std::memcmp(b + cand[k] - 1, b + p, 5) == 0;
+            uint32_t cand[64];
+            for (uint32_t j = 0; j < 64; ++j) {
+                const uint32_t p = r0 + j * hs;
+                cand[j] = p < s0 && p + hb <= N ? table[hash5(b + p)] : 0;
             }
-            g_hist_inserts += np;
-            hs = hit ? 1 : std::min(hs * 2, kHistMaxStep);
+            for (uint32_t j = 0; j < kHistRound; ++j) {
+                const uint32_t p = r0 + j * hs;
+                if (p >= s0) break;
+                if (p + hb <= N) {
+                    table[hash5(b + p)] = p + 1;
+                    ++g_hist_inserts;
+                }
+            }
+            bool hit = false;
+            for (uint32_t j = 0; j < 64; ++j) {
+                const uint32_t p = r0 + j * hs;
+                if (!cand[j]) continue;
+                const bool run = rd32(b + p) == b[p] * 0x01010101u && b[p + 4] == b[p];
+                hit |= !run && std::memcmp(b + cand[j] - 1, b + p, hb) == 0;
+            }
+            hs = hit ? 1 : std::min(2 * hs, kHistMaxStep);
         }
-        // the first rounds keep the history's step; rep 0: no offset in this sub-block yet
-        uint32_t cur = s0, step = std::min(hs, kMaxStep), rep = 0;
+        uint32_t cur = s0, step = std::min(hs, kMaxStep), rep = 0;  // rep 0: no offset in this sub-block yet
         for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
             rn = r0 + kRound * step;
-            uint32_t pos[kRound], cand[kRound], len[kRound], np = 0;
+            uint32_t pos[kRound], cand[kRound], len[kRound], msrc[kRound], back[kRound], np = 0;
             for (uint32_t j = 0; j < kRound && r0 + j * step < se; ++j) pos[np++] = r0 + j * step;
-            for (uint32_t k = 0; k < np; ++k) {
-                const uint32_t p = pos[k];
-                cand[k] = p + hb <= N ? table[hash5(b + p)] : 0;
-            }
+            for (uint32_t k = 0; k < np; ++k) cand[k] = pos[k] + hb <= N ? table[hash5(b + pos[k])] : 0;
             for (uint32_t k = 0; k < np; ++k) {
                 const uint32_t p = pos[k];
                 if (p + hb > N) continue;
                 uint32_t& t = table[hash5(b + p)];
                 if (p + 1 > t) t = p + 1;
             }
+            // per position, from the round-start state (cur, rep) only
             for (uint32_t k = 0; k < np; ++k) {
                 const uint32_t p = pos[k];
+                len[k] = 0;
+                if (p < cur || p + hb > se) continue;
                 const uint32_t lim = std::min(se - p, kCap);
-                uint32_t L = 0, R = 0;
-                if (cand[k]) L = prefix(b, cand[k] - 1, p, lim);
-                if (p > wlo) R = prefix(b, p - 1, p, lim);
-                if (L < kMinMatch) L = 0;
-                if (R >= kMinMatch && R > L) {
-                    L = R;
-                    cand[k] = p;  // 1 + (p - 1)
+                const bool mrep = rep && p >= wlo + rep && std::memcmp(b + p - rep, b + p, hb) == 0;
+                const bool mt = cand[k] && std::memcmp(b + cand[k] - 1, b + p, hb) == 0;
+                const bool mr = p > wlo && std::memcmp(b + p - 1, b + p, hb) == 0;
+                uint32_t s = 0, L = 0;
+                if (mrep) {
+                    s = p - rep;
+                } else if (mt && mr) {
+                    const uint32_t Lt = prefix(b, cand[k] - 1, p, lim), Lr = prefix(b, p - 1, p, lim);
+                    s = Lr > Lt ? p - 1 : cand[k] - 1;
+                } else if (mt) {
+                    s = cand[k] - 1;
+                } else if (mr) {
+                    s = p - 1;
+                } else {
+                    continue;
                 }
+                L = prefix(b, s, p, lim);
+                uint32_t e = 0;  // backwards (table and run candidates)
+                if (!mrep)
+                    while (e < kBack && s - e > wlo && b[p - 1 - e] == b[s - 1 - e]) ++e;
                 len[k] = L;
+                msrc[k] = s;
+                back[k] = e;
             }
+            // the walk
             bool found = false;
-            uint32_t k = 0;
-            for (;;) {
-                while (k < np && (pos[k] < cur || !len[k])) ++k;
-                // the hash match the walk would take next (none: the round's end)
-                const uint32_t ph = k < np ? pos[k] : std::min(rn, se);
-                uint32_t mpos = 0, msrc = 0, mlen = 0;
-                bool take = false;
-                if (rep && cur < ph) {  // rep check over [cur, min(ph, cur + 64))
-                    const uint32_t hi = std::min(ph, cur + 64);
-                    for (uint32_t x = cur; x < hi; ++x) {
-                        if (x < wlo + rep || x + kMinMatch > se) continue;
-                        const uint32_t L = prefix(b, x - rep, x, std::min(se - x, kCap));
-                        if (L >= kMinMatch) {
-                            mpos = x;
-                            msrc = x - rep;
-                            mlen = L;
-                            take = true;
-                            break;
-                        }
-                    }
-                }
-                if (!take) {
-                    if (k >= np) break;
-                    mpos = pos[k];
-                    msrc = cand[k] - 1;
-                    mlen = len[k];
-                    // catch-up over the literals before it (at most 64 bytes)
-                    for (uint32_t q = 0; q < 64 && mpos > cur && msrc > wlo && b[mpos - 1] == b[msrc - 1]; ++q) {
-                            --mpos;
-                            --msrc;
-                            ++mlen;
-                        }
-                }
-                // to its true end (a length under the cap already stopped at a mismatch)
-                while (mpos + mlen < se && b[msrc + mlen] == b[mpos + mlen]) ++mlen;
-                seqs.push_back({mpos - avail, mlen, mpos - msrc});
-                rep = mpos - msrc;
+            for (uint32_t k = 0; k < np; ++k) {
+                if (pos[k] < cur || !len[k]) continue;
+                const uint32_t p = pos[k], e = std::min(back[k], p - cur);
+                const uint32_t mpos = p - e, ms = msrc[k] - e;
+                uint32_t mlen = len[k] + e;
+                if (len[k] == kCap)  // to its true end (a shorter length already stopped there)
+                    while (mpos + mlen < se && b[ms + mlen] == b[mpos + mlen]) ++mlen;
+                seqs.push_back({mpos - avail, mlen, mpos - ms});
+                rep = mpos - ms;
                 cur = mpos + mlen;
                 found = true;
             }
@@ -929,6 +929,19 @@ size_t frame_header(uint8_t* o, uint64_t len) {
 extern "C" {
 
 uint64_t zstd_twin_hist_inserts(void) { return g_hist_inserts; }
+
+// The parse of one block (diagnostics: the GPU's PBS_ZSTD_DEBUG_ITEM dump is compared with
+// it): src = the block, src[-avail..-1] the chunk before it; {pos, ml, off} triples.
+uint64_t zstd_twin_parse(const uint8_t* src, uint32_t n, uint32_t avail, uint32_t* out, uint64_t cap) {
+    std::vector<Seq> s;
+    parse(src, n, avail, s);
+    for (size_t i = 0; i < s.size() && i < cap; ++i) {
+        out[3 * i] = s[i].pos;
+        out[3 * i + 1] = s[i].ml;
+        out[3 * i + 2] = s[i].off;
+    }
+    return s.size();
+}
 
 uint64_t zstd_twin_bound(uint64_t len) {
     const uint64_t nb = len ? (len + kBlock - 1) / kBlock : 1;

@@ -1583,10 +1583,12 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
             t[i] = rotl32(kBuzhashTable[i], kScanFrame == 1 ? prm.rot : prm.rot + 1);
             t[256 + i] = rotl32(kBuzhashTable[i], prm.rot);
         }
-        // landed before any launch on the handle's stream, which may be a non-blocking
-        // stream that does not wait for the null stream
-        ok = hipMemcpy(c->d_table.p, t, sizeof(t), hipMemcpyHostToDevice) == hipSuccess &&
-             hipStreamSynchronize(nullptr) == hipSuccess;
+        // landed before any launch: copied on the handle's own non-blocking stream and waited
+        // for there.  (Not the null stream: a null-stream copy waits for every blocking
+        // stream's work, e.g. the pipeline's resident digest queue grid, whose drain can in
+        // turn wait for this thread -- pbs_pipeline.cpp.)
+        ok = hipMemcpyAsync(c->d_table.p, t, sizeof(t), hipMemcpyHostToDevice, c->own_stream) == hipSuccess &&
+             hipStreamSynchronize(c->own_stream) == hipSuccess;
     }
     if (!ok) {
         destroy(c);

@@ -279,10 +279,15 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     // two workgroups (48 KiB LDS each) per digest CU.  The grid stays resident until the final
     // count -- nothing on this path may wait for the whole device meanwhile (the chunker's
     // buffers retire instead of hipFree, the CRC tables load on their own stream) -- or until
-    // PBS_PIPE_IDLE_MS (10 s) pass without a new job; it is launched again when jobs come
-    // after such an exit, and jobs it never took are hashed on the host at the end
+    // PBS_PIPE_IDLE_MS (50 ms) pass without a new job; it is launched again when jobs come
+    // after such an exit, and jobs it never took are hashed on the host at the end.  The
+    // queue's stream is a blocking one (CU-masked streams take no flags), so null-stream work
+    // of another thread waits for the grid while the grid waits for this thread's next
+    // publish, which may wait for that work (a blocking scan stream): the idle exit bounds
+    // such a cycle to 50 ms (round 4's 10 s turned it into a stall;
+    // tests/test_gpu_digest.py::test_pipeline_beside_null_stream_work)
     const int q_wgs = (int)env_u64("PBS_PIPE_QUEUE_WGS", (uint64_t)dig * 2);
-    const uint64_t q_idle = env_u64("PBS_PIPE_IDLE_MS", 10000) * 100000ull;  // wall_clock64: 100 MHz
+    const uint64_t q_idle = env_u64("PBS_PIPE_IDLE_MS", 50) * 100000ull;  // wall_clock64: 100 MHz
     uint64_t q_launches = 0;
     auto q_launch = [&]() {
         if (!q_running) return;

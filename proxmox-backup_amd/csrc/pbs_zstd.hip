@@ -74,11 +74,10 @@ __device__ __host__ constexpr uint32_t zsub_start(int w) {  // block position of
     return w <= 4 ? (uint32_t)w * kZSubA : 4 * kZSubA + (uint32_t)(w - 4) * kZSubB;
 }
 constexpr uint32_t kZHist = 16384;   // window before a sub-block
-constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8, kZHistMaxStep = 32,
-                   kZHistStep0 = 4;  // the history rounds start at step 4 (1: pxar 1.038 -> 1.042 x libzstd, text 1.074 -> 1.079)
-constexpr int kZPer = kZRound / 64;  // positions per lane and round
-constexpr uint32_t kZHistRound = 512;  // history rounds (no walk: wider, fewer)
-constexpr int kZPerH = kZHistRound / 64;
+constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8, kZBack = 8;
+constexpr uint32_t kZHistRound = 512, kZHistStep0 = 1, kZHistMaxStep = 8;  // history rounds (see parse_subblock)
+constexpr int kZPer = kZRound / 64;        // positions per lane and round
+constexpr int kZPerH = kZHistRound / 64;   // history positions per lane and round
 constexpr uint32_t kZTab = 1u << kZHashLog;
 constexpr uint32_t kZStageWords = (kZHist + kEncBlock) / 16 + 3;  // 16-byte words at any alignment + 2 zero words
 constexpr uint32_t kZSubSeq = kZSubA / kZMin + 2;                 // sequences one sub-block can emit
@@ -966,94 +965,96 @@ __device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) 
         ctl.root = nn - 1;
 }
 
-// The parse of one 8 KiB sub-block by ONE WAVE (wave w: window positions [s0, se)):
-// history rounds, then the rounds + greedy walk; the sequences go to wseq (block
-// positions); returns their count | the end of the last match (block position) << 32.
+// The parse of one ~8 KiB sub-block by ONE WAVE (wave w: window positions [s0, se)), the
+// twin's `parse` (oracle/zstd_twin.cpp) step for step:
+//   history  every position of [wlo, s0) enters the table, 8 per lane a step (insert only:
+//            the table keeps the last position per hash, whatever the order);
+//   rounds   of kZRound positions (lane l, slot i: r0 + (l + 64 i) step): the table lookups
+//            before this round's inserts, then per position -- from the walk's position `cur`
+//            and repeat offset `rep` at the round start only -- the candidate (the repeat
+//            offset when it matches kZMin bytes, else the longer of the table's and the run
+//            candidate p - 1), its length capped at kZCap and how far it extends backwards
+//            (<= kZBack bytes), packed into one VGPR per slot;
+//   walk     wave-uniform scalar steps over the round's match masks: the first match at or
+//            after cur is taken (started up to its backward extension earlier, never before
+//            cur), a capped one extended forwards to its end, cur moved to the end.  A step
+//            is a few scalar instructions and one readlane -- no LDS round trip, no ballot --
+//            except for a capped match.  (Round 4's walk measured every length, repeat match
+//            and backward extension inside the step: ~280 instructions and two LDS round trips
+//            per sequence, ~0.75 us.)
+// The sequences go to wseq (block positions, 64 at a time from lane registers); returns
+// their count | the end of the last match (block position) << 32.
 __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restrict__ tabs, Seq* __restrict__ wseq_g,
                                                 uint32_t hist, uint32_t N, int wave, int lane,
                                                 unsigned long long* probe) {
     PBS_GLOBAL uint32_t* const wseq_w = (PBS_GLOBAL uint32_t*)(wseq_g + (uint64_t)wave * kZSubSeq);
     const uint64_t t_in = probe ? wall_clock64() : 0;
     uint64_t t_hist = t_in;
-    const uint32_t s0 = hist + zsub_start(wave);
+    const uint32_t s0 = uni(hist + zsub_start(wave));
     uint32_t ns = 0, lastend = 0;
     if (s0 < N) {
-        const uint32_t se = min(hist + zsub_start(wave + 1), N);
-        const uint32_t wlo = s0 - min(s0, kZHist);
+        const uint32_t se = uni(min(hist + zsub_start(wave + 1), N));
+        const uint32_t wlo = uni(s0 - min(s0, kZHist));
         uint16_t* const tw = tabs + wave * kZTab;
 #pragma unroll
         for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<uint32_t*>(tw)[lane + 64 * i] = 0;
-        // history: accelerated rounds over [wlo, s0)
+        // history: [wlo, s0) in rounds of kZHistRound positions every hs bytes (inserts only);
+        // slot 0 (the round's first 64 positions) also looks up its candidates first: a
+        // kZMin-byte match (not a run of one byte) sets the next round's step to 1, else it
+        // doubles up to kZHistMaxStep (random bytes need no dense history)
         uint32_t hs = kZHistStep0;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kZHistRound * hs;
-            uint32_t h[kZPerH], t[kZPerH], wp[kZPerH], b4[kZPerH], lo[kZPerH], hi[kZPerH], o3[kZPerH];
+            uint32_t h[kZPerH], v[kZPerH], lo[kZPerH], hi[kZPerH], o3[kZPerH];
             bool ok[kZPerH];
-            // all the round's LDS reads in flight together (the scheduler would otherwise
-            // wait for each before issuing the next)
 #pragma unroll
             for (int i = 0; i < kZPerH; ++i) {
-                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * hs;
-                ok[i] = p < s0 && p + 5 <= N;
+                const uint32_t p = r0 + ((uint32_t)lane + 64u * (uint32_t)i) * hs;
+                ok[i] = p < s0 && p + kZMin <= N;
                 const uint32_t o = (ok[i] ? p : wlo) + W.r;
                 lo[i] = W.w[o >> 2];
                 hi[i] = W.w[(o >> 2) + 1];
                 o3[i] = o & 3;
+                v[i] = p - wlo + 1;
             }
             __builtin_amdgcn_sched_group_barrier(0x100, 2 * kZPerH, 0);  // the DS reads first
 #pragma unroll
-            for (int i = 0; i < kZPerH; ++i) {
-                b4[i] = (hi[i] >> (8 * o3[i])) & 0xFF;
-                wp[i] = __builtin_amdgcn_alignbyte(hi[i], lo[i], o3[i]);
-                h[i] = hash5(wp[i], b4[i]);
-                t[i] = tw[h[i]];
-            }
-            {
-                uint32_t v[kZPerH];
-#pragma unroll
-                for (int i = 0; i < kZPerH; ++i) v[i] = r0 + ((uint32_t)lane + 64 * i) * hs - wlo + 1;
-                tab_max_batch<kZPerH>(tw, h, v, ok);
-            }
-            // the candidates' words: all reads first
-            uint32_t cw[kZPerH], c4[kZPerH];
-#pragma unroll
-            for (int i = 0; i < kZPerH; ++i) {
-                const uint32_t c = ok[i] && t[i] ? wlo + t[i] - 1 : wlo;
-                const uint32_t o = c + W.r;
-                lo[i] = W.w[o >> 2];
-                hi[i] = W.w[(o >> 2) + 1];
-                o3[i] = o & 3;
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 * kZPerH, 0);
-            bool hit = false;
-#pragma unroll
-            for (int i = 0; i < kZPerH; ++i) {
-                c4[i] = (hi[i] >> (8 * o3[i])) & 0xFF;
-                cw[i] = __builtin_amdgcn_alignbyte(hi[i], lo[i], o3[i]);
-                const uint32_t b = wp[i] & 0xFF;
-                const bool run = wp[i] == b * 0x01010101u && b4[i] == b;
-                hit |= ok[i] && t[i] && !run && cw[i] == wp[i] && c4[i] == b4[i];
-            }
-            hs = __ballot(hit) ? 1 : min(2 * hs, kZHistMaxStep);
+            for (int i = 0; i < kZPerH; ++i)
+                h[i] = hash5(__builtin_amdgcn_alignbyte(hi[i], lo[i], o3[i]), (hi[i] >> (8 * o3[i])) & 0xFF);
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(hi[0], lo[0], o3[0]), b40 = (hi[0] >> (8 * o3[0])) & 0xFF;
+            const uint32_t t0 = ok[0] ? (uint32_t)tw[h[0]] : 0u;  // slot 0: before the inserts
+            tab_max_batch<kZPerH>(tw, h, v, ok);
+            uint32_t c4;
+            const uint32_t cw = W.word5(t0 ? wlo + t0 - 1 : wlo, c4);
+            const uint32_t b = w0 & 0xFF;
+            const bool run = w0 == b * 0x01010101u && b40 == b;
+            const bool hit = t0 && !run && cw == w0 && c4 == b40;
+            hs = uni(__ballot(hit) ? 1u : min(2 * hs, kZHistMaxStep));
         }
         if (probe) t_hist = wall_clock64();
-        // rounds + walk
-        // (the first rounds keep the history's step: no matches there, few here)
+        uint64_t t_walk = 0;
         uint32_t cur = s0, step = min(hs, kZMaxStep), lstep = 31 - __builtin_clz(step), rep = 0;
-        uint32_t rep_chk = 0;  // [cur, rep_chk) already tested for a repeat match: none there
         for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {
+            uint64_t tq = probe ? wall_clock64() : 0;
+            auto qmark = [&](int idx) {  // (probe: the round's parts)
+                if (probe) {
+                    const uint64_t t2 = wall_clock64();
+                    probe[idx] += t2 - tq;
+                    tq = t2;
+                }
+            };
             rn = r0 + kZRound * step;
-            uint32_t h[kZPer], t[kZPer], wp[kZPer], b4[kZPer], lo[kZPer], hi[kZPer], o3[kZPer], pm1[kZPer];
+            uint32_t P[kZPer], h[kZPer], t[kZPer], wp[kZPer], b4[kZPer], lo[kZPer], hi[kZPer], o3[kZPer], pm1[kZPer];
             bool okp[kZPer];
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
-                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
-                okp[i] = p < se && p + 5 <= N;
-                const uint32_t o = (okp[i] ? p : s0) + W.r;
+                P[i] = r0 + ((uint32_t)lane + 64u * (uint32_t)i) * step;
+                okp[i] = P[i] < se && P[i] + kZMin <= N;
+                const uint32_t o = (okp[i] ? P[i] : s0) + W.r;
                 lo[i] = W.w[o >> 2];
                 hi[i] = W.w[(o >> 2) + 1];
                 o3[i] = o & 3;
-                pm1[i] = W.byte(p > wlo && okp[i] ? p - 1 : s0);  // (the run candidate's first byte)
+                pm1[i] = W.byte(P[i] > wlo && okp[i] ? P[i] - 1 : s0);  // (the run candidate's first byte)
             }
             __builtin_amdgcn_sched_group_barrier(0x100, 3 * kZPer, 0);
 #pragma unroll
@@ -1066,192 +1067,220 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
             {
                 uint32_t v[kZPer];
 #pragma unroll
-                for (int i = 0; i < kZPer; ++i) v[i] = r0 + ((uint32_t)lane + 64 * i) * step - wlo + 1;
+                for (int i = 0; i < kZPer; ++i) v[i] = P[i] - wlo + 1;
                 tab_max_batch<kZPer>(tw, h, v, okp);
             }
-            // the table candidates' words: all reads first
+            qmark(43);
+            // the table's and the repeat offset's candidate words: all reads first
+            uint32_t clo[kZPer], chi[kZPer], co3[kZPer], rlo[kZPer], rhi[kZPer], ro3[kZPer];
+            bool rok[kZPer];
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
-                const uint32_t o = (t[i] ? wlo + t[i] - 1 : s0) + W.r;
-                lo[i] = W.w[o >> 2];
-                hi[i] = W.w[(o >> 2) + 1];
-                o3[i] = o & 3;
+                const uint32_t oc = (t[i] ? wlo + t[i] - 1 : s0) + W.r;
+                clo[i] = W.w[oc >> 2];
+                chi[i] = W.w[(oc >> 2) + 1];
+                co3[i] = oc & 3;
+                rok[i] = rep && okp[i] && P[i] >= wlo + rep;
+                const uint32_t orp = (rok[i] ? P[i] - rep : s0) + W.r;
+                rlo[i] = W.w[orp >> 2];
+                rhi[i] = W.w[(orp >> 2) + 1];
+                ro3[i] = orp & 3;
             }
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 * kZPer, 0);
-            // per position: its table candidate and which candidates match 5 bytes (bit 2i:
-            // the table's, 2i + 1: the run's p - 1); the lengths are measured by the walk,
-            // for the positions it takes only
-            uint32_t Cm[kZPer], F = 0;
+            __builtin_amdgcn_sched_group_barrier(0x100, 4 * kZPer, 0);
+            // per position: the candidate S (+ the run candidate as the alternative when the
+            // table's and the run's both match), from the round-start cur and rep only
+            uint32_t S[kZPer], lim[kZPer], L[kZPer], La[kZPer];
+            bool go[kZPer], goA[kZPer], both[kZPer], has[kZPer], isrep[kZPer];
+            bool anyA = false;
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const bool live = okp[i] && P[i] >= cur && P[i] + kZMin <= se;
+                const uint32_t c4 = (chi[i] >> (8 * co3[i])) & 0xFF;
+                const uint32_t cw = __builtin_amdgcn_alignbyte(chi[i], clo[i], co3[i]);
+                const bool mt = live && t[i] && cw == wp[i] && c4 == b4[i];
+                const uint32_t b = wp[i] & 0xFF;
+                const bool mr = live && P[i] > wlo && wp[i] == b * 0x01010101u && b4[i] == b && pm1[i] == b;
+                const uint32_t r4 = (rhi[i] >> (8 * ro3[i])) & 0xFF;
+                const uint32_t rw = __builtin_amdgcn_alignbyte(rhi[i], rlo[i], ro3[i]);
+                const bool mrep = live && rok[i] && rw == wp[i] && r4 == b4[i];
+                S[i] = mrep ? P[i] - rep : mt ? wlo + t[i] - 1 : P[i] - 1;
+                has[i] = mrep || mt || mr;
+                isrep[i] = mrep;
+                go[i] = has[i];
+                both[i] = !mrep && mt && mr;
+                goA[i] = both[i];
+                anyA |= goA[i];
+                lim[i] = has[i] ? min(se - P[i], kZCap) : 0u;
+                L[i] = lim[i];
+                La[i] = lim[i];
+            }
+            qmark(44);
+            // lengths: the common prefix from byte 4 on (bytes 0-4 are equal), a word a step,
+            // every slot's reads of a step issued together, until no lane goes on
+            const bool alt = __ballot(anyA) != 0;
+            for (uint32_t k = 4; k < kZCap; k += 4) {
+                uint32_t dx[kZPer], da[kZPer];
+#pragma unroll
+                for (int i = 0; i < kZPer; ++i) {
+                    const bool g = go[i] && k < lim[i];
+                    dx[i] = g ? W.word(S[i] + k) ^ W.word(P[i] + k) : 0u;
+                    da[i] = 0;
+                    if (alt) {
+                        const bool ga = goA[i] && k < lim[i];
+                        da[i] = ga ? W.word(P[i] - 1 + k) ^ W.word(P[i] + k) : 0u;
+                    }
+                }
+                bool more = false;
+#pragma unroll
+                for (int i = 0; i < kZPer; ++i) {
+                    if (go[i]) {
+                        if (k >= lim[i]) {
+                            go[i] = false;
+                        } else if (dx[i]) {
+                            L[i] = min(lim[i], k + ((uint32_t)__builtin_ctz(dx[i]) >> 3));
+                            go[i] = false;
+                        }
+                    }
+                    if (goA[i]) {
+                        if (k >= lim[i]) {
+                            goA[i] = false;
+                        } else if (da[i]) {
+                            La[i] = min(lim[i], k + ((uint32_t)__builtin_ctz(da[i]) >> 3));
+                            goA[i] = false;
+                        }
+                    }
+                    more |= go[i] || goA[i];
+                }
+                if (!__ballot(more)) break;
+            }
+            qmark(45);
+            // the choice, the backward extension (table and run candidates, at most kZBack
+            // bytes, never before the window) and the packed record per slot
+            uint32_t D[kZPer];
             unsigned long long m[kZPer];
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
-                const uint32_t p = r0 + ((uint32_t)lane + 64 * i) * step;
-                const bool live = p >= cur && p + 5 <= se;
-                const uint32_t c = t[i] ? wlo + t[i] - 1 : s0;
-                const uint32_t c4 = (hi[i] >> (8 * o3[i])) & 0xFF;
-                const uint32_t cw = __builtin_amdgcn_alignbyte(hi[i], lo[i], o3[i]);
-                const bool mt = live && t[i] && cw == wp[i] && c4 == b4[i];
-                // the run candidate p - 1 matches 5 bytes iff bytes p - 1 .. p + 4 are equal
-                const uint32_t b = wp[i] & 0xFF;
-                const bool mr = live && p > wlo && wp[i] == b * 0x01010101u && b4[i] == b && pm1[i] == b;
-                Cm[i] = c;
-                F |= (mt ? 1u : 0u) << (2 * i) | (mr ? 2u : 0u) << (2 * i);
-                m[i] = __ballot(mt || mr);
+                if (both[i] && La[i] > L[i]) {  // the run's is longer (ties: the table's)
+                    S[i] = P[i] - 1;
+                    L[i] = La[i];
+                }
+                uint32_t e = 0;
+                if (has[i] && !isrep[i]) {
+                    const uint32_t emax = min(kZBack, S[i] - wlo);
+                    if (S[i] >= 8) {
+                        const uint32_t x1 = W.word(P[i] - 4) ^ W.word(S[i] - 4);
+                        const uint32_t x2 = W.word(P[i] - 8) ^ W.word(S[i] - 8);
+                        e = x1 ? (uint32_t)__builtin_clz(x1) >> 3 : 4u + (x2 ? (uint32_t)__builtin_clz(x2) >> 3 : 4u);
+                    } else {
+                        while (e < emax && W.byte(P[i] - 1 - e) == W.byte(S[i] - 1 - e)) ++e;
+                    }
+                    e = min(e, emax);
+                }
+                D[i] = has[i] ? (S[i] - wlo) | L[i] << 16 | e << 24 : 0u;
+                m[i] = __ballot(has[i]);
             }
-            uint64_t t_walk = 0;
+            qmark(46);
             if (probe) {
                 t_walk = wall_clock64();
                 probe[33] += 1;  // rounds
             }
-            // the greedy walk (wave-uniform); bit q = position r0 + q * step
-            bool found = false;
-            // (the walk's state is wave-uniform: readfirstlane keeps it in SGPRs, so its
-            // branches are scalar)
-            uint32_t q = uni(cur > r0 ? (cur - r0 + step - 1) >> lstep : 0);
-            for (;;) {
-                cur = uni(cur);
-                rep = uni(rep);
-                uint32_t wi = q >> 6;
-                unsigned long long mm = 0;
-                for (; wi < (uint32_t)kZPer; ++wi) {
-                    mm = (wi == 0 ? m[0] : wi == 1 ? m[1] : wi == 2 ? m[2] : m[3]) &
-                         (wi == (q >> 6) ? (~0ull << (q & 63)) : ~0ull);
-                    if (mm) break;
-                }
-                const bool have = q < kZRound && mm != 0;
-                const int l = have ? __builtin_ctzll(mm) : 0;
-                const uint32_t ph = uni(have ? r0 + (wi * 64 + (uint32_t)l) * step : min(rn, se));
-                const uint32_t rep_hi = min(ph, cur + 64);  // the repeat test's window end
-#if PBS_ZV_NOREPCHK
-                rep_chk = 0;
-#endif
-                const bool rep_try = rep && rep_hi > max(cur, rep_chk);
-                if (!have && !rep_try) break;  // nothing left in this round
-                // every LDS read of the step issued before the first ballot: the repeat-match
-                // test over [cur, min(ph, cur + 64)), and for the hash match at ph the
-                // catch-up bytes before it and the first 256 bytes after its capped length
-                uint32_t hl = 0, hsrc = 0;
-                if (have) {
-                    const uint32_t Cw = wi == 0 ? Cm[0] : wi == 1 ? Cm[1] : wi == 2 ? Cm[2] : Cm[3];
-                    const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane((int)Cw, l);
-                    const uint32_t f = ((uint32_t)__builtin_amdgcn_readlane((int)F, l) >> (2 * wi)) & 3u;
-                    hl = 5;
-                    hsrc = f & 1u ? ct : ph - 1;
-                    if (f == 3u) {
-                        // both: the longer within the cap (and the sub-block) wins, ties the
-                        // table's -- lanes 0-7 measure the table's, 8-15 the run's, 4 bytes each
-                        const uint32_t lim = min(se - ph, kZCap);
-                        const uint32_t k = (uint32_t)lane & 7u;
-                        const uint32_t src = lane < 8 ? ct : ph - 1;
-                        const uint32_t x = ph + 4 * k;
-                        uint32_t mis = 4;
-                        if (lane < 16) {
-                            const uint32_t d = W.word(src + 4 * k) ^ W.word(x);
-                            if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
-                        }
-                        const unsigned long long bt = __ballot(lane < 8 && mis < 4);
-                        const unsigned long long br = __ballot(lane >= 8 && lane < 16 && mis < 4) >> 8;
-                        const uint32_t ft = bt ? (uint32_t)__builtin_ctzll(bt) : 8u;
-                        const uint32_t fr = br ? (uint32_t)__builtin_ctzll(br) : 8u;
-                        const uint32_t Lt = min(lim, 4 * ft + (bt ? (uint32_t)__builtin_amdgcn_readlane((int)mis, (int)ft) : 0u));
-                        const uint32_t Lr =
-                            min(lim, 4 * fr + (br ? (uint32_t)__builtin_amdgcn_readlane((int)mis, (int)(8 + fr)) : 0u));
-                        hsrc = Lr > Lt ? ph - 1 : ct;
-                        hl = Lr > Lt ? Lr : Lt;
-                    }
-                }
-                const uint32_t kk = (uint32_t)lane;
-                const uint32_t x = cur + kk;
-                const bool okx = rep_try && x < rep_hi && x >= rep_chk && x >= wlo + rep && x + 5 <= se;
-                const uint32_t xc = okx ? x : wlo + rep;
-                const uint32_t ra = W.word(xc), rbw = W.word(xc - rep), r4 = W.byte(xc + 4), r4b = W.byte(xc - rep + 4);
-                const bool okb = have && ph > cur + kk && hsrc > wlo + kk;
-                const uint32_t ba = W.byte(okb ? ph - 1 - kk : s0), bbv = W.byte(okb ? hsrc - 1 - kk : s0);
-                auto fwd_mis = [&](uint32_t src, uint32_t dst) {  // first mismatch of my 4 bytes (4: none)
-                    const uint32_t xf = dst + 4 * kk;
-                    uint32_t mis = 4;
-                    if (xf + 4 <= se) {
-                        const uint32_t d = W.word(src + 4 * kk) ^ W.word(xf);
-                        if (d) mis = (uint32_t)__builtin_ctz(d) >> 3;
-                    } else {
-                        mis = 0;
-                        while (xf + mis < se && W.byte(src + 4 * kk + mis) == W.byte(xf + mis)) ++mis;
-                    }
-                    return mis;
-                };
-                const uint32_t mis0 = have ? fwd_mis(hsrc + hl, ph + hl) : 0u;
-                const unsigned long long bal = __ballot(okx && ra == rbw && r4 == r4b);
-                uint32_t mpos, msrc, mlen;
-                bool ext;  // the forward extension continues from mpos + mlen
-                if (bal) {  // a repeat match
-                    mpos = cur + (uint32_t)__builtin_ctzll(bal);
-                    msrc = mpos - rep;
-                    mlen = 5;
-                    ext = true;
-                } else {
-                    rep_chk = uni(max(rep_chk, rep_hi));  // (no repeat match up to there)
-                    if (!have) break;
-                    const unsigned long long bb = __ballot(okb && ba == bbv);
-                    const uint32_t e = ~bb ? (uint32_t)__builtin_ctzll(~bb) : 64u;
-                    const unsigned long long bad = __ballot(mis0 < 4);
-                    mlen = hl;
-                    ext = !bad;
-                    if (bad) {
-                        const int f = __builtin_ctzll(bad);
-                        mlen += 4 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis0, f);
-                    } else {
-                        mlen += 256;
-                    }
-                    mpos = ph - e;
-                    msrc = hsrc - e;
-                    mlen += e;
-                }
-                // forwards to the end (within the sub-block): 16 bytes per lane a step, their
-                // word reads issued together (4 bytes a step took 16 dependent LDS round trips
-                // per zero page of a VM image)
-                auto fwd_mis16 = [&](uint32_t src, uint32_t dst) {  // first mismatch of my 16 bytes (16: none)
-                    const uint32_t xf = dst + 16 * kk, xs = src + 16 * kk;
-                    uint32_t mis = 16;
-                    if (xf + 16 <= se) {
-                        uint32_t d[4];
+            // the walk: wave-uniform scalar steps that only follow the chain -- the first match
+            // at or after cur, its end -- and mark the positions taken (T, bit l of slot i); the
+            // backward extension (bounded by the previous match's end) and a capped length's
+            // extension go to the position's lane (Ef, Lf).  Slot by slot, so each slot's mask
+            // and record register are named directly.
+            uint32_t Lf[kZPer], Ef[kZPer];
+            unsigned long long T[kZPer];
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) d[k] = W.word(xs + 4 * k) ^ W.word(xf + 4 * k);
-#pragma unroll
-                        for (int k = 3; k >= 0; --k)
-                            if (d[k]) mis = 4 * (uint32_t)k + ((uint32_t)__builtin_ctz(d[k]) >> 3);
-                    } else {
-                        mis = 0;
-                        while (xf + mis < se && W.byte(xs + mis) == W.byte(xf + mis)) ++mis;
-                    }
-                    return mis;
-                };
-                while (ext) {
-                    const uint32_t mis = fwd_mis16(msrc + mlen, mpos + mlen);
-                    const unsigned long long bad = __ballot(mis < 16);
-                    if (bad) {
-                        const int f = __builtin_ctzll(bad);
-                        mlen += 16 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
-                        break;
-                    }
-                    mlen += 1024;
-                }
-                mpos = uni(mpos);
-                msrc = uni(msrc);
-                mlen = uni(mlen);
-                if (lane == 0 && ns < kZSubSeq) {
-                    wseq_w[3 * ns] = mpos - hist;
-                    wseq_w[3 * ns + 1] = mlen;
-                    wseq_w[3 * ns + 2] = mpos - msrc;
-                }
-                ++ns;
-                rep = mpos - msrc;
-                rep_chk = 0;
-                cur = mpos + mlen;
-                lastend = cur - hist;
-                found = true;
-                q = uni((cur - r0 + step - 1) >> lstep);
+            for (int i = 0; i < kZPer; ++i) {
+                Lf[i] = L[i];
+                Ef[i] = 0;
             }
-            if (probe) probe[32] += wall_clock64() - t_walk;  // walk time
+            uint32_t q = uni(cur > r0 ? (cur - r0 + step - 1) >> lstep : 0);
+#pragma unroll
+            for (int wi = 0; wi < kZPer; ++wi) {
+                unsigned long long tk = 0;
+                while (q < 64u * (uint32_t)(wi + 1)) {
+                    const uint32_t qq = q > 64u * (uint32_t)wi ? q - 64u * (uint32_t)wi : 0u;
+                    const unsigned long long mm = m[wi] & (~0ull << qq);
+                    if (!mm) break;
+                    const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+                    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)D[wi], (int)l);
+                    uint32_t Lc = (d >> 16) & 0xFF;
+                    const uint32_t p = uni(r0 + ((64u * (uint32_t)wi + l) << lstep));
+                    const uint32_t e = min(d >> 24, p - cur);  // (cur: the previous match's end)
+                    if ((uint32_t)lane == l) Ef[wi] = e;
+                    if (Lc == kZCap) {
+                        // forwards to the end (within the sub-block): 16 bytes per lane a step,
+                        // their word reads issued together
+                        const uint32_t S0 = wlo + (d & 0xFFFF);
+                        const uint32_t kk = (uint32_t)lane;
+                        for (;;) {
+                            const uint32_t xf = p + Lc + 16 * kk, xs = S0 + Lc + 16 * kk;
+                            uint32_t mis = 16;
+                            if (xf + 16 <= se) {
+                                uint32_t dd[4];
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) dd[k] = W.word(xs + 4 * k) ^ W.word(xf + 4 * k);
+#pragma unroll
+                                for (int k = 3; k >= 0; --k)
+                                    if (dd[k]) mis = 4 * (uint32_t)k + ((uint32_t)__builtin_ctz(dd[k]) >> 3);
+                            } else {
+                                mis = 0;
+                                while (xf + mis < se && W.byte(xs + mis) == W.byte(xf + mis)) ++mis;
+                            }
+                            const unsigned long long bad = __ballot(mis < 16);
+                            if (bad) {
+                                const int f = __builtin_ctzll(bad);
+                                Lc += 16 * (uint32_t)f + (uint32_t)__builtin_amdgcn_readlane((int)mis, f);
+                                break;
+                            }
+                            Lc += 1024;
+                        }
+                        Lc = uni(Lc);
+                        if ((uint32_t)lane == l) Lf[wi] = Lc;
+                    }
+                    tk |= 1ull << l;
+                    cur = p + Lc;
+                    q = (cur - r0 + step - 1) >> lstep;
+                }
+                T[wi] = tk;
+            }
+            if (probe) {
+                const uint64_t t2 = wall_clock64();
+                probe[32] += t2 - t_walk;  // walk time
+                t_walk = t2;
+            }
+            // the sequences, every lane its taken positions, placed by their rank
+            const bool found = (T[0] | T[1] | T[2] | T[3]) != 0;
+            if (found) {
+                uint32_t base = ns;
+#pragma unroll
+                for (int i = 0; i < kZPer; ++i) {
+                    const bool tkn = (T[i] >> lane) & 1ull;
+                    const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(T[i] >> 32),
+                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)T[i], 0u));
+                    if (tkn && rank < kZSubSeq) {
+                        const uint32_t Si = wlo + (D[i] & 0xFFFF);
+                        PBS_GLOBAL uint32_t* const rec = wseq_w + 3 * rank;
+                        rec[0] = P[i] - Ef[i] - hist;
+                        rec[1] = Lf[i] + Ef[i];
+                        rec[2] = P[i] - Si;
+                    }
+                    base += (uint32_t)__builtin_popcountll(T[i]);
+                }
+                ns = uni(base);
+                // the repeat offset of the next round: the last taken match's
+                const int li = T[3] ? 3 : T[2] ? 2 : T[1] ? 1 : 0;
+                const unsigned long long Tl = li == 3 ? T[3] : li == 2 ? T[2] : li == 1 ? T[1] : T[0];
+                const uint32_t l = 63u - (uint32_t)__builtin_clzll(Tl);
+                const uint32_t Dl = li == 3 ? D[3] : li == 2 ? D[2] : li == 1 ? D[1] : D[0];
+                const uint32_t d = uni((uint32_t)__builtin_amdgcn_readlane((int)Dl, (int)l));
+                const uint32_t p = r0 + ((64u * (uint32_t)li + l) << lstep);
+                rep = uni(p - (wlo + (d & 0xFFFF)));
+                lastend = cur - hist;
+            }
+            if (probe) probe[42] += wall_clock64() - t_walk;  // sequence records
             step = found ? 1 : min(2 * step, kZMaxStep);
             lstep = 31 - __builtin_clz(step);
             if (cur > rn) rn = cur;  // positions inside a match that ran past the round: not searched
@@ -1657,6 +1686,10 @@ __device__ __noinline__ void rep_code_wave(const Ctl& ctl, const Seq* __restrict
 // lengths, 29 canonical codes, 30 description; 32/33 wave 0's walk ticks / rounds, 34 + w
 // wave w's parse.
 __device__ unsigned long long g_zprobe[48];
+// PBS_ZSTD_DEBUG_ITEM=k (diagnostics): the parse's sequences of item k -- per sub-block its
+// count, then its kZSubSeq {pos, ml, off} records -- copied out for a diff with the twin's
+// (zstd_twin_parse)
+__device__ uint32_t g_zdbg[kZWaves * (1 + 3 * kZSubSeq)];
 #define ZMARK(ph)                                  \
     do {                                           \
         if (probe) {                               \
@@ -1670,14 +1703,16 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, uint8_t* __restrict__ slots,
     uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch, Coded* __restrict__ coded_scratch,
-    uint32_t* __restrict__ chain_scratch, int probe_on) {
+    uint32_t* __restrict__ chain_scratch, int probe_on, int64_t dbg_item) {
     __shared__ uint4 stage[kZStageWords];
     __shared__ __attribute__((aligned(16))) uint8_t work[64 * 1024];
     __shared__ FseT fse[3];  // LL, OF, ML
     __shared__ FseT fse_huf;  // the Huffman description's scratch (beside the sequence tables)
     __shared__ PreT pre[3];  // the predefined tables, same order
     __shared__ Ctl ctl;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // (the wave index as a provably uniform value: everything derived from it -- a sub-block's
+    // bounds, the parse's walk state -- then lives in SGPRs and branches on the scalar unit)
+    const int tid = threadIdx.x, lane = tid & 63, wave = (int)uni((uint32_t)tid >> 6);
     const bool probe = probe_on && blockIdx.x == 0 && tid == 0;
     uint64_t tp = probe ? wall_clock64() : 0;
     uint16_t* const tabs = reinterpret_cast<uint16_t*>(work);
@@ -1781,6 +1816,13 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
         __syncthreads();
         ZMARK(1);
+        if ((int64_t)k == dbg_item) {
+            for (uint32_t i = tid; i < kZWaves * (1 + 3 * kZSubSeq); i += kZThreads) {
+                const uint32_t w2 = i / (1 + 3 * kZSubSeq), r2 = i % (1 + 3 * kZSubSeq);
+                g_zdbg[i] = r2 == 0 ? ctl.nseq[w2]
+                                    : reinterpret_cast<const uint32_t*>(wseq_all + (uint64_t)w2 * kZSubSeq)[r2 - 1];
+            }
+        }
 
         // ---- literals: bitmap of the unmatched bytes, literal index per thread range
         for (uint32_t i = tid; i < kEncBlock / 32; i += kZThreads) {
@@ -2417,13 +2459,27 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
             const char* e = std::getenv("PBS_ZSTD_PROBE");
             return e && e[0] == '1';
         }();
+        static const int64_t dbg_item = [] {
+            const char* e = std::getenv("PBS_ZSTD_DEBUG_ITEM");
+            return e ? (int64_t)std::strtoll(e, nullptr, 0) : (int64_t)-1;
+        }();
         if (compress && zprobe) {
             const unsigned long long z[48] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
         }
         if (compress)
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
-                               ni, z_slots, d_sizes, z_seqs, z_coded, z_chains, zprobe ? 1 : 0);
+                               ni, z_slots, d_sizes, z_seqs, z_coded, z_chains, zprobe ? 1 : 0, dbg_item);
+        if (compress && dbg_item >= 0) {
+            static uint32_t h[kZWaves * (1 + 3 * kZSubSeq)];
+            (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zdbg), sizeof h, 0, hipMemcpyDeviceToHost, st);
+            (void)hipStreamSynchronize(st);
+            if (const char* path = std::getenv("PBS_ZSTD_DEBUG_OUT"))
+                if (FILE* f = std::fopen(path, "wb")) {
+                    std::fwrite(h, sizeof h, 1, f);
+                    std::fclose(f);
+                }
+        }
         if (compress && zprobe) {
             unsigned long long h[48] = {};
             (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
@@ -2435,7 +2491,8 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
                          "literals %.1f seqstream %.1f end %.1f | wave 0: history %.1f rounds+walk %.1f | litmap: bitmap %.1f "
                          "sampled %.1f | roles: litmode %.1f repcode %.1f LLtable %.1f LLchain %.1f litsection %.1f | long LL "
                          "chains %llu: pass 1 %.1f rounds %.1f (%.2f rounds) | Huffman: rank %.1f merge %.1f lengths %.1f codes "
-                         "%.1f describe %.1f | wave 0 walk %.1f in %.1f rounds | parse by wave %.1f %.1f %.1f %.1f %.1f %.1f %.1f %.1f\n",
+                         "%.1f describe %.1f | wave 0 walk %.1f in %.1f rounds | parse by wave %.1f %.1f %.1f %.1f %.1f %.1f %.1f %.1f "
+                         "| wave 0 rounds: table %.1f candidates %.1f lengths %.1f pack %.1f records %.1f\n",
                          h[10], h[11] / nb, h[12] / nb, h[0] / nb / 100, h[1] / nb / 100, h[2] / nb / 100,
                          h[3] / nb / 100, h[4] / nb / 100, h[5] / nb / 100, h[6] / nb / 100, h[7] / nb / 100,
                          h[8] / nb / 100, h[9] / nb / 100, h[13] / nb / 100, h[14] / nb / 100, h[15] / nb / 100,
@@ -2444,7 +2501,8 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
                          h[25] ? h[23] / (double)h[25] / 100 : 0.0, h[25] ? h[24] / (double)h[25] : 0.0,
                          h[26] / nb / 100, h[27] / nb / 100, h[28] / nb / 100, h[29] / nb / 100, h[30] / nb / 100,
                          h[32] / nb / 100, h[33] / nb, h[34] / nb / 100, h[35] / nb / 100, h[36] / nb / 100,
-                         h[37] / nb / 100, h[38] / nb / 100, h[39] / nb / 100, h[40] / nb / 100, h[41] / nb / 100);
+                         h[37] / nb / 100, h[38] / nb / 100, h[39] / nb / 100, h[40] / nb / 100, h[41] / nb / 100,
+                         h[43] / nb / 100, h[44] / nb / 100, h[45] / nb / 100, h[46] / nb / 100, h[42] / nb / 100);
         }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);

@@ -82,6 +82,9 @@ def test_bench_launcher_two_ranks():
     recs = sorted(out["per_rank"], key=lambda r: r["rank"])
     assert [r["rank"] for r in recs] == [0, 1]
     assert recs[1]["seed"] == recs[0]["seed"] + 1
+    # every record names its world, its device (here the stand-in process) and its own time
+    assert all(r["world_size"] == 2 and r["avg_launch_ms"] > 0 for r in recs)
+    assert recs[0]["device"]["pid"] != recs[1]["device"]["pid"]
     mx = max(r["elapsed_s"] for r in recs)
     tot = sum(r["bytes"] for r in recs)
     assert out["value"] == pytest.approx(tot * 2 / (1 << 30) / mx, rel=1e-3)
@@ -228,6 +231,9 @@ def test_bench_share_gpu_rehearsal(oracle, mode):
     assert out["backend"] == "gloo"
     recs = sorted(out["per_rank"], key=lambda r: r["rank"])
     assert [r["rank"] for r in recs] == [0, 1]
+    for r in recs:  # device identity and the rank's own kernel time (one shared GPU here)
+        assert r["world_size"] == 2 and r["avg_launch_ms"] > 0
+        assert r["device"]["index"] == 0 and r["device"].get("pci")
     if mode == "streams":
         assert recs[1]["seed"] == recs[0]["seed"] + 1
         for r in recs:
@@ -269,6 +275,7 @@ def test_bench_rccl_world1(oracle, mode):
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["n_gpus"] == 1 and out["backend"] == "nccl"
     (r,) = out["per_rank"]
+    assert r["world_size"] == 1 and r["avg_launch_ms"] > 0 and r["device"].get("pci")
     assert r["bytes"] == size
     assert r["cuts"] == _oracle_cuts(oracle, "vmimage", r["seed"], size, 4 << 20)
     assert out["value"] == pytest.approx(size * 2 / (1 << 30) / r["elapsed_s"], rel=1e-2)

@@ -241,6 +241,73 @@ def test_pipeline_area_changes(gpu, oracle):
                 gpu.pipeline_host(data[:ln], 3 << 19, piece=5 << 20)
 
 
+def test_pipeline_queue_idle_exit(gpu, oracle, monkeypatch):
+    """The digest queue grid's idle exit (PBS_PIPE_IDLE_MS=0: a workgroup leaves as soon as
+    one poll finds no new job), its relaunch when the next piece publishes jobs, and the
+    end-of-call host hashing of jobs no grid claimed: digests and blob CRCs still equal the
+    oracle, and the run did relaunch the grid or leave jobs to the host (the paths round 4
+    left untested)."""
+    monkeypatch.setenv("PBS_PIPE_IDLE_MS", "0")
+    monkeypatch.setenv("PBS_PIPE_HOST_MIN", "0")  # every digest on the GPU queue
+    n = 48 * MiB + 5
+    data = gen_np.gen_vmimage(n, 0x5EED0003, 0)
+    ends, dig, crcs, t = gpu.pipeline_host(data, 256 << 10, piece=1 << 20, digest_cus=32, crc=True)
+    ref = oracle.chunk_feed(256 << 10, data)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    assert np.array_equal(ends, ref)
+    bounds = np.concatenate([[0], ref]).astype(np.uint64)
+    assert np.array_equal(dig, oracle.chunk_digests(data, bounds))
+    assert np.array_equal(crcs, oracle.chunk_crcs(data, bounds))
+    assert t["gpu_jobs"] == ref.size and t["host_chunks"] == 0
+    assert t["queue_launches"] > 1 or t["gpu_claimed"] < t["gpu_jobs"], t
+
+
+def test_pipeline_beside_null_stream_work(gpu, oracle, torch_dev):
+    """pbs_pipeline_host while another thread keeps issuing null-stream work (torch's
+    default stream, and new Chunker handles, whose table upload once went through the null
+    stream): the pipeline's resident queue grid sits on a blocking stream, so each such
+    operation waits for the grid, the grid for the main thread's next publish, and that
+    for a scan queued behind the null-stream work.  The idle exit (50 ms) breaks the cycle;
+    the call finishes in bounded time and the results equal the oracle."""
+    import threading
+    import time
+
+    torch = torch_dev
+    n = 96 * MiB + 3
+    data = gen_np.gen_vmimage(n, 0x5EED0003, 0)
+    gpu.pipeline_host(data[: 8 * MiB], 1 << 20, piece=2 << 20)  # warm-up (work area, code objects)
+    stop = threading.Event()
+    ops = [0]
+
+    def other():
+        x = torch.zeros(1 << 20, device="cuda")
+        while not stop.is_set():
+            with gpu.Chunker(64 << 10):
+                pass
+            x.add_(1)  # the default (null) stream
+            torch.cuda.current_stream().synchronize()
+            ops[0] += 1
+
+    th = threading.Thread(target=other)
+    th.start()
+    try:
+        t0 = time.perf_counter()
+        ends, dig, t = gpu.pipeline_host(data, 1 << 20, piece=2 << 20, digest_cus=32)
+        wall = time.perf_counter() - t0
+    finally:
+        stop.set()
+        th.join()
+    ref = oracle.chunk_feed(1 << 20, data)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    assert np.array_equal(ends, ref)
+    assert np.array_equal(dig, oracle.chunk_digests(data, np.concatenate([[0], ref]).astype(np.uint64)))
+    assert ops[0] > 0
+    # 48 pieces: with round 4's 10 s idle exit one such cycle alone took 10 s
+    assert wall < 8.0, (wall, ops[0], t)
+
+
 @pytest.mark.parametrize("prev", [0, 5, 40])
 def test_upload_stream_host(gpu, oracle, prev):
     """backup_writer.rs:638-700 end to end from a host buffer: cut list, digests, blob
