@@ -1086,7 +1086,6 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                 rhi[i] = W.w[(orp >> 2) + 1];
                 ro3[i] = orp & 3;
             }
-            __builtin_amdgcn_sched_group_barrier(0x100, 4 * kZPer, 0);
             // per position: the candidate S (+ the run candidate as the alternative when the
             // table's and the run's both match), from the round-start cur and rep only
             uint32_t S[kZPer], lim[kZPer], L[kZPer], La[kZPer];
@@ -1115,38 +1114,39 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                 La[i] = lim[i];
             }
             qmark(44);
-            // lengths: the common prefix from byte 4 on (bytes 0-4 are equal), a word a step,
-            // every slot's reads of a step issued together, until no lane goes on
+            // lengths: the common prefix from byte 4 on (bytes 0-4 are equal), 8 bytes a step
+            // (a lane done, or not matching, reads its own position on both sides), a slot only
+            // while one of its lanes goes on
             const bool alt = __ballot(anyA) != 0;
-            for (uint32_t k = 4; k < kZCap; k += 4) {
-                uint32_t dx[kZPer], da[kZPer];
-#pragma unroll
-                for (int i = 0; i < kZPer; ++i) {
-                    const bool g = go[i] && k < lim[i];
-                    dx[i] = g ? W.word(S[i] + k) ^ W.word(P[i] + k) : 0u;
-                    da[i] = 0;
-                    if (alt) {
-                        const bool ga = goA[i] && k < lim[i];
-                        da[i] = ga ? W.word(P[i] - 1 + k) ^ W.word(P[i] + k) : 0u;
-                    }
-                }
+            for (uint32_t k = 4; k < kZCap; k += 8) {
                 bool more = false;
 #pragma unroll
                 for (int i = 0; i < kZPer; ++i) {
+                    if (!__ballot(go[i] || goA[i])) continue;
+                    const bool g = go[i] && k < lim[i];
+                    const uint32_t sa = g ? S[i] + k : P[i], pa = g ? P[i] + k : P[i];
+                    const uint32_t d0 = W.word(sa) ^ W.word(pa), d1 = W.word(sa + 4) ^ W.word(pa + 4);
                     if (go[i]) {
                         if (k >= lim[i]) {
                             go[i] = false;
-                        } else if (dx[i]) {
-                            L[i] = min(lim[i], k + ((uint32_t)__builtin_ctz(dx[i]) >> 3));
+                        } else if (d0 | d1) {
+                            const uint32_t f = d0 ? (uint32_t)__builtin_ctz(d0) >> 3 : 4u + ((uint32_t)__builtin_ctz(d1) >> 3);
+                            L[i] = min(lim[i], k + f);
                             go[i] = false;
                         }
                     }
-                    if (goA[i]) {
-                        if (k >= lim[i]) {
-                            goA[i] = false;
-                        } else if (da[i]) {
-                            La[i] = min(lim[i], k + ((uint32_t)__builtin_ctz(da[i]) >> 3));
-                            goA[i] = false;
+                    if (alt) {
+                        const bool ga = goA[i] && k < lim[i];
+                        const uint32_t sb2 = ga ? P[i] - 1 + k : P[i], pb2 = ga ? P[i] + k : P[i];
+                        const uint32_t a0 = W.word(sb2) ^ W.word(pb2), a1 = W.word(sb2 + 4) ^ W.word(pb2 + 4);
+                        if (goA[i]) {
+                            if (k >= lim[i]) {
+                                goA[i] = false;
+                            } else if (a0 | a1) {
+                                const uint32_t f = a0 ? (uint32_t)__builtin_ctz(a0) >> 3 : 4u + ((uint32_t)__builtin_ctz(a1) >> 3);
+                                La[i] = min(lim[i], k + f);
+                                goA[i] = false;
+                            }
                         }
                     }
                     more |= go[i] || goA[i];
@@ -1177,8 +1177,9 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                     e = min(e, emax);
                 }
                 D[i] = has[i] ? (S[i] - wlo) | L[i] << 16 | e << 24 : 0u;
-                m[i] = __ballot(has[i]);
             }
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) m[i] = __ballot(has[i]);
             qmark(46);
             if (probe) {
                 t_walk = wall_clock64();
@@ -1209,8 +1210,8 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                     uint32_t Lc = (d >> 16) & 0xFF;
                     const uint32_t p = uni(r0 + ((64u * (uint32_t)wi + l) << lstep));
                     const uint32_t e = min(d >> 24, p - cur);  // (cur: the previous match's end)
-                    if ((uint32_t)lane == l) Ef[wi] = e;
-                    if (Lc == kZCap) {
+                    asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(Ef[wi]) : "s"(e), "{m0}"(l));
+                    if (__builtin_expect(Lc == kZCap, 0)) {
                         // forwards to the end (within the sub-block): 16 bytes per lane a step,
                         // their word reads issued together
                         const uint32_t S0 = wlo + (d & 0xFFFF);
@@ -1238,7 +1239,7 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                             Lc += 1024;
                         }
                         Lc = uni(Lc);
-                        if ((uint32_t)lane == l) Lf[wi] = Lc;
+                        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(Lf[wi]) : "s"(Lc), "{m0}"(l));
                     }
                     tk |= 1ull << l;
                     cur = p + Lc;
