@@ -77,6 +77,14 @@ def parse():
                     help="also time the host-stream pipeline (copy -> chunk -> SHA-256 per chunk, "
                          "pbs_pipeline_host) over this many GiB of a pageable host copy of the "
                          "stream, with the oracle + hashlib on the host cores beside it")
+    ap.add_argument("--upload-gib", type=float, default=0.0,
+                    help="also time the client's upload path with compression (pbs_upload_stream_host: "
+                         "copy -> chunk -> SHA-256 -> known-chunk test -> zstd blobs of the new chunks -> "
+                         "blobs in host memory) over this many GiB, beside the host cores' oracle chunker + "
+                         "hashlib + libzstd level 1 + zlib.crc32")
+    ap.add_argument("--upload-corpus", choices=["stream", "text", "pxar"], default="stream",
+                    help="the upload stage's bytes: the bench stream, or a seeded text-like / pxar-like "
+                         "corpus (tests/corpus_gen.py, 32 MiB tiled)")
     ap.add_argument("--verify", type=int, default=1,
                     help="1: after the timed region compare every rank's cut list (and the "
                          "secondary line's) with tests/golden/bench_cuts.json (oracle-made) and "
@@ -627,6 +635,114 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
                              "sample": f"{nth} x 256 MiB slices: chunk_feed then sha256 + crc32 per chunk"}}
 
 
+def upload_stage(args, buf, piece: int = 1 << 30):
+    """backup_writer.rs:631-706 with compress = true (proxmox-backup-client main.rs:1011-1016)
+    from a pageable host buffer to the new chunks' blobs in (pinned) host memory, through
+    pbs_upload_stream_host; the CPU path beside it over a bounded sample: the oracle
+    chunker, hashlib SHA-256, libzstd level 1 (the reference's compressor, data_blob.rs:151;
+    the image's 1.4.8) and zlib.crc32 per chunk on the host cores."""
+    import hashlib
+    import zlib
+
+    import numpy as np
+    import torch
+
+    import pbschunk
+
+    oracle = _oracle()
+    n = int(args.upload_gib * (1 << 30)) // 8 * 8
+    if args.upload_corpus == "stream":
+        host = buf[:n].cpu().numpy()
+        what = f"{args.workload} stream (seed {hex(SEEDS[args.workload])})"
+    else:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import corpus_gen
+        base = {"text": lambda: corpus_gen.text(32 << 20, 21), "pxar": lambda: corpus_gen.pxar(32 << 20, 22)}[
+            args.upload_corpus]()
+        host = np.tile(base, -(-n // base.size))[:n]
+        # every 4 KiB page of every tile but the first stamped with its page number (8 bytes
+        # at the page start): the tiles stop repeating each other's chunks, so the known-chunk
+        # test finds no duplicates and every chunk is compressed, at ~0.2 % of the bytes
+        pages = host[base.size:].reshape(-1)[: (n - base.size) // 4096 * 4096].reshape(-1, 4096)
+        pages[:, :8] = np.arange(1, pages.shape[0] + 1, dtype="<u8").view(np.uint8).reshape(-1, 8)
+        what = (f"{args.upload_corpus}-like corpus (tests/corpus_gen.py seed {21 if args.upload_corpus == 'text' else 22}, "
+                f"32 MiB tiled, every later 4 KiB page stamped with its number)")
+    # the bench stream's HBM goes (the last stage): a 64 GiB upload holds the stream copy,
+    # the blob slots and the blobs in HBM at once
+    buf.set_()
+    torch.cuda.empty_cache()
+    pbschunk.blob_encode_release()
+    pbschunk.pipeline_release()
+    cap = n // max(args.avg >> 2, 65) + 4
+    blobs = torch.empty(12 * cap + n, dtype=torch.uint8, pin_memory=True).numpy()
+    cold = pbschunk.upload_stream_host(host, args.avg, piece=piece, blobs_out=blobs)  # allocations
+    t0 = time.perf_counter()
+    out = pbschunk.upload_stream_host(host, args.avg, piece=piece, blobs_out=blobs)
+    wall = time.perf_counter() - t0
+    same = (np.array_equal(cold["ends"], out["ends"]) and np.array_equal(cold["digests"], out["digests"])
+            and np.array_equal(cold["blob_offsets"], out["blob_offsets"]))
+    del cold
+    cuts = None
+    if args.upload_corpus == "stream":
+        cuts = verify_record({"chunks": int(out["ends"].size), **cut_record(out["ends"], keep=0)}, args.workload,
+                             n, args.avg, SEEDS[args.workload])
+    # the first new chunks' blobs against the host twin's (oracle.blob_compressed), and their
+    # zstd payloads through libzstd
+    checked = 0
+    offs = out["blob_offsets"]
+    for i in np.flatnonzero(out["known"] == 0)[:3]:
+        s0 = int(out["ends"][i - 1]) if i else 0
+        chunk = host[s0:int(out["ends"][i])].tobytes()
+        ln = len(chunk)
+        blob = out["blobs"][int(offs[i]):int(offs[i + 1])].tobytes()
+        assert blob == oracle.blob_compressed(chunk), f"upload blob at {s0} differs from the twin's"
+        if blob[:8] == oracle.COMPRESSED_BLOB_MAGIC:
+            assert oracle.zstd_decompress(blob[12:], ln) == chunk
+        checked += 1
+    t = out["timing"]
+    # CPU path: every thread chunks its own slice, then SHA-256 + libzstd-1 + CRC per chunk
+    L = oracle.libzstd()
+    threads = cpu_threads(args)
+    per = 128 << 20
+    nth = min(threads, max(1, n // per))
+
+    def work(k):
+        sl = np.ascontiguousarray(host[k * per:(k + 1) * per])
+        cc = oracle.chunk_feed(args.avg, sl)
+        b = np.concatenate([[0], cc, [sl.size]]).astype(np.int64)
+        mv = memoryview(sl)
+        dst = np.empty(L.ZSTD_compressBound(int(np.diff(b).max())), np.uint8)
+        for i in range(b.size - 1):
+            if b[i + 1] > b[i]:
+                hashlib.sha256(mv[b[i]:b[i + 1]]).digest()
+                r = L.ZSTD_compress(dst.ctypes.data, dst.size, sl.ctypes.data + int(b[i]), int(b[i + 1] - b[i]), 1)
+                zlib.crc32(memoryview(dst)[:r])
+
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(nth)]
+    c0 = time.perf_counter()
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    cpu = nth * per / (1 << 30) / (time.perf_counter() - c0)
+    st = out["stats"]
+    return {"metric": "GiB/s host stream -> chunks + SHA-256 + known-chunk test + compressed blobs of the new "
+                      "chunks in host memory (end to end, backup_writer.rs:631-706 with compress = true)",
+            "value": round(n / (1 << 30) / wall, 3), "wall_ms": round(wall * 1e3, 2), "bytes": n, "data": what,
+            "piece": piece,
+            "chunks": int(out["ends"].size), "cuts": cuts, "same_result_as_first_call": same,
+            "blobs_checked_against_twin": checked,
+            "upload_stats": st, "compressed_over_new": round(st["size_compressed"] / max(1, st["size"] - st["size_reused"]), 4),
+            "compressed_chunks": t["compressed_chunks"],
+            "pipeline_detail_ms": {k: (round(v, 2) if isinstance(v, float) else v) for k, v in t["pipe"].items()},
+            "timing_ms": {"total": round(t["total_ms"], 2), "pipeline": round(t["pipe"]["total_ms"], 2),
+                          "h2d": round(t["pipe"]["h2d_ms"], 2), "known": round(t["known_ms"], 2),
+                          "encode": round(t["encode_ms"], 2), "blobs_d2h": round(t["d2h_ms"], 2),
+                          "zstd_blocks": round(t["blob"]["compress_ms"], 2)},
+            "cpu_baseline": {"value": round(cpu, 3), "unit": "GiB/s", "cores": nth,
+                             "kind": "port (oracle chunker) + hashlib + libzstd level 1 + zlib.crc32",
+                             "libzstd_version": int(L.ZSTD_versionNumber()),
+                             "sample": f"{nth} x {per >> 20} MiB slices: chunk_feed then sha256 + zstd-1 + crc32 per chunk"}}
+
+
 def free_port() -> int:
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -1041,6 +1157,8 @@ def main():
         out["blobs"] = blob_stage(args, buf, cuts, stream)
     if args.secondary_random and args.mode == "streams" and world == 1 and args.workload != "random":
         out["secondary_random"] = secondary_random(args, ch, buf, stream)
+    if args.upload_gib > 0 and args.mode == "streams" and world == 1:
+        out["upload"] = upload_stage(args, buf)  # (last GPU stage: it frees the bench stream)
     if args.cpu_baseline:  # (rank 0 only: the other ranks have returned; after every timed region)
         del buf
         out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)
@@ -1049,6 +1167,8 @@ def main():
     extra = [out["secondary_random"]] if "secondary_random" in out else []
     if "pipeline" in out and out["pipeline"]["cuts"]["verified"] is not None:  # a golden stream length
         extra.append(out["pipeline"]["cuts"])
+    if "upload" in out and out["upload"]["cuts"] and out["upload"]["cuts"]["verified"] is not None:
+        extra.append(out["upload"]["cuts"])
     if args.verify:
         # every timed cut list (each rank's, the secondary line's) equals the oracle's
         out["verified"] = verdict(recs, extra)

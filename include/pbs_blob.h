@@ -79,6 +79,13 @@ int pbs_blob_encode_chunks_device(const uint8_t *dev_data, size_t data_len, uint
                                   size_t blobs_cap, uint64_t *blob_offsets, uint32_t *crcs,
                                   uint8_t *compressed, pbs_blob_encode_timing *timing,
                                   void *hip_stream);
+/* The same for chunks given as spans: chunk i = [spans[2i], spans[2i+1]) (host, absolute
+ * offsets in any order, gaps allowed -- e.g. the new chunks of an upload stream). */
+int pbs_blob_encode_spans_device(const uint8_t *dev_data, size_t data_len, uint64_t base,
+                                 const uint64_t *spans, size_t n, int compress, uint8_t *blobs_dev,
+                                 size_t blobs_cap, uint64_t *blob_offsets, uint32_t *crcs,
+                                 uint8_t *compressed, pbs_blob_encode_timing *timing,
+                                 void *hip_stream);
 /* Frees the device scratch pbs_blob_encode_chunks_device keeps between calls. */
 void pbs_blob_encode_release(void);
 /* 12 n + (bounds[n] - bounds[0]): the largest blob stream of n chunks. */

@@ -25,6 +25,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "pbs_blob.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -144,6 +146,38 @@ int pbs_pipeline_host(size_t avg, const uint8_t *host, size_t len, size_t piece,
                       const uint8_t *key, size_t key_len, int digest_cus, uint64_t *ends,
                       uint8_t *digests, uint32_t *crcs, size_t cap, size_t *n_out,
                       pbs_pipeline_timing *timing);
+
+/* The client's upload of one dynamic-index stream up to the network
+ * (pbs-client/src/backup_writer.rs:631-706, upload_chunk_info_stream, with
+ * proxmox-backup-client's `compress: true`, main.rs:1011-1016): pbs_pipeline_host's chunks
+ * and digests, then on the GPU from the same HBM copy the known-chunk test
+ * (pbs_known_chunks_device: `known`, 32 n_known bytes sorted ascending = the previous
+ * index's digests, :524-547; and repeats of earlier chunks of this stream, :697) and the
+ * blob of every new chunk, `DataChunkBuilder::new(data).compress(compress).build()`
+ * (:671, :698; DataBlob::encode, pbs-datastore/src/data_blob.rs:139-176 -- the zstd frame
+ * of include/pbs_blob.h, parity of its bytes unpinned).  Writes `ends`, `digests`,
+ * `is_known` (n bytes), the blobs back to back into `blobs` (host, blobs_cap >= 12 n +
+ * len suffices) with chunk i's blob at [blob_offsets[i], blob_offsets[i+1]) (n + 1
+ * entries; a known chunk's blob is empty -- it is uploaded as a reference) and
+ * `compressed` (n bytes, may be NULL).  Timing: the pipeline's, the stages after it, and
+ * the reference's UploadStats (backup_writer.rs:56-64; size_compressed = the new blobs'
+ * raw sizes, :699).  Synchronous. */
+typedef struct {
+    pbs_pipeline_timing pipe; /* chunks + digests */
+    double known_ms;          /* digests H2D + known-chunk test + flags D2H */
+    double encode_ms;         /* blob encoding of the new chunks (GPU, HBM -> HBM) */
+    double d2h_ms;            /* blobs to the host buffer */
+    double total_ms;          /* call entry .. everything on the host */
+    uint64_t chunk_count, chunk_reused, size, size_reused, size_compressed;
+    uint64_t compressed_chunks; /* new chunks stored as zstd blobs */
+    pbs_blob_encode_timing blob;
+} pbs_upload_timing;
+int pbs_upload_stream_host(size_t avg, const uint8_t *host, size_t len, size_t piece,
+                           const uint8_t *key, size_t key_len, int digest_cus, const uint8_t *known,
+                           size_t n_known, int compress, uint64_t *ends, uint8_t *digests,
+                           uint8_t *is_known, size_t cap, size_t *n_out, uint8_t *blobs,
+                           size_t blobs_cap, uint64_t *blob_offsets, uint8_t *compressed,
+                           pbs_upload_timing *timing);
 
 /* Frees the idle pipeline work areas (device memory of the last stream lengths). */
 void pbs_pipeline_release(void);

@@ -21,6 +21,29 @@ namespace pbs {
 // repeated call allocates nothing)
 inline std::atomic<uint64_t> g_arena_allocs{0};
 
+class ArenaPool;
+// Every pool of the process, and other keepers of idle device memory (the pipeline's work
+// areas): when an allocation fails, the idle memory of all of them is freed and the
+// allocation tried once more -- one large call (a 64 GiB pipeline or blob stage) must not
+// make the next, different call fail until someone calls a *_release.
+struct Reclaimers {
+    std::mutex mu;
+    std::vector<ArenaPool*> pools;
+    std::vector<void (*)()> hooks;
+};
+inline Reclaimers& reclaimers() {
+    static Reclaimers* r = new Reclaimers;  // never destroyed
+    return *r;
+}
+inline void add_reclaim_hook(void (*f)()) {
+    Reclaimers& r = reclaimers();
+    std::lock_guard<std::mutex> g(r.mu);
+    for (auto h : r.hooks)
+        if (h == f) return;
+    r.hooks.push_back(f);
+}
+inline void reclaim_idle_device_memory();  // below ArenaPool
+
 class DevArena {
 public:
     explicit DevArena(int dev) : dev_(dev) {}
@@ -41,7 +64,12 @@ public:
             const size_t want = headroom ? bytes + bytes / 8 : bytes;
             if (hipMalloc(&b.p, want) != hipSuccess) {
                 (void)hipGetLastError();
-                return nullptr;
+                reclaim_idle_device_memory();  // (this arena is leased: not among the idle ones)
+                if (hipMalloc(&b.p, want) != hipSuccess) {
+                    (void)hipGetLastError();
+                    b.p = nullptr;
+                    return nullptr;
+                }
             }
             b.cap = want;
             ++grows_;
@@ -84,6 +112,11 @@ private:
 // The idle arenas of one kind of call, per device.
 class ArenaPool {
 public:
+    ArenaPool() {
+        Reclaimers& r = reclaimers();
+        std::lock_guard<std::mutex> g(r.mu);
+        r.pools.push_back(this);
+    }
     DevArena* acquire(int dev) {
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -129,6 +162,19 @@ private:
     std::map<int, std::vector<DevArena*>> idle_;
     long leased_ = 0;
 };
+
+inline void reclaim_idle_device_memory() {
+    std::vector<ArenaPool*> pools;
+    std::vector<void (*)()> hooks;
+    {
+        Reclaimers& r = reclaimers();
+        std::lock_guard<std::mutex> g(r.mu);
+        pools = r.pools;
+        hooks = r.hooks;
+    }
+    for (ArenaPool* p : pools) p->clear();
+    for (auto h : hooks) h();
+}
 
 // Scoped lease: the arena goes back to the pool at the end of the call.
 class ArenaLease {

@@ -64,9 +64,13 @@ struct DevBuf {
         if (e == hipSuccess) cap = want;
         return e;
     }
-    void release() {
+    // the outgrown buffers (the handle is idle: no launch of it can still read them)
+    void drop_retired() {
         for (void* r : retired) (void)hipFree(r);
         retired.clear();
+    }
+    void release() {
+        drop_retired();
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -1606,6 +1610,20 @@ void pbs_chunker_free(pbs_chunker* c) {
 int pbs_chunker_reset(pbs_chunker* c) {
     if (!c) return PBS_ERR_INVALID;
     reset_stream(c);
+    // the buffers this handle outgrew (DevBuf): freed now that it is idle -- its server
+    // stopped, its stream drained -- so a handle whose batches grew does not keep ~2x its
+    // peak scratch for its whole life (hipFree waits for the device: only when there are any)
+    DevBuf* const bufs[] = {&c->d_table, &c->d_pre, &c->d_counters, &c->d_susp, &c->d_cand, &c->d_C,
+                            &c->d_sort_tmp, &c->d_nxt, &c->d_jtmp, &c->d_nf, &c->d_on, &c->d_cnt, &c->d_off,
+                            &c->d_scan_tmp, &c->d_cuts, &c->d_res, &c->d_in, &c->d_stage, &c->d_hits, &c->d_rec,
+                            &c->d_scratch};
+    bool any = false;
+    for (DevBuf* b : bufs) any |= !b->retired.empty();
+    if (any) {
+        server_stop(c);
+        if (hipStreamSynchronize(c->stream) != hipSuccess) return PBS_ERR_HIP;
+        for (DevBuf* b : bufs) b->drop_retired();
+    }
     return PBS_OK;
 }
 

@@ -418,8 +418,11 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
 // `next`; the control word is read over PCIe by at most one workgroup every ~2 us
 // (`last_poll`) and mirrored in device memory, where the others see it.  A workgroup
 // exits when every job is claimed and the final bit is set, or after idle_ticks (wall
-// clock, 100 MHz) without a new job -- the host relaunches the grid when it publishes
-// jobs after that.  Exiting when idle matters: a resident grid holds up whatever waits
+// clock, 100 MHz) in which no new job was PUBLISHED (the count it sees moved: claimed by
+// another workgroup or not, the stream is alive; round 5's first 50 ms idle exit counted
+// only this workgroup's own claims, so most of the grid left while the host was still
+// publishing and the 64 GiB pipeline's digests took 4 s instead of 1.25) -- the host
+// relaunches the grid when it publishes jobs after that.  Exiting when idle matters: a resident grid holds up whatever waits
 // for the whole device or for its stream (hipFree, null-stream copies).
 __global__ __launch_bounds__(64 * kShaWaves) void sha256_queue_kernel(
     const uint8_t* __restrict__ data, DigestKey key, const volatile DigestJob* __restrict__ jobs,
@@ -429,7 +432,7 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_queue_kernel(
     __shared__ uint32_t s_blocks;
     __shared__ uint64_t s_j0, s_k;
     const int lane = threadIdx.x & 63;
-    uint64_t t_job = wall_clock64();
+    uint64_t t_job = wall_clock64(), seen_avail = 0;
     for (;;) {
         if (threadIdx.x == 0) {
             uint64_t j0 = 0, k = 0;
@@ -437,6 +440,10 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_queue_kernel(
                 const uint64_t m = __hip_atomic_load(&q->mirror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t avail = m & 0xFFFFFFFFull, nx = __hip_atomic_load(&q->next, __ATOMIC_RELAXED,
                                                                                  __HIP_MEMORY_SCOPE_AGENT);
+                if (avail != seen_avail) {  // new jobs were published: not idle
+                    seen_avail = avail;
+                    t_job = wall_clock64();
+                }
                 if (avail > nx) {
                     const uint64_t want = avail - nx < 64 ? avail - nx : 64;
                     unsigned long long exp = nx;

@@ -120,7 +120,10 @@ struct PipePool {
 };
 
 PipePool& pipe_pool() {
-    static PipePool* p = new PipePool();  // never destroyed: no HIP calls at exit
+    static PipePool* p = [] {
+        pbs::add_reclaim_hook(&pbs_pipeline_release);  // idle work areas go when memory runs out
+        return new PipePool();  // never destroyed: no HIP calls at exit
+    }();
     return *p;
 }
 
@@ -166,10 +169,27 @@ extern "C" void pbs_pipeline_release(void) {
     if (have) (void)hipSetDevice(cur);
 }
 
-extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, size_t piece,
-                                 const uint8_t* key, size_t key_len, int digest_cus,
-                                 uint64_t* ends, uint8_t* digests, uint32_t* crcs, size_t cap,
-                                 size_t* n_out, pbs_pipeline_timing* timing) {
+namespace {
+
+// pbs_upload_stream_host's part after the digests (see upload_stage)
+struct UploadExt {
+    const uint8_t* known;
+    size_t n_known;
+    int compress;
+    uint8_t* known_out;
+    uint8_t* blobs;
+    size_t blobs_cap;
+    uint64_t* blob_offsets;
+    uint8_t* compressed;
+    pbs_upload_timing* t;
+};
+
+int upload_stage(UploadExt& x, pbs::DevArena* area, const uint8_t* d_data, size_t len, const uint64_t* ends,
+                 const uint8_t* digests, size_t n, hipStream_t st);
+
+int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, const uint8_t* key, size_t key_len,
+                 int digest_cus, uint64_t* ends, uint8_t* digests, uint32_t* crcs, size_t cap, size_t* n_out,
+                 pbs_pipeline_timing* timing, UploadExt* ext) {
     if (!n_out || (len && !host) || piece == 0 || (cap && (!ends || !digests)) ||
         key_len > PBS_DIGEST_MAX_KEY || (key_len && !key))
         return PBS_ERR_INVALID;
@@ -578,6 +598,9 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
         work();
         for (auto& th : fb) th.join();
     }
+    // the upload's part after the digests: known-chunk test and blobs, from the HBM copy
+    // (on the copy stream: not CU-masked, idle since the last piece landed)
+    if (ext && rc == PBS_OK) rc = upload_stage(*ext, area, d_data, len, ends, digests, n, s_copy);
     const double total = ms_since(t0);
     if (timing) {
         timing->total_ms = total;
@@ -609,4 +632,109 @@ extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, si
     }
     *n_out = n;
     return rc;  // the work area goes back to the pool (give_back)
+}
+
+// backup_writer.rs:677-706 for every chunk of the stream, on the GPU from the HBM copy the
+// pipeline made: the known-chunk test (previous index + earlier chunks of this stream), then
+// DataBlob::encode(chunk, None, compress) of the new chunks (data_blob.rs:139-176), their
+// blobs copied back to back into the caller's host buffer in chunk order; a known chunk's
+// blob is empty.  UploadStats (backup_writer.rs:56-64): size_compressed = the blobs' raw
+// sizes (`chunk.raw_size()`, :699).
+int upload_stage(UploadExt& x, pbs::DevArena* area, const uint8_t* d_data, size_t len, const uint64_t* ends,
+                 const uint8_t* digests, size_t n, hipStream_t st) {
+    pbs_upload_timing* const t = x.t;
+    const Clock::time_point t0 = Clock::now();
+    uint8_t* const d_dig = area->get<uint8_t>(6, std::max<size_t>(n, 1) * 32);
+    uint8_t* const d_kn = area->get<uint8_t>(7, std::max<size_t>(x.n_known, 1) * 32);
+    uint8_t* const d_fl = area->get<uint8_t>(8, std::max<size_t>(n, 1));
+    if (!d_dig || !d_kn || !d_fl) return PBS_ERR_NOMEM;
+    if (hipMemcpyAsync(d_dig, digests, n * 32, hipMemcpyHostToDevice, st) != hipSuccess ||
+        (x.n_known && hipMemcpyAsync(d_kn, x.known, x.n_known * 32, hipMemcpyHostToDevice, st) != hipSuccess))
+        return PBS_ERR_HIP;
+    size_t reused = 0;
+    int rc = pbs_known_chunks_device(d_dig, n, x.n_known ? d_kn : nullptr, x.n_known, d_fl, &reused, st);
+    if (rc != PBS_OK) return rc;
+    if (hipMemcpyAsync(x.known_out, d_fl, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return PBS_ERR_HIP;
+    const Clock::time_point t1 = Clock::now();
+    // the new chunks as spans of the stream
+    std::vector<uint64_t> spans;
+    std::vector<size_t> idx;
+    uint64_t size_reused = 0, new_bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t a = i ? ends[i - 1] : 0, b = ends[i];
+        if (x.known_out[i]) {
+            size_reused += b - a;
+            continue;
+        }
+        spans.push_back(a);
+        spans.push_back(b);
+        idx.push_back(i);
+        new_bytes += b - a;
+    }
+    const size_t m = idx.size();
+    const size_t bound = 12 * m + new_bytes;
+    uint8_t* const d_blobs = area->get<uint8_t>(9, std::max<size_t>(bound, 1), false);
+    if (!d_blobs) return PBS_ERR_NOMEM;
+    std::vector<uint64_t> offm(m + 1, 0);
+    std::vector<uint8_t> compm(std::max<size_t>(m, 1), 0);
+    rc = pbs_blob_encode_spans_device(d_data, len, 0, spans.data(), m, x.compress, d_blobs, bound, offm.data(),
+                                      nullptr, compm.data(), t ? &t->blob : nullptr, st);
+    if (rc != PBS_OK) return rc;
+    const Clock::time_point t2 = Clock::now();
+    if (offm[m] > x.blobs_cap) return PBS_ERR_CAPACITY;
+    if (offm[m] && (hipMemcpyAsync(x.blobs, d_blobs, offm[m], hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess))
+        return PBS_ERR_HIP;
+    // every chunk's blob range (a known chunk's is empty) and compressed flag
+    size_t k = 0;
+    x.blob_offsets[0] = 0;
+    uint64_t compressed_chunks = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const bool fresh = k < m && idx[k] == i;
+        x.blob_offsets[i + 1] = fresh ? offm[k + 1] : x.blob_offsets[i];
+        if (x.compressed) x.compressed[i] = fresh ? compm[k] : 0;
+        compressed_chunks += fresh ? compm[k] : 0;
+        k += fresh ? 1 : 0;
+    }
+    if (t) {
+        t->known_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        t->encode_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        t->d2h_ms = ms_since(t2);
+        t->chunk_count = n;
+        t->chunk_reused = reused;
+        t->size = len;
+        t->size_reused = size_reused;
+        t->size_compressed = offm[m];
+        t->compressed_chunks = compressed_chunks;
+    }
+    return PBS_OK;
+}
+
+}  // namespace
+
+extern "C" int pbs_pipeline_host(size_t avg, const uint8_t* host, size_t len, size_t piece,
+                                 const uint8_t* key, size_t key_len, int digest_cus,
+                                 uint64_t* ends, uint8_t* digests, uint32_t* crcs, size_t cap,
+                                 size_t* n_out, pbs_pipeline_timing* timing) {
+    return pipeline_run(avg, host, len, piece, key, key_len, digest_cus, ends, digests, crcs, cap, n_out, timing,
+                        nullptr);
+}
+
+extern "C" int pbs_upload_stream_host(size_t avg, const uint8_t* host, size_t len, size_t piece,
+                                      const uint8_t* key, size_t key_len, int digest_cus,
+                                      const uint8_t* known, size_t n_known, int compress, uint64_t* ends,
+                                      uint8_t* digests, uint8_t* is_known, size_t cap, size_t* n_out,
+                                      uint8_t* blobs, size_t blobs_cap, uint64_t* blob_offsets,
+                                      uint8_t* compressed, pbs_upload_timing* timing) {
+    if (!is_known || !blob_offsets || (n_known && !known) || (blobs_cap && !blobs)) return PBS_ERR_INVALID;
+    if (timing) std::memset(timing, 0, sizeof(*timing));
+    blob_offsets[0] = 0;
+    const Clock::time_point t0 = Clock::now();
+    UploadExt x{known, n_known, compress, is_known, blobs, blobs_cap, blob_offsets, compressed, timing};
+    const int rc = pipeline_run(avg, host, len, piece, key, key_len, digest_cus, ends, digests, nullptr, cap, n_out,
+                                timing ? &timing->pipe : nullptr, len ? &x : nullptr);
+    if (timing) timing->total_ms = ms_since(t0);
+    return rc;
 }

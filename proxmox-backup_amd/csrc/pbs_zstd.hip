@@ -1741,7 +1741,7 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         ZMARK(9);
         const uint64_t it = items[k];
         const uint64_t ci = it >> 32, j = (uint32_t)it;
-        const uint64_t c0 = bounds[ci], c1 = bounds[ci + 1];
+        const uint64_t c0 = bounds[2 * ci], c1 = bounds[2 * ci + 1];  // (chunk spans {start, end})
         const uint64_t len = c1 - c0, off = j * (uint64_t)kEncBlock;
         const uint32_t n = (uint32_t)(len > off ? (len - off < kEncBlock ? len - off : kEncBlock) : 0);
         const bool last = off + n == len;
@@ -2290,7 +2290,7 @@ __global__ void zstd_frame_sizes_kernel(const uint64_t* __restrict__ bounds, con
         bsz[n] = 0;
         return;
     }
-    const uint64_t len = bounds[ci + 1] - bounds[ci];
+    const uint64_t len = bounds[2 * ci + 1] - bounds[2 * ci];
     bool c = false;
     uint64_t fs = 0;
     if (compress) {
@@ -2312,7 +2312,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_assemble_kernel(
     for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
         const uint64_t it = items[k];
         const uint64_t ci = it >> 32, j = (uint32_t)it;
-        const uint64_t len = bounds[ci + 1] - bounds[ci];
+        const uint64_t len = bounds[2 * ci + 1] - bounds[2 * ci];
         uint8_t* const blob = blobs + boff[ci];
         const bool c = comp[ci] != 0;
         const uint32_t fh = frame_header_size(len);
@@ -2324,7 +2324,7 @@ __global__ __launch_bounds__(kZThreads) void zstd_assemble_kernel(
         } else {
             const uint64_t off = j * (uint64_t)kEncBlock;
             const uint64_t n = len > off ? (len - off < kEncBlock ? len - off : kEncBlock) : 0;
-            const uint8_t* const src = data + (bounds[ci] - base) + off;
+            const uint8_t* const src = data + (bounds[2 * ci] - base) + off;
             copy_global(blob + 12 + off, src, n, threadIdx.x, kZThreads);
         }
     }
@@ -2372,24 +2372,29 @@ extern "C" size_t pbs_blob_stream_bound(const uint64_t* bounds, size_t n) {
     return 12 * n + (size_t)(bounds[n] - bounds[0]);
 }
 
-extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t data_len, uint64_t base,
-                                             const uint64_t* bounds, size_t n, int compress, uint8_t* blobs_dev,
-                                             size_t blobs_cap, uint64_t* blob_offsets, uint32_t* crcs,
-                                             uint8_t* compressed, pbs_blob_encode_timing* timing,
-                                             void* hip_stream) {
+// The chunks as spans {start, end} (absolute stream offsets; any order, gaps allowed):
+// pbs_blob_encode_spans_device, and pbs_blob_encode_chunks_device through it.
+extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data_len, uint64_t base,
+                                            const uint64_t* spans, size_t n, int compress, uint8_t* blobs_dev,
+                                            size_t blobs_cap, uint64_t* blob_offsets, uint32_t* crcs,
+                                            uint8_t* compressed, pbs_blob_encode_timing* timing,
+                                            void* hip_stream) {
     using Clock = std::chrono::steady_clock;
     const Clock::time_point t0 = Clock::now();
     if (timing) std::memset(timing, 0, sizeof(*timing));
     if (!blob_offsets) return PBS_ERR_INVALID;
     blob_offsets[0] = 0;
     if (n == 0) return PBS_OK;
-    if (!bounds || !blobs_dev || (data_len && !dev_data) || n >= 0xFFFFFFFFull) return PBS_ERR_INVALID;
-    for (size_t i = 0; i < n; ++i)
-        if (bounds[i] > bounds[i + 1] || bounds[i] < base || bounds[i + 1] - base > data_len)
+    if (!spans || !blobs_dev || (data_len && !dev_data) || n >= 0xFFFFFFFFull) return PBS_ERR_INVALID;
+    uint64_t bytes_in = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (spans[2 * i] > spans[2 * i + 1] || spans[2 * i] < base || spans[2 * i + 1] - base > data_len)
             return PBS_ERR_INVALID;
-    // the reference refuses blobs over MAX_BLOB_SIZE (data_blob.rs:92, 128 MiB, :13)
-    for (size_t i = 0; i < n; ++i)
-        if (bounds[i + 1] - bounds[i] > (128ull << 20)) return PBS_ERR_INVALID;
+        // the reference refuses blobs over MAX_BLOB_SIZE (data_blob.rs:92, 128 MiB, :13)
+        if (spans[2 * i + 1] - spans[2 * i] > (128ull << 20)) return PBS_ERR_INVALID;
+        bytes_in += spans[2 * i + 1] - spans[2 * i];
+    }
+    const uint64_t* const bounds = spans;  // (device copies below: 2 n entries)
     hipStream_t st = (hipStream_t)hip_stream;
     int dev = 0, ncu = 0;
     if (hipStreamGetDevice(st, &dev) != hipSuccess ||
@@ -2403,7 +2408,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     std::vector<uint64_t> items, first(n + 1);
     for (size_t i = 0; i < n; ++i) {
         first[i] = items.size();
-        const uint64_t len = bounds[i + 1] - bounds[i];
+        const uint64_t len = bounds[2 * i + 1] - bounds[2 * i];
         const uint64_t nb = len ? (len + zstd::kEncBlock - 1) / zstd::kEncBlock : 1;
         for (uint64_t j = 0; j < nb; ++j) items.push_back((uint64_t)i << 32 | j);
     }
@@ -2422,7 +2427,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     size_t tmpb = std::max(t1b, t2b);
     const unsigned grid = (unsigned)std::min<uint64_t>(ni, (uint64_t)ncu);  // one 512-thread workgroup per CU
     ArenaLease ar(zpool(), dev);
-    uint64_t* d_bounds = ar->get<uint64_t>(kZsBounds, (n + 1) * 8);
+    uint64_t* d_bounds = ar->get<uint64_t>(kZsBounds, 2 * n * 8);
     uint64_t* d_items = ar->get<uint64_t>(kZsItems, ni * 8);
     uint64_t* d_first = ar->get<uint64_t>(kZsFirst, (n + 1) * 8);
     uint64_t* d_sizes = ar->get<uint64_t>(kZsSizes, (ni + 1) * 8);
@@ -2449,7 +2454,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     for (unsigned i = 0; i < 4 && rc == PBS_OK; ++i)
         if (!(ev[i] = ar->event(i))) fail(PBS_ERR_HIP);
     if (rc == PBS_OK)
-        ok(hipMemcpyAsync(d_bounds, bounds, (n + 1) * 8, hipMemcpyHostToDevice, st)) &&
+        ok(hipMemcpyAsync(d_bounds, bounds, 2 * n * 8, hipMemcpyHostToDevice, st)) &&
             ok(hipMemcpyAsync(d_items, items.data(), ni * 8, hipMemcpyHostToDevice, st)) &&
             ok(hipMemcpyAsync(d_first, first.data(), (n + 1) * 8, hipMemcpyHostToDevice, st)) &&
             ok(hipMemsetAsync(d_sizes, 0, (ni + 1) * 8, st));
@@ -2542,7 +2547,7 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
         timing->compress_ms = a;
         timing->assemble_ms = b;
         timing->crc_ms = c;
-        timing->bytes_in = bounds[n] - bounds[0];
+        timing->bytes_in = bytes_in;
         timing->bytes_out = blob_offsets[n];
         timing->blocks = ni;
         if (compressed)
@@ -2551,4 +2556,25 @@ extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t dat
     if (rc != PBS_OK) (void)hipStreamSynchronize(st);  // the arena goes back idle
     if (timing) timing->total_ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
     return rc;
+}
+
+extern "C" int pbs_blob_encode_chunks_device(const uint8_t* dev_data, size_t data_len, uint64_t base,
+                                             const uint64_t* bounds, size_t n, int compress, uint8_t* blobs_dev,
+                                             size_t blobs_cap, uint64_t* blob_offsets, uint32_t* crcs,
+                                             uint8_t* compressed, pbs_blob_encode_timing* timing,
+                                             void* hip_stream) {
+    if (!blob_offsets) return PBS_ERR_INVALID;
+    if (n == 0) {
+        if (timing) std::memset(timing, 0, sizeof(*timing));
+        blob_offsets[0] = 0;
+        return PBS_OK;
+    }
+    if (!bounds) return PBS_ERR_INVALID;
+    std::vector<uint64_t> spans(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        spans[2 * i] = bounds[i];
+        spans[2 * i + 1] = bounds[i + 1];
+    }
+    return pbs_blob_encode_spans_device(dev_data, data_len, base, spans.data(), n, compress, blobs_dev, blobs_cap,
+                                        blob_offsets, crcs, compressed, timing, hip_stream);
 }

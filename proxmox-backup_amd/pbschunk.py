@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = (
     "pbs_crc32_chunks_device", "pbs_crc32_chunks_async", "pbs_crc32", "pbs_blob_encode_uncompressed",
     "pbs_blob_encode_chunks_device", "pbs_blob_stream_bound", "pbs_zstd_frame_bound",
     "pbs_blob_encode_release", "pbs_digest_hybrid_release", "pbs_debug_arena_allocs",
-    "pbs_pipeline_release",
+    "pbs_pipeline_release", "pbs_blob_encode_spans_device", "pbs_upload_stream_host",
 )
 
 
@@ -109,6 +109,20 @@ class BlobEncodeTiming(ctypes.Structure):
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class UploadTiming(ctypes.Structure):
+    _fields_ = [
+        ("pipe", PipelineTiming), ("known_ms", ctypes.c_double), ("encode_ms", ctypes.c_double),
+        ("d2h_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+        ("chunk_count", ctypes.c_uint64), ("chunk_reused", ctypes.c_uint64), ("size", ctypes.c_uint64),
+        ("size_reused", ctypes.c_uint64), ("size_compressed", ctypes.c_uint64),
+        ("compressed_chunks", ctypes.c_uint64), ("blob", BlobEncodeTiming),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: (getattr(self, k).as_dict() if k in ("pipe", "blob") else getattr(self, k))
+                for k, _ in self._fields_}
 
 
 class HybridOpts(ctypes.Structure):
@@ -193,6 +207,10 @@ def lib():
         "pbs_blob_encode_uncompressed": ([p, sz, ctypes.c_uint32, p, sz], sz),
         "pbs_blob_encode_chunks_device": ([p, sz, u64, p, sz, i, p, sz, p, p, p,
                                            ctypes.POINTER(BlobEncodeTiming), p], i),
+        "pbs_blob_encode_spans_device": ([p, sz, u64, p, sz, i, p, sz, p, p, p,
+                                          ctypes.POINTER(BlobEncodeTiming), p], i),
+        "pbs_upload_stream_host": ([sz, p, sz, sz, p, sz, i, p, sz, i, p, p, p, sz, ctypes.POINTER(sz),
+                                    p, sz, p, p, ctypes.POINTER(UploadTiming)], i),
         "pbs_blob_stream_bound": ([p, sz], sz),
         "pbs_zstd_frame_bound": ([sz], sz),
         "pbs_blob_encode_release": ([], None),
@@ -801,35 +819,56 @@ def index_stream_device(chunker: "Chunker", dev_ptr: int, length: int, key=None,
 
 
 def upload_stream_host(data, avg: int, known=None, key=None, piece: int = 1 << 30,
-                       uuid: bytes = bytes(16), ctime: int = 0) -> dict:
+                       uuid: bytes = bytes(16), ctime: int = 0, compress: bool = True,
+                       digest_cus: int = 64, blobs_out=None) -> dict:
     """The client's upload of one dynamic-index stream from a host buffer, up to the
-    network (pbs-client/src/backup_writer.rs:638-700 upload_chunk_info_stream /
-    :683-688 index csum): chunk (ChunkStream), digest every chunk, mark it known when
-    its digest is in ``known`` (the previous index's digests, :524-547) or repeats an
-    earlier chunk of this stream (:697), and build the .didx image.  Chunking, digests,
-    the blob CRCs and the known-chunk test run on the GPU (pipeline_host,
-    known_chunks_device).  Returns a dict: ends, digests, crcs, known (uint8 mask),
-    csum, didx (bytes), and new_chunks = [(start, length, crc), ...] -- the chunks whose
-    uncompressed blob (blob_encode_uncompressed) would be uploaded."""
-    import torch
-
-    ends, dig, crcs, _ = pipeline_host(data, avg, piece=piece, key=key, crc=True)
-    n = ends.size
-    d_dig = torch.from_numpy(dig.reshape(-1)).to("cuda")
-    flags = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+    network (pbs-client/src/backup_writer.rs:631-706 upload_chunk_info_stream; the client
+    backs up with compress = true, proxmox-backup-client/src/main.rs:1011-1016): chunk
+    (ChunkStream), digest every chunk, mark it known when its digest is in ``known`` (the
+    previous index's digests, :524-547) or repeats an earlier chunk of this stream (:697),
+    build each new chunk's blob -- DataChunkBuilder::new(data).compress(compress).build()
+    (:671, :698; zstd frames where shorter, data_blob.rs:139-176) -- and the .didx image.
+    Everything up to the blobs runs on the GPU from one HBM copy of the stream
+    (pbs_upload_stream_host).  Returns a dict: ends, digests, known (uint8 mask), csum,
+    didx (bytes), blobs (uint8 array: the new chunks' blobs back to back; chunk i's is
+    blobs[blob_offsets[i]:blob_offsets[i + 1]], empty for a known chunk), blob_offsets
+    (n + 1), compressed (n flags), new_chunks = [(start, length), ...], stats (UploadStats,
+    backup_writer.rs:56-64) and timing.
+    ``blobs_out``: an optional preallocated uint8 array (e.g. pinned) for the blobs."""
+    a = _as_u8(data)
+    cap = a.size // max(int(avg) >> 2, 65) + 4
+    ends = np.empty(cap, dtype=np.uint64)
+    dig = np.empty((cap, 32), dtype=np.uint8)
+    is_known = np.empty(cap, dtype=np.uint8)
+    offs = np.zeros(cap + 1, dtype=np.uint64)
+    comp = np.empty(cap, dtype=np.uint8)
+    bcap = 12 * cap + a.size
+    blobs = blobs_out if blobs_out is not None else np.empty(max(bcap, 1), dtype=np.uint8)
+    if blobs.size < bcap:
+        raise ValueError(f"blobs_out holds {blobs.size} bytes, the stream needs up to {bcap}")
     kd = np.zeros((0, 32), dtype=np.uint8)
     if known is not None and len(known):
         kd = np.frombuffer(b"".join(sorted(bytes(x) for x in known)), dtype=np.uint8).reshape(-1, 32)
-    d_known = torch.from_numpy(kd.reshape(-1).copy()).to("cuda") if kd.size else None
-    torch.cuda.synchronize()
-    known_chunks_device(d_dig.data_ptr(), n, d_known.data_ptr() if d_known is not None else 0,
-                        kd.shape[0], flags.data_ptr())
-    mask = flags[:n].cpu().numpy()
+    kb, kl = _key_arg(key)
+    n = ctypes.c_size_t(0)
+    t = UploadTiming()
+    rc = lib().pbs_upload_stream_host(avg, _ptr(a), a.size, piece, kb, kl, digest_cus,
+                                      kd.ctypes.data if kd.size else None, kd.shape[0], 1 if compress else 0,
+                                      ends.ctypes.data, dig.ctypes.data, is_known.ctypes.data, cap,
+                                      ctypes.byref(n), blobs.ctypes.data, blobs.size, offs.ctypes.data,
+                                      comp.ctypes.data, ctypes.byref(t))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_upload_stream_host")
+    m = n.value
+    ends, dig, is_known, offs, comp = ends[:m].copy(), dig[:m].copy(), is_known[:m].copy(), offs[:m + 1].copy(), comp[:m].copy()
     image, csum = didx_build(ends, dig, uuid, ctime)
-    starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64) if n else np.zeros(0, np.uint64)
-    new = [(int(starts[i]), int(ends[i] - starts[i]), int(crcs[i])) for i in range(n) if not mask[i]]
-    return {"ends": ends, "digests": dig, "crcs": crcs, "known": mask, "csum": csum, "didx": image,
-            "new_chunks": new}
+    starts = np.concatenate([[0], ends[:-1]]).astype(np.uint64) if m else np.zeros(0, np.uint64)
+    new = [(int(starts[i]), int(ends[i] - starts[i])) for i in np.flatnonzero(is_known == 0)]
+    td = t.as_dict()
+    stats = {k: td[k] for k in ("chunk_count", "chunk_reused", "size", "size_reused", "size_compressed")}
+    return {"ends": ends, "digests": dig, "known": is_known, "csum": csum, "didx": image,
+            "blobs": blobs[:int(offs[-1])] if m else blobs[:0], "blob_offsets": offs, "compressed": comp,
+            "new_chunks": new, "stats": stats, "timing": td}
 
 
 def pipeline_host(data, avg: int, piece: int = 1 << 30, key=None, digest_cus: int = 64, crc: bool = False):

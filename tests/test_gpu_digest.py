@@ -308,11 +308,14 @@ def test_pipeline_beside_null_stream_work(gpu, oracle, torch_dev):
     assert wall < 8.0, (wall, ops[0], t)
 
 
-@pytest.mark.parametrize("prev", [0, 5, 40])
-def test_upload_stream_host(gpu, oracle, prev):
-    """backup_writer.rs:638-700 end to end from a host buffer: cut list, digests, blob
-    CRCs, the known-chunk mask against a previous index holding some of this stream's
-    digests (plus unrelated ones) and repeats inside the stream, and the .didx image."""
+@pytest.mark.parametrize("prev,compress", [(0, True), (5, True), (40, True), (5, False)])
+def test_upload_stream_host(gpu, oracle, prev, compress):
+    """backup_writer.rs:631-706 end to end from a host buffer: cut list, digests, the
+    known-chunk mask against a previous index holding some of this stream's digests (plus
+    unrelated ones) and repeats inside the stream, the .didx image, and every new chunk's
+    blob as DataChunkBuilder::new(data).compress(compress).build() writes it (oracle: the
+    twin's frame behind the blob header where shorter, data_blob.rs:139-176; the
+    uncompressed blob otherwise), plus UploadStats."""
     n = 48 * MiB + 5
     data = gen_np.gen_vmimage(n, 0x5EED0003, 0)
     ref_ends = oracle.chunk_feed(1 * MiB, data)
@@ -323,16 +326,59 @@ def test_upload_stream_host(gpu, oracle, prev):
     rng = np.random.default_rng(prev)
     pick = rng.choice(ref_dig.shape[0], size=min(prev, ref_dig.shape[0]), replace=False)
     known = [bytes(ref_dig[i]) for i in pick] + [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(prev)]
-    out = gpu.upload_stream_host(data, 1 * MiB, known=known, piece=16 * MiB, uuid=bytes(range(16)), ctime=77)
+    out = gpu.upload_stream_host(data, 1 * MiB, known=known, piece=16 * MiB, uuid=bytes(range(16)), ctime=77,
+                                 compress=compress)
     assert np.array_equal(out["ends"], ref_ends)
     assert np.array_equal(out["digests"], ref_dig)
-    assert np.array_equal(out["crcs"], oracle.chunk_crcs(data, bounds))
     ref_known = oracle.known_chunks(ref_dig, known)
     assert np.array_equal(out["known"], ref_known)
     img, csum = oracle.didx_image(ref_ends, ref_dig, bytes(range(16)), 77)
     assert out["didx"] == img and out["csum"] == csum
-    new = [(int(bounds[i]), int(bounds[i + 1] - bounds[i])) for i in range(ref_known.size) if not ref_known[i]]
-    assert [(s, l) for s, l, _ in out["new_chunks"]] == new
+    _check_blobs(oracle, data, bounds, ref_known, out, compress)
+
+
+def _check_blobs(oracle, data, bounds, ref_known, out, compress):
+    new = [i for i in range(ref_known.size) if not ref_known[i]]
+    assert out["new_chunks"] == [(int(bounds[i]), int(bounds[i + 1] - bounds[i])) for i in new]
+    size_compressed = 0
+    offs = out["blob_offsets"]
+    for (s, ln), i in zip(out["new_chunks"], new):
+        chunk = data[s:s + ln].tobytes()
+        blob = out["blobs"][int(offs[i]):int(offs[i + 1])].tobytes()
+        exp = oracle.blob_compressed(chunk) if compress else oracle.blob_uncompressed(chunk)
+        assert blob == exp, f"chunk {i} ({ln} bytes)"
+        assert bool(out["compressed"][i]) == (blob[:8] == oracle.COMPRESSED_BLOB_MAGIC)
+        if out["compressed"][i]:
+            assert oracle.zstd_decompress(blob[12:], ln) == chunk
+        size_compressed += len(blob)
+    assert all(out["blob_offsets"][i + 1] == out["blob_offsets"][i] for i in range(ref_known.size) if ref_known[i])
+    st = out["stats"]
+    assert st["chunk_count"] == ref_known.size and st["chunk_reused"] == int(ref_known.sum())
+    assert st["size"] == data.size and st["size_compressed"] == size_compressed
+    assert st["size_reused"] == sum(int(bounds[i + 1] - bounds[i]) for i in range(ref_known.size) if ref_known[i])
+
+
+def test_upload_stream_mixed_compressed(gpu, oracle):
+    """The compressing upload over a mixed stream -- English-like text, a pxar-like
+    archive, VM-image pages, and a second copy of the text (its chunks repeat once the
+    chunker resyncs: known within the stream) -- with a previous index holding a few of
+    its digests: blobs equal the twin's, every zstd payload decodes with libzstd."""
+    import corpus_gen
+    text = corpus_gen.text(6 * MiB, 11)
+    data = np.concatenate([text, corpus_gen.pxar(6 * MiB, 12), gen_np.gen_vmimage(8 * MiB, 0x5EED0003, 0), text])
+    avg = 256 << 10
+    ref_ends = oracle.chunk_feed(avg, data)
+    if ref_ends.size == 0 or int(ref_ends[-1]) != data.size:
+        ref_ends = np.append(ref_ends, np.uint64(data.size))
+    bounds = np.concatenate([[0], ref_ends]).astype(np.uint64)
+    ref_dig = oracle.chunk_digests(data, bounds)
+    known = [bytes(ref_dig[i]) for i in (3, 40, 77)]
+    out = gpu.upload_stream_host(data, avg, known=known, piece=5 * MiB + 3)
+    assert np.array_equal(out["ends"], ref_ends) and np.array_equal(out["digests"], ref_dig)
+    ref_known = oracle.known_chunks(ref_dig, known)
+    assert np.array_equal(out["known"], ref_known)
+    assert int(ref_known.sum()) > 10  # the repeated text's chunks
+    _check_blobs(oracle, data, bounds, ref_known, out, True)
 
 
 def test_reference_digest_vectors(gpu, torch_dev):
