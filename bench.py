@@ -89,6 +89,8 @@ def parse():
                     help="1: after the timed region compare every rank's cut list (and the "
                          "secondary line's) with tests/golden/bench_cuts.json (oracle-made) and "
                          "exit 3 unless all match; 0: skip (streams without a golden entry)")
+    ap.add_argument("--traffic-random-json", default=os.path.join(ROOT, "profiles", "traffic_random.json"),
+                    help="the same for the secondary random-data line")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per scan launch (written by profiles/collect_traffic.py)")
     return ap.parse_args()
@@ -275,6 +277,23 @@ def cpu_config1(args):
     return out
 
 
+def traffic_record(path, workload, size, avg, streams=True):
+    """(HBM bytes per launch, note) from a PMC traffic record (profiles/collect_traffic.py)
+    when it is of this library build and this stream, else (None, why not)."""
+    import pbschunk
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, "no PMC record"
+    bid = pbschunk.build_id()
+    if tj.get("build_id") != bid:
+        return None, f"PMC record is of build {tj.get('build_id')}, this is {bid}: not reported"
+    if not (tj.get("size") == size and tj.get("avg") == avg and tj.get("workload") == workload and streams):
+        return None, "PMC record is of another workload"
+    return tj.get("hbm_bytes_per_launch"), f"rocprofv3 FETCH_SIZE x 1024 x 2, build {bid}"
+
+
 def secondary_random(args, ch, buf, stream, steps: int = 3):
     """The same-size stream of random bytes (GEN_RANDOM, seed 0x5EED0002) through the same
     handle: every window hashes uniformly, so no zero extents shortcut anything; timed
@@ -305,12 +324,13 @@ def secondary_random(args, ch, buf, stream, steps: int = 3):
     rec = {"chunks": n, **cut_record(cuts, keep=0)}
     if args.verify:
         verify_record(rec, "random", size, args.avg, SEEDS["random"])
+    traffic, traffic_note = traffic_record(args.traffic_random_json, "random", size, args.avg)
     return {"workload": f"random-{args.size_gib:g}GiB-avg{args.avg}", "seed": hex(SEEDS["random"]),
             "value": round(size / (1 << 30) / (ms / 1e3), 3), "unit": "GiB/s", "steps": steps,
             "ms_per_step": round(ms, 3), **rec,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "kernel": kernel_name(fused), "avg_launch_ms": round(sk, 4)}}
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_note": traffic_note, "kernel": kernel_name(fused), "avg_launch_ms": round(sk, 4)}}
 
 
 def blob_stage(args, buf, cuts, stream, reps: int = 2):
@@ -1087,22 +1107,8 @@ def main():
     value = total_bytes * args.steps / (1 << 30) / elapsed
     avg_scan_s = float(np.mean(scan_ms)) / 1e3 if scan_ms else float("nan")
     achieved = work_bytes / avg_scan_s / 1e9  # algorithmic bytes (input read once) per launch
-    traffic, traffic_note = None, "no PMC record"
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        bid = pbschunk.build_id()
-        if tj.get("build_id") != bid:
-            traffic_note = f"PMC record is of build {tj.get('build_id')}, this is {bid}: not reported"
-        elif not (tj.get("size") == work_bytes and tj.get("avg") == args.avg
-                  and tj.get("workload") == args.workload and args.mode == "streams"):
-            traffic_note = "PMC record is of another workload"
-        else:
-            traffic = tj.get("hbm_bytes_per_launch")
-            traffic_note = f"rocprofv3 FETCH_SIZE x 1024 x 2, build {bid}"
-    except (OSError, ValueError):
-        pass
-
+    traffic, traffic_note = traffic_record(args.traffic_json, args.workload, work_bytes, args.avg,
+                                           args.mode == "streams")
     host_incl = None
     if rank == 0 and world == 1 and args.host_inclusive_gib > 0 and args.mode == "streams":
         hn = int(args.host_inclusive_gib * (1 << 30)) // 8 * 8

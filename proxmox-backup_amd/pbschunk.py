@@ -30,6 +30,10 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "csrc", "libpbschunk.so")
+# (diagnostics only: an A/B against another build of the same library, e.g. a PMC run of
+# the previous round's kernels; the product path loads the in-tree build)
+if os.environ.get("PBS_LIBPBSCHUNK_AB"):
+    LIB_PATH = os.environ["PBS_LIBPBSCHUNK_AB"]
 
 PBS_OK = 0
 PBS_ERR_NOT_POW2 = -1
@@ -218,6 +222,8 @@ def lib():
         "pbs_pipeline_release": ([], None),
     }
     for name, (args, res) in sig.items():
+        if os.environ.get("PBS_LIBPBSCHUNK_AB") and not hasattr(L, name):
+            continue  # (an older build in an A/B run: the symbols it has)
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
