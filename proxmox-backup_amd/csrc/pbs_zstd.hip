@@ -1180,41 +1180,96 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
             }
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) m[i] = __ballot(has[i]);
+            // each match position's successor on the chain: the first match position at or
+            // after its end (index q + ceil(L / step); a length under kZCap is at most 31, so
+            // the end lies in this slot or the next), 256 when the chain leaves the round,
+            // kZCapped when the length is capped (the walk extends it and looks itself)
+            constexpr uint32_t kZNone = 256, kZCapped = 512;
+            uint32_t first_from[kZPer + 2];  // first match index in slots >= i (uniform)
+            first_from[kZPer] = first_from[kZPer + 1] = kZNone;
+#pragma unroll
+            for (int i = kZPer - 1; i >= 0; --i)
+                first_from[i] = m[i] ? 64u * (uint32_t)i + (uint32_t)__builtin_ctzll(m[i]) : first_from[i + 1];
+            uint32_t Sx[kZPer];
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
+                const uint32_t q = 64u * (uint32_t)i + (uint32_t)lane;
+                const uint32_t Lh = (D[i] >> 16) & 0xFF;
+                const uint32_t b = (uint32_t)lane + ((Lh + step - 1) >> lstep);  // the end, from slot i's start
+                const unsigned long long mi = b < 64 ? m[i] & (~0ull << b) : 0ull;
+                const unsigned long long mn = i + 1 < kZPer ? (b < 64 ? m[i + 1 < kZPer ? i + 1 : i]
+                                                                     : m[i + 1 < kZPer ? i + 1 : i] & (~0ull << (b - 64)))
+                                                            : 0ull;
+                const uint32_t next = mi ? 64u * (uint32_t)i + (uint32_t)__builtin_ctzll(mi)
+                                         : mn ? 64u * (uint32_t)(i + 1) + (uint32_t)__builtin_ctzll(mn) : first_from[i + 2];
+                Sx[i] = Lh == kZCap ? kZCapped : q + ((Lh + step - 1) >> lstep) >= kZRound ? kZNone : next;
+            }
             qmark(46);
             if (probe) {
                 t_walk = wall_clock64();
                 probe[33] += 1;  // rounds
             }
-            // the walk: wave-uniform scalar steps that only follow the chain -- the first match
-            // at or after cur, its end -- and mark the positions taken (T, bit l of slot i); the
-            // backward extension (bounded by the previous match's end) and a capped length's
-            // extension go to the position's lane (Ef, Lf).  Slot by slot, so each slot's mask
-            // and record register are named directly.
-            uint32_t Lf[kZPer], Ef[kZPer];
-            unsigned long long T[kZPer];
-#pragma unroll
-            for (int i = 0; i < kZPer; ++i) {
-                Lf[i] = L[i];
-                Ef[i] = 0;
-            }
+            // the walk: wave-uniform scalar steps along the chain -- read the successor of the
+            // position taken, append the position to the path (lane k of `path`; a capped
+            // match's full length to `pathL`).  Slot by slot, so each slot's successor register
+            // is named directly.  Every 64 positions (and at the end) the path's records are
+            // written by the lanes in parallel (flush).
+            const uint32_t cur0 = cur;
+            uint32_t path = 0, pathL = 0, k = 0;
+            uint32_t carry = cur0;  // the previous match's end
+            bool found = false;
+            auto flush = [&](uint32_t K) {
+                // lane j < K: path position q; its packed record from its slot and lane
+                const uint32_t q = path & 0x3FF, l4 = (q & 63) * 4;
+                const uint32_t d0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l4, (int)D[0]),
+                               d1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l4, (int)D[1]),
+                               d2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l4, (int)D[2]),
+                               d3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)l4, (int)D[3]);
+                const uint32_t sl = q >> 6;
+                const uint32_t d = sl == 0 ? d0 : sl == 1 ? d1 : sl == 2 ? d2 : d3;
+                const uint32_t pq = r0 + (q << lstep);
+                const uint32_t Lq = (path & 0x400) ? pathL : (d >> 16) & 0xFF;
+                const uint32_t end = pq + Lq;
+                const uint32_t up = (uint32_t)__shfl_up((int)end, 1, 64);
+                const uint32_t prev_end = lane ? up : carry;
+                const uint32_t e = min(d >> 24, pq - prev_end);
+                const uint32_t Sq = wlo + (d & 0xFFFF);
+                if ((uint32_t)lane < K && ns + (uint32_t)lane < kZSubSeq) {
+                    PBS_GLOBAL uint32_t* const rec = wseq_w + 3 * (ns + (uint32_t)lane);
+                    rec[0] = pq - e - hist;
+                    rec[1] = Lq + e;
+                    rec[2] = pq - Sq;
+                }
+                carry = uni((uint32_t)__builtin_amdgcn_readlane((int)end, (int)K - 1));
+                rep = uni((uint32_t)__builtin_amdgcn_readlane((int)(pq - Sq), (int)K - 1));
+                ns = uni(ns + K);
+                found = true;
+            };
+            // the first match at or after the round-start position
             uint32_t q = uni(cur > r0 ? (cur - r0 + step - 1) >> lstep : 0);
+            {
+                const uint32_t w0 = q >> 6;
+                uint32_t f = kZNone;
+                if (q < kZRound) {
+                    const unsigned long long mm =
+                        (w0 == 0 ? m[0] : w0 == 1 ? m[1] : w0 == 2 ? m[2] : m[3]) & (~0ull << (q & 63));
+                    f = mm ? 64u * w0 + (uint32_t)__builtin_ctzll(mm)
+                           : (w0 == 0 ? first_from[1] : w0 == 1 ? first_from[2] : w0 == 2 ? first_from[3] : kZNone);
+                }
+                q = uni(f);
+            }
 #pragma unroll
             for (int wi = 0; wi < kZPer; ++wi) {
-                unsigned long long tk = 0;
                 while (q < 64u * (uint32_t)(wi + 1)) {
-                    const uint32_t qq = q > 64u * (uint32_t)wi ? q - 64u * (uint32_t)wi : 0u;
-                    const unsigned long long mm = m[wi] & (~0ull << qq);
-                    if (!mm) break;
-                    const uint32_t l = (uint32_t)__builtin_ctzll(mm);
-                    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)D[wi], (int)l);
-                    uint32_t Lc = (d >> 16) & 0xFF;
-                    const uint32_t p = uni(r0 + ((64u * (uint32_t)wi + l) << lstep));
-                    const uint32_t e = min(d >> 24, p - cur);  // (cur: the previous match's end)
-                    asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(Ef[wi]) : "s"(e), "{m0}"(l));
-                    if (__builtin_expect(Lc == kZCap, 0)) {
+                    const uint32_t l = q & 63;
+                    uint32_t nxt = (uint32_t)__builtin_amdgcn_readlane((int)Sx[wi], (int)l);
+                    uint32_t tag = q;
+                    if (__builtin_expect(nxt == kZCapped, 0)) {
                         // forwards to the end (within the sub-block): 16 bytes per lane a step,
                         // their word reads issued together
-                        const uint32_t S0 = wlo + (d & 0xFFFF);
+                        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)D[wi], (int)l);
+                        const uint32_t p = uni(r0 + (q << lstep)), S0 = wlo + (d & 0xFFFF);
+                        uint32_t Lc = kZCap;
                         const uint32_t kk = (uint32_t)lane;
                         for (;;) {
                             const uint32_t xf = p + Lc + 16 * kk, xs = S0 + Lc + 16 * kk;
@@ -1222,10 +1277,10 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                             if (xf + 16 <= se) {
                                 uint32_t dd[4];
 #pragma unroll
-                                for (int k = 0; k < 4; ++k) dd[k] = W.word(xs + 4 * k) ^ W.word(xf + 4 * k);
+                                for (int k2 = 0; k2 < 4; ++k2) dd[k2] = W.word(xs + 4 * k2) ^ W.word(xf + 4 * k2);
 #pragma unroll
-                                for (int k = 3; k >= 0; --k)
-                                    if (dd[k]) mis = 4 * (uint32_t)k + ((uint32_t)__builtin_ctz(dd[k]) >> 3);
+                                for (int k2 = 3; k2 >= 0; --k2)
+                                    if (dd[k2]) mis = 4 * (uint32_t)k2 + ((uint32_t)__builtin_ctz(dd[k2]) >> 3);
                             } else {
                                 mis = 0;
                                 while (xf + mis < se && W.byte(xs + mis) == W.byte(xf + mis)) ++mis;
@@ -1239,46 +1294,37 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                             Lc += 1024;
                         }
                         Lc = uni(Lc);
-                        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(Lf[wi]) : "s"(Lc), "{m0}"(l));
+                        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(pathL) : "s"(Lc), "{m0}"(k));
+                        tag = q | 0x400;
+                        // the first match at or after its end
+                        const uint32_t x = uni(q + ((Lc + step - 1) >> lstep));
+                        uint32_t f = kZNone;
+                        if (x < kZRound) {
+                            const uint32_t w0 = x >> 6;
+                            const unsigned long long mm =
+                                (w0 == 0 ? m[0] : w0 == 1 ? m[1] : w0 == 2 ? m[2] : m[3]) & (~0ull << (x & 63));
+                            f = mm ? 64u * w0 + (uint32_t)__builtin_ctzll(mm)
+                                   : (w0 == 0 ? first_from[1] : w0 == 1 ? first_from[2] : w0 == 2 ? first_from[3] : kZNone);
+                        }
+                        nxt = uni(f);
                     }
-                    tk |= 1ull << l;
-                    cur = p + Lc;
-                    q = (cur - r0 + step - 1) >> lstep;
+                    asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(path) : "s"(tag), "{m0}"(k));
+                    ++k;
+                    if (k == 64) {
+                        flush(64);
+                        k = 0;
+                    }
+                    q = nxt;
                 }
-                T[wi] = tk;
             }
+            if (k) flush(k);
             if (probe) {
                 const uint64_t t2 = wall_clock64();
-                probe[32] += t2 - t_walk;  // walk time
+                probe[32] += t2 - t_walk;  // walk time (records inside)
                 t_walk = t2;
             }
-            // the sequences, every lane its taken positions, placed by their rank
-            const bool found = (T[0] | T[1] | T[2] | T[3]) != 0;
             if (found) {
-                uint32_t base = ns;
-#pragma unroll
-                for (int i = 0; i < kZPer; ++i) {
-                    const bool tkn = (T[i] >> lane) & 1ull;
-                    const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(T[i] >> 32),
-                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)T[i], 0u));
-                    if (tkn && rank < kZSubSeq) {
-                        const uint32_t Si = wlo + (D[i] & 0xFFFF);
-                        PBS_GLOBAL uint32_t* const rec = wseq_w + 3 * rank;
-                        rec[0] = P[i] - Ef[i] - hist;
-                        rec[1] = Lf[i] + Ef[i];
-                        rec[2] = P[i] - Si;
-                    }
-                    base += (uint32_t)__builtin_popcountll(T[i]);
-                }
-                ns = uni(base);
-                // the repeat offset of the next round: the last taken match's
-                const int li = T[3] ? 3 : T[2] ? 2 : T[1] ? 1 : 0;
-                const unsigned long long Tl = li == 3 ? T[3] : li == 2 ? T[2] : li == 1 ? T[1] : T[0];
-                const uint32_t l = 63u - (uint32_t)__builtin_clzll(Tl);
-                const uint32_t Dl = li == 3 ? D[3] : li == 2 ? D[2] : li == 1 ? D[1] : D[0];
-                const uint32_t d = uni((uint32_t)__builtin_amdgcn_readlane((int)Dl, (int)l));
-                const uint32_t p = r0 + ((64u * (uint32_t)li + l) << lstep);
-                rep = uni(p - (wlo + (d & 0xFFFF)));
+                cur = carry;  // the last match's end
                 lastend = cur - hist;
             }
             if (probe) probe[42] += wall_clock64() - t_walk;  // sequence records
