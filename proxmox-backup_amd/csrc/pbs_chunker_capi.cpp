@@ -131,6 +131,7 @@ struct ScanServer {
     ServerMailbox* mb_dev = nullptr;
     ServerReq* req = nullptr;  // host view of the request record (the mailbox's, or in VRAM)
     ServerReq* req_dev = nullptr;
+    ServerDispatch* disp_dev = nullptr;  // split requests (in the VRAM allocation; none without it)
     uint8_t* slot = nullptr;  // host view
     uint8_t* slot_dev = nullptr;
     uint8_t* hslot = nullptr;  // pinned host slot (the slot itself without VRAM; else the
@@ -142,6 +143,9 @@ struct ScanServer {
     bool running = false;
     bool enabled = true;  // PBS_SCAN_SERVER=0: every scan() takes the batch path (A/B)
     bool broken = false;  // a request timed out: never used again by this handle
+    uint32_t n_wg = kSrvDefaultWgs;  // PBS_SERVER_WGS: workgroups (1 = the one-workgroup server)
+    uint32_t epoch = 0;              // launches so far (ServerDispatch tags)
+    uint64_t vram_max = kServerVramMax;  // PBS_SERVER_VRAM_MAX: longer requests use the pinned slot (A/B)
     uint32_t flags = 0;  // PBS_SERVER_POLL=4: lane 0 of every wave polls, staggered (A/B; no faster)
     // PBS_SERVER_PROBE=1: requests, host round trip (us) and the kernel's phases (ticks of
     // 10 ns: request seen -> staged -> hashed -> acknowledged), printed when the handle is freed
@@ -702,8 +706,11 @@ int server_launch(pbs_chunker* c, uint64_t last) {
     ScanServer& sv = c->srv;
     __atomic_store_n(&sv.mb->exited, ~0ull, __ATOMIC_RELEASE);
     const uint32_t flags = sv.flags | (sv.vram ? kSrvDevReq : 0u);
-    HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.req_dev, sv.slot_dev, sv.hslot_dev, c->d_table.as<uint32_t>(), c->prm.thr,
-                                  last, kServerIdleTicks, flags, sv.stream));
+    sv.epoch = (sv.epoch + 1) & 0x7FFFFFFFu;
+    if (!sv.epoch) sv.epoch = 1;  // 0 is the header's initial state
+    HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.req_dev, sv.disp_dev, sv.slot_dev, sv.hslot_dev,
+                                  c->d_table.as<uint32_t>(), c->prm.thr, last, kServerIdleTicks, flags,
+                                  sv.disp_dev ? sv.n_wg : 1u, sv.epoch, sv.stream));
     sv.running = true;
     return PBS_OK;
 }
@@ -716,9 +723,9 @@ int server_launch(pbs_chunker* c, uint64_t last) {
 void server_map_vram(pbs_chunker* c) {  // on the handle's device (server_scan's guard)
     ScanServer& sv = c->srv;
     void* p = nullptr;
-    // the request record, then the slot: only requests up to kServerVramMax use it (longer
-    // ones go to the pinned host slot)
-    const size_t bytes = 256 + kServerHist + kServerVramMax;
+    // the request record, the dispatch record, then the slot: only requests up to vram_max
+    // use it (longer ones go to the pinned host slot)
+    const size_t bytes = kServerHeader + kServerHist + sv.vram_max;
     if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess || !p) return;
     bool mapped = false;
     int fds[2];
@@ -729,7 +736,7 @@ void server_map_vram(pbs_chunker* c) {  // on the handle's device (server_scan's
     }
     if (mapped) {
         ServerReq* r = static_cast<ServerReq*>(p);
-        std::memset(r, 0, sizeof(ServerReq));
+        std::memset(r, 0, kServerHeader);  // ServerDispatch tag 0: no launch's epoch
         r->pad0[0] = 0x5CA17E57u;
         __builtin_ia32_sfence();
         ServerReq back{};
@@ -744,7 +751,8 @@ void server_map_vram(pbs_chunker* c) {  // on the handle's device (server_scan's
     }
     sv.vram = p;
     sv.req = sv.req_dev = static_cast<ServerReq*>(p);
-    sv.slot = sv.slot_dev = static_cast<uint8_t*>(p) + 256;
+    sv.disp_dev = reinterpret_cast<ServerDispatch*>(static_cast<uint8_t*>(p) + 128);
+    sv.slot = sv.slot_dev = static_cast<uint8_t*>(p) + kServerHeader;
 }
 
 // scan() of host bytes [pos, pos + bl) through the scan server: their candidates are
@@ -776,7 +784,7 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
     }
     // slot: the history right-aligned in its first kServerHist bytes, then the data; long
     // requests of a VRAM-mode server go to the pinned slot (kServerVramMax)
-    const bool host_slot = sv.vram && bl > kServerVramMax;
+    const bool host_slot = sv.vram && bl > sv.vram_max;
     uint8_t* const slot = host_slot ? sv.hslot : sv.slot;
     std::memcpy(slot + kServerHist - c->carry_len, c->carry, c->carry_len);
     std::memcpy(slot + kServerHist, hsrc, bl);
@@ -824,6 +832,8 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
     const size_t old = c->pending.size();
     c->pending.resize(old + k);
     std::memcpy(c->pending.data() + old, sv.mb->cand, k * 8);
+    // a request split over workgroups returns their runs in the order they reserved slots
+    std::sort(c->pending.begin() + (ptrdiff_t)old, c->pending.end());
     c->timing.bytes += bl;
     c->timing.candidates += k;
     update_carry(c, hsrc, bl);
@@ -1559,6 +1569,14 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     }
     if (const char* e = std::getenv("PBS_SCAN_SERVER")) c->srv.enabled = e[0] != '0';
     if (const char* e = std::getenv("PBS_SERVER_VRAM")) c->srv.dev_req = e[0] != '0';
+    if (const char* e = std::getenv("PBS_SERVER_WGS")) {
+        const long v = std::atol(e);
+        c->srv.n_wg = v < 1 ? 1u : (v > (long)kSrvMaxWgs ? kSrvMaxWgs : (uint32_t)v);
+    }
+    if (const char* e = std::getenv("PBS_SERVER_VRAM_MAX")) {
+        const long long v = std::atoll(e);
+        c->srv.vram_max = v < 0 ? 0 : std::min<uint64_t>((uint64_t)v, kServerMaxBytes);
+    }
     if (const char* e = std::getenv("PBS_SCAN_PASS")) c->scan_pass = e[0] != '0';
     if (const char* e = std::getenv("PBS_SERVER_POLL")) c->srv.flags = e[0] == '4' ? kSrvPollAll : 0u;
     if (const char* e = std::getenv("PBS_SERVER_PROBE"))

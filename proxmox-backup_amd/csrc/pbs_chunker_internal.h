@@ -211,11 +211,31 @@ constexpr uint32_t kServerCand = 16384;         // candidates one request may re
 constexpr uint32_t kServerHist = 64;            // slot bytes before the data: the history
 constexpr uint32_t kServerQuit = 1u << 31;      // req_len flag
 constexpr uint32_t kServerHostSlot = 1u << 30;  // req_len flag: the data are in the pinned host slot
-// requests up to this size go to the VRAM slot when there is one: the host's write-combined
-// BAR stores (~47 GB/s) beat the kernel's PCIe reads of pinned memory for short requests
-// only (8 KiB 7.2 -> 4.9 us round trip, 256 KiB reads 3.8 -> 3.6 GB/s, mb_bar.hip and
-// profiles/r03/vram)
-constexpr uint32_t kServerVramMax = 128u << 10;
+// requests up to this size go to the VRAM slot when there is one (PBS_SERVER_VRAM_MAX for
+// A/B): the host's write-combined BAR stores (~47 GB/s) beat the kernel's PCIe reads of
+// pinned memory (8 KiB 7.2 -> 4.9 us round trip, mb_bar.hip).  Until round 5 it was 128 KiB:
+// one workgroup hashing ~6 GB/s made the copy's speed moot for longer requests
+// (profiles/r03/vram); with several workgroups per request (kSrvMaxWgs) it is not.
+constexpr uint32_t kServerVramMax = kServerMaxBytes;
+// Requests of at least 2 kSrvMinPasses passes are split over up to `n_wg` workgroups of the
+// server (PBS_SERVER_WGS): workgroup 0 polls the host's record and publishes such a
+// request here, in the same fine-grained VRAM allocation (+128 bytes); the others poll
+// this record (one L2/HBM load, no PCIe), each hashes a contiguous range of passes,
+// reserves candidate slots with a device atomic and counts itself done; the last one
+// stores the acknowledgement.  tag = seq | epoch << 32 | quit << 63 (epoch: the launch
+// number, so a record left by an earlier launch is never taken for a request).
+struct alignas(64) ServerDispatch {
+    uint64_t tag;
+    uint32_t len;   // the record's req_len (kServerHostSlot kept)
+    uint32_t gu;    // workgroups serving this request
+    uint64_t base;
+    uint32_t cnt_cand;  // candidates reserved so far
+    uint32_t cnt_done;  // workgroups done
+};
+constexpr uint32_t kSrvMaxWgs = 32;
+constexpr uint32_t kSrvDefaultWgs = 16;
+constexpr uint32_t kServerHeader = 256;  // VRAM allocation: record (0), dispatch (128), then the slot
+static_assert(sizeof(ServerDispatch) <= kServerHeader - 128, "dispatch record past the header");
 struct alignas(64) ServerMailbox {
     // host -> device: ONE 16-byte record the kernel polls with one load (the host stores
     // len and base before seq, all in one cache line, so a record with the new seq has them)
@@ -247,10 +267,10 @@ static_assert(sizeof(ServerReq) == 64, "ServerReq is one cache line");
 constexpr uint32_t kSrvPollAll = 1;  // launch flag: every wave polls (staggered), not one lane
 constexpr uint32_t kSrvProbe = 2;    // launch flag: per-request phase stamps into probe[]
 constexpr uint32_t kSrvDevReq = 4;   // launch flag: request + slot in fine-grained VRAM written by the host
-hipError_t launch_scan_server(ServerMailbox* mb_dev, const ServerReq* req_dev, const uint8_t* slot_dev,
-                              const uint8_t* hslot_dev, const uint32_t* table_rot,
+hipError_t launch_scan_server(ServerMailbox* mb_dev, const ServerReq* req_dev, ServerDispatch* disp_dev,
+                              const uint8_t* slot_dev, const uint8_t* hslot_dev, const uint32_t* table_rot,
                               uint32_t thr, uint64_t last_seq, uint64_t idle_ticks,
-                              uint32_t flags, hipStream_t stream);
+                              uint32_t flags, uint32_t n_wg, uint32_t epoch, hipStream_t stream);
 
 // Makes `dev` the calling thread's current device for a scope (allocations and stream /
 // event creation land on the current device, not on the device of the stream a call was

@@ -1028,12 +1028,14 @@ hipError_t launch_fused_gather(const unsigned long long* rec, uint64_t nrec, uin
     return hipGetLastError();
 }
 
-hipError_t launch_scan_server(ServerMailbox* mb_dev, const ServerReq* req_dev, const uint8_t* slot_dev,
-                              const uint8_t* hslot_dev, const uint32_t* table_rot, uint32_t thr, uint64_t last_seq,
-                              uint64_t idle_ticks, uint32_t flags, hipStream_t stream) {
+hipError_t launch_scan_server(ServerMailbox* mb_dev, const ServerReq* req_dev, ServerDispatch* disp_dev,
+                              const uint8_t* slot_dev, const uint8_t* hslot_dev, const uint32_t* table_rot,
+                              uint32_t thr, uint64_t last_seq, uint64_t idle_ticks, uint32_t flags, uint32_t n_wg,
+                              uint32_t epoch, hipStream_t stream) {
     (void)hipGetLastError();
-    hipLaunchKernelGGL(scan_server_kernel, dim3(1), dim3(kSrvThreads), 0, stream, mb_dev, req_dev, slot_dev,
-                       hslot_dev, table_rot, thr, last_seq, idle_ticks, flags);
+    if (n_wg < 1 || n_wg > kSrvMaxWgs || (n_wg > 1 && !disp_dev)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(scan_server_kernel, dim3(n_wg), dim3(kSrvThreads), 0, stream, mb_dev, req_dev, disp_dev,
+                       slot_dev, hslot_dev, table_rot, thr, last_seq, idle_ticks, flags, n_wg, epoch);
     return hipGetLastError();
 }
 

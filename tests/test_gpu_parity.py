@@ -333,15 +333,29 @@ def test_scan_feed_granularity(gpu, oracle, feed, avg, n):
     assert np.array_equal(np.array(got, dtype=np.uint64), ref)
 
 
-@pytest.mark.parametrize("vram", ["1", "0"])
-@pytest.mark.parametrize("feed", [8192, 256 * KiB + 3])
-def test_scan_server_request_placement(gpu, oracle, monkeypatch, vram, feed):
-    """scan() per read with the server's request record + slot in BAR-written VRAM (default;
-    requests over 128 KiB in the pinned slot) and in pinned host memory
-    (PBS_SERVER_VRAM=0): the oracle's cuts either way, over many requests that reuse the
-    same slots (stale lines would show here)."""
-    monkeypatch.setenv("PBS_SERVER_VRAM", vram)
-    n, avg = 6 * MiB + 333, 64 * KiB
+SERVER_MODES = {  # PBS_SERVER_VRAM, PBS_SERVER_VRAM_MAX, PBS_SERVER_WGS
+    "vram": ("1", None, None),             # default: BAR-written slot, requests split over 16 WGs
+    "vram-host-slot": ("1", "131072", None),  # requests over 128 KiB split, read from the pinned slot
+    "vram-one-wg": ("1", None, "1"),       # the one-workgroup server
+    "pinned": ("0", None, None),           # record + slot in pinned host memory (one workgroup)
+}
+
+
+@pytest.mark.parametrize("mode", list(SERVER_MODES))
+@pytest.mark.parametrize("feed,avg", [(8192, 64 * KiB), (256 * KiB + 3, 64 * KiB),
+                                      (1 * MiB, 64 * KiB), (1 * MiB, 1 * KiB)])
+def test_scan_server_request_placement(gpu, oracle, monkeypatch, mode, feed, avg):
+    """scan() per read with the server's request record + slot in BAR-written VRAM (default),
+    long requests in the pinned slot, one workgroup, and everything in pinned host memory
+    (PBS_SERVER_VRAM=0): the oracle's cuts every way, over many requests that reuse the
+    same slots (stale lines would show here); avg 1 KiB puts hundreds of candidates of
+    one request in every workgroup's range (the atomic reservation + host sort)."""
+    for var, val in zip(("PBS_SERVER_VRAM", "PBS_SERVER_VRAM_MAX", "PBS_SERVER_WGS"), SERVER_MODES[mode]):
+        if val is None:
+            monkeypatch.delenv(var, raising=False)
+        else:
+            monkeypatch.setenv(var, val)
+    n = 6 * MiB + 333
     data = gen_np.gen_random(n, 0x5EED0011)
     ref = oracle.chunk_feed(avg, data, 0)
     got = []
