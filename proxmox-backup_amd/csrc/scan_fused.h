@@ -61,8 +61,9 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 }
 
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {  // wave-uniform value into SGPRs
-    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+    // (readfirstlane returns int: through uint32_t, or the low word sign-extends)
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
 
 __device__ __forceinline__ void store_wt(uint64_t* p, uint64_t v) {  // write-through (sc1)

@@ -578,6 +578,11 @@ FUSED_CASES = [
     ("zebra_64x(600K+200K)_128K", lambda: _zebra(64, 600 * KiB, 200 * KiB, 45), 128 * KiB, 3),
     ("vm_300M_128K", lambda: gen_np.gen_vmimage(300 * MiB, 0x5EED0003, 3 * GiB), 128 * KiB, 1),
     ("random_200M_256K_x7", lambda: gen_np.gen_random(200 * MiB + 9, 46), 256 * KiB, 7),
+    # 64 KiB averages forced through the one-launch pass (the product serves them with the
+    # scan pass; random bytes make it stand down: > 64 flagged blocks per tile)
+    ("vm_96M+5_64K_x3", lambda: gen_np.gen_vmimage(96 * MiB + 5, 0x5EED0003, 9 * GiB), 64 * KiB, 3),
+    ("random_72M+3_64K_x2", lambda: gen_np.gen_random(72 * MiB + 3, 47), 64 * KiB, 2),
+    ("holes_64M_64K_x4", lambda: _holes(64 * MiB + 11, 48, 2 * MiB), 64 * KiB, 4),
 ]
 
 
@@ -594,12 +599,44 @@ def test_fused_pass(gpu, oracle, monkeypatch, name, mk, avg, pieces):
     bounds[1:-1] += 4093  # unaligned piece starts
     for fused in ("1", "0"):
         monkeypatch.setenv("PBS_FUSED", fused)
+        monkeypatch.setenv("PBS_FUSED_MIN_AVG", "65536")
         got = []
         with gpu.Chunker(avg) as c:
             for a, b in zip(bounds[:-1], bounds[1:]):
                 got.append(c.find_cuts(data[a:b], is_final=b == n))
         got = np.concatenate(got)
         assert np.array_equal(got, ref), (name, fused, got.size, ref.size)
+
+
+@pytest.mark.parametrize("kind,avg", [(1, 64 * KiB), (2, 64 * KiB), (2, 128 * KiB), (1, 4 * MiB)],
+                         ids=["random-64K", "vm-64K", "vm-128K", "random-4M"])
+def test_fused_pass_pinned_out(gpu, oracle, monkeypatch, kind, avg):
+    """A pass from HBM into the caller's pinned cut array (as bench.py hands it), 640 MiB + 5
+    split in two calls, the one-launch pass forced from 64 KiB: the oracle's cuts (random
+    bytes at 64 KiB stand down to the multi-launch path)."""
+    import torch
+    monkeypatch.setenv("PBS_FUSED", "1")
+    monkeypatch.setenv("PBS_FUSED_MIN_AVG", "65536")
+    n = 640 * MiB + 5
+    seed = 0x5EED0002 if kind == 1 else 0x5EED0003
+    n8 = (n + 7) // 8 * 8
+    dev = torch.empty(n8, dtype=torch.uint8, device="cuda")
+    gpu.generate_device(dev.data_ptr(), n8, kind, seed, 0)
+    host = dev[:n].cpu().numpy()
+    got = []
+    with gpu.Chunker(avg) as c:
+        half = 300 * MiB + 3
+        for a, b in ((0, half), (half, n)):
+            out = torch.empty(c.cuts_bound(b - a), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+            got.append(c.find_cuts_device(dev.data_ptr() + a, b - a, is_final=b == n, out=out).copy())
+            if avg >= 128 * KiB:
+                assert c.last_timing()["fused"] == b - a
+    del dev
+    got = np.concatenate(got)
+    ref = oracle.chunk_feed(avg, host)
+    if ref.size == 0 or int(ref[-1]) != n:
+        ref = np.append(ref, np.uint64(n))
+    assert np.array_equal(got, ref)
 
 
 def test_fused_pass_stands_down_on_dense_input(gpu, oracle, monkeypatch):
