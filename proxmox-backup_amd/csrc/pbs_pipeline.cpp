@@ -94,6 +94,8 @@ struct PipeArea {
     void drop_streams() {
         if (s_copy) (void)hipStreamDestroy(s_copy);
         if (s_scan) (void)hipStreamDestroy(s_scan);
+        if (s_up) (void)hipStreamDestroy(s_up);
+        s_up = nullptr;
         for (auto& s : s_dig)
             if (s) {
                 pbs::release_stream_counter(s);
@@ -108,7 +110,7 @@ struct PipeArea {
     pbs_chunker* c = nullptr;
     size_t avg = 0;
     int dig = -1;  // digest CUs the streams are masked for
-    hipStream_t s_copy = nullptr, s_scan = nullptr, s_dig[kDigestStreams] = {};
+    hipStream_t s_copy = nullptr, s_scan = nullptr, s_up = nullptr, s_dig[kDigestStreams] = {};
     std::vector<hipEvent_t> ev;
     uint8_t* hq = nullptr;
     size_t hq_bytes = 0;
@@ -182,6 +184,16 @@ struct UploadExt {
     uint64_t* blob_offsets;
     uint8_t* compressed;
     pbs_upload_timing* t;
+    // a full backup (no previous index): every chunk's blob is encoded as its piece is
+    // chunked, beside the copies (`spec`), into the device area at b_off[i] (b_len[i] bytes);
+    // upload_stage then only tests for repeats and copies the new ones out
+    bool spec = false;
+    uint8_t* d_blobs = nullptr;
+    std::vector<uint64_t> b_off, b_len;
+    std::vector<uint8_t> b_comp;
+    double enc_ms = 0;
+    pbs_blob_encode_timing enc_t{};
+    int enc_rc = PBS_OK;
 };
 
 int upload_stage(UploadExt& x, pbs::DevArena* area, const uint8_t* d_data, size_t len, const uint64_t* ends,
@@ -231,7 +243,8 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     if (A->dig != dig) {  // CU masks for this split
         A->drop_streams();
         ok = hip_ok(hipStreamCreateWithFlags(&A->s_copy, hipStreamNonBlocking)) &&
-             hip_ok(masked_stream(&A->s_scan, dig, ncu - dig, ncu));
+             hip_ok(masked_stream(&A->s_scan, dig, ncu - dig, ncu)) &&
+             hip_ok(masked_stream(&A->s_up, dig, ncu - dig, ncu));
         for (auto& s : A->s_dig) ok = ok && hip_ok(masked_stream(&s, 0, dig, ncu));
         if (ok) A->dig = dig;
     }
@@ -435,6 +448,85 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         });
     }
 
+    // the upload's speculative blob encoder (UploadExt::spec): the chunks of each piece, in
+    // order, as the main loop finds them, on the scan's CUs (its own stream, after the piece's
+    // copy); encoding is GPU work beside DMA copies, so the blobs are ready when the digests
+    // are.  With a previous index most chunks may be known: encoding waits for the test then.
+    std::deque<std::array<size_t, 3>> upq;  // {first chunk, end chunk, piece}
+    std::mutex upmu;
+    std::condition_variable upcv;
+    bool updone = false;
+    std::thread upw;
+    if (ok && ext && ext->n_known == 0 && env_u64("PBS_UPLOAD_SPEC", 1) != 0) {
+        const size_t bcap = len + 16 * cap + 64;
+        ext->d_blobs = area->get<uint8_t>(9, bcap, false);
+        if (ext->d_blobs) {
+            ext->b_off.assign(cap, 0);
+            ext->b_len.assign(cap, 0);
+            ext->b_comp.assign(cap, 0);
+            ext->spec = true;
+            hipStream_t const su = A->s_up;
+            upw = std::thread([&, bcap, su] {
+                (void)hipSetDevice(dev);
+                uint64_t off = 0;
+                std::vector<uint64_t> spans, offm;
+                std::vector<uint8_t> compm;
+                for (;;) {
+                    std::array<size_t, 3> b;
+                    {
+                        std::unique_lock<std::mutex> g(upmu);
+                        upcv.wait(g, [&] { return updone || !upq.empty(); });
+                        if (upq.empty()) break;
+                        b = upq.front();
+                        upq.pop_front();
+                    }
+                    if (ext->enc_rc != PBS_OK) continue;  // drain after an error
+                    const size_t i0 = b[0], m = b[1] - b[0];
+                    spans.resize(2 * m);
+                    offm.assign(m + 1, 0);
+                    compm.assign(m, 0);
+                    for (size_t k = 0; k < m; ++k) {
+                        spans[2 * k] = i0 + k ? ends[i0 + k - 1] : 0;
+                        spans[2 * k + 1] = ends[i0 + k];
+                    }
+                    const Clock::time_point te = Clock::now();
+                    pbs_blob_encode_timing bt{};
+                    int r = hipStreamWaitEvent(su, ev_copied[b[2]], 0) == hipSuccess ? PBS_OK : PBS_ERR_HIP;
+                    if (r == PBS_OK)
+                        r = pbs_blob_encode_spans_device(d_data, len, 0, spans.data(), m, ext->compress, ext->d_blobs + off,
+                                                         bcap - off, offm.data(), nullptr, compm.data(), &bt, su);
+                    ext->enc_ms += ms_since(te);
+                    if (r != PBS_OK) {
+                        ext->enc_rc = r;
+                        continue;
+                    }
+                    ext->enc_t.compress_ms += bt.compress_ms;
+                    ext->enc_t.assemble_ms += bt.assemble_ms;
+                    ext->enc_t.crc_ms += bt.crc_ms;
+                    ext->enc_t.bytes_in += bt.bytes_in;
+                    ext->enc_t.bytes_out += bt.bytes_out;
+                    ext->enc_t.blocks += bt.blocks;
+                    ext->enc_t.compressed_chunks += bt.compressed_chunks;
+                    for (size_t k = 0; k < m; ++k) {
+                        ext->b_off[i0 + k] = off + offm[k];
+                        ext->b_len[i0 + k] = offm[k + 1] - offm[k];
+                        ext->b_comp[i0 + k] = compm[k];
+                    }
+                    off = (off + offm[m] + 15) & ~15ull;
+                }
+            });
+        }
+    }
+    auto up_finish = [&] {  // every path: the encoder thread ends before its state does
+        if (!upw.joinable()) return;
+        {
+            std::lock_guard<std::mutex> g(upmu);
+            updone = true;
+        }
+        upcv.notify_all();
+        upw.join();
+    };
+
     double chunk_ms = 0, last_chunk_at = 0;
     size_t n = 0, nb = 0, launches = 0, launched = 0;
     uint64_t start = 0;  // start of the first chunk not yet digested
@@ -478,6 +570,13 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         if (m) {
             std::memcpy(ends + n, tmp.data(), m * 8);
             n += m;
+        }
+        if (upw.joinable() && n > n0) {
+            {
+                std::lock_guard<std::mutex> g(upmu);
+                upq.push_back({n0, n, k});
+            }
+            upcv.notify_one();
         }
         // route the chunks completed in this piece: the GPU's digest queue when the chain
         // ends before the copy's projected end (+ slack), else the host threads
@@ -598,6 +697,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         work();
         for (auto& th : fb) th.join();
     }
+    up_finish();
     // the upload's part after the digests: known-chunk test and blobs, from the HBM copy
     // (on the copy stream: not CU-masked, idle since the last piece landed)
     if (ext && rc == PBS_OK) rc = upload_stage(*ext, area, d_data, len, ends, digests, n, s_copy);
@@ -658,6 +758,48 @@ int upload_stage(UploadExt& x, pbs::DevArena* area, const uint8_t* d_data, size_
         hipStreamSynchronize(st) != hipSuccess)
         return PBS_ERR_HIP;
     const Clock::time_point t1 = Clock::now();
+    if (x.spec) {
+        // the blobs were encoded beside the copies: the new ones out of the device area in
+        // runs of adjacent blobs, in chunk order
+        if (x.enc_rc != PBS_OK) return x.enc_rc;
+        uint64_t size_reused = 0, compressed_chunks = 0;
+        x.blob_offsets[0] = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const bool fresh = !x.known_out[i];
+            if (!fresh) size_reused += ends[i] - (i ? ends[i - 1] : 0);
+            x.blob_offsets[i + 1] = x.blob_offsets[i] + (fresh ? x.b_len[i] : 0);
+            if (x.compressed) x.compressed[i] = fresh ? x.b_comp[i] : 0;
+            compressed_chunks += fresh ? x.b_comp[i] : 0;
+        }
+        if (x.blob_offsets[n] > x.blobs_cap) return PBS_ERR_CAPACITY;
+        for (size_t i = 0; i < n;) {
+            if (x.known_out[i]) {
+                ++i;
+                continue;
+            }
+            size_t j = i + 1;
+            while (j < n && !x.known_out[j] && x.b_off[j] == x.b_off[j - 1] + x.b_len[j - 1]) ++j;
+            const uint64_t bytes = x.b_off[j - 1] + x.b_len[j - 1] - x.b_off[i];
+            if (bytes && hipMemcpyAsync(x.blobs + x.blob_offsets[i], x.d_blobs + x.b_off[i], bytes,
+                                        hipMemcpyDeviceToHost, st) != hipSuccess)
+                return PBS_ERR_HIP;
+            i = j;
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) return PBS_ERR_HIP;
+        if (t) {
+            t->known_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+            t->encode_ms = x.enc_ms;  // beside the copies (not on this stage's clock)
+            t->d2h_ms = ms_since(t1);
+            t->blob = x.enc_t;
+            t->chunk_count = n;
+            t->chunk_reused = reused;
+            t->size = len;
+            t->size_reused = size_reused;
+            t->size_compressed = x.blob_offsets[n];
+            t->compressed_chunks = compressed_chunks;
+        }
+        return PBS_OK;
+    }
     // the new chunks as spans of the stream
     std::vector<uint64_t> spans;
     std::vector<size_t> idx;

@@ -2471,7 +2471,20 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
     (void)exclusive_sum_u64(nullptr, &t1b, nullptr, nullptr, (uint32_t)(n + 1), st);
     (void)exclusive_sum_u64(nullptr, &t2b, nullptr, nullptr, (uint32_t)(ni + 1), st);
     size_t tmpb = std::max(t1b, t2b);
-    const unsigned grid = (unsigned)std::min<uint64_t>(ni, (uint64_t)ncu);  // one 512-thread workgroup per CU
+    // one 512-thread workgroup per CU the stream may use (a CU-masked stream, e.g. the upload
+    // path's beside the digest queue, gets as many workgroups as its mask has CUs: the items
+    // are dealt statically, and a workgroup waiting for a CU would hold the whole kernel)
+    int use_cu = ncu;
+    {
+        uint32_t mask[16] = {};
+        if (ncu <= 512 && hipExtStreamGetCUMask(st, 16, mask) == hipSuccess) {
+            int bits = 0;
+            for (uint32_t w : mask) bits += __builtin_popcount(w);
+            if (bits > 0 && bits < use_cu) use_cu = bits;
+        }
+        (void)hipGetLastError();
+    }
+    const unsigned grid = (unsigned)std::min<uint64_t>(ni, (uint64_t)use_cu);
     ArenaLease ar(zpool(), dev);
     uint64_t* d_bounds = ar->get<uint64_t>(kZsBounds, 2 * n * 8);
     uint64_t* d_items = ar->get<uint64_t>(kZsItems, ni * 8);
