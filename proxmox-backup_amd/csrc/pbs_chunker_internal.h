@@ -301,7 +301,8 @@ struct DigestJob {   // in pinned host memory, written by the host before the co
     uint64_t start;  // chunk start, bytes from the device buffer's start
     uint64_t len;
     uint64_t idx;    // output slot (the chunk's index): digests + 32 * idx
-    uint64_t pad;
+    uint64_t done;   // written 1 by the GPU once the digest is in memory (system-scope release
+                     // before it): the upload path's encoder waits for it (the host zeroes it)
 };
 struct DigestQueueDev {  // device memory, zeroed before the launch
     unsigned long long next;       // jobs claimed

@@ -425,7 +425,7 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_chunks_split_kernel(
 // relaunches the grid when it publishes jobs after that.  Exiting when idle matters: a resident grid holds up whatever waits
 // for the whole device or for its stream (hipFree, null-stream copies).
 __global__ __launch_bounds__(64 * kShaWaves) void sha256_queue_kernel(
-    const uint8_t* __restrict__ data, DigestKey key, const volatile DigestJob* __restrict__ jobs,
+    const uint8_t* __restrict__ data, DigestKey key, volatile DigestJob* __restrict__ jobs,
     const volatile uint64_t* __restrict__ ctl_host, DigestQueueDev* __restrict__ q, uint8_t* __restrict__ digests,
     uint64_t idle_ticks) {
     __shared__ uint4 sw[3][16][64];
@@ -495,6 +495,13 @@ __global__ __launch_bounds__(64 * kShaWaves) void sha256_queue_kernel(
             idx = jobs[j0 + lane].idx;
         }
         sha_batch(data, st0, st0 + len, live, key, digests + 32 * idx, sw, s_blocks);
+        // every wave's digest stores out to memory, then the jobs say done (pinned host
+        // memory: the upload path's encoder reads the digests as soon as it sees the flags)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (threadIdx.x < 64 && live)
+            __hip_atomic_store(const_cast<uint64_t*>(&jobs[j0 + lane].done), (uint64_t)1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
         t_job = wall_clock64();  // idle from here: look for new jobs for idle_ticks
         __syncthreads();         // s_j0 / s_k and the LDS are reused
     }
@@ -624,7 +631,7 @@ hipError_t launch_sha256_queue(const uint8_t* data, const uint8_t* key, size_t k
     k.len = (uint32_t)key_len;
     if (key_len) std::memcpy(k.bytes, key, key_len);
     hipLaunchKernelGGL(sha256_queue_kernel, dim3((unsigned)grid), dim3(64 * kShaWaves), 0, st, data, k,
-                       (const volatile DigestJob*)jobs_dev, (const volatile uint64_t*)ctl_dev, q, digests,
+                       (volatile DigestJob*)const_cast<DigestJob*>(jobs_dev), (const volatile uint64_t*)ctl_dev, q, digests,
                        idle_ticks);
     return hipGetLastError();
 }

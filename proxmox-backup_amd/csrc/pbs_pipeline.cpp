@@ -45,7 +45,9 @@
 #include <map>
 #include <mutex>
 #include <numeric>
+#include <memory>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "pbs_blob.h"
@@ -95,7 +97,9 @@ struct PipeArea {
         if (s_copy) (void)hipStreamDestroy(s_copy);
         if (s_scan) (void)hipStreamDestroy(s_scan);
         if (s_up) (void)hipStreamDestroy(s_up);
-        s_up = nullptr;
+        if (s_dh) (void)hipStreamDestroy(s_dh);
+        if (s_full) (void)hipStreamDestroy(s_full);
+        s_up = s_dh = s_full = nullptr;
         for (auto& s : s_dig)
             if (s) {
                 pbs::release_stream_counter(s);
@@ -110,7 +114,8 @@ struct PipeArea {
     pbs_chunker* c = nullptr;
     size_t avg = 0;
     int dig = -1;  // digest CUs the streams are masked for
-    hipStream_t s_copy = nullptr, s_scan = nullptr, s_up = nullptr, s_dig[kDigestStreams] = {};
+    hipStream_t s_copy = nullptr, s_scan = nullptr, s_up = nullptr, s_dh = nullptr, s_full = nullptr,
+                s_dig[kDigestStreams] = {};
     std::vector<hipEvent_t> ev;
     uint8_t* hq = nullptr;
     size_t hq_bytes = 0;
@@ -184,14 +189,12 @@ struct UploadExt {
     uint64_t* blob_offsets;
     uint8_t* compressed;
     pbs_upload_timing* t;
-    // a full backup (no previous index): every chunk's blob is encoded as its piece is
-    // chunked, beside the copies (`spec`), into the device area at b_off[i] (b_len[i] bytes);
-    // upload_stage then only tests for repeats and copies the new ones out
+    // `spec`: the known test, the encoding and the blobs' copy run per piece beside the
+    // copies (pipeline_run's upload worker); upload_stage then only checks and counts
     bool spec = false;
     uint8_t* d_blobs = nullptr;
-    std::vector<uint64_t> b_off, b_len;
-    std::vector<uint8_t> b_comp;
-    double enc_ms = 0;
+    size_t n_done = 0;  // chunks whose known flag, blob range and compressed flag are out
+    double known_ms = 0, enc_ms = 0, d2h_ms = 0;
     pbs_blob_encode_timing enc_t{};
     int enc_rc = PBS_OK;
 };
@@ -244,7 +247,9 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         A->drop_streams();
         ok = hip_ok(hipStreamCreateWithFlags(&A->s_copy, hipStreamNonBlocking)) &&
              hip_ok(masked_stream(&A->s_scan, dig, ncu - dig, ncu)) &&
-             hip_ok(masked_stream(&A->s_up, dig, ncu - dig, ncu));
+             hip_ok(masked_stream(&A->s_up, dig, ncu - dig, ncu)) &&
+             hip_ok(hipStreamCreateWithFlags(&A->s_dh, hipStreamNonBlocking)) &&
+             hip_ok(hipStreamCreateWithFlags(&A->s_full, hipStreamNonBlocking));
         for (auto& s : A->s_dig) ok = ok && hip_ok(masked_stream(&s, 0, dig, ncu));
         if (ok) A->dig = dig;
     }
@@ -378,6 +383,11 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     std::map<uint64_t, std::array<uint8_t, 32>> zero_dig;  // digest of an all-zero chunk per length
     std::vector<std::thread> hpool;
     hmask.assign(ok ? cap : 0, 0);
+    // the upload path's encoder waits per chunk for its digest: a host-routed chunk's flag
+    // here, a GPU job's `done` in the job record; dig_final once every digest is in `digests`
+    std::unique_ptr<std::atomic<uint8_t>[]> hflag(new std::atomic<uint8_t>[ok ? cap : 1]());
+    std::vector<uint64_t> jobof(ok ? cap : 0, 0);
+    std::atomic<bool> dig_final{false};
     // one host worker: takes routed chunks until the queue is empty and the routing done,
     // up to four in step (pbs::sha256_host_lanes); an all-zero chunk is hashed once per length
     auto host_work = [&] {
@@ -400,6 +410,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
                     if (it != zero_dig.end()) {
                         std::memcpy(out, it->second.data(), 32);
                         host_chunks += 1;
+                        hflag[i].store(1, std::memory_order_release);
                         continue;
                     }
                 }
@@ -414,6 +425,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
             }
             host_chunks += 1;
             host_bytes += j.len;
+            hflag[(size_t)(j.out - digests) / 32].store(1, std::memory_order_release);
             const uint64_t us = (uint64_t)(ms_since(t0) * 1000.0);
             for (uint64_t cur = host_work_us.load(); us > cur && !host_work_us.compare_exchange_weak(cur, us);) {
             }
@@ -448,29 +460,46 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         });
     }
 
-    // the upload's speculative blob encoder (UploadExt::spec): the chunks of each piece, in
-    // order, as the main loop finds them, on the scan's CUs (its own stream, after the piece's
-    // copy); encoding is GPU work beside DMA copies, so the blobs are ready when the digests
-    // are.  With a previous index most chunks may be known: encoding waits for the test then.
+    // the upload's per-piece stage (UploadExt::spec): for each piece's chunks, as the main
+    // loop finds them -- wait for their digests, the known-chunk test against the previous
+    // index and the earlier chunks of the stream (the client's HashSet, backup_writer.rs:
+    // 677-697), encode the new chunks' blobs on the scan partition's CUs (its own stream,
+    // after the piece's copy), and copy them out to their final place in the caller's buffer;
+    // all of it beside the next pieces' copies.  PBS_UPLOAD_SPEC=0: the whole stage after the
+    // pipeline (upload_stage's other path).
     std::deque<std::array<size_t, 3>> upq;  // {first chunk, end chunk, piece}
     std::mutex upmu;
     std::condition_variable upcv;
     bool updone = false;
     std::thread upw;
-    if (ok && ext && ext->n_known == 0 && env_u64("PBS_UPLOAD_SPEC", 1) != 0) {
+    if (ok && ext && env_u64("PBS_UPLOAD_SPEC", 1) != 0) {
         const size_t bcap = len + 16 * cap + 64;
         ext->d_blobs = area->get<uint8_t>(9, bcap, false);
         if (ext->d_blobs) {
-            ext->b_off.assign(cap, 0);
-            ext->b_len.assign(cap, 0);
-            ext->b_comp.assign(cap, 0);
             ext->spec = true;
-            hipStream_t const su = A->s_up;
-            upw = std::thread([&, bcap, su] {
+            hipStream_t const su_masked = A->s_up, sdh = A->s_dh, su_full = A->s_full;
+            upw = std::thread([&, bcap, su_masked, sdh, su_full] {
                 (void)hipSetDevice(dev);
-                uint64_t off = 0;
+                struct DigHash {
+                    size_t operator()(const std::array<uint8_t, 32>& d) const {
+                        uint64_t h;
+                        std::memcpy(&h, d.data(), 8);
+                        return (size_t)h;
+                    }
+                };
+                std::unordered_set<std::array<uint8_t, 32>, DigHash> seen, prev;
+                for (size_t q = 0; q < ext->n_known; ++q) {
+                    std::array<uint8_t, 32> d;
+                    std::memcpy(d.data(), ext->known + 32 * q, 32);
+                    prev.insert(d);
+                }
+                uint64_t hoff = 0;  // the caller's buffer: bytes of blobs so far
+                uint64_t dbase = 0;  // the device area: where this batch's blobs go (the copies
+                                     // out of earlier batches may still be running on sdh)
                 std::vector<uint64_t> spans, offm;
-                std::vector<uint8_t> compm;
+                std::vector<uint8_t> compm, gdig;
+                std::vector<size_t> fresh;
+                ext->blob_offsets[0] = 0;
                 for (;;) {
                     std::array<size_t, 3> b;
                     {
@@ -481,39 +510,139 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
                         upq.pop_front();
                     }
                     if (ext->enc_rc != PBS_OK) continue;  // drain after an error
-                    const size_t i0 = b[0], m = b[1] - b[0];
-                    spans.resize(2 * m);
-                    offm.assign(m + 1, 0);
-                    compm.assign(m, 0);
-                    for (size_t k = 0; k < m; ++k) {
-                        spans[2 * k] = i0 + k ? ends[i0 + k - 1] : 0;
-                        spans[2 * k + 1] = ends[i0 + k];
+                    const size_t i0 = b[0], i1 = b[1], m = i1 - i0;
+                    // the scan partition's CUs while the digest queue holds the others; every CU
+                    // once all digests are in (compressible streams encode past the copies' end)
+                    hipStream_t const su = dig_final.load(std::memory_order_acquire) ? su_full : su_masked;
+                    // encode: every chunk of the batch before its digests are in when there is
+                    // no previous index (a full backup: nearly all new; the blobs are ready when
+                    // the test is), else only the new ones after the test
+                    auto encode = [&](const std::vector<uint64_t>& sp, size_t cnt) -> int {
+                        offm.assign(cnt + 1, 0);
+                        compm.assign(std::max<size_t>(cnt, 1), 0);
+                        if (!cnt) return PBS_OK;
+                        const Clock::time_point te = Clock::now();
+                        pbs_blob_encode_timing bt{};
+                        int r = hipStreamWaitEvent(su, ev_copied[b[2]], 0) == hipSuccess ? PBS_OK : PBS_ERR_HIP;
+                        if (r == PBS_OK)
+                            r = pbs_blob_encode_spans_device(d_data, len, 0, sp.data(), cnt, ext->compress,
+                                                             ext->d_blobs + dbase, bcap - dbase, offm.data(), nullptr,
+                                                             compm.data(), &bt, su);
+                        ext->enc_ms += ms_since(te);
+                        ext->enc_t.compress_ms += bt.compress_ms;
+                        ext->enc_t.assemble_ms += bt.assemble_ms;
+                        ext->enc_t.crc_ms += bt.crc_ms;
+                        ext->enc_t.bytes_in += bt.bytes_in;
+                        ext->enc_t.bytes_out += bt.bytes_out;
+                        ext->enc_t.blocks += bt.blocks;
+                        return r;
+                    };
+                    const bool early = ext->n_known == 0;
+                    if (early) {
+                        spans.resize(2 * m);
+                        for (size_t k = 0; k < m; ++k) {
+                            spans[2 * k] = i0 + k ? ends[i0 + k - 1] : 0;
+                            spans[2 * k + 1] = ends[i0 + k];
+                        }
+                        const int r = encode(spans, m);
+                        if (r != PBS_OK) {
+                            ext->enc_rc = r;
+                            continue;
+                        }
                     }
-                    const Clock::time_point te = Clock::now();
-                    pbs_blob_encode_timing bt{};
-                    int r = hipStreamWaitEvent(su, ev_copied[b[2]], 0) == hipSuccess ? PBS_OK : PBS_ERR_HIP;
-                    if (r == PBS_OK)
-                        r = pbs_blob_encode_spans_device(d_data, len, 0, spans.data(), m, ext->compress, ext->d_blobs + off,
-                                                         bcap - off, offm.data(), nullptr, compm.data(), &bt, su);
-                    ext->enc_ms += ms_since(te);
+                    // the batch's digests: host-routed ones by their flags, GPU jobs by theirs
+                    const Clock::time_point tw = Clock::now();
+                    bool fin = false;
+                    for (;;) {
+                        fin = dig_final.load(std::memory_order_acquire);
+                        if (fin) break;
+                        bool all = true;
+                        for (size_t i = i0; i < i1 && all; ++i)
+                            all = hmask[i] ? hflag[i].load(std::memory_order_acquire) != 0
+                                           : __atomic_load_n(&q_jobs[jobof[i]].done, __ATOMIC_ACQUIRE) != 0;
+                        if (all) break;
+                        std::this_thread::sleep_for(std::chrono::microseconds(20));
+                    }
+                    if (!fin) {  // the GPU's digests of the batch from device memory
+                        gdig.resize(m * 32);
+                        if (hipMemcpyAsync(gdig.data(), d_dig + 32 * i0, m * 32, hipMemcpyDeviceToHost, su) != hipSuccess ||
+                            hipStreamSynchronize(su) != hipSuccess) {
+                            ext->enc_rc = PBS_ERR_HIP;
+                            continue;
+                        }
+                    }
+                    fresh.clear();
+                    std::vector<uint64_t> fsp;
+                    for (size_t i = i0; i < i1; ++i) {
+                        std::array<uint8_t, 32> d;
+                        std::memcpy(d.data(), (fin || hmask[i]) ? digests + 32 * i : gdig.data() + 32 * (i - i0), 32);
+                        const bool kn = prev.count(d) || !seen.insert(d).second;
+                        ext->known_out[i] = kn ? 1 : 0;
+                        if (!kn) {
+                            fresh.push_back(i);
+                            fsp.push_back(i ? ends[i - 1] : 0);
+                            fsp.push_back(ends[i]);
+                        }
+                    }
+                    ext->known_ms += ms_since(tw);
+                    const size_t mf = fresh.size();
+                    int r = PBS_OK;
+                    std::vector<uint64_t> dev_off(mf), blen(mf);  // the new blobs in the device area
+                    std::vector<uint8_t> bcomp(mf);
+                    if (early) {
+                        for (size_t q = 0; q < mf; ++q) {
+                            const size_t k = fresh[q] - i0;
+                            dev_off[q] = offm[k];
+                            blen[q] = offm[k + 1] - offm[k];
+                            bcomp[q] = compm[k];
+                        }
+                    } else {
+                        r = encode(fsp, mf);
+                        for (size_t q = 0; q < mf && r == PBS_OK; ++q) {
+                            dev_off[q] = offm[q];
+                            blen[q] = offm[q + 1] - offm[q];
+                            bcomp[q] = compm[q];
+                        }
+                    }
+                    uint64_t bytes = 0;
+                    for (size_t q = 0; q < mf; ++q) bytes += blen[q];
+                    if (r == PBS_OK && hoff + bytes > ext->blobs_cap) r = PBS_ERR_CAPACITY;
+                    // out in runs of blobs adjacent in the device area, to their final place, on
+                    // their own stream (the encoder has synced su: the blobs are complete), not
+                    // waited for here -- the next batch encodes beside them
+                    const Clock::time_point td = Clock::now();
+                    uint64_t h = hoff;
+                    for (size_t q = 0; q < mf && r == PBS_OK;) {
+                        size_t e = q + 1;
+                        while (e < mf && dev_off[e] == dev_off[e - 1] + blen[e - 1]) ++e;
+                        const uint64_t nbytes = dev_off[e - 1] + blen[e - 1] - dev_off[q];
+                        if (nbytes && hipMemcpyAsync(ext->blobs + h, ext->d_blobs + dbase + dev_off[q], nbytes,
+                                                     hipMemcpyDeviceToHost, sdh) != hipSuccess)
+                            r = PBS_ERR_HIP;
+                        h += nbytes;
+                        q = e;
+                    }
+                    ext->d2h_ms += ms_since(td);
+                    dbase = (dbase + offm.back() + 15) & ~15ull;
                     if (r != PBS_OK) {
                         ext->enc_rc = r;
                         continue;
                     }
-                    ext->enc_t.compress_ms += bt.compress_ms;
-                    ext->enc_t.assemble_ms += bt.assemble_ms;
-                    ext->enc_t.crc_ms += bt.crc_ms;
-                    ext->enc_t.bytes_in += bt.bytes_in;
-                    ext->enc_t.bytes_out += bt.bytes_out;
-                    ext->enc_t.blocks += bt.blocks;
-                    ext->enc_t.compressed_chunks += bt.compressed_chunks;
-                    for (size_t k = 0; k < m; ++k) {
-                        ext->b_off[i0 + k] = off + offm[k];
-                        ext->b_len[i0 + k] = offm[k + 1] - offm[k];
-                        ext->b_comp[i0 + k] = compm[k];
+                    size_t k = 0;
+                    uint64_t run = hoff;
+                    for (size_t i = i0; i < i1; ++i) {
+                        const bool fr = k < mf && fresh[k] == i;
+                        if (fr) run += blen[k];
+                        ext->blob_offsets[i + 1] = run;
+                        if (ext->compressed) ext->compressed[i] = fr ? bcomp[k] : 0;
+                        k += fr ? 1 : 0;
                     }
-                    off = (off + offm[m] + 15) & ~15ull;
+                    hoff = run;
+                    ext->n_done = i1;
                 }
+                const Clock::time_point td = Clock::now();
+                if (hipStreamSynchronize(sdh) != hipSuccess && ext->enc_rc == PBS_OK) ext->enc_rc = PBS_ERR_HIP;
+                ext->d2h_ms += ms_since(td);
             });
         }
     }
@@ -571,13 +700,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
             std::memcpy(ends + n, tmp.data(), m * 8);
             n += m;
         }
-        if (upw.joinable() && n > n0) {
-            {
-                std::lock_guard<std::mutex> g(upmu);
-                upq.push_back({n0, n, k});
-            }
-            upcv.notify_one();
-        }
+
         // route the chunks completed in this piece: the GPU's digest queue when the chain
         // ends before the copy's projected end (+ slack), else the host threads
         if (n > n0) {
@@ -597,6 +720,8 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
                     q_jobs[nj].start = s0;
                     q_jobs[nj].len = cl;
                     q_jobs[nj].idx = i;
+                    q_jobs[nj].done = 0;
+                    jobof[i] = nj;
                     ++nj;
                 }
             }
@@ -610,6 +735,14 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
                 }
                 hcv.notify_all();
             }
+        }
+        // the upload's encoder takes this piece's chunks (routed: their digests will come)
+        if (upw.joinable() && n > n0) {
+            {
+                std::lock_guard<std::mutex> g(upmu);
+                upq.push_back({n0, n, k});
+            }
+            upcv.notify_one();
         }
         // the blob CRC of the chunks completed since the last launch once they cover dbatch
         // bytes (or at the end), on the digest streams other than the queue's
@@ -697,6 +830,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         work();
         for (auto& th : fb) th.join();
     }
+    dig_final.store(true, std::memory_order_release);
     up_finish();
     // the upload's part after the digests: known-chunk test and blobs, from the HBM copy
     // (on the copy stream: not CU-masked, idle since the last piece landed)
@@ -743,6 +877,32 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
 int upload_stage(UploadExt& x, pbs::DevArena* area, const uint8_t* d_data, size_t len, const uint64_t* ends,
                  const uint8_t* digests, size_t n, hipStream_t st) {
     pbs_upload_timing* const t = x.t;
+    if (x.spec) {
+        // done per piece beside the copies (pipeline_run's upload worker): count it up
+        if (x.enc_rc != PBS_OK) return x.enc_rc;
+        if (x.n_done != n) return PBS_ERR_HIP;
+        uint64_t size_reused = 0, compressed_chunks = 0, reused = 0;
+        for (size_t i = 0; i < n; ++i) {
+            if (x.known_out[i]) {
+                size_reused += ends[i] - (i ? ends[i - 1] : 0);
+                ++reused;
+            }
+            if (x.compressed) compressed_chunks += x.compressed[i];
+        }
+        if (t) {
+            t->known_ms = x.known_ms;  // (these three beside the copies, summed per piece)
+            t->encode_ms = x.enc_ms;
+            t->d2h_ms = x.d2h_ms;
+            t->blob = x.enc_t;
+            t->chunk_count = n;
+            t->chunk_reused = reused;
+            t->size = len;
+            t->size_reused = size_reused;
+            t->size_compressed = x.blob_offsets[n];
+            t->compressed_chunks = compressed_chunks;
+        }
+        return PBS_OK;
+    }
     const Clock::time_point t0 = Clock::now();
     uint8_t* const d_dig = area->get<uint8_t>(6, std::max<size_t>(n, 1) * 32);
     uint8_t* const d_kn = area->get<uint8_t>(7, std::max<size_t>(x.n_known, 1) * 32);
@@ -758,48 +918,6 @@ int upload_stage(UploadExt& x, pbs::DevArena* area, const uint8_t* d_data, size_
         hipStreamSynchronize(st) != hipSuccess)
         return PBS_ERR_HIP;
     const Clock::time_point t1 = Clock::now();
-    if (x.spec) {
-        // the blobs were encoded beside the copies: the new ones out of the device area in
-        // runs of adjacent blobs, in chunk order
-        if (x.enc_rc != PBS_OK) return x.enc_rc;
-        uint64_t size_reused = 0, compressed_chunks = 0;
-        x.blob_offsets[0] = 0;
-        for (size_t i = 0; i < n; ++i) {
-            const bool fresh = !x.known_out[i];
-            if (!fresh) size_reused += ends[i] - (i ? ends[i - 1] : 0);
-            x.blob_offsets[i + 1] = x.blob_offsets[i] + (fresh ? x.b_len[i] : 0);
-            if (x.compressed) x.compressed[i] = fresh ? x.b_comp[i] : 0;
-            compressed_chunks += fresh ? x.b_comp[i] : 0;
-        }
-        if (x.blob_offsets[n] > x.blobs_cap) return PBS_ERR_CAPACITY;
-        for (size_t i = 0; i < n;) {
-            if (x.known_out[i]) {
-                ++i;
-                continue;
-            }
-            size_t j = i + 1;
-            while (j < n && !x.known_out[j] && x.b_off[j] == x.b_off[j - 1] + x.b_len[j - 1]) ++j;
-            const uint64_t bytes = x.b_off[j - 1] + x.b_len[j - 1] - x.b_off[i];
-            if (bytes && hipMemcpyAsync(x.blobs + x.blob_offsets[i], x.d_blobs + x.b_off[i], bytes,
-                                        hipMemcpyDeviceToHost, st) != hipSuccess)
-                return PBS_ERR_HIP;
-            i = j;
-        }
-        if (hipStreamSynchronize(st) != hipSuccess) return PBS_ERR_HIP;
-        if (t) {
-            t->known_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-            t->encode_ms = x.enc_ms;  // beside the copies (not on this stage's clock)
-            t->d2h_ms = ms_since(t1);
-            t->blob = x.enc_t;
-            t->chunk_count = n;
-            t->chunk_reused = reused;
-            t->size = len;
-            t->size_reused = size_reused;
-            t->size_compressed = x.blob_offsets[n];
-            t->compressed_chunks = compressed_chunks;
-        }
-        return PBS_OK;
-    }
     // the new chunks as spans of the stream
     std::vector<uint64_t> spans;
     std::vector<size_t> idx;

@@ -8,3 +8,4 @@ for sp in 1 0; do
   PBS_UPLOAD_SPEC=$sp timeout -k 10 300 python bench.py --steps 2 --warmup 1 $NOEXTRA --upload-gib 64 > gpurun_out/up/vm_$sp.log 2>&1 || exit 1
   PBS_UPLOAD_SPEC=$sp timeout -k 10 300 python bench.py --steps 2 --warmup 1 $NOEXTRA --upload-gib 16 --upload-corpus text > gpurun_out/up/text_$sp.log 2>&1 || exit 1
 done
+PBS_UPLOAD_SPEC=1 timeout -k 10 300 python bench.py --steps 2 --warmup 1 $NOEXTRA --upload-gib 16 --upload-corpus pxar > gpurun_out/up/pxar_1.log 2>&1 || exit 1

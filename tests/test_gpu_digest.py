@@ -308,14 +308,17 @@ def test_pipeline_beside_null_stream_work(gpu, oracle, torch_dev):
     assert wall < 8.0, (wall, ops[0], t)
 
 
+@pytest.mark.parametrize("spec", ["1", "0"])
 @pytest.mark.parametrize("prev,compress", [(0, True), (5, True), (40, True), (5, False)])
-def test_upload_stream_host(gpu, oracle, prev, compress):
+def test_upload_stream_host(gpu, oracle, monkeypatch, prev, compress, spec):
     """backup_writer.rs:631-706 end to end from a host buffer: cut list, digests, the
     known-chunk mask against a previous index holding some of this stream's digests (plus
     unrelated ones) and repeats inside the stream, the .didx image, and every new chunk's
     blob as DataChunkBuilder::new(data).compress(compress).build() writes it (oracle: the
     twin's frame behind the blob header where shorter, data_blob.rs:139-176; the
-    uncompressed blob otherwise), plus UploadStats."""
+    uncompressed blob otherwise), plus UploadStats.  spec 1 (default): the known test,
+    the encoding and the blobs' copy per piece beside the copies; 0: after the pipeline."""
+    monkeypatch.setenv("PBS_UPLOAD_SPEC", spec)
     n = 48 * MiB + 5
     data = gen_np.gen_vmimage(n, 0x5EED0003, 0)
     ref_ends = oracle.chunk_feed(1 * MiB, data)
