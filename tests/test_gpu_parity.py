@@ -372,6 +372,45 @@ def test_scan_server_request_placement(gpu, oracle, monkeypatch, mode, feed, avg
     assert np.array_equal(np.array(got, dtype=np.uint64), ref)
 
 
+@pytest.mark.parametrize("wgs", [None, "3"])
+@pytest.mark.parametrize("avg", [4 * KiB, 64 * KiB])
+def test_scan_server_ragged_reads(gpu, oracle, monkeypatch, wgs, avg):
+    """scan() over reads of seeded ragged sizes (1 byte to 1.5 MiB, many just around the
+    server's pass and split sizes), so requests split over the workgroups end at every
+    kind of boundary; the oracle's cuts (chunker.rs:127-181 driven like a reader loop)."""
+    if wgs is None:
+        monkeypatch.delenv("PBS_SERVER_WGS", raising=False)
+    else:
+        monkeypatch.setenv("PBS_SERVER_WGS", wgs)
+    rng = np.random.default_rng(0x5EED0012 + avg)
+    n = 12 * MiB + 77
+    data = gen_np.gen_random(n, 0x5EED0013)
+    ref = oracle.chunk_feed(avg, data, 0)
+    sizes = []
+    while sum(sizes) < n:
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            sizes.append(int(rng.integers(1, 64)))
+        elif kind == 1:
+            base = int(rng.choice([4096, 8192, 16384, 65536, 131072, 262144]))
+            sizes.append(max(1, base + int(rng.integers(-65, 66))))
+        else:
+            sizes.append(int(rng.integers(1, 3 * MiB // 2)))
+    got, pos = [], 0
+    with gpu.Chunker(avg) as c:
+        for s in sizes:
+            p = data[pos:pos + s]
+            off = 0
+            while off < p.size:
+                k = c.scan(p[off:])
+                if k == 0:
+                    break
+                off += k
+                got.append(pos + off)
+            pos += p.size
+    assert np.array_equal(np.array(got, dtype=np.uint64), ref)
+
+
 def test_chunker1_whole_buffer(gpu):
     """test_chunker1's test2 loop on its own 1 MiB counter buffer (chunker.rs:246-257)."""
     buf = gen_np.gen_counter(1 * MiB)
