@@ -405,7 +405,6 @@ __device__ __noinline__ void fse_build_wave(FseT& t_g, const int16_t* norm_g, in
         t.cum[lane] = (int32_t)(ci - cells);
         spc[lane] = (uint16_t)(si - spread);
         if (low) t.sym_at[size - 1 - (li - low)] = (uint8_t)lane;
-        t.dfs[lane] = (int32_t)(ci - cells);  // running next[] slot per symbol (dfs is set last)
     }
     __builtin_amdgcn_wave_barrier();
     // spread: placement k at the k-th position <= high
@@ -429,8 +428,10 @@ __device__ __noinline__ void fse_build_wave(FseT& t_g, const int16_t* norm_g, in
         kb += (uint32_t)__builtin_popcountll(b);
     }
     __builtin_amdgcn_wave_barrier();
-    // next: the cells of each symbol in increasing order
+    // next: the cells of each symbol in increasing order; the running slot of symbol s in
+    // lane s of `run` (a readlane and a writelane a symbol: no LDS round trip in the loop)
     const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t run = lane < nsym ? ci - cells : 0u;
     for (uint32_t u0 = 0; u0 < size; u0 += 64) {
         const uint32_t u = u0 + (uint32_t)lane;
         const uint32_t sy = u < size ? t.sym_at[u] : 0xFFFFu;
@@ -438,13 +439,12 @@ __device__ __noinline__ void fse_build_wave(FseT& t_g, const int16_t* norm_g, in
         uint32_t slot = 0;
         while (rem) {
             const int f = __builtin_ctzll(rem);
-            const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)sy, f);
+            const uint32_t s0 = uni((uint32_t)__builtin_amdgcn_readlane((int)sy, f));
             const unsigned long long mm = __ballot(sy == s0) & rem;
-            const uint32_t base = (uint32_t)t.dfs[s0];
+            const uint32_t base = uni((uint32_t)__builtin_amdgcn_readlane((int)run, (int)s0));
             if (sy == s0) slot = base + (uint32_t)__builtin_popcountll(mm & lt);
-            __builtin_amdgcn_wave_barrier();
-            if (lane == f) t.dfs[s0] = (int32_t)(base + (uint32_t)__builtin_popcountll(mm));
-            __builtin_amdgcn_wave_barrier();
+            const uint32_t nb = uni(base + (uint32_t)__builtin_popcountll(mm));
+            asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(run) : "s"(nb), "{m0}"(s0));
             rem &= ~mm;
         }
         if (u < size) t.next[slot] = (uint16_t)(size + u);
@@ -690,77 +690,168 @@ struct Ctl {
     uint8_t desc[264];          // Huffman tree description (FSE form: <= ~210 bytes before the 128 check)
 };
 
-// Huffman tree description (RFC 8878 4.2.1, one lane): the weights of symbols 0 ..
-// last-1 (the last one is implied), FSE-compressed (two interleaved states) when that is
-// shorter, else in the direct 4-bit form; false when neither applies (raw literals).
-__device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scratch, uint32_t mb, uint32_t lastsym) {
-    const int nwt = (int)lastsym;
-    uint32_t* const wc = reinterpret_cast<uint32_t*>(t_scratch.cum);  // weight counts (LDS)
-    for (int v = 0; v < 16; ++v) wc[v] = 0;
-    uint32_t maxw = 0;
-    for (int s = 0; s < nwt; ++s) {
-        const uint32_t wv = E.len[s] ? mb + 1 - E.len[s] : 0;
-        ++wc[wv];
-        maxw = max(maxw, wv);
+// Wave-uniform element i of a lane-distributed array (element i in lane i & 63 of register
+// i >> 6): read and write.
+__device__ __forceinline__ uint32_t rd_q(const uint32_t (&r)[4], uint32_t i) {  // i: wave-uniform
+    const int l = (int)(i & 63);
+    const uint32_t k = i >> 6;
+    const uint32_t v = k == 0   ? (uint32_t)__builtin_amdgcn_readlane((int)r[0], l)
+                       : k == 1 ? (uint32_t)__builtin_amdgcn_readlane((int)r[1], l)
+                       : k == 2 ? (uint32_t)__builtin_amdgcn_readlane((int)r[2], l)
+                                : (uint32_t)__builtin_amdgcn_readlane((int)r[3], l);
+    return uni(v);
+}
+__device__ __forceinline__ void wr_q(uint32_t (&r)[4], uint32_t i, uint32_t v) {  // i, v: wave-uniform
+    const int l = (int)(i & 63);
+    switch (i >> 6) {
+        case 0: asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r[0]) : "s"(v), "{m0}"(l)); break;
+        case 1: asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r[1]) : "s"(v), "{m0}"(l)); break;
+        case 2: asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r[2]) : "s"(v), "{m0}"(l)); break;
+        default: asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r[3]) : "s"(v), "{m0}"(l)); break;
     }
+}
+// Huffman tree description (RFC 8878 4.2.1), by ONE WAVE: the weights of symbols 0 ..
+// last-1 (the last one is implied), FSE-compressed (two interleaved states) when that is
+// shorter, else in the direct 4-bit form; false when neither applies (raw literals).  The
+// weights, the table (log <= 6: one cell per lane) and the output bytes live in registers,
+// so the serial encode is readlanes and scalar arithmetic (round 4's one-lane version
+// waited on LDS at every weight: ~40-60 us a block); counts and the direct form by lanes.
+__device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scratch, uint32_t mb, uint32_t lastsym,
+                                          int lane) {
+    const uint32_t nwt = uni(lastsym);
+    uint32_t wreg[4], wmax = 0;  // weight of symbol lane + 64 j
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t sy = (uint32_t)lane + 64u * (uint32_t)j;
+        const uint32_t ln = sy < nwt ? (uint32_t)E.len[sy] : 0u;
+        wreg[j] = ln ? mb + 1 - ln : 0u;
+        wmax = max(wmax, wreg[j]);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, d, 64));
+    const uint32_t maxw = uni(wmax);
+    // weight counts: lane v < 16 holds the count of weight v
+    uint32_t wcnt = 0;
+    bool single = false;
+#pragma unroll
+    for (uint32_t v = 0; v < 16; ++v) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            c += (uint32_t)__builtin_popcountll(__ballot((uint32_t)lane + 64u * (uint32_t)j < nwt && wreg[j] == v));
+        if ((uint32_t)lane == v) wcnt = c;
+        single |= c == nwt;
+    }
+    uint32_t* const wc = reinterpret_cast<uint32_t*>(t_scratch.cum);  // weight counts (LDS)
+    if (lane < 16) wc[lane] = wcnt;
+    __builtin_amdgcn_wave_barrier();
     bool fse_ok = false;
     uint32_t fl = 0;
-    if (nwt > 2) {
-        bool single = false;
-        for (int v = 0; v < 16; ++v) single |= wc[v] == (uint32_t)nwt;
-        if (!single) {
-            const int lg = fse_log((uint32_t)nwt, maxw, 6);
-            FseT& t = t_scratch;
-            int16_t* const norm = t.norm;
-            fse_normalize(norm, wc, (int)maxw + 1, (uint32_t)nwt, lg);
-            fl = fse_ncount(ctl.desc + 1, norm, (int)maxw + 1, lg);
-            fse_build(t, norm, (int)maxw + 1, lg);  // (overwrites wc: no longer needed)
-            const FseView tv = view(t);
-            LBits bw;
-            bw.init(ctl.desc + 1 + fl);
-            auto wt = [&](int s) { return E.len[s] ? mb + 1 - E.len[s] : 0u; };
-            uint32_t v1, v2;
-            int i = nwt;
-            if (nwt & 1) {
-                v1 = fse_init(tv, wt(--i));
-                v2 = fse_init(tv, wt(--i));
-                fse_enc(bw, tv, v1, wt(--i));
-            } else {
-                v2 = fse_init(tv, wt(--i));
-                v1 = fse_init(tv, wt(--i));
+    if (nwt > 2 && !single) {
+        const int lg = fse_log(nwt, maxw, 6);
+        FseT& t = t_scratch;
+        uint32_t f0 = 0;
+        if (lane == 0) {
+            fse_normalize(t.norm, wc, (int)maxw + 1, nwt, lg);
+            f0 = fse_ncount(ctl.desc + 1, t.norm, (int)maxw + 1, lg);
+        }
+        f0 = uni((uint32_t)__builtin_amdgcn_readlane((int)f0, 0));
+        __builtin_amdgcn_wave_barrier();
+        fse_build_wave(t, t.norm, (int)maxw + 1, lg, lane);  // (overwrites wc: no longer needed)
+        const uint32_t size = 1u << lg;
+        const uint32_t nxr = (uint32_t)lane < size ? (uint32_t)t.next[lane] : 0u;
+        const uint32_t dnr = (uint32_t)lane <= maxw ? (uint32_t)t.dnb[lane] : 0u;
+        const uint32_t dfr = (uint32_t)lane <= maxw ? (uint32_t)t.dfs[lane] : 0u;
+        auto dnb = [&](uint32_t sy) { return uni((uint32_t)__builtin_amdgcn_readlane((int)dnr, (int)sy)); };
+        auto dfs = [&](uint32_t sy) { return uni((uint32_t)__builtin_amdgcn_readlane((int)dfr, (int)sy)); };
+        auto nxt = [&](uint32_t u) { return uni((uint32_t)__builtin_amdgcn_readlane((int)nxr, (int)u)); };
+        auto init = [&](uint32_t sy) {
+            const uint32_t nb = (dnb(sy) + (1u << 15)) >> 16;
+            const uint32_t v0 = (nb << 16) - dnb(sy);
+            return nxt((v0 >> nb) + dfs(sy));
+        };
+        // the bit stream: bytes into lane k of ob[k >> 6] (bytes past 127 are not kept: the
+        // description must stay under 128 bytes anyway)
+        uint32_t ob[4] = {0, 0, 0, 0};
+        uint64_t acc = 0;
+        uint32_t n = 0, nbytes = 0;
+        auto put = [&](uint32_t v, uint32_t nb) {
+            acc |= (uint64_t)(v & ((1u << nb) - 1u)) << n;
+            n += nb;
+            while (n >= 8) {
+                if (nbytes < 128) wr_q(ob, nbytes, uni((uint32_t)acc & 0xFFu));
+                ++nbytes;
+                acc >>= 8;
+                n -= 8;
             }
-            while (i > 0) {
-                fse_enc(bw, tv, v2, wt(--i));
-                fse_enc(bw, tv, v1, wt(--i));
+        };
+        auto enc = [&](uint32_t& v, uint32_t sy) {
+            const uint32_t nb = (v + dnb(sy)) >> 16;
+            put(v, nb);
+            v = nxt((v >> nb) + dfs(sy));
+        };
+        uint32_t v1, v2, i = nwt;
+        if (nwt & 1) {
+            v1 = init(rd_q(wreg, --i));
+            v2 = init(rd_q(wreg, --i));
+            enc(v1, rd_q(wreg, --i));
+        } else {
+            v2 = init(rd_q(wreg, --i));
+            v1 = init(rd_q(wreg, --i));
+        }
+        while (i > 0) {
+            enc(v2, rd_q(wreg, --i));
+            enc(v1, rd_q(wreg, --i));
+        }
+        put(v2, (uint32_t)lg);
+        put(v1, (uint32_t)lg);
+        put(1, 1);  // close
+        if (n) {
+            if (nbytes < 128) wr_q(ob, nbytes, uni((uint32_t)acc & 0xFFu));
+            ++nbytes;
+        }
+        fl = f0 + nbytes;
+        fse_ok = fl < 128;
+        if (fse_ok) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t k = (uint32_t)lane + 64u * (uint32_t)j;
+                if (k < nbytes) ctl.desc[1 + f0 + k] = (uint8_t)ob[j];
             }
-            bw.put(v2, (uint32_t)t.log);
-            bw.put(v1, (uint32_t)t.log);
-            bw.close();
-            fl = (uint32_t)(bw.p - ctl.desc - 1);
-            fse_ok = fl < 128;
         }
     }
-    const uint32_t direct = nwt <= 128 ? 1 + (uint32_t)(nwt + 1) / 2 : 0xFFFFFFFFu;
+    const uint32_t direct = nwt <= 128 ? 1 + (nwt + 1) / 2 : 0xFFFFFFFFu;
+    bool ok = true;
     if (fse_ok && fl + 1 < direct) {
-        ctl.desc[0] = (uint8_t)fl;
-        ctl.desc_len = fl + 1;
-    } else if (direct != 0xFFFFFFFFu) {
-        ctl.desc[0] = (uint8_t)(127 + nwt);
-        for (int s = 0; s < nwt; s += 2) {
-            const uint32_t a = E.len[s] ? mb + 1 - E.len[s] : 0;
-            const uint32_t b = s + 1 < nwt && E.len[s + 1] ? mb + 1 - E.len[s + 1] : 0;
-            ctl.desc[1 + s / 2] = (uint8_t)(a << 4 | b);
+        if (lane == 0) {
+            ctl.desc[0] = (uint8_t)fl;
+            ctl.desc_len = fl + 1;
         }
-        ctl.desc_len = direct;
+    } else if (direct != 0xFFFFFFFFu) {
+        // byte k: the weights of symbols 2k and 2k + 1 (lane k: symbols 2 lane, 2 lane + 1)
+        const uint32_t s0 = 2u * (uint32_t)lane, s1 = s0 + 1;
+        const uint32_t w0 = (uint32_t)__shfl((int)wreg[0], (int)(s0 & 63), 64);
+        const uint32_t w0b = (uint32_t)__shfl((int)wreg[1], (int)(s0 & 63), 64);
+        const uint32_t w1 = (uint32_t)__shfl((int)wreg[0], (int)(s1 & 63), 64);
+        const uint32_t w1b = (uint32_t)__shfl((int)wreg[1], (int)(s1 & 63), 64);
+        const uint32_t a = s0 < 64 ? w0 : w0b;
+        const uint32_t b = s1 < nwt ? (s1 < 64 ? w1 : w1b) : 0u;
+        if (s0 < nwt) ctl.desc[1 + lane] = (uint8_t)(a << 4 | b);
+        if (lane == 0) {
+            ctl.desc[0] = (uint8_t)(127 + nwt);
+            ctl.desc_len = direct;
+        }
     } else {
-        return false;  // no description fits: raw literals
+        ok = false;  // no description fits: raw literals
     }
-    return true;
+    __builtin_amdgcn_wave_barrier();
+    return ok;
 }
 
 // One FSE state chain of the sequences bit stream, by ONE WAVE: the state is initialised
 // from the last sequence's code and then encodes sequences ns-2 .. 0 (steps j = 0 .. m-1,
-// sequence ns-2-j); chain[q] = the bits it emits for sequence q (value | count << 16),
+// sequence ns-2-j); chain[j] = the bits step j emits, i.e. for sequence ns-2-j (value |
+// count << 16, in step order so a lane's batch of steps is one run of words),
 // *last = the final state (flushed after sequence 0).  `shift` picks the code byte (0 LL,
 // 8 ML, 16 OF).  The chain is serial, but tANS states forget their past quickly (every
 // encode maps many states to one), so lane l runs steps [l seg, (l+1) seg) from a guessed
@@ -791,19 +882,22 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
                 if ((uint32_t)lane == u) mine_bits = (x & ((1u << nb) - 1u)) | nb << 16;
                 x = t.next[(x >> nb) + t.dfs[sym]];
             }
-            if (jl < m) chain[ns - 2 - jl] = mine_bits;
+            if (jl < m) chain[jl] = mine_bits;
         }
         if (lane == 0) *last = m ? x : fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
         return;
     }
-    const uint32_t seg = (m + 63) / 64;
+    // kB steps a batch; segments are whole batches, so a batch starts kB-aligned and its
+    // records go out as 16-byte stores (a store per lane per step, 64 lanes in 64 segments,
+    // was a cache line per lane and store: 2 x 64 line requests per step)
+    constexpr uint32_t kB = 8;
+    const uint32_t seg = ((m + 63) / 64 + kB - 1) / kB * kB;
     const uint32_t a = min(m, (uint32_t)lane * seg), b = min(m, a + seg);
     const uint32_t x0 = fse_init(t, (coded[ns - 1].codes >> shift) & 0xFF);
-    // kB steps a batch; the next batch's codes (and recorded states) are loaded before this
-    // batch's stores: loads and stores share one in-order counter, so loads issued after the
-    // stores would wait for them.  Loads past the segment read its last step (unused), so
-    // the loads are unconditional and the counter waits exact.
-    constexpr uint32_t kB = 8;
+    // the next batch's codes (and recorded states) are loaded before this batch's stores:
+    // loads and stores share one in-order counter, so loads issued after the stores would
+    // wait for them.  Loads past the segment read its last step (unused), so the loads are
+    // unconditional and the counter waits exact.
     auto run = [&](uint32_t x, bool stop_on_meet) -> uint32_t {  // returns the end state, ~0u: met
         if (a >= b) return x;
         auto load = [&](uint32_t j, uint32_t (&c)[kB], uint32_t (&sv)[kB]) {
@@ -821,16 +915,37 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
             const uint32_t jn = j + kB;
             const bool more = jn < b;
             if (more) load(jn, cB, sB);
+            uint32_t cv[kB], st[kB];
+            uint32_t meet = kB;  // the step whose recorded state equals the running one
+            const uint32_t nj = min(kB, b - j);
 #pragma unroll
             for (int u = 0; u < (int)kB; ++u)
-                if (j + (uint32_t)u < b) {
-                    if (stop_on_meet && sA[u] == x) return ~0u;
-                    states[j + u] = (uint16_t)x;
-                    const uint32_t sym = cA[u];
-                    const uint32_t nb = (x + (uint32_t)t.dnb[sym]) >> 16;
-                    chain[ns - 2 - (j + u)] = (x & ((1u << nb) - 1u)) | nb << 16;
-                    x = t.next[(x >> nb) + t.dfs[sym]];
+                if ((uint32_t)u < nj && meet == kB) {
+                    if (stop_on_meet && sA[u] == x) {
+                        meet = (uint32_t)u;
+                    } else {
+                        st[u] = x;
+                        const uint32_t sym = cA[u];
+                        const uint32_t nb = (x + (uint32_t)t.dnb[sym]) >> 16;
+                        cv[u] = (x & ((1u << nb) - 1u)) | nb << 16;
+                        x = t.next[(x >> nb) + t.dfs[sym]];
+                    }
                 }
+            if (nj == kB && meet == kB) {
+                *reinterpret_cast<PBS_GLOBAL v4u*>(states + j) =
+                    v4u{st[0] | st[1] << 16, st[2] | st[3] << 16, st[4] | st[5] << 16, st[6] | st[7] << 16};
+                *reinterpret_cast<PBS_GLOBAL v4u*>(chain + j) = v4u{cv[0], cv[1], cv[2], cv[3]};
+                *reinterpret_cast<PBS_GLOBAL v4u*>(chain + j + 4) = v4u{cv[4], cv[5], cv[6], cv[7]};
+            } else {
+                const uint32_t nd = min(nj, meet);
+#pragma unroll
+                for (int u = 0; u < (int)kB; ++u)
+                    if ((uint32_t)u < nd) {
+                        states[j + u] = (uint16_t)st[u];
+                        chain[j + u] = cv[u];
+                    }
+            }
+            if (meet != kB) return ~0u;
             if (!more) break;
 #pragma unroll
             for (int u = 0; u < (int)kB; ++u) {
@@ -881,9 +996,10 @@ __device__ __forceinline__ uint32_t seq_bits(const Coded& x, uint32_t q, uint32_
     const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
     uint32_t b = kLLBits[llc] + kMLBits[mlc] + ofc;
     if (q + 1 < ns) {
-        if (mode[0] != 1) b += chains[q] >> 16;
-        if (mode[1] != 1) b += chains[stride + q] >> 16;
-        if (mode[2] != 1) b += chains[2 * stride + q] >> 16;
+        const uint32_t j = ns - 2 - q;  // the chains are in step order
+        if (mode[0] != 1) b += chains[j] >> 16;
+        if (mode[1] != 1) b += chains[stride + j] >> 16;
+        if (mode[2] != 1) b += chains[2 * stride + j] >> 16;
     }
     return b;
 }
@@ -943,27 +1059,6 @@ struct OrBitsL {
         if (n && (uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
     }
 };
-
-// Two-queue Huffman merge (one lane): leaves 0..m-1 = the symbols sorted by (count,
-// symbol) (E.tw holds their sorted keys on entry), internal nodes m.. in creation order,
-// ties taking the leaf; parents in E.par, the root in ctl.root.
-__device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) {
-        // two-queue merge: leaves 0..m-1 sorted, internal nodes m.. in creation order
-        const int m = (int)dist;
-        for (int i = 0; i < m; ++i) E.keys[i] = E.tw[i] & 0xFF;  // sorted symbols
-        for (int i = 0; i < m; ++i) E.tw[i] = E.tw[i] >> 8;      // leaf weights
-        int li = 0, ii = m, nn = m;
-        while (nn < 2 * m - 1) {
-            int a, b;
-            if (li < m && (ii >= nn || E.tw[li] <= E.tw[ii])) a = li++; else a = ii++;
-            if (li < m && (ii >= nn || E.tw[li] <= E.tw[ii])) b = li++; else b = ii++;
-            E.tw[nn] = E.tw[a] + E.tw[b];
-            E.par[a] = (uint16_t)nn;
-            E.par[b] = (uint16_t)nn;
-            ++nn;
-        }
-        ctl.root = nn - 1;
-}
 
 // The parse of one ~8 KiB sub-block by ONE WAVE (wave w: window positions [s0, se)), the
 // twin's `parse` (oracle/zstd_twin.cpp) step for step:
@@ -1120,12 +1215,28 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
             const bool alt = __ballot(anyA) != 0;
             for (uint32_t k = 4; k < kZCap; k += 8) {
                 bool more = false;
+                // every slot's words read together (one wait for all of them), the alternative's
+                // too when any lane has one
+                uint32_t xd0[kZPer], xd1[kZPer], xa0[kZPer], xa1[kZPer];
 #pragma unroll
                 for (int i = 0; i < kZPer; ++i) {
-                    if (!__ballot(go[i] || goA[i])) continue;
                     const bool g = go[i] && k < lim[i];
                     const uint32_t sa = g ? S[i] + k : P[i], pa = g ? P[i] + k : P[i];
-                    const uint32_t d0 = W.word(sa) ^ W.word(pa), d1 = W.word(sa + 4) ^ W.word(pa + 4);
+                    xd0[i] = W.word(sa) ^ W.word(pa);
+                    xd1[i] = W.word(sa + 4) ^ W.word(pa + 4);
+                }
+                if (alt) {
+#pragma unroll
+                    for (int i = 0; i < kZPer; ++i) {
+                        const bool ga = goA[i] && k < lim[i];
+                        const uint32_t sb2 = ga ? P[i] - 1 + k : P[i], pb2 = ga ? P[i] + k : P[i];
+                        xa0[i] = W.word(sb2) ^ W.word(pb2);
+                        xa1[i] = W.word(sb2 + 4) ^ W.word(pb2 + 4);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < kZPer; ++i) {
+                    const uint32_t d0 = xd0[i], d1 = xd1[i];
                     if (go[i]) {
                         if (k >= lim[i]) {
                             go[i] = false;
@@ -1135,18 +1246,14 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
                             go[i] = false;
                         }
                     }
-                    if (alt) {
-                        const bool ga = goA[i] && k < lim[i];
-                        const uint32_t sb2 = ga ? P[i] - 1 + k : P[i], pb2 = ga ? P[i] + k : P[i];
-                        const uint32_t a0 = W.word(sb2) ^ W.word(pb2), a1 = W.word(sb2 + 4) ^ W.word(pb2 + 4);
-                        if (goA[i]) {
-                            if (k >= lim[i]) {
-                                goA[i] = false;
-                            } else if (a0 | a1) {
-                                const uint32_t f = a0 ? (uint32_t)__builtin_ctz(a0) >> 3 : 4u + ((uint32_t)__builtin_ctz(a1) >> 3);
-                                La[i] = min(lim[i], k + f);
-                                goA[i] = false;
-                            }
+                    if (alt && goA[i]) {
+                        const uint32_t a0 = xa0[i], a1 = xa1[i];
+                        if (k >= lim[i]) {
+                            goA[i] = false;
+                        } else if (a0 | a1) {
+                            const uint32_t f = a0 ? (uint32_t)__builtin_ctz(a0) >> 3 : 4u + ((uint32_t)__builtin_ctz(a1) >> 3);
+                            La[i] = min(lim[i], k + f);
+                            goA[i] = false;
                         }
                     }
                     more |= go[i] || goA[i];
@@ -1158,18 +1265,27 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
             // bytes, never before the window) and the packed record per slot
             uint32_t D[kZPer];
             unsigned long long m[kZPer];
+            // the backward extension's words, every slot's read together (a slot without a
+            // table or run candidate, or too near the window start, reads its own position)
+            uint32_t bx1[kZPer], bx2[kZPer];
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
                 if (both[i] && La[i] > L[i]) {  // the run's is longer (ties: the table's)
                     S[i] = P[i] - 1;
                     L[i] = La[i];
                 }
+                const bool ok = has[i] && !isrep[i] && S[i] >= 8;
+                const uint32_t pp = ok ? P[i] : 8u, ss = ok ? S[i] : 8u;
+                bx1[i] = W.word(pp - 4) ^ W.word(ss - 4);
+                bx2[i] = W.word(pp - 8) ^ W.word(ss - 8);
+            }
+#pragma unroll
+            for (int i = 0; i < kZPer; ++i) {
                 uint32_t e = 0;
                 if (has[i] && !isrep[i]) {
                     const uint32_t emax = min(kZBack, S[i] - wlo);
                     if (S[i] >= 8) {
-                        const uint32_t x1 = W.word(P[i] - 4) ^ W.word(S[i] - 4);
-                        const uint32_t x2 = W.word(P[i] - 8) ^ W.word(S[i] - 8);
+                        const uint32_t x1 = bx1[i], x2 = bx2[i];
                         e = x1 ? (uint32_t)__builtin_clz(x1) >> 3 : 4u + (x2 ? (uint32_t)__builtin_clz(x2) >> 3 : 4u);
                     } else {
                         while (e < emax && W.byte(P[i] - 1 - e) == W.byte(S[i] - 1 - e)) ++e;
@@ -1340,6 +1456,28 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
     return (uint64_t)ns | (uint64_t)lastend << 32;
 }
 
+// Two-queue Huffman merge (one lane): leaves 0..m-1 = the symbols sorted by (count,
+// symbol) (E.tw holds their sorted keys on entry), internal nodes m.. in creation order,
+// ties taking the leaf; parents in E.par, the root in ctl.root.
+__device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) {
+        // two-queue merge: leaves 0..m-1 sorted, internal nodes m.. in creation order
+        const int m = (int)dist;
+        for (int i = 0; i < m; ++i) E.keys[i] = E.tw[i] & 0xFF;  // sorted symbols
+        for (int i = 0; i < m; ++i) E.tw[i] = E.tw[i] >> 8;      // leaf weights
+        int li = 0, ii = m, nn = m;
+        while (nn < 2 * m - 1) {
+            int a, b;
+            if (li < m && (ii >= nn || E.tw[li] <= E.tw[ii])) a = li++; else a = ii++;
+            if (li < m && (ii >= nn || E.tw[li] <= E.tw[ii])) b = li++; else b = ii++;
+            E.tw[nn] = E.tw[a] + E.tw[b];
+            E.par[a] = (uint16_t)nn;
+            E.par[b] = (uint16_t)nn;
+            ++nn;
+        }
+        ctl.root = nn - 1;
+}
+
+
 // Literal section mode of a block (ONE WAVE): RLE (one distinct byte), raw, or Huffman
 // when the entropy estimate says it may pay -- then the code lengths (two-queue merge,
 // limited to 11 bits), canonical codes and the tree description.  ctl.lit_mode = lane 0's.
@@ -1501,7 +1639,7 @@ __device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& f
                 if (ls[i]) E.code[lane + 64 * i] = (uint16_t)(start[ls[i]] + rk[i]);
         }
         mark(29);
-        if (lane == 0 && !huf_describe(E, ctl, fsc, mb, lastsym)) mode = 0;
+        if (!huf_describe(E, ctl, fsc, mb, lastsym, lane)) mode = 0;
         mark(30);
     }
     if (lane == 0) ctl.lit_mode = mode;  // (lane 0's: it may have fallen back to raw)
@@ -2232,16 +2370,17 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                     const Coded x = coded[q];
                     const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
                     if (q + 1 < ns) {
+                        const uint32_t j = ns - 2 - q;  // (step order)
                         if (mode[1] != 1) {
-                            const uint32_t c = chains[kZBlockSeq + q];
+                            const uint32_t c = chains[kZBlockSeq + j];
                             ob.put(c & 0xFFFF, c >> 16);
                         }
                         if (mode[2] != 1) {
-                            const uint32_t c = chains[2 * kZBlockSeq + q];
+                            const uint32_t c = chains[2 * kZBlockSeq + j];
                             ob.put(c & 0xFFFF, c >> 16);
                         }
                         if (mode[0] != 1) {
-                            const uint32_t c = chains[q];
+                            const uint32_t c = chains[j];
                             ob.put(c & 0xFFFF, c >> 16);
                         }
                     }
@@ -2278,16 +2417,17 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                     const Coded x = coded[q];
                     const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
                     if (q + 1 < ns) {
+                        const uint32_t j = ns - 2 - q;  // (step order)
                         if (mode[1] != 1) {
-                            const uint32_t c = chains[kZBlockSeq + q];
+                            const uint32_t c = chains[kZBlockSeq + j];
                             ob.put(c & 0xFFFF, c >> 16);
                         }
                         if (mode[2] != 1) {
-                            const uint32_t c = chains[2 * kZBlockSeq + q];
+                            const uint32_t c = chains[2 * kZBlockSeq + j];
                             ob.put(c & 0xFFFF, c >> 16);
                         }
                         if (mode[0] != 1) {
-                            const uint32_t c = chains[q];
+                            const uint32_t c = chains[j];
                             ob.put(c & 0xFFFF, c >> 16);
                         }
                     }
