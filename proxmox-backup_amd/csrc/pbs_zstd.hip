@@ -918,6 +918,14 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
             uint32_t cv[kB], st[kB];
             uint32_t meet = kB;  // the step whose recorded state equals the running one
             const uint32_t nj = min(kB, b - j);
+            // the batch's symbol entries first (they do not depend on the state): a step then
+            // waits for one LDS read, its next[] cell
+            uint32_t dn[kB], df[kB];
+#pragma unroll
+            for (int u = 0; u < (int)kB; ++u) {
+                dn[u] = (uint32_t)t.dnb[cA[u]];
+                df[u] = (uint32_t)t.dfs[cA[u]];
+            }
 #pragma unroll
             for (int u = 0; u < (int)kB; ++u)
                 if ((uint32_t)u < nj && meet == kB) {
@@ -925,10 +933,9 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
                         meet = (uint32_t)u;
                     } else {
                         st[u] = x;
-                        const uint32_t sym = cA[u];
-                        const uint32_t nb = (x + (uint32_t)t.dnb[sym]) >> 16;
+                        const uint32_t nb = (x + dn[u]) >> 16;
                         cv[u] = (x & ((1u << nb) - 1u)) | nb << 16;
-                        x = t.next[(x >> nb) + t.dfs[sym]];
+                        x = t.next[(x >> nb) + df[u]];
                     }
                 }
             if (nj == kB && meet == kB) {
@@ -1457,19 +1464,27 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
 }
 
 // Two-queue Huffman merge (one lane): leaves 0..m-1 = the symbols sorted by (count,
-// symbol) (E.tw holds their sorted keys on entry), internal nodes m.. in creation order,
-// ties taking the leaf; parents in E.par, the root in ctl.root.
+// symbol) (E.tw holds their weights on entry, E.keys the symbols), internal nodes m.. in
+// creation order, ties taking the leaf; parents in E.par, the root in ctl.root.  A step reads
+// the two heads of both queues at once (one LDS wait, not one per pop): the second pop
+// takes from these four; a head past its queue is read but not used.
 __device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) {
-        // two-queue merge: leaves 0..m-1 sorted, internal nodes m.. in creation order
         const int m = (int)dist;
-        for (int i = 0; i < m; ++i) E.keys[i] = E.tw[i] & 0xFF;  // sorted symbols
-        for (int i = 0; i < m; ++i) E.tw[i] = E.tw[i] >> 8;      // leaf weights
         int li = 0, ii = m, nn = m;
         while (nn < 2 * m - 1) {
+            const uint32_t l0 = E.tw[li], l1 = E.tw[li + 1], i0 = E.tw[ii], i1 = E.tw[ii + 1];
             int a, b;
-            if (li < m && (ii >= nn || E.tw[li] <= E.tw[ii])) a = li++; else a = ii++;
-            if (li < m && (ii >= nn || E.tw[li] <= E.tw[ii])) b = li++; else b = ii++;
-            E.tw[nn] = E.tw[a] + E.tw[b];
+            uint32_t wa, wb;
+            if (li < m && (ii >= nn || l0 <= i0)) {
+                a = li++;
+                wa = l0;
+                if (li < m && (ii >= nn || l1 <= i0)) { b = li++; wb = l1; } else { b = ii++; wb = i0; }
+            } else {
+                a = ii++;
+                wa = i0;
+                if (li < m && (ii >= nn || l0 <= i1)) { b = li++; wb = l0; } else { b = ii++; wb = i1; }
+            }
+            E.tw[nn] = wa + wb;
             E.par[a] = (uint16_t)nn;
             E.par[b] = (uint16_t)nn;
             ++nn;
@@ -1532,6 +1547,17 @@ __device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& f
         for (int i = 0; i < 4; ++i)
             if (c4[i]) E.tw[rk[i]] = key[i];  // sorted keys (temporarily in tw)
         mark(26);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // sorted symbols and leaf weights, by lane
+            const uint32_t q = (uint32_t)lane + 64u * (uint32_t)i;
+            if (q < dist) {
+                const uint32_t kv = E.tw[q];
+                E.keys[q] = kv & 0xFF;
+                E.tw[q] = kv >> 8;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
         if (lane == 0) huf_merge(E, ctl, dist);
         __builtin_amdgcn_wave_barrier();
         mark(27);
