@@ -82,6 +82,10 @@ constexpr uint32_t kZTab = 1u << kZHashLog;
 constexpr uint32_t kZStageWords = (kZHist + kEncBlock) / 16 + 3;  // 16-byte words at any alignment + 2 zero words
 constexpr uint32_t kZSubSeq = kZSubA / kZMin + 2;                 // sequences one sub-block can emit
 constexpr uint32_t kZBlockSeq = kZWaves * kZSubSeq;
+// (the per-block chain scratch: 3 x u32 chains, 3 x u16 states, 3 x (kZBlockSeq + 16) code
+// bytes inside 6 x kZBlockSeq words, the 16-byte batch accesses aligned)
+static_assert(kZBlockSeq % 8 == 0, "chain scratch alignment");
+static_assert(3 * kZBlockSeq + 3 * kZBlockSeq / 2 + (3 * (kZBlockSeq + 16) + 3) / 4 <= 6 * kZBlockSeq, "chain scratch size");
 constexpr uint64_t kSlot = kEncBlock + 1024;  // block header + up to 64 KiB + slack (section headers, flushes)
 constexpr uint32_t kHufStreams = 48 * 1024;  // Huffman streams staged in LDS (longer: raw literals)
 constexpr uint32_t kHufMax = 11;
@@ -861,8 +865,8 @@ __device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scra
 // true state, so after r rounds lanes 0..r are exact; usually one round settles all.
 __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__ coded_g, uint32_t ns,
                                             uint32_t shift, uint32_t* __restrict__ chain_g,
-                                            uint16_t* __restrict__ states_g, uint32_t* last, int lane,
-                                            unsigned long long* probe) {
+                                            uint16_t* __restrict__ states_g, uint8_t* __restrict__ codes_g,
+                                            uint32_t* last, int lane, unsigned long long* probe) {
     const PBS_GLOBAL Coded* const coded = (const PBS_GLOBAL Coded*)coded_g;
     PBS_GLOBAL uint32_t* const chain = (PBS_GLOBAL uint32_t*)chain_g;
     PBS_GLOBAL uint16_t* const states = (PBS_GLOBAL uint16_t*)states_g;
@@ -898,14 +902,28 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
     // loads and stores share one in-order counter, so loads issued after the stores would
     // wait for them.  Loads past the segment read its last step (unused), so the loads are
     // unconditional and the counter waits exact.
+    // the stream's codes in step order, a byte per step, so a lane's batch is one 8-byte load
+    // (its recorded states one 16-byte load) instead of 2 x 8 loads of 64 cache lines each
+    PBS_GLOBAL uint8_t* const cs = (PBS_GLOBAL uint8_t*)codes_g;
+    for (uint32_t j = (uint32_t)lane; j < m; j += 64) cs[j] = (uint8_t)((coded[ns - 2 - j].codes >> shift) & 0xFF);
+    __threadfence_block();  // (the other lanes' bytes before the batch loads)
     auto run = [&](uint32_t x, bool stop_on_meet) -> uint32_t {  // returns the end state, ~0u: met
         if (a >= b) return x;
+        // (a batch starts kB-aligned; its bytes past the segment or the stream are read, not used)
         auto load = [&](uint32_t j, uint32_t (&c)[kB], uint32_t (&sv)[kB]) {
+            const uint64_t w = *reinterpret_cast<const PBS_GLOBAL uint64_t*>(cs + j);
 #pragma unroll
-            for (int u = 0; u < (int)kB; ++u) {
-                const uint32_t jj = min(j + (uint32_t)u, b - 1);
-                c[u] = (coded[ns - 2 - jj].codes >> shift) & 0xFF;
-                sv[u] = stop_on_meet ? (uint32_t)states[jj] : 0u;
+            for (int u = 0; u < (int)kB; ++u) c[u] = (uint32_t)(w >> (8 * u)) & 0xFFu;
+            if (stop_on_meet) {
+                const v4u q = *reinterpret_cast<const PBS_GLOBAL v4u*>(states + j);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    sv[2 * u] = q[u] & 0xFFFFu;
+                    sv[2 * u + 1] = q[u] >> 16;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < (int)kB; ++u) sv[u] = 0u;
             }
         };
         uint32_t cA[kB], sA[kB];
@@ -1930,7 +1948,8 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
     EntropyArea& E = *reinterpret_cast<EntropyArea*>(work);
     Seq* const wseq_all = seq_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
     Coded* const coded = coded_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
-    // per stream, per sequence: the emitted bits, then (as u16) the state before each step
+    // per stream, per sequence: the emitted bits, then (as u16) the state before each step,
+    // then (as bytes) the stream's codes in step order
     uint32_t* const chains = chain_scratch + (uint64_t)blockIdx.x * 6 * kZBlockSeq;
     if (wave == 0 && lane < 3) {  // the predefined tables, once per launch (fse[] as scratch)
         FseT& t = fse[lane];
@@ -2230,6 +2249,8 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                 const FseView tv = fse[k].mode == 2 ? view(fse[k]) : view(pre[k]);
                 seq_chain_wave(tv, coded, nseq, sh, chains + (uint64_t)k * kZBlockSeq,
                                reinterpret_cast<uint16_t*>(chains + 3ull * kZBlockSeq) + (uint64_t)k * kZBlockSeq,
+                               reinterpret_cast<uint8_t*>(chains + 3ull * kZBlockSeq + 3ull * kZBlockSeq / 2) +
+                                   (uint64_t)k * (kZBlockSeq + 16),
                                &ctl.seq_last[k], lane, role_probe && k == 0 ? g_zprobe : nullptr);
                 __threadfence_block();
             }
