@@ -85,6 +85,14 @@ def parse():
     ap.add_argument("--upload-corpus", choices=["stream", "text", "pxar"], default="stream",
                     help="the upload stage's bytes: the bench stream, or a seeded text-like / pxar-like "
                          "corpus (tests/corpus_gen.py, 32 MiB tiled)")
+    ap.add_argument("--stages", type=int, default=-1,
+                    help="the SURVEY 8(f) stages after the headline, each with its CPU path and its own "
+                         "verification: digest + blob CRC over the 64 GiB stream, the host pipeline and the "
+                         "compressing upload over its first --stage-gib GiB, the blob stage, zstd blobs of "
+                         "1 GiB text-like and pxar-like corpora, the compressing upload of a 4 GiB text-like "
+                         "corpus.  -1 (default): on for one GPU at the default config, off otherwise")
+    ap.add_argument("--stage-gib", type=float, default=16.0,
+                    help="bytes of the stream's host copy the pipeline and VM-image upload stages take")
     ap.add_argument("--verify", type=int, default=1,
                     help="1: after the timed region compare every rank's cut list (and the "
                          "secondary line's) with tests/golden/bench_cuts.json (oracle-made) and "
@@ -383,6 +391,17 @@ def blob_stage(args, buf, cuts, stream, reps: int = 2):
     [x.join() for x in ths]
     cpu_gib_s = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
     ours = int(offs[take]) - 12 * take
+    # the sample's blobs through DataBlob's load/decode check; the first two against the twin
+    import hashlib
+    img = out[: int(offs[take])].cpu().numpy().tobytes()
+    ok = True
+    for i in range(take):
+        ch = host[int(bounds[i]):int(bounds[i + 1])].tobytes()
+        blob = img[int(offs[i]):int(offs[i + 1])]
+        ok &= oracle.blob_load_decode(blob, hashlib.sha256(ch).digest(), read_sizes=(1 << 17,)) == ch
+        ok &= int.from_bytes(blob[8:12], "little") == int(crcs[i])
+        if i < 2:
+            ok &= blob == oracle.blob_compressed(ch)
     del out
     pbschunk.blob_encode_release()
     return {"metric": "GiB/s chunks -> compressed DataBlob images (zstd frames + CRC, device-resident)",
@@ -393,6 +412,9 @@ def blob_stage(args, buf, cuts, stream, reps: int = 2):
             "ratio_out_in": round(best["bytes_out"] / max(1, best["bytes_in"]), 4),
             "sample_payload_bytes": {"ours": ours, "libzstd_level1": int(sizes.sum()),
                                      "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"},
+            "unit": "GiB/s", "verified": bool(ok),
+            "verify_note": f"the first {take} chunks' blobs load + decode (oracle.blob_load_decode) to their "
+                           "chunks with the CRCs returned; the first 2 byte-equal to the host twin",
             "parity": "frames decode with libzstd to the chunks (tests); bytes are not libzstd's: unpinned",
             "cpu_baseline": {"value": round(cpu_gib_s, 3), "unit": "GiB/s", "cores": threads,
                              "kind": f"libzstd {L.ZSTD_versionNumber()} level 1 + zlib.crc32 (ctypes)",
@@ -485,6 +507,10 @@ def digest_stage(args, buf, cuts, stream, ch=None, reps: int = 3):
     [x.start() for x in ths]
     [x.join() for x in ths]
     cpu_gib_s = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
+    # the GPU's digests of the sample's chunks (and the last chunk) against hashlib
+    last = buf[int(bounds[n - 1]):int(bounds[n])].cpu().numpy()
+    dig_ok = all(bytes(ref[i]) == hashlib.sha256(mv[int(bounds[i]):int(bounds[i + 1])]).digest() for i in range(take))
+    dig_ok = dig_ok and bytes(ref[n - 1]) == hashlib.sha256(last).digest()
     crc = crc_stage(args, buf, bd, od, n, bounds, take, threads, stream, reps)
     best = min(t, hb["total_ms"] / 1e3)
     # chunk + digest makespan from HBM (backup_writer.rs:671-678: every chunk of the stream
@@ -527,7 +553,10 @@ def digest_stage(args, buf, cuts, stream, ch=None, reps: int = 3):
                         "GPU only (longest-first lanes; floor = the pass + the longest chunk's serial SHA "
                         "chain) or hybrid (the longest chunks copied to host cores); ms = the faster"}
     return {"metric": "GiB/s SHA-256 digested (per chunk, device-resident)",
-            "value": round(size / (1 << 30) / best, 3), "ms": round(best * 1e3, 3), "chunks": n,
+            "value": round(size / (1 << 30) / best, 3), "unit": "GiB/s", "ms": round(best * 1e3, 3), "chunks": n,
+            "verified": bool(dig_ok and crc["verified"]),
+            "verify_note": f"GPU digests of the first {take} chunks and the last vs hashlib; the hybrid's and "
+                           "chunk+digest's equal to the GPU's (else the stage raises); blob CRCs vs zlib",
             "gpu_only": {"ms": round(t * 1e3, 3), "GiB/s": round(size / (1 << 30) / t, 3),
                          "classes": classes},
             "hybrid": hybrid, "chunk_and_digest": span,
@@ -577,8 +606,11 @@ def crc_stage(args, buf, bd, od, n, bounds, take, threads, stream, reps):
     [x.start() for x in ths]
     [x.join() for x in ths]
     cpu = int(bounds[take]) / (1 << 30) / (time.perf_counter() - t0)
+    got = out[:take].cpu().numpy().view("<u4")
+    ok = all(int(got[i]) == zlib.crc32(mv[int(bounds[i]):int(bounds[i + 1])]) for i in range(take))
     return {"metric": "GiB/s blob CRC-32 (per chunk, device-resident)",
-            "value": round(size / (1 << 30) / t, 3), "ms": round(t * 1e3, 3),
+            "value": round(size / (1 << 30) / t, 3), "unit": "GiB/s", "ms": round(t * 1e3, 3),
+            "verified": bool(ok), "verify_note": f"the first {take} chunks' CRCs vs zlib.crc32",
             "roofline": {"bound": "hbm", "achieved": round(size / t / 1e9, 1), "peak": 8000.0,
                          "unit": "GB/s", "frac": round(size / t / 8e12, 4)},
             "cpu_baseline": {"value": round(cpu, 3), "unit": "GiB/s", "cores": threads,
@@ -586,7 +618,7 @@ def crc_stage(args, buf, bd, od, n, bounds, take, threads, stream, reps):
                              "sample": f"first {take} chunks ({int(bounds[take]) >> 20} MiB)"}}
 
 
-def pipeline_stage(args, buf, piece: int = 1 << 30):
+def pipeline_stage(args, buf, piece: int = 1 << 30, host=None):
     """a pageable host copy of the stream's first --pipeline-gib GiB
     through pbs_pipeline_host (copy thread -> HBM, chunker on CU-masked stream, per-chunk
     SHA-256 and blob CRC-32 on the other CUs, overlapped), end to end; the CPU path beside
@@ -601,8 +633,10 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
 
     oracle = _oracle()
 
-    n = int(args.pipeline_gib * (1 << 30)) // 8 * 8
-    host = buf[:n].cpu().numpy()  # pageable, untimed
+    if host is None:
+        n = int(args.pipeline_gib * (1 << 30)) // 8 * 8
+        host = buf[:n].cpu().numpy()  # pageable, untimed
+    n = host.size
     # warm-up at full size: the first call also allocates the device work area (kept
     # between calls), reported as first_call; the timed call is the steady state
     t0 = time.perf_counter()
@@ -635,7 +669,16 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
     [x.start() for x in ths]
     [x.join() for x in ths]
     cpu = nth * per / (1 << 30) / (time.perf_counter() - c0)
+    # digests and CRCs of a sample of chunks (the first 32 and the last) against hashlib / zlib
+    bnd = np.concatenate([[0], ends]).astype(np.int64)
+    pick = list(range(min(32, ends.size))) + [int(ends.size) - 1]
+    mv = memoryview(host)
+    sample_ok = all(bytes(dig[i]) == hashlib.sha256(mv[bnd[i]:bnd[i + 1]]).digest() and
+                    int(crcs[i]) == zlib.crc32(mv[bnd[i]:bnd[i + 1]]) for i in pick)
     return {"metric": "GiB/s host stream -> chunk boundaries + SHA-256 + blob CRC-32 per chunk (end to end)",
+            "verified": bool(cuts["verified"] is True and sample_ok and same),
+            "verify_note": "cut list vs tests/golden/bench_cuts.json (oracle); digests + CRCs of "
+                           f"{len(pick)} chunks vs hashlib / zlib; same result as the first call",
             "value": round(n / (1 << 30) / wall, 3), "bytes": n, "piece": piece,
             "first_call": {"value": round(n / (1 << 30) / cold_wall, 3),
                            "note": "same stream, first call: includes allocating the device work area",
@@ -655,12 +698,41 @@ def pipeline_stage(args, buf, piece: int = 1 << 30):
                              "sample": f"{nth} x 256 MiB slices: chunk_feed then sha256 + crc32 per chunk"}}
 
 
-def upload_stage(args, buf, piece: int = 1 << 30):
+def corpus_host(name: str, n: int, base=None):
+    """A seeded text-like / pxar-like corpus (tests/corpus_gen.py, 32 MiB) tiled to n bytes;
+    every 4 KiB page of every tile but the first stamped with its page number (8 bytes at
+    the page start): the tiles stop repeating each other's chunks, so the known-chunk test
+    finds no duplicates and every chunk is compressed, at ~0.2 % of the bytes."""
+    import numpy as np
+
+    if base is None:
+        base = corpus_base(name)
+    host = np.tile(base, -(-n // base.size))[:n]
+    pages = host[base.size:].reshape(-1)[: (n - base.size) // 4096 * 4096].reshape(-1, 4096)
+    pages[:, :8] = np.arange(1, pages.shape[0] + 1, dtype="<u8").view(np.uint8).reshape(-1, 8)
+    return host, (f"{name}-like corpus (tests/corpus_gen.py seed {CORPUS_SEEDS[name]}, 32 MiB tiled, every later "
+                  f"4 KiB page stamped with its number)")
+
+
+CORPUS_SEEDS = {"text": 21, "pxar": 22}
+
+
+def corpus_base(name: str):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import corpus_gen
+    return {"text": corpus_gen.text, "pxar": corpus_gen.pxar}[name](32 << 20, CORPUS_SEEDS[name])
+
+
+def upload_stage(args, host, what: str, piece: int = 1 << 30, golden=None):
     """backup_writer.rs:631-706 with compress = true (proxmox-backup-client main.rs:1011-1016)
     from a pageable host buffer to the new chunks' blobs in (pinned) host memory, through
     pbs_upload_stream_host; the CPU path beside it over a bounded sample: the oracle
     chunker, hashlib SHA-256, libzstd level 1 (the reference's compressor, data_blob.rs:151;
-    the image's 1.4.8) and zlib.crc32 per chunk on the host cores."""
+    the image's 1.4.8) and zlib.crc32 per chunk on the host cores.  Verified after the
+    timing: the cut list (against `golden` = (workload, seed) of tests/golden/bench_cuts.json,
+    else against the oracle run over the same bytes), the first new chunks' blobs against
+    the host twin's, their zstd payloads through libzstd and DataBlob's load/decode check
+    (oracle.blob_load_decode) with the upload's own digests."""
     import hashlib
     import zlib
 
@@ -670,29 +742,7 @@ def upload_stage(args, buf, piece: int = 1 << 30):
     import pbschunk
 
     oracle = _oracle()
-    n = int(args.upload_gib * (1 << 30)) // 8 * 8
-    if args.upload_corpus == "stream":
-        host = buf[:n].cpu().numpy()
-        what = f"{args.workload} stream (seed {hex(SEEDS[args.workload])})"
-    else:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import corpus_gen
-        base = {"text": lambda: corpus_gen.text(32 << 20, 21), "pxar": lambda: corpus_gen.pxar(32 << 20, 22)}[
-            args.upload_corpus]()
-        host = np.tile(base, -(-n // base.size))[:n]
-        # every 4 KiB page of every tile but the first stamped with its page number (8 bytes
-        # at the page start): the tiles stop repeating each other's chunks, so the known-chunk
-        # test finds no duplicates and every chunk is compressed, at ~0.2 % of the bytes
-        pages = host[base.size:].reshape(-1)[: (n - base.size) // 4096 * 4096].reshape(-1, 4096)
-        pages[:, :8] = np.arange(1, pages.shape[0] + 1, dtype="<u8").view(np.uint8).reshape(-1, 8)
-        what = (f"{args.upload_corpus}-like corpus (tests/corpus_gen.py seed {21 if args.upload_corpus == 'text' else 22}, "
-                f"32 MiB tiled, every later 4 KiB page stamped with its number)")
-    # the bench stream's HBM goes (the last stage): a 64 GiB upload holds the stream copy,
-    # the blob slots and the blobs in HBM at once
-    buf.set_()
-    torch.cuda.empty_cache()
-    pbschunk.blob_encode_release()
-    pbschunk.pipeline_release()
+    n = host.size
     cap = n // max(args.avg >> 2, 65) + 4
     blobs = torch.empty(12 * cap + n, dtype=torch.uint8, pin_memory=True).numpy()
     cold = pbschunk.upload_stream_host(host, args.avg, piece=piece, blobs_out=blobs)  # allocations
@@ -702,22 +752,26 @@ def upload_stage(args, buf, piece: int = 1 << 30):
     same = (np.array_equal(cold["ends"], out["ends"]) and np.array_equal(cold["digests"], out["digests"])
             and np.array_equal(cold["blob_offsets"], out["blob_offsets"]))
     del cold
-    cuts = None
-    if args.upload_corpus == "stream":
-        cuts = verify_record({"chunks": int(out["ends"].size), **cut_record(out["ends"], keep=0)}, args.workload,
-                             n, args.avg, SEEDS[args.workload])
-    # the first new chunks' blobs against the host twin's (oracle.blob_compressed), and their
-    # zstd payloads through libzstd
-    checked = 0
+    rec = {"chunks": int(out["ends"].size), **cut_record(out["ends"], keep=0)}
+    if golden is not None:
+        cuts = verify_record(rec, golden[0], n, args.avg, golden[1])
+    else:  # the oracle over the same bytes (every cut, the tail appended as find_cuts does)
+        ref = oracle.chunk_feed(args.avg, host)
+        if ref.size == 0 or int(ref[-1]) != n:
+            ref = np.append(ref, np.uint64(n))
+        cuts = {**rec, "verified": bool(np.array_equal(ref, out["ends"])),
+                "verify_note": "against oracle.chunk_feed over the same host bytes"}
+    # the first new chunks' blobs against the host twin's (oracle.blob_compressed), and the
+    # reference's own check of a blob (load: magic + CRC; decode; digest)
+    checked, blobs_ok = 0, True
     offs = out["blob_offsets"]
     for i in np.flatnonzero(out["known"] == 0)[:3]:
         s0 = int(out["ends"][i - 1]) if i else 0
         chunk = host[s0:int(out["ends"][i])].tobytes()
-        ln = len(chunk)
         blob = out["blobs"][int(offs[i]):int(offs[i + 1])].tobytes()
-        assert blob == oracle.blob_compressed(chunk), f"upload blob at {s0} differs from the twin's"
-        if blob[:8] == oracle.COMPRESSED_BLOB_MAGIC:
-            assert oracle.zstd_decompress(blob[12:], ln) == chunk
+        blobs_ok &= blob == oracle.blob_compressed(chunk)
+        blobs_ok &= bytes(out["digests"][i]) == hashlib.sha256(chunk).digest()
+        blobs_ok &= oracle.blob_load_decode(blob, bytes(out["digests"][i]), read_sizes=(1 << 17,)) == chunk
         checked += 1
     t = out["timing"]
     # CPU path: every thread chunks its own slice, then SHA-256 + libzstd-1 + CRC per chunk
@@ -746,10 +800,11 @@ def upload_stage(args, buf, piece: int = 1 << 30):
     st = out["stats"]
     return {"metric": "GiB/s host stream -> chunks + SHA-256 + known-chunk test + compressed blobs of the new "
                       "chunks in host memory (end to end, backup_writer.rs:631-706 with compress = true)",
-            "value": round(n / (1 << 30) / wall, 3), "wall_ms": round(wall * 1e3, 2), "bytes": n, "data": what,
-            "piece": piece,
+            "value": round(n / (1 << 30) / wall, 3), "unit": "GiB/s", "wall_ms": round(wall * 1e3, 2), "bytes": n,
+            "data": what, "piece": piece,
+            "verified": bool(cuts["verified"] is True and blobs_ok and same),
             "chunks": int(out["ends"].size), "cuts": cuts, "same_result_as_first_call": same,
-            "blobs_checked_against_twin": checked,
+            "blobs_checked_against_twin_and_decoded": checked,
             "upload_stats": st, "compressed_over_new": round(st["size_compressed"] / max(1, st["size"] - st["size_reused"]), 4),
             "compressed_chunks": t["compressed_chunks"],
             "pipeline_detail_ms": {k: (round(v, 2) if isinstance(v, float) else v) for k, v in t["pipe"].items()},
@@ -761,6 +816,90 @@ def upload_stage(args, buf, piece: int = 1 << 30):
                              "kind": "port (oracle chunker) + hashlib + libzstd level 1 + zlib.crc32",
                              "libzstd_version": int(L.ZSTD_versionNumber()),
                              "sample": f"{nth} x {per >> 20} MiB slices: chunk_feed then sha256 + zstd-1 + crc32 per chunk"}}
+
+
+def zstd_stage(args, name: str, base, gib: float = 1.0, reps: int = 3):
+    """SURVEY 8(f) rank 4 on compressible data: DataBlob::encode(chunk, None, true)
+    (data_blob.rs:139-176; zstd level 1 in the reference, :151) of every chunk of a
+    seeded text-like / pxar-like corpus (32 MiB tiled to `gib` GiB in HBM, a chunk's
+    window never reaches a neighbouring tile), cut by the GPU chunker; wall clock of the
+    synchronous pbs_blob_encode_chunks_device, best of `reps`.  Beside it libzstd level 1
+    + zlib.crc32 over every chunk on the host cores.  Verified: the payloads within 10 %
+    of libzstd-1's over the first 64 MiB of chunks, the first two blobs byte-equal to the
+    host twin's, and every blob of that sample through DataBlob's load/decode check."""
+    import hashlib
+    import zlib
+
+    import numpy as np
+    import torch
+
+    import pbschunk
+
+    oracle = _oracle()
+    n = int(gib * (1 << 30)) // base.size * base.size
+    host = np.tile(base, n // base.size)
+    dev = torch.from_numpy(host).to("cuda")
+    with pbschunk.Chunker(args.avg) as c:
+        ends = c.find_cuts_device(dev.data_ptr(), n, is_final=True)
+    bounds = np.concatenate([[0], ends]).astype(np.uint64)
+    cap = pbschunk.blob_stream_bound(bounds)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    pbschunk.blob_encode_chunks_device(dev.data_ptr(), n, bounds, out.data_ptr(), cap)  # warm-up
+    best = None
+    for _ in range(reps):
+        offs, crcs, comp, tm = pbschunk.blob_encode_chunks_device(dev.data_ptr(), n, bounds, out.data_ptr(), cap)
+        if best is None or tm["total_ms"] < best["total_ms"]:
+            best = tm
+    L = oracle.libzstd()
+    take = max(1, int(np.searchsorted(bounds, 64 << 20)))
+    img = out[: int(offs[take])].cpu().numpy().tobytes()
+    ours = int(offs[take]) - 12 * take
+    ref, ok = 0, True
+    for i in range(take):
+        ch = np.ascontiguousarray(host[int(bounds[i]):int(bounds[i + 1])])
+        dst = np.empty(L.ZSTD_compressBound(ch.size), np.uint8)
+        ref += L.ZSTD_compress(dst.ctypes.data, dst.size, ch.ctypes.data, ch.size, 1)
+        blob = img[int(offs[i]):int(offs[i + 1])]
+        ok &= oracle.blob_load_decode(blob, hashlib.sha256(ch).digest(), read_sizes=(1 << 17,)) == ch.tobytes()
+        ok &= struct_crc(blob) == int(crcs[i])
+        if i < 2:
+            ok &= blob == oracle.blob_compressed(ch.tobytes())
+    nb = int(bounds.size - 1)
+    threads = cpu_threads(args)
+    lens = np.diff(bounds.astype(np.int64))
+
+    def work(ix):
+        dst = np.empty(L.ZSTD_compressBound(int(lens.max())), np.uint8)
+        for i in ix:
+            a0, b0 = int(bounds[i]), int(bounds[i + 1])
+            r = L.ZSTD_compress(dst.ctypes.data, dst.size, host.ctypes.data + a0, b0 - a0, 1)
+            zlib.crc32(memoryview(dst)[:r])
+
+    ths = [threading.Thread(target=work, args=(list(range(k, nb, threads)),)) for k in range(threads)]
+    h0 = time.perf_counter()
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    cpu = n / (1 << 30) / (time.perf_counter() - h0)
+    del dev, out
+    pbschunk.blob_encode_release()
+    ratio = ours / max(1, ref)
+    return {"metric": f"GiB/s chunks -> compressed DataBlob images (zstd frames + CRC, device-resident), {name}-like corpus",
+            "value": round(n / (1 << 30) / (best["total_ms"] / 1e3), 3), "unit": "GiB/s", "bytes": n,
+            "data": f"{name}-like corpus (tests/corpus_gen.py seed {CORPUS_SEEDS[name]}, 32 MiB tiled)",
+            "chunks": nb, "ms": {k: round(best[k], 3) for k in ("total_ms", "compress_ms", "assemble_ms", "crc_ms")},
+            "out_in": round(best["bytes_out"] / n, 4),
+            "sample_payload": {"ours": ours, "libzstd_level1": ref, "ratio": round(ratio, 4), "chunks": take},
+            "verified": bool(ok and ratio <= 1.10),
+            "verify_note": f"the first {take} chunks' blobs load + decode to their chunks (DataBlob load/decode, "
+                           "oracle.blob_load_decode) with the CRCs returned; the first 2 byte-equal to the host twin; "
+                           "payload <= 1.10 x libzstd level 1 over them",
+            "cpu_baseline": {"value": round(cpu, 3), "unit": "GiB/s", "cores": threads,
+                             "kind": f"libzstd {L.ZSTD_versionNumber()} level 1 + zlib.crc32 (ctypes)",
+                             "sample": f"all {nb} chunks of the corpus"}}
+
+
+def struct_crc(blob: bytes) -> int:
+    return int.from_bytes(blob[8:12], "little")
 
 
 def free_port() -> int:
@@ -1155,26 +1294,72 @@ def main():
         out["backend"] = dist.get_backend()
     if host_incl is not None:
         out["host_inclusive_gib_s"] = round(host_incl, 3)
-    if args.digest and args.mode == "streams":
+    stages = args.stages if args.stages >= 0 else int(default_cfg and world == 1 and not share)
+    if stages and (world != 1 or args.mode != "streams"):
+        stages = 0  # the f-stages are one-GPU measurements
+    if stages:
+        out["stages_note"] = ("SURVEY 8(f) stages after the headline's timed region, each with its CPU path "
+                              "and its own verification; none of them changes value / roofline / cpu_baseline")
+    if (args.digest or stages) and args.mode == "streams":
         out["digest"] = digest_stage(args, buf, cuts, stream, ch=ch if args.mode == "streams" else None)
-    if args.pipeline_gib > 0 and args.mode == "streams" and world == 1:
-        out["pipeline"] = pipeline_stage(args, buf)  # before the blob stage's 64 GiB scratch
-    if args.blobs and args.mode == "streams":
+    stage_host = None
+    if stages:  # one pageable host copy of the stream's prefix for the pipeline and the upload
+        stage_host = buf[: int(args.stage_gib * (1 << 30)) // 8 * 8].cpu().numpy()
+    if (args.pipeline_gib > 0 or stages) and args.mode == "streams" and world == 1:
+        out["pipeline"] = pipeline_stage(args, buf, host=stage_host)  # before the blob stage's 64 GiB scratch
+    if stages:
+        pbschunk.pipeline_release()
+        out["upload_vm"] = upload_stage(args, stage_host, f"{args.workload} stream prefix (seed "
+                                        f"{hex(SEEDS[args.workload])})", golden=(args.workload, SEEDS[args.workload]))
+        del stage_host
+        pbschunk.pipeline_release()
+    if (args.blobs or stages) and args.mode == "streams":
         out["blobs"] = blob_stage(args, buf, cuts, stream)
     if args.secondary_random and args.mode == "streams" and world == 1 and args.workload != "random":
         out["secondary_random"] = secondary_random(args, ch, buf, stream)
-    if args.upload_gib > 0 and args.mode == "streams" and world == 1:
-        out["upload"] = upload_stage(args, buf)  # (last GPU stage: it frees the bench stream)
-    if args.cpu_baseline:  # (rank 0 only: the other ranks have returned; after every timed region)
+    if stages:
+        ch.close()
         del buf
+        torch.cuda.empty_cache()
+        bases = {}
+        for name in ("text", "pxar"):
+            bases[name] = corpus_base(name)
+            out[f"zstd_{name}"] = zstd_stage(args, name, bases[name])
+            torch.cuda.empty_cache()
+        host, what = corpus_host("text", 4 << 30, bases["text"])
+        out["upload_text"] = upload_stage(args, host, what)
+        del host, bases
+        pbschunk.pipeline_release()
+    elif args.upload_gib > 0 and args.mode == "streams" and world == 1:
+        # (the last GPU stage: a 64 GiB upload holds the stream copy, the blob slots and the
+        # blobs in HBM at once, so the bench stream goes first)
+        n = int(args.upload_gib * (1 << 30)) // 8 * 8
+        if args.upload_corpus == "stream":
+            host, what, golden = buf[:n].cpu().numpy(), f"{args.workload} stream (seed {hex(SEEDS[args.workload])})", \
+                (args.workload, SEEDS[args.workload])
+        else:
+            (host, what), golden = corpus_host(args.upload_corpus, n), None
+        buf.set_()
+        torch.cuda.empty_cache()
+        pbschunk.blob_encode_release()
+        pbschunk.pipeline_release()
+        out["upload"] = upload_stage(args, host, what, golden=golden)
+        del host
+    if args.cpu_baseline:  # (rank 0 only: the other ranks have returned; after every timed region)
+        buf = None
         out["cpu_baseline"] = cpu_baseline(args, args.workload, SEEDS[args.workload], args.avg)
         if args.cpu_config1:
             out["cpu_config1"] = cpu_config1(args)
     extra = [out["secondary_random"]] if "secondary_random" in out else []
     if "pipeline" in out and out["pipeline"]["cuts"]["verified"] is not None:  # a golden stream length
         extra.append(out["pipeline"]["cuts"])
-    if "upload" in out and out["upload"]["cuts"] and out["upload"]["cuts"]["verified"] is not None:
-        extra.append(out["upload"]["cuts"])
+    for k in ("upload", "upload_vm", "upload_text"):
+        if k in out and out[k]["cuts"]["verified"] is not None:
+            extra.append(out[k]["cuts"])
+    # every stage's own verification (digests, CRCs, blobs, cut lists)
+    for k in ("digest", "pipeline", "upload_vm", "blobs", "zstd_text", "zstd_pxar", "upload_text"):
+        if k in out and out[k].get("verified") is not True:
+            extra.append({"verified": out[k].get("verified"), "stage": k})
     if args.verify:
         # every timed cut list (each rank's, the secondary line's) equals the oracle's
         out["verified"] = verdict(recs, extra)

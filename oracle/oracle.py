@@ -331,3 +331,85 @@ def blob_compressed(chunk: bytes) -> bytes:
     if len(frame) < len(chunk):
         return COMPRESSED_BLOB_MAGIC + struct.pack("<I", zlib.crc32(frame)) + frame
     return blob_uncompressed(chunk)
+
+
+# ---- DataBlob load + decode (the reference's own pin for compressed blobs) ------------
+# The reference never compares compressed bytes: tests/blob_writer.rs:35-87
+# (verify_test_blob) writes TEST_DATA through DataBlobWriter and checks that the blob
+# loads (DataBlob::load_from_reader -> from_raw + verify_crc, data_blob.rs:256-265,
+# :268-300, :78-84), reads back through DataBlobReader with 1-, 3- and 64 KiB read buffers
+# (a streaming zstd decoder over the payload), and decodes (DataBlob::decode,
+# data_blob.rs:196-225: zstd::stream::decode_all of the payload) to TEST_DATA, whose
+# SHA-256 is TEST_DIGEST_PLAIN (verify_digest, :335-350).  blob_load_decode restates
+# exactly that for the two unencrypted magics; libzstd is the image's (1.4.8).
+ENCRYPTED_BLOB_MAGIC = bytes([123, 103, 133, 190, 34, 45, 76, 240])  # file_formats.rs:15
+ENCR_COMPR_BLOB_MAGIC = bytes([230, 89, 27, 191, 11, 191, 216, 11])  # file_formats.rs:18
+
+
+class _ZBuf(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("size", ctypes.c_size_t), ("pos", ctypes.c_size_t)]
+
+
+def zstd_decode_stream(frame: bytes, read_size: int) -> bytes:
+    """zstd::stream::read::Decoder as DataBlobReader drives it: the payload decoded into
+    an output buffer of `read_size` bytes at a time (ZSTD_decompressStream), until the
+    frame ends and the input is consumed."""
+    L = libzstd()
+    if not hasattr(L, "_dstream_ready"):
+        sz, p = ctypes.c_size_t, ctypes.c_void_p
+        L.ZSTD_createDCtx.restype = p
+        L.ZSTD_createDCtx.argtypes = []
+        L.ZSTD_freeDCtx.restype = sz
+        L.ZSTD_freeDCtx.argtypes = [p]
+        L.ZSTD_decompressStream.restype = sz
+        L.ZSTD_decompressStream.argtypes = [p, ctypes.POINTER(_ZBuf), ctypes.POINTER(_ZBuf)]
+        L._dstream_ready = True
+    src = np.frombuffer(bytes(frame), dtype=np.uint8)
+    dst = np.empty(max(read_size, 1), dtype=np.uint8)
+    inb = _ZBuf(src.ctypes.data if src.size else None, src.size, 0)
+    out = bytearray()
+    dctx = L.ZSTD_createDCtx()
+    try:
+        while True:
+            ob = _ZBuf(dst.ctypes.data, read_size, 0)
+            r = L.ZSTD_decompressStream(dctx, ctypes.byref(ob), ctypes.byref(inb))
+            if L.ZSTD_isError(r):
+                raise ValueError(L.ZSTD_getErrorName(r).decode())
+            out += dst[:ob.pos].tobytes()
+            if r == 0 and inb.pos == inb.size:
+                return bytes(out)  # frame complete and flushed, input consumed
+            if ob.pos == 0 and inb.pos == inb.size and r != 0:
+                raise ValueError("truncated zstd frame")
+    finally:
+        L.ZSTD_freeDCtx(dctx)
+
+
+def blob_load_decode(raw: bytes, digest: bytes | None = None, read_sizes=(1, 3, 64 * 1024)) -> bytes:
+    """DataBlob::load_from_reader(raw).decode(None, digest) plus DataBlobReader's reads
+    (tests/blob_writer.rs:35-68): raises ValueError where the reference bails."""
+    import hashlib
+    import struct
+    import zlib
+
+    raw = bytes(raw)
+    if len(raw) < 12:  # from_raw, data_blob.rs:269-271
+        raise ValueError(f"blob too small ({len(raw)} bytes).")
+    magic = raw[:8]
+    if magic in (ENCRYPTED_BLOB_MAGIC, ENCR_COMPR_BLOB_MAGIC):
+        raise ValueError("encrypted blob: not produced by this path")
+    if magic not in (UNCOMPRESSED_BLOB_MAGIC, COMPRESSED_BLOB_MAGIC):  # from_raw :290-292
+        raise ValueError("unable to parse raw blob - wrong magic")
+    if struct.unpack("<I", raw[8:12])[0] != zlib.crc32(raw[12:]):  # verify_crc :78-84
+        raise ValueError("Data blob has wrong CRC checksum.")
+    if magic == UNCOMPRESSED_BLOB_MAGIC:  # decode :201-207
+        data = raw[12:]
+        reads = [data] * len(read_sizes)
+    else:  # decode :208-216 (decode_all) and DataBlobReader's streaming reads
+        data = zstd_decode_stream(raw[12:], 1 << 17)
+        reads = [zstd_decode_stream(raw[12:], s) for s in read_sizes]
+    for s, r in zip(read_sizes, reads):
+        if r != data:
+            raise ValueError(f"blob data is wrong (read buffer size {s})")
+    if digest is not None and hashlib.sha256(data).digest() != bytes(digest):  # verify_digest
+        raise ValueError("detected chunk with wrong digest.")
+    return data

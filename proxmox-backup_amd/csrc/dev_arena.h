@@ -64,7 +64,11 @@ public:
             const size_t want = headroom ? bytes + bytes / 8 : bytes;
             if (hipMalloc(&b.p, want) != hipSuccess) {
                 (void)hipGetLastError();
-                reclaim_idle_device_memory();  // (this arena is leased: not among the idle ones)
+                // (this arena is leased: not among the idle ones).  The hipFrees wait for the
+                // whole device: inside a pipeline run that includes its own resident digest
+                // queue grid, which drains on its idle exit (50 ms) -- a stall, taken only
+                // when device memory has run out, instead of a failed call
+                reclaim_idle_device_memory();
                 if (hipMalloc(&b.p, want) != hipSuccess) {
                     (void)hipGetLastError();
                     b.p = nullptr;

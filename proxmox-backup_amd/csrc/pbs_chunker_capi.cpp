@@ -204,6 +204,17 @@ struct pbs_chunker {
     int last_error = 0;
     bool debug_phases = false;  // PBS_DEBUG_PHASES=1: small-resolve phase times to stderr
     ScanServer srv;
+    // The fused pass's resolver gives up after fused_timeout_ticks (wall_clock64, 100 MHz;
+    // PBS_FUSED_TIMEOUT_TICKS, tests) and stores status 2; the host's spin on that status
+    // word gives up host_wait_s after the launch (PBS_HOST_WAIT_MS; default: the kernel's
+    // bound + 10 s), so a device wait that escapes the kernel's own bound fails the call
+    // with PBS_ERR_HIP instead of hanging the caller.  The handle is then `lost`: a kernel
+    // of it may still be running, so every call but reset / free fails with PBS_ERR_HIP,
+    // reset succeeds once the handle's stream has drained, and free leaks the device
+    // memory of a handle whose kernel still runs rather than wait for it.
+    uint64_t fused_timeout_ticks = 100000000ull * 20;
+    double host_wait_s = 0;
+    bool lost = false;
 };
 
 namespace {
@@ -706,7 +717,7 @@ int server_launch(pbs_chunker* c, uint64_t last) {
     ScanServer& sv = c->srv;
     __atomic_store_n(&sv.mb->exited, ~0ull, __ATOMIC_RELEASE);
     const uint32_t flags = sv.flags | (sv.vram ? kSrvDevReq : 0u);
-    sv.epoch = (sv.epoch + 1) & 0x7FFFFFFFu;
+    sv.epoch = (sv.epoch + 1) & 0x3FFFFFFFu;  // kSrvEpochMask (scan_server.h)
     if (!sv.epoch) sv.epoch = 1;  // 0 is the header's initial state
     HIP_TRY(c, launch_scan_server(sv.mb_dev, sv.req_dev, sv.disp_dev, sv.slot_dev, sv.hslot_dev,
                                   c->d_table.as<uint32_t>(), c->prm.thr, last, kServerIdleTicks, flags,
@@ -1137,7 +1148,7 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     a.tail_src = dsrc + bl - tl;
     a.tail_host = reinterpret_cast<uint8_t*>(small_dev + 24);
     a.tail_len = (uint32_t)tl;
-    a.timeout_ticks = 100000000ull * 20;  // 20 s of wall_clock64 (100 MHz)
+    a.timeout_ticks = c->fused_timeout_ticks;  // 20 s of wall_clock64 (100 MHz) by default
     volatile uint64_t* status_word = c->h_small + 8 + 3;
     volatile uint64_t* progress = c->h_small + 8 + 9;  // cuts in h_cuts so far (every 8 steps)
     *status_word = ~0ull;
@@ -1149,7 +1160,9 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
     HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
     // the resolver stores its status word last (system-scope release) once every tile is
     // resolved: spin on it rather than wait for the kernel to retire; the event tells when
-    // the kernel ended without one (launch failure)
+    // the kernel ended without one (launch failure), the wall clock when neither comes
+    const auto t_launch = std::chrono::steady_clock::now();
+    const double wait_s = c->host_wait_s > 0 ? c->host_wait_s : (double)c->fused_timeout_ticks * 1e-8 + 10.0;
     for (uint32_t spin = 1;; ++spin) {
         if (__atomic_load_n(status_word, __ATOMIC_ACQUIRE) != ~0ull) break;
         const uint64_t pr = std::min<uint64_t>(__atomic_load_n(progress, __ATOMIC_ACQUIRE), cap - *n);
@@ -1164,6 +1177,10 @@ int fused_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, uint64_
                 return fail(c, PBS_ERR_HIP);
             }
             if (q != hipErrorNotReady) return fail(c, PBS_ERR_HIP);
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t_launch).count() > wait_s) {
+                c->lost = true;
+                return fail(c, PBS_ERR_HIP);
+            }
         }
         __builtin_ia32_pause();
     }
@@ -1346,6 +1363,7 @@ int fused_scan_pass(pbs_chunker* c, const uint8_t* dsrc, const uint8_t* hsrc, ui
 int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final, uint64_t* out,
                    size_t cap, size_t* n_out, bool device) {
     if (!c) return PBS_ERR_INVALID;
+    if (c->lost) return fail(c, PBS_ERR_HIP);
     if (!n_out || (len && !data) || (!out && cap)) return fail(c, PBS_ERR_INVALID);
     *n_out = 0;
     if (cap < pbs_chunker_cuts_bound(c, len)) return fail(c, PBS_ERR_CAPACITY);
@@ -1475,7 +1493,28 @@ int find_cuts_impl(pbs_chunker* c, const uint8_t* data, size_t len, int is_final
     return PBS_OK;
 }
 
+// A lost handle's stream, drained within `seconds`? (hipStreamQuery only: no call that
+// could wait for a kernel that never retires)
+bool drained(pbs_chunker* c, double seconds) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) return true;
+        if (q != hipErrorNotReady) return false;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > seconds) return false;
+        usleep(1000);
+    }
+}
+
 void destroy(pbs_chunker* c) {
+    if (c->lost && !drained(c, 2.0)) {
+        // a kernel of this handle still runs and may write its buffers: they are leaked
+        // (freeing them would wait for it, possibly forever)
+        std::fprintf(stderr, "pbs_chunker_free: a kernel of this handle did not finish; its device "
+                             "buffers are not freed\n");
+        delete c;
+        return;
+    }
     server_stop(c);
     if (c->srv.probe_n) {
         const ScanServer& sv = c->srv;
@@ -1589,6 +1628,8 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     c->fused_min_bytes = kFusedMinBytes;
     if (const char* e = std::getenv("PBS_FUSED_MIN_BYTES")) c->fused_min_bytes = std::strtoull(e, nullptr, 0);
     if (const char* e = std::getenv("PBS_FUSED_MIN_AVG")) c->fused_min_avg = std::strtoull(e, nullptr, 0);
+    if (const char* e = std::getenv("PBS_FUSED_TIMEOUT_TICKS")) c->fused_timeout_ticks = std::strtoull(e, nullptr, 0);
+    if (const char* e = std::getenv("PBS_HOST_WAIT_MS")) c->host_wait_s = std::strtod(e, nullptr) * 1e-3;
     bool ok = hipGetDevice(&c->device) == hipSuccess;
     hipDeviceProp_t prop;
     if (ok && hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -1627,6 +1668,10 @@ void pbs_chunker_free(pbs_chunker* c) {
 
 int pbs_chunker_reset(pbs_chunker* c) {
     if (!c) return PBS_ERR_INVALID;
+    if (c->lost) {  // usable again once the kernel that outlived its bound has retired
+        if (!drained(c, 0.0)) return fail(c, PBS_ERR_HIP);
+        c->lost = false;
+    }
     reset_stream(c);
     // the buffers this handle outgrew (DevBuf): freed now that it is idle -- its server
     // stopped, its stream drained -- so a handle whose batches grew does not keep ~2x its
@@ -1644,6 +1689,20 @@ int pbs_chunker_reset(pbs_chunker* c) {
     }
     return PBS_OK;
 }
+
+}  // extern "C"
+
+int pbs::chunker_rewind(pbs_chunker* c) {
+    if (!c) return PBS_ERR_INVALID;
+    if (c->lost) {
+        if (!drained(c, 0.0)) return fail(c, PBS_ERR_HIP);
+        c->lost = false;
+    }
+    reset_stream(c);
+    return PBS_OK;
+}
+
+extern "C" {
 
 int pbs_chunker_set_cu_count(pbs_chunker* c, int cus) {
     if (!c || cus < 1) return PBS_ERR_INVALID;
@@ -1681,6 +1740,10 @@ int pbs_chunker_last_timing(const pbs_chunker* c, pbs_timing* t) {
 
 size_t pbs_chunker_scan(pbs_chunker* c, const uint8_t* data, size_t len) {
     if (!c) return SIZE_MAX;
+    if (c->lost) {
+        fail(c, PBS_ERR_HIP);
+        return SIZE_MAX;
+    }
     if (len && !data) {
         fail(c, PBS_ERR_INVALID);
         return SIZE_MAX;
@@ -1784,6 +1847,7 @@ int pbs_chunker_candidates_device(pbs_chunker* c, const uint8_t* dev, size_t len
                                   const uint8_t* pre, size_t pre_len, uint64_t base,
                                   uint64_t* out_dev, size_t cap, size_t* n_out) {
     if (!c) return PBS_ERR_INVALID;
+    if (c->lost) return fail(c, PBS_ERR_HIP);
     if (!n_out || (len && !dev) || (pre_len && !pre) || (cap && !out_dev) ||
         pre_len != std::min<uint64_t>(base, kWindow - 1))
         return fail(c, PBS_ERR_INVALID);
@@ -1815,6 +1879,7 @@ int pbs_chunker_candidates_device(pbs_chunker* c, const uint8_t* dev, size_t len
 int pbs_chunker_resolve_device(pbs_chunker* c, const uint64_t* cand_dev, size_t n, uint64_t end,
                                int is_final, uint64_t* out, size_t cap, size_t* n_out) {
     if (!c) return PBS_ERR_INVALID;
+    if (c->lost) return fail(c, PBS_ERR_HIP);
     if (!n_out || (n && !cand_dev) || (!out && cap)) return fail(c, PBS_ERR_INVALID);
     *n_out = 0;
     if (n > 0xFFFFFFF0ull) return fail(c, PBS_ERR_NOMEM);

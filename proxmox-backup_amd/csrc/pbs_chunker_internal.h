@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+typedef struct pbs_chunker pbs_chunker;  // include/pbs_chunker.h
+
 namespace pbs {
 
 // Hash frame of the product scan_main_kernel (scan_main.h): 1 =
@@ -222,8 +224,9 @@ constexpr uint32_t kServerVramMax = kServerMaxBytes;
 // request here, in the same fine-grained VRAM allocation (+128 bytes); the others poll
 // this record (one L2/HBM load, no PCIe), each hashes a contiguous range of passes,
 // reserves candidate slots with a device atomic and counts itself done; the last one
-// stores the acknowledgement.  tag = seq | epoch << 32 | quit << 63 (epoch: the launch
-// number, so a record left by an earlier launch is never taken for a request).
+// stores the acknowledgement.  tag = seq | epoch << 32 | busy << 62 | quit << 63 (epoch: the
+// launch number mod 2^30, so a record left by an earlier launch is never taken for a
+// request; busy: the leader is rewriting the fields -- a seqlock, scan_server.h).
 struct alignas(64) ServerDispatch {
     uint64_t tag;
     uint32_t len;   // the record's req_len (kServerHostSlot kept)
@@ -326,5 +329,11 @@ hipError_t launch_sha256_queue(const uint8_t* data, const uint8_t* key, size_t k
 void release_thread_counters();
 hipError_t launch_gen(uint64_t* out, uint64_t nwords, uint64_t seed, uint64_t word_offset,
                       int kind, hipStream_t stream);
+
+// pbs_chunker_reset without freeing the buffers the handle outgrew (pbs_chunker_reset's
+// hipFree waits for the whole device, e.g. for a digest queue grid another thread's
+// pipeline keeps resident): the pipeline's reused handle starts each stream with this;
+// its outgrown buffers go when the handle is freed.
+int chunker_rewind(::pbs_chunker* c);
 
 }  // namespace pbs

@@ -238,7 +238,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         A->c = pbs_chunker_new(avg, &err);
         A->avg = A->c ? avg : 0;
         if (!A->c) return rc = err;
-    } else if (pbs_chunker_reset(A->c) != PBS_OK) {
+    } else if (pbs::chunker_rewind(A->c) != PBS_OK) {
         return rc = PBS_ERR_HIP;
     }
     pbs_chunker* const c = A->c;
@@ -473,7 +473,9 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     bool updone = false;
     std::thread upw;
     if (ok && ext && env_u64("PBS_UPLOAD_SPEC", 1) != 0) {
-        const size_t bcap = len + 16 * cap + 64;
+        // every chunk's blob (the early encode writes the whole batch: <= len + 12 per chunk)
+        // plus up to 15 bytes of alignment per batch (a batch holds >= 1 chunk): 27 per chunk
+        const size_t bcap = len + 28 * cap + 64;
         ext->d_blobs = area->get<uint8_t>(9, bcap, false);
         if (ext->d_blobs) {
             ext->spec = true;
@@ -510,6 +512,10 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
                         upq.pop_front();
                     }
                     if (ext->enc_rc != PBS_OK) continue;  // drain after an error
+                    if (dbase > bcap) {  // (cannot happen with the bound above; never wrap bcap - dbase)
+                        ext->enc_rc = PBS_ERR_CAPACITY;
+                        continue;
+                    }
                     const size_t i0 = b[0], i1 = b[1], m = i1 - i0;
                     // the scan partition's CUs while the digest queue holds the others; every CU
                     // once all digests are in (compressible streams encode past the copies' end)

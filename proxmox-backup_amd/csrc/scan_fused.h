@@ -345,7 +345,8 @@ __device__ void fused_main(const FusedPassArgs& a, uint64_t* keep, int lane) {
     const FusedStep sc{a.sc_c, a.sc_sk, a.sc_pm, a.sc_nx};
     const uint64_t timeout = a.timeout_ticks, end = a.end;
     uint64_t s = a.s0, ncut = 0;
-    uint32_t nkeep = 0, status = 0;
+    // timeout_ticks 0 (PBS_FUSED_TIMEOUT_TICKS=0): fail at once -- the error path's test
+    uint32_t nkeep = 0, status = timeout == 0 ? 2u : 0u;
     const uint64_t t_start = wall_clock64();
     uint64_t t_wait = 0, t_ready = t_start;
     const unsigned long long below = (1ull << lane) - 1;

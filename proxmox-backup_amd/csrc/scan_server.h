@@ -66,6 +66,8 @@ constexpr int kSrvPass = kSrvLaneBytes * kSrvThreads;  // bytes per pass (8 KiB)
 constexpr int kSrvRows = kSrvThreads + 2;              // chain rows: the two before the pass, then one per lane
 constexpr int kSrvAhead = 4;                           // passes whose bytes are in flight
 constexpr uint32_t kSrvMinPasses = 2;                  // split requests: passes per workgroup at least
+constexpr uint32_t kSrvEpochMask = 0x3FFFFFFFu;         // ServerDispatch tag bits 32..61: the launch's epoch
+constexpr uint64_t kSrvTagBusy = 1ull << 62;           // ServerDispatch tag: fields being rewritten
 
 typedef uint32_t srv_u32x4 __attribute__((ext_vector_type(4)));
 
@@ -139,22 +141,32 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             }
         } else if (tid == 0) {
             // the leader's dispatch record (split requests and the exit only)
+            // a seqlock: the leader marks the tag busy before it rewrites the fields and
+            // publishes the new tag after them, so fields read between two equal, not-busy
+            // loads of the tag are that request's.  (A follower with no share of request N
+            // may still be reading when N + 1 is published: without the re-check it could
+            // pair N's seq with N + 1's len, base and gu and serve N + 1 twice.)
             for (;;) {
                 const uint64_t t = __hip_atomic_load(&disp->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (((uint32_t)(t >> 32) & 0x7FFFFFFFu) == epoch && ((t >> 63) || (uint32_t)t != last)) {
+                if (((uint32_t)(t >> 32) & kSrvEpochMask) == epoch && !(t & kSrvTagBusy) &&
+                    ((t >> 63) || (uint32_t)t != last)) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the record's fields after its tag
                     if (t >> 63) {
                         s_go = 2;
                         break;
                     }
-                    if ((uint32_t)t != last) {
-                        ctl[0] = (uint64_t)(uint32_t)t |
-                                 (uint64_t)__hip_atomic_load(&disp->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32;
-                        ctl[1] = __hip_atomic_load(&disp->base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        s_gu = __hip_atomic_load(&disp->gu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t len = __hip_atomic_load(&disp->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t b = __hip_atomic_load(&disp->base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t gu = __hip_atomic_load(&disp->gu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the fields before the re-check
+                    if (__hip_atomic_load(&disp->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == t) {
+                        ctl[0] = (uint64_t)(uint32_t)t | (uint64_t)len << 32;
+                        ctl[1] = b;
+                        s_gu = gu;
                         s_go = 1;
                         break;
                     }
+                    continue;  // rewritten while read: load it again
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
@@ -185,6 +197,11 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
             const uint32_t want = npass / kSrvMinPasses;
             gu = want < 1 ? 1 : (want < n_wg ? want : n_wg);
             if (gu > 1 && tid == 0) {
+                // busy first (the release orders it before the field stores), then the fields,
+                // then the tag (release: the fields before it)
+                __hip_atomic_store(&disp->tag, (uint64_t)last | (uint64_t)epoch << 32 | kSrvTagBusy,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 __hip_atomic_store(&disp->len, (uint32_t)(ctl[0] >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&disp->base, ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&disp->gu, gu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

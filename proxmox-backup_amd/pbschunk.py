@@ -674,6 +674,26 @@ def blob_encode_chunks_device(dev_ptr: int, data_len: int, bounds, blobs_dev: in
     return offs, crcs, comp, t.as_dict()
 
 
+def blob_encode_spans_device(dev_ptr: int, data_len: int, spans, blobs_dev: int, blobs_cap: int,
+                             base: int = 0, compress: bool = True, hip_stream: int = 0):
+    """pbs_blob_encode_spans_device: as blob_encode_chunks_device for chunks given as
+    (start, end) absolute spans in any order (e.g. an upload's new chunks); blob i is
+    written for span i.  Returns (offsets (n + 1), crcs (n), compressed flags (n), timing)."""
+    sp = np.ascontiguousarray(np.asarray(spans, dtype=np.uint64).reshape(-1, 2))
+    n = sp.shape[0]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    crcs = np.empty(n, dtype=np.uint32)
+    comp = np.empty(n, dtype=np.uint8)
+    t = BlobEncodeTiming()
+    rc = lib().pbs_blob_encode_spans_device(ctypes.c_void_p(dev_ptr), data_len, base, sp.ctypes.data, n,
+                                            1 if compress else 0, ctypes.c_void_p(blobs_dev), blobs_cap,
+                                            offs.ctypes.data, crcs.ctypes.data, comp.ctypes.data,
+                                            ctypes.byref(t), ctypes.c_void_p(hip_stream))
+    if rc != PBS_OK:
+        raise ChunkerError(rc, "pbs_blob_encode_spans_device")
+    return offs, crcs, comp, t.as_dict()
+
+
 def debug_arena_allocs() -> int:
     """Device buffers the per-device work areas have allocated so far (tests)."""
     return int(lib().pbs_debug_arena_allocs())

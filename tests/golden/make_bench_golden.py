@@ -18,6 +18,8 @@ Streams (bench.py's generators, seeds as in bench.SEEDS / stream_seed):
     (pbs-datastore/src/chunk_store.rs:33-48: 64 KiB .. 4 MiB; config 5 = vmimage 256 KiB;
     random 4 MiB = bench.py's secondary line);
   * random 8 GiB, 4 MiB (config 2);
+  * vmimage 16 GiB, 4 MiB: the first 16 GiB of config 3's stream (bench.py's pipeline and
+    upload stages);
   * the small streams tests/test_dist.py runs bench.py on.
 
     python tests/golden/make_bench_golden.py [--threads 8] [--only SUBSTR] [--check]
@@ -63,6 +65,9 @@ def streams():
             out.append(("vmimage", big, avg, SEED_VM))
         out.append(("random", big, avg, SEED_RANDOM))
     out.append(("random", stream_bytes(8), 4 * MiB, SEED_RANDOM))
+    # bench.py's f-stages: the host pipeline and the compressing upload over the first
+    # --stage-gib (16) GiB of the config-3 stream
+    out.append(("vmimage", stream_bytes(16), 4 * MiB, SEED_VM))
     # tests/test_dist.py: 2 ranks of 0.25 GiB (4 MiB) and of 0.01 GiB (4 MiB, 64 KiB)
     for gib, avg in ((0.25, 4 * MiB), (0.01, 4 * MiB), (0.01, 64 * KiB)):
         for r in range(2):
