@@ -54,6 +54,7 @@
 #include "pbs_chunker.h"
 #include "pbs_chunker_internal.h"
 #include "dev_arena.h"
+#include "host_share.h"
 #include "pbs_digest.h"
 #include "sha_host.h"
 
@@ -367,71 +368,21 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     // (profiles/r04/sha_lanes/) 25/20 -> 1321-1326, 20/0 -> 1279, 10-17 MB/s with 0-10 ms ->
     // 1240-1256
     const uint64_t host_min = env_u64("PBS_PIPE_HOST_MIN", ~0ull);
-    const bool deadline = host_min == ~0ull;
     const double gpu_bpms = (double)env_u64("PBS_PIPE_GPU_MBS", 15) * 1e3;  // bytes per ms
     const double slack_ms = (double)env_u64("PBS_PIPE_SLACK_MS", 10);
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     const int hthreads = host_min ? (int)env_u64("PBS_PIPE_HOST_THREADS", (uint64_t)std::max(1, std::min(hw, 16) - 2)) : 0;
-    std::deque<uint64_t> hq;  // chunk indices
-    std::mutex hmu;
-    std::condition_variable hcv;
-    bool hdone = false;
-    std::atomic<uint64_t> host_chunks{0}, host_bytes{0};
     double host_done_at = 0;
-    std::atomic<uint64_t> host_work_us{0};  // the host threads' last digest done (us after t0)
     std::vector<uint8_t> hmask;  // 1 = digest computed on the host
-    std::map<uint64_t, std::array<uint8_t, 32>> zero_dig;  // digest of an all-zero chunk per length
     std::vector<std::thread> hpool;
     hmask.assign(ok ? cap : 0, 0);
-    // the upload path's encoder waits per chunk for its digest: a host-routed chunk's flag
-    // here, a GPU job's `done` in the job record; dig_final once every digest is in `digests`
-    std::unique_ptr<std::atomic<uint8_t>[]> hflag(new std::atomic<uint8_t>[ok ? cap : 1]());
+    // the host threads' queue and zero-chunk memo (host_share.h); the upload path's encoder
+    // waits per chunk for its digest: a host-routed chunk's flag there, a GPU job's `done` in
+    // the job record; dig_final once every digest is in `digests`
+    pbs::HostShare hs(host, ends, digests, ok ? cap : 0, key, key_len, t0);
     std::vector<uint64_t> jobof(ok ? cap : 0, 0);
     std::atomic<bool> dig_final{false};
-    // one host worker: takes routed chunks until the queue is empty and the routing done,
-    // up to four in step (pbs::sha256_host_lanes); an all-zero chunk is hashed once per length
-    auto host_work = [&] {
-        auto next = [&](pbs::ShaJob& j, bool block) {
-            for (;;) {
-                uint64_t i;
-                {
-                    std::unique_lock<std::mutex> g(hmu);
-                    if (block) hcv.wait(g, [&] { return hdone || !hq.empty(); });
-                    if (hq.empty()) return false;
-                    i = hq.front();
-                    hq.pop_front();
-                }
-                const uint64_t s0 = i ? ends[i - 1] : 0, cl = ends[i] - s0;
-                uint8_t* out = digests + 32 * i;
-                const bool zero = pbs::all_zero(host + s0, cl);
-                if (zero) {
-                    std::lock_guard<std::mutex> g(hmu);
-                    auto it = zero_dig.find(cl);
-                    if (it != zero_dig.end()) {
-                        std::memcpy(out, it->second.data(), 32);
-                        host_chunks += 1;
-                        hflag[i].store(1, std::memory_order_release);
-                        continue;
-                    }
-                }
-                j = pbs::ShaJob{host + s0, cl, out, zero ? 1ull : 0ull};
-                return true;
-            }
-        };
-        auto done = [&](const pbs::ShaJob& j) {
-            if (j.tag) {
-                std::lock_guard<std::mutex> g(hmu);
-                std::memcpy(zero_dig[j.len].data(), j.out, 32);
-            }
-            host_chunks += 1;
-            host_bytes += j.len;
-            hflag[(size_t)(j.out - digests) / 32].store(1, std::memory_order_release);
-            const uint64_t us = (uint64_t)(ms_since(t0) * 1000.0);
-            for (uint64_t cur = host_work_us.load(); us > cur && !host_work_us.compare_exchange_weak(cur, us);) {
-            }
-        };
-        pbs::sha256_host_lanes(next, done, key, key_len);
-    };
+    auto host_work = [&] { hs.work(); };
     if (ok && hthreads > 0)
         for (int j = 0; j < hthreads; ++j) hpool.emplace_back(host_work);
     std::thread copier;
@@ -564,7 +515,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
                         if (fin) break;
                         bool all = true;
                         for (size_t i = i0; i < i1 && all; ++i)
-                            all = hmask[i] ? hflag[i].load(std::memory_order_acquire) != 0
+                            all = hmask[i] ? hs.flag(i)
                                            : __atomic_load_n(&q_jobs[jobof[i]].done, __ATOMIC_ACQUIRE) != 0;
                         if (all) break;
                         std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -713,12 +664,11 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
             const double now = ms_since(t0);
             // projected end of the copy: the rate at which pieces have become resident so
             // far (this loop waits for each piece's copy), ~55 GB/s before two pieces
-            const double rate = k >= 1 && now > 0 ? (double)(off + pn) / now : 55e6;  // bytes per ms
-            const double t_end = (double)len / rate + slack_ms;
+            const double t_end = pbs::projected_copy_end(len, off + pn, k, now, slack_ms);
             size_t nh = 0;
             for (size_t i = n0; i < n; ++i) {
                 const uint64_t s0 = i ? ends[i - 1] : 0, cl = ends[i] - s0;
-                const bool to_host = hthreads > 0 && (deadline ? now + (double)cl / gpu_bpms > t_end : cl >= host_min);
+                const bool to_host = pbs::route_to_host(hthreads, host_min, now, cl, gpu_bpms, t_end);
                 if (to_host) {
                     hmask[i] = 1;
                     ++nh;
@@ -733,14 +683,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
             }
             publish(false);  // the jobs above were written before the count (release)
             if (nj) q_launch();  // (again, if the grid went idle and exited)
-            if (nh) {
-                {
-                    std::lock_guard<std::mutex> g(hmu);
-                    for (size_t i = n0; i < n; ++i)
-                        if (hmask[i]) hq.push_back(i);
-                }
-                hcv.notify_all();
-            }
+            if (nh) hs.push(hmask.data(), n0, n);
         }
         // the upload's encoder takes this piece's chunks (routed: their digests will come)
         if (upw.joinable() && n > n0) {
@@ -785,11 +728,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     }
     if (q_running) publish(true);  // every path: the queue grid drains
     if (q_launches && rc != PBS_OK) (void)hipStreamSynchronize(s_dig[0]);  // before its memory goes
-    {
-        std::lock_guard<std::mutex> g(hmu);
-        hdone = true;
-    }
-    hcv.notify_all();
+    hs.finish();
     // the routing is done: this thread hashes what is left of the host share, beside the
     // pool and the copy thread (16 threads in the drain instead of 14)
     if (hthreads > 0 && rc == PBS_OK) host_work();
@@ -820,7 +759,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     // the pool (no hipFree any more to wait for it)
     for (hipStream_t s : {s_copy, s_scan, s_dig[0], s_dig[1], s_dig[2], s_dig[3]})
         if (s) (void)hipStreamSynchronize(s);
-    if (!host_done_at && host_chunks) host_done_at = ms_since(t0);
+    if (!host_done_at && hs.chunks()) host_done_at = ms_since(t0);
     pbs::DigestQueueDev qd{};
     if (q_launches) (void)hipMemcpy(&qd, d_q, sizeof qd, hipMemcpyDeviceToHost);
     // jobs the queue grid never took (it drains after stall_ticks without a new job, e.g.
@@ -850,15 +789,15 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         timing->bytes = len;
         timing->chunks = n;
         timing->pieces = npieces;
-        timing->host_chunks = host_chunks;
-        timing->host_bytes = host_bytes;
+        timing->host_chunks = hs.chunks();
+        timing->host_bytes = hs.bytes();
         timing->host_done_ms = host_done_at;
         timing->host_threads = hthreads;
         timing->gpu_jobs = nj;
         timing->gpu_claimed = qd.next;
         timing->queue_launches = q_launches;
         timing->gpu_done_ms = gpu_done_at;
-        timing->host_work_ms = host_work_us.load() / 1000.0;
+        timing->host_work_ms = hs.last_done_us() / 1000.0;
         if (std::getenv("PBS_PIPE_DEBUG")) {
             std::fprintf(stderr, "digest queue: jobs %llu claimed %llu launches %llu mirror %llx polls %llu last_h %llx; seen:",
                          (unsigned long long)nj, qd.next, (unsigned long long)q_launches, qd.mirror, qd.polls,
