@@ -1620,6 +1620,8 @@ pbs_chunker* pbs_chunker_new(size_t chunk_size_avg, int* err) {
     if (const char* e = std::getenv("PBS_SERVER_POLL")) c->srv.flags = e[0] == '4' ? kSrvPollAll : 0u;
     if (const char* e = std::getenv("PBS_SERVER_PROBE"))
         if (e[0] == '1') c->srv.flags |= kSrvProbe;
+    if (const char* e = std::getenv("PBS_SERVER_MINPASS"))  // passes per workgroup of a split request (A/B)
+        c->srv.flags |= (uint32_t)(std::min(255L, std::max(1L, std::atol(e)))) << kSrvMinPassShift;
     c->fused_min_avg = kFusedMinAvg;
     if (const char* e = std::getenv("PBS_BALANCE")) c->balance = std::atoi(e);
     if (const char* e = std::getenv("PBS_DIRECT_OUT")) c->direct_out = e[0] != '0';

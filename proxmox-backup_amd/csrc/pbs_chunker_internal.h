@@ -270,6 +270,7 @@ static_assert(sizeof(ServerReq) == 64, "ServerReq is one cache line");
 constexpr uint32_t kSrvPollAll = 1;  // launch flag: every wave polls (staggered), not one lane
 constexpr uint32_t kSrvProbe = 2;    // launch flag: per-request phase stamps into probe[]
 constexpr uint32_t kSrvDevReq = 4;   // launch flag: request + slot in fine-grained VRAM written by the host
+constexpr uint32_t kSrvMinPassShift = 8;  // launch flags bits 8-15: passes per workgroup of a split request (0: default)
 hipError_t launch_scan_server(ServerMailbox* mb_dev, const ServerReq* req_dev, ServerDispatch* disp_dev,
                               const uint8_t* slot_dev, const uint8_t* hslot_dev, const uint32_t* table_rot,
                               uint32_t thr, uint64_t last_seq, uint64_t idle_ticks,

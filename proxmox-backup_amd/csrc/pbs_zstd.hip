@@ -1837,17 +1837,17 @@ __device__ __forceinline__ void st_coded(PBS_GLOBAL Coded* p, const Coded& c) {
     *(PBS_GLOBAL v4u*)p = v4u{c.ll, c.ml, c.ofv, c.codes};
 }
 
-__device__ __noinline__ void rep_code_wave(const Ctl& ctl, const Seq* __restrict__ wseq_g, Coded* __restrict__ coded_g,
-                                           uint32_t w2, int lane) {
+__device__ __noinline__ void rep_code_wave(const uint32_t* nseq, const uint32_t* lastend, const Seq* __restrict__ wseq_g,
+                                           Coded* __restrict__ coded_g, uint32_t w2, int lane) {
     const PBS_GLOBAL Seq* const wseq_all = (const PBS_GLOBAL Seq*)wseq_g;
     PBS_GLOBAL Coded* const coded = (PBS_GLOBAL Coded*)coded_g;
     uint32_t first = 0, lit_end = 0;
     for (uint32_t v = 0; v < w2; ++v) {
-        first += min(ctl.nseq[v], kZSubSeq);
-        if (ctl.nseq[v]) lit_end = ctl.lastend[v];
+        first += min(nseq[v], kZSubSeq);
+        if (nseq[v]) lit_end = lastend[v];
     }
     const PBS_GLOBAL Seq* const ws = wseq_all + (uint64_t)w2 * kZSubSeq;
-    const uint32_t cnt = min(ctl.nseq[w2], kZSubSeq);
+    const uint32_t cnt = min(nseq[w2], kZSubSeq);
     if (!cnt) return;
     const uint32_t seg = (cnt + 63) / 64;
     const uint32_t a = min(cnt, (uint32_t)lane * seg), b = min(cnt, a + seg);
@@ -2193,7 +2193,7 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                 zt = t2;
             }
         };
-        rep_code_wave(ctl, wseq_all, coded, (uint32_t)wave, lane);
+        rep_code_wave(ctl.nseq, ctl.lastend, wseq_all, coded, (uint32_t)wave, lane);
         __threadfence_block();
         {
             // this sub-block's code histograms (LL | ML | OF, 121 bins) into the wave's own copy

@@ -194,7 +194,8 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
         // split the request over gu workgroups (the leader decides and publishes it)
         uint32_t gu = 1;
         if (leader) {
-            const uint32_t want = npass / kSrvMinPasses;
+            const uint32_t minp = (flags >> kSrvMinPassShift) & 0xFFu;  // 0: kSrvMinPasses
+            const uint32_t want = npass / (minp ? minp : kSrvMinPasses);
             gu = want < 1 ? 1 : (want < n_wg ? want : n_wg);
             if (gu > 1 && tid == 0) {
                 // busy first (the release orders it before the field stores), then the fields,
