@@ -812,10 +812,32 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
     __atomic_store_n(&sv.req->req_seq, seq, __ATOMIC_RELEASE);
     __builtin_ia32_sfence();
     const auto t0 = std::chrono::steady_clock::now();
+    // the kernel's split of this request (scan_server.h: gu workgroups, each acknowledging
+    // its own region of the candidates; 1: the leader alone, mb->ack_seq)
+    const uint32_t npass = (uint32_t)((bl + 8191) / 8192);
+    const uint32_t minp = (sv.flags >> kSrvMinPassShift) & 0xFFu;
+    const uint32_t want = npass / (minp ? minp : kSrvMinPasses), nwg = sv.disp_dev ? sv.n_wg : 1u;
+    const uint32_t gu = want < 1 ? 1u : std::min(want, nwg);
     uint64_t ack = 0;
     for (uint32_t spin = 0;; ++spin) {
-        ack = __atomic_load_n(&sv.mb->ack_seq, __ATOMIC_ACQUIRE);
-        if ((uint32_t)ack == seq) break;
+        if (gu > 1) {
+            uint32_t got = 0, cnt = 0;
+            bool ovf = false;
+            for (uint32_t g = 0; g < gu; ++g) {
+                const uint64_t a = __atomic_load_n(&sv.mb->wg_ack[8 * g], __ATOMIC_ACQUIRE);
+                if ((uint32_t)a != seq) break;
+                ++got;
+                cnt += (uint32_t)((a >> 32) & 0x7FFFFFFFull);
+                ovf |= (a >> 63) != 0;
+            }
+            if (got == gu) {
+                ack = (uint64_t)seq | (uint64_t)cnt << 32 | (ovf ? 1ull << 63 : 0ull);
+                break;
+            }
+        } else {
+            ack = __atomic_load_n(&sv.mb->ack_seq, __ATOMIC_ACQUIRE);
+            if ((uint32_t)ack == seq) break;
+        }
         const bool late = (spin & 1023) == 1023 &&
                           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kServerTimeoutS;
         if (!late && __atomic_load_n(&sv.mb->exited, __ATOMIC_ACQUIRE) == (uint32_t)(seq - 1)) {
@@ -842,9 +864,17 @@ int server_scan(pbs_chunker* c, const uint8_t* hsrc, uint64_t pos, uint64_t bl, 
     const uint64_t k = (ack >> 32) & 0x7FFFFFFFull;
     const size_t old = c->pending.size();
     c->pending.resize(old + k);
-    std::memcpy(c->pending.data() + old, sv.mb->cand, k * 8);
-    // a request split over workgroups returns their runs in the order they reserved slots
-    std::sort(c->pending.begin() + (ptrdiff_t)old, c->pending.end());
+    if (gu > 1) {  // the regions in workgroup order: stream order
+        const uint32_t rcap = kServerCand / gu;
+        uint64_t at = old;
+        for (uint32_t g = 0; g < gu; ++g) {
+            const uint64_t kg = (sv.mb->wg_ack[8 * g] >> 32) & 0x7FFFFFFFull;
+            std::memcpy(c->pending.data() + at, sv.mb->cand + (uint64_t)g * rcap, kg * 8);
+            at += kg;
+        }
+    } else {
+        std::memcpy(c->pending.data() + old, sv.mb->cand, k * 8);
+    }
     c->timing.bytes += bl;
     c->timing.candidates += k;
     update_carry(c, hsrc, bl);

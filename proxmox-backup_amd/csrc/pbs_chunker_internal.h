@@ -232,10 +232,9 @@ struct alignas(64) ServerDispatch {
     uint32_t len;   // the record's req_len (kServerHostSlot kept)
     uint32_t gu;    // workgroups serving this request
     uint64_t base;
-    uint32_t cnt_cand;  // candidates reserved so far
-    uint32_t cnt_done;  // workgroups done
 };
 constexpr uint32_t kSrvMaxWgs = 32;
+constexpr uint32_t kSrvMinPasses = 2;  // split requests: passes per workgroup at least (PBS_SERVER_MINPASS)
 constexpr uint32_t kSrvDefaultWgs = 16;
 constexpr uint32_t kServerHeader = 256;  // VRAM allocation: record (0), dispatch (128), then the slot
 static_assert(sizeof(ServerDispatch) <= kServerHeader - 128, "dispatch record past the header");
@@ -254,6 +253,11 @@ struct alignas(64) ServerMailbox {
                                    // more than kServerCand (nothing usable)
     uint64_t exited;               // last served request when the kernel exited; ~0 while up
     uint64_t probe[4];             // kSrvProbe: wall_clock64 at request seen, chains done, hashed, acked
+    // a split request (gu > 1 workgroups, scan_server.h): workgroup g stores its candidates in
+    // cand[g * (kServerCand / gu) ..] and then acknowledges alone in wg_ack[8 g] (its own cache
+    // line; the same word layout as ack_seq, the count of its region) -- no device atomics,
+    // and the host reads the regions in order (ascending already)
+    alignas(64) uint64_t wg_ack[8 * kSrvMaxWgs];
     uint64_t cand[kServerCand];
 };
 // The request record alone (the layout of ServerMailbox's first 64 bytes).  With the

@@ -2513,6 +2513,727 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
     }
 }
 
+// ---------------------------------------------------------------- split form (round 6)
+// The same blocks in two kernels, byte for byte: zstd_parse_kernel (one 512-thread workgroup
+// per CU: stage, RLE test, parse, then per sub-block the repeat coding and code histograms,
+// the literal bitmap, the literal histogram and the literals compacted to global memory) and
+// zstd_entropy_kernel (256-thread workgroups, two per CU: literal mode on wave 0 beside the
+// LL / OF / ML tables and state chains on waves 1-3, then the literal section and the
+// sequence bit stream from the compacted literals and the coded sequences).  In the fused
+// kernel the entropy half ran on 4 of the block's 8 waves while the others waited at a
+// barrier and no other block could use the CU's LDS; here a CU runs two blocks' entropy
+// halves at once (~75 KiB of LDS each) and the parse kernel's waves never wait for one.
+// The batch of items between the two kernels lives in global memory (ZItem, the coded
+// sequences, the literals).
+constexpr int kEThreads = 256;
+constexpr int kEWaves = kEThreads / 64;
+struct ZItem {
+    uint32_t kind;  // 0: the entropy kernel encodes the block; 1: complete (empty or RLE)
+    uint32_t nlit, need_full, pad;
+    uint32_t nseq[kZWaves];
+    uint32_t shist[36 + 53 + 32];  // LL | ML | OF code histograms
+    uint32_t pad2[3];
+    uint32_t hist[256];  // literal histogram (need_full)
+};
+// the parse kernel's work area after the parse (the tables are dead then)
+struct PArea {
+    uint32_t bitmap[kEncBlock / 32];
+    uint32_t wh[kZWaves * 256];  // per-wave literal histograms
+    uint32_t wc[kZWaves * 128];  // per-wave code histograms (LL | ML | OF)
+    uint32_t hist[256];
+    uint8_t lit[32 * 1024];  // literals compacted in pieces, then copied out
+};
+static_assert(sizeof(PArea) <= 64 * 1024, "the parse kernel's buffers fit the work area");
+struct PCtl {
+    uint32_t nseq[kZWaves], lastend[kZWaves], wsum[kZWaves], wsum2[kZWaves], need_full;
+};
+
+__global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zstd_parse_kernel(
+    const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
+    const uint64_t* __restrict__ items, uint64_t nitems, uint64_t item_base, uint8_t* __restrict__ slots,
+    uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch, Coded* __restrict__ coded_items,
+    uint8_t* __restrict__ lit_items, ZItem* __restrict__ zitems, int probe_on, int64_t dbg_item) {
+    __shared__ uint4 stage[kZStageWords];
+    __shared__ __attribute__((aligned(16))) uint8_t work[64 * 1024];
+    __shared__ PCtl pc;
+    const int tid = threadIdx.x, lane = tid & 63, wave = (int)uni((uint32_t)tid >> 6);
+    const bool probe = probe_on && blockIdx.x == 0 && tid == 0;
+    uint64_t tp = probe ? wall_clock64() : 0;
+    uint16_t* const tabs = reinterpret_cast<uint16_t*>(work);
+    PArea& A = *reinterpret_cast<PArea*>(work);
+    Seq* const wseq_all = seq_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
+    for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
+        __syncthreads();  // LDS of the previous item
+        ZMARK(9);
+        ZItem* const zi = zitems + k;
+        const uint64_t it = items[k];
+        const uint64_t ci = it >> 32, j = (uint32_t)it;
+        const uint64_t c0 = bounds[2 * ci], c1 = bounds[2 * ci + 1];
+        const uint64_t len = c1 - c0, off = j * (uint64_t)kEncBlock;
+        const uint32_t n = (uint32_t)(len > off ? (len - off < kEncBlock ? len - off : kEncBlock) : 0);
+        const bool last = off + n == len;
+        uint8_t* const out = slots + k * kSlot;
+        if (n == 0) {  // the empty chunk's frame: one empty raw block
+            if (tid == 0) {
+                write_block_header(out, true, 0, 0);
+                sizes[k] = 3;
+                zi->kind = 1;
+            }
+            continue;
+        }
+        const uint32_t hist = (uint32_t)(off < kZHist ? off : kZHist);
+        const uint32_t N = hist + n;
+        const uint8_t* const wsrc = data + (c0 - base) + off - hist;
+        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(wsrc) & 15);
+        const uint8_t* const a0 = wsrc - r;
+        const uint32_t nw = (N + r + 15) >> 4;
+        const uint32_t b0 = data[(c0 - base) + off];
+        const uint32_t bb = b0 * 0x01010101u, blo = r + hist, bhi = r + N;
+        auto same_dw = [&](uint32_t a, uint32_t val) {
+            if (a + 4 <= blo || a >= bhi) return true;
+            uint32_t mk = 0xFFFFFFFFu;
+            if (a < blo) mk &= 0xFFFFFFFFu << (8 * (blo - a));
+            if (a + 4 > bhi) mk &= 0xFFFFFFFFu >> (8 * (a + 4 - bhi));
+            return ((val ^ bb) & mk) == 0;
+        };
+        bool same = true;
+        for (uint32_t i0 = tid; i0 < nw; i0 += 4 * kZThreads) {
+            v4u v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t i = i0 + kZThreads * q;
+                if (i < nw) v[q] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(a0) + i);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t i = i0 + kZThreads * q;
+                if (i < nw) {
+                    stage[i] = make_uint4(v[q].x, v[q].y, v[q].z, v[q].w);
+                    same = same && same_dw(16 * i, v[q].x) && same_dw(16 * i + 4, v[q].y) &&
+                           same_dw(16 * i + 8, v[q].z) && same_dw(16 * i + 12, v[q].w);
+                }
+            }
+        }
+        if (tid < 2) stage[nw + tid] = make_uint4(0, 0, 0, 0);
+        if (__syncthreads_and(same)) {  // RLE block: every byte equal
+            ZMARK(0);
+            if (tid == 0) {
+                write_block_header(out, last, 1, n);
+                out[3] = (uint8_t)b0;
+                sizes[k] = 4;
+                zi->kind = 1;
+            }
+            continue;
+        }
+        ZMARK(0);
+        const Win W{reinterpret_cast<const uint32_t*>(stage), r};
+        {
+            const uint64_t tw0 = probe_on && blockIdx.x == 0 ? wall_clock64() : 0;
+            const uint64_t pr = parse_subblock(W, tabs, wseq_all, hist, N, wave, lane,
+                                               probe_on && blockIdx.x == 0 && wave == 0 ? g_zprobe : nullptr);
+            if (probe_on && blockIdx.x == 0 && lane == 0) atomicAdd(&g_zprobe[34 + wave], wall_clock64() - tw0);
+            if (lane == 0) {
+                pc.nseq[wave] = (uint32_t)pr;
+                pc.lastend[wave] = (uint32_t)(pr >> 32);
+            }
+            __threadfence_block();  // the sequence list (global) before the other waves read it
+        }
+        __syncthreads();
+        ZMARK(1);
+        if ((int64_t)(k + item_base) == dbg_item) {
+            for (uint32_t i = tid; i < kZWaves * (1 + 3 * kZSubSeq); i += kZThreads) {
+                const uint32_t w2 = i / (1 + 3 * kZSubSeq), r2 = i % (1 + 3 * kZSubSeq);
+                g_zdbg[i] = r2 == 0 ? pc.nseq[w2]
+                                    : reinterpret_cast<const uint32_t*>(wseq_all + (uint64_t)w2 * kZSubSeq)[r2 - 1];
+            }
+        }
+        // ---- per sub-block (its wave): the matches out of the literal bitmap, the repeat
+        // coding, the code histogram
+        for (uint32_t i = tid; i < kEncBlock / 32; i += kZThreads) {
+            const uint32_t b = 32 * i;
+            A.bitmap[i] = b + 32 <= n ? 0xFFFFFFFFu : (b >= n ? 0u : (0xFFFFFFFFu >> (32 - (n - b))));
+        }
+        for (uint32_t i = tid; i < kZWaves * 256; i += kZThreads) A.wh[i] = 0;
+        for (uint32_t i = tid; i < kZWaves * 128; i += kZThreads) A.wc[i] = 0;
+        __syncthreads();
+        Coded* const coded = coded_items + k * (uint64_t)kZBlockSeq;
+        {
+            const Seq* const wseq = wseq_all + (uint64_t)wave * kZSubSeq;
+            const uint32_t nsw = min(pc.nseq[wave], kZSubSeq);
+            for (uint32_t q0 = 0; q0 < nsw; q0 += 64) {
+                uint32_t a = 0, b = 0;
+                if (q0 + lane < nsw) {
+                    const Seq e = wseq[q0 + lane];
+                    a = e.pos;
+                    b = e.pos + e.ml;
+                }
+                uint32_t wa = 0, wb = 0;
+                if (a < b) {
+                    if ((a >> 5) == ((b - 1) >> 5)) {
+                        const uint32_t cnt = b - a;
+                        const uint32_t mask = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << (a & 31);
+                        if (cnt == 32)
+                            A.bitmap[a >> 5] = 0;
+                        else
+                            atomicAnd(&A.bitmap[a >> 5], ~mask);
+                    } else {
+                        if (a & 31) atomicAnd(&A.bitmap[a >> 5], (1u << (a & 31)) - 1u);
+                        if (b & 31) atomicAnd(&A.bitmap[b >> 5], ~((1u << (b & 31)) - 1u));
+                        wa = (a + 31) >> 5;
+                        wb = b >> 5;
+                        if (wb - wa <= 4) {
+                            for (uint32_t w = wa; w < wb; ++w) A.bitmap[w] = 0;
+                            wb = wa;
+                        }
+                    }
+                }
+                for (unsigned long long lg = __ballot(wb > wa); lg; lg &= lg - 1) {
+                    const int l = __builtin_ctzll(lg);
+                    const uint32_t la = (uint32_t)__builtin_amdgcn_readlane((int)wa, l);
+                    const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)wb, l);
+                    for (uint32_t w = la + lane; w < lb; w += 64) A.bitmap[w] = 0;
+                }
+            }
+        }
+        rep_code_wave(pc.nseq, pc.lastend, wseq_all, coded, (uint32_t)wave, lane);
+        __threadfence_block();
+        {
+            uint32_t* const wc = A.wc + wave * 128;
+            uint32_t first = 0;
+            for (int w2 = 0; w2 < wave; ++w2) first += min(pc.nseq[w2], kZSubSeq);
+            const uint32_t cnt = min(pc.nseq[wave], kZSubSeq);
+            for (uint32_t q0 = 0; q0 < cnt; q0 += 64 * 4) {
+                uint32_t cv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t q = q0 + 64 * (uint32_t)u + (uint32_t)lane;
+                    cv[u] = q < cnt ? coded[first + q].codes : 0xFFFFFFFFu;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (cv[u] != 0xFFFFFFFFu) {
+                        atomicAdd(&wc[cv[u] & 0xFF], 1u);
+                        atomicAdd(&wc[36 + ((cv[u] >> 8) & 0xFF)], 1u);
+                        atomicAdd(&wc[36 + 53 + (cv[u] >> 16)], 1u);
+                    }
+            }
+        }
+        __syncthreads();
+        ZMARK(3);
+        // ---- literals: per thread (block positions [128 t, 128 t + 128)) its count and the
+        // sampled histogram; the full histogram only when the sample says Huffman may pay
+        uint32_t bmw[4], cnt_t = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bmw[i] = A.bitmap[4 * tid + i];
+            cnt_t += __builtin_popcount(bmw[i]);
+        }
+        uint32_t* const wh = A.wh + wave * 256;
+        uint32_t samp_t = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if ((bmw[q >> 1] >> ((16 * q) & 31)) & 1u) {
+                atomicAdd(&wh[W.byte(hist + 128 * tid + 16 * q)], 1u);
+                ++samp_t;
+            }
+        }
+        const uint32_t incl = wave_incl(cnt_t, lane);
+        const uint32_t sincl = wave_incl(samp_t, lane);
+        if (lane == 63) {
+            pc.wsum[wave] = incl;
+            pc.wsum2[wave] = sincl;
+        }
+        __syncthreads();
+        uint32_t litbase = incl - cnt_t, nlit = 0, nsamp = 0;
+        for (int w2 = 0; w2 < kZWaves; ++w2) {
+            litbase += w2 < wave ? pc.wsum[w2] : 0u;
+            nlit += pc.wsum[w2];
+            nsamp += pc.wsum2[w2];
+        }
+        if (tid < 256) {
+            uint32_t c = 0;
+            for (int w2 = 0; w2 < kZWaves; ++w2) c += A.wh[w2 * 256 + tid];
+            A.hist[tid] = c;
+        }
+        __syncthreads();
+        if (wave == 0) {  // 1: the full histogram is needed; 0: raw literals
+            uint32_t need = nlit > 0;
+            if (nlit >= 32 && nsamp > 0) {
+                uint64_t es = 0;
+                const uint32_t lm = lg256(nsamp);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t c = A.hist[lane + 64 * i];
+                    if (c) es += (uint64_t)c * (lm - lg256(c));
+                }
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) es += __shfl_xor(es, d, 64);
+                if (es * nlit / nsamp / 2048 + 64 >= (uint64_t)nlit - nlit / 64) need = 0;
+            }
+            if (lane == 0) pc.need_full = need;
+        }
+        __syncthreads();
+        const uint32_t need_full = pc.need_full;
+        if (need_full) {
+            for (uint32_t i = tid; i < kZWaves * 256; i += kZThreads) A.wh[i] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1)
+                    atomicAdd(&wh[W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2))], 1u);
+            __syncthreads();
+            if (tid < 256) {
+                uint32_t c = 0;
+                for (int w2 = 0; w2 < kZWaves; ++w2) c += A.wh[w2 * 256 + tid];
+                zi->hist[tid] = c;
+            }
+        }
+        if (tid < 36 + 53 + 32) {
+            uint32_t c = 0;
+            for (int w2 = 0; w2 < kZWaves; ++w2) c += A.wc[w2 * 128 + tid];
+            zi->shist[tid] = c;
+        }
+        if (tid < kZWaves) zi->nseq[tid] = pc.nseq[tid];
+        if (tid == 0) {
+            zi->kind = 0;
+            zi->nlit = nlit;
+            zi->need_full = need_full;
+        }
+        ZMARK(2);
+        // ---- the literals compacted in order to global memory (through LDS, dword stores)
+        uint8_t* const lo = lit_items + k * (uint64_t)kEncBlock;
+        for (uint32_t pb = 0; pb < nlit; pb += (uint32_t)sizeof(A.lit)) {
+            const uint32_t pe = min(nlit, pb + (uint32_t)sizeof(A.lit));
+            uint32_t idx = litbase;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                for (uint32_t m2 = bmw[i]; m2; m2 &= m2 - 1, ++idx)
+                    if (idx >= pb && idx < pe) A.lit[idx - pb] = (uint8_t)W.byte(hist + 128 * tid + 32 * i + __builtin_ctz(m2));
+            __syncthreads();
+            lds_to_global(lo + pb, reinterpret_cast<const uint32_t*>(A.lit), pe - pb, (uint32_t)tid, kZThreads);
+            __syncthreads();
+        }
+        if (probe) {
+            g_zprobe[10] += 1;
+            g_zprobe[11] += min(pc.nseq[0], kZSubSeq) + min(pc.nseq[1], kZSubSeq) + min(pc.nseq[2], kZSubSeq) +
+                            min(pc.nseq[3], kZSubSeq) + min(pc.nseq[4], kZSubSeq) + min(pc.nseq[5], kZSubSeq) +
+                            min(pc.nseq[6], kZSubSeq) + min(pc.nseq[7], kZSubSeq);
+            g_zprobe[12] += nlit;
+        }
+        ZMARK(15);
+    }
+}
+
+// thread t of nt: the compacted literals [i0, i1) of `lits` (16-byte aligned) in order,
+// fn(index, byte); the next 16 bytes are loaded before the current ones are used
+template <typename F>
+__device__ __forceinline__ void for_literals(const uint8_t* __restrict__ lits, uint32_t i0, uint32_t i1, F&& fn) {
+    if (i0 >= i1) return;
+    const v4u* const q = reinterpret_cast<const v4u*>(lits);
+    uint32_t w0 = i0 >> 4;
+    const uint32_t wl = (i1 - 1) >> 4;
+    v4u cur = q[w0];
+    for (;;) {
+        const v4u nxt = w0 < wl ? q[w0 + 1] : cur;
+        const uint32_t d[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            const uint32_t i = 16 * w0 + (uint32_t)b;
+            if (i >= i0 && i < i1) fn(i, (d[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+        }
+        if (w0 == wl) break;
+        ++w0;
+        cur = nxt;
+    }
+}
+
+__global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zstd_entropy_kernel(
+    const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
+    const uint64_t* __restrict__ items, uint64_t nitems, uint8_t* __restrict__ slots, uint64_t* __restrict__ sizes,
+    const Coded* __restrict__ coded_items, const uint8_t* __restrict__ lit_items, const ZItem* __restrict__ zitems,
+    uint32_t* __restrict__ chain_scratch, int probe_on) {
+    __shared__ __attribute__((aligned(16))) EntropyArea E;
+    __shared__ FseT fse[3];   // LL, OF, ML
+    __shared__ FseT fse_huf;  // the Huffman description's scratch
+    __shared__ PreT pre[3];
+    __shared__ Ctl ctl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = (int)uni((uint32_t)tid >> 6);
+    const bool probe = probe_on && blockIdx.x == 0 && tid == 0;
+    uint64_t tp = probe ? wall_clock64() : 0;
+    uint32_t* const chains = chain_scratch + (uint64_t)blockIdx.x * 6 * kZBlockSeq;
+    if (wave == 0 && lane < 3) {  // the predefined tables, once per launch
+        FseT& t = fse[lane];
+        if (lane == 0) fse_build(t, kLLNorm, 36, kLLLog);
+        if (lane == 1) fse_build(t, kOFNorm, 29, kOFLog);
+        if (lane == 2) fse_build(t, kMLNorm, 53, kMLLog);
+        PreT& q = pre[lane];
+        for (int i = 0; i < 64; ++i) q.next[i] = t.next[i];
+        for (int i = 0; i < 53; ++i) {
+            q.dnb[i] = t.dnb[i];
+            q.dfs[i] = t.dfs[i];
+        }
+        q.log = t.log;
+    }
+    for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
+        __syncthreads();  // LDS of the previous item
+        ZMARK(9);
+        const ZItem* const zi = zitems + k;
+        if (uni(zi->kind)) continue;
+        const uint64_t it = items[k];
+        const uint64_t ci = it >> 32, j = (uint32_t)it;
+        const uint64_t c0 = bounds[2 * ci], c1 = bounds[2 * ci + 1];
+        const uint64_t len = c1 - c0, off = j * (uint64_t)kEncBlock;
+        const uint32_t n = (uint32_t)(len - off < kEncBlock ? len - off : kEncBlock);
+        const bool last = off + n == len;
+        uint8_t* const out = slots + k * kSlot;
+        const Coded* const coded = coded_items + k * (uint64_t)kZBlockSeq;
+        const uint8_t* const lits = lit_items + k * (uint64_t)kEncBlock;
+        const uint32_t nlit = uni(zi->nlit), need_full = uni(zi->need_full);
+        uint32_t nseq = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kZWaves; ++w2) nseq += min(uni(zi->nseq[w2]), kZSubSeq);
+        if (tid < kZWaves) ctl.nseq[tid] = zi->nseq[tid];
+        if (tid < 36 + 53 + 32) E.shist[tid] = zi->shist[tid];
+        if (need_full) E.hist[tid] = zi->hist[tid];  // (kEThreads == 256)
+        if (tid == 0) ctl.lit_mode = 0;
+        __syncthreads();
+        ZMARK(3);
+        // ---- the literal mode (wave 0) beside the sequence tables and chains (waves 1-3)
+        const bool role_probe = probe_on && blockIdx.x == 0;
+        uint64_t zt = role_probe ? wall_clock64() : 0;
+        auto role_end = [&](int idx) {
+            if (role_probe && lane == 0) {
+                const uint64_t t2 = wall_clock64();
+                atomicAdd(&g_zprobe[idx], t2 - zt);
+                zt = t2;
+            }
+        };
+        if (wave == 0) {
+            if (need_full) literal_mode_wave(E, ctl, fse_huf, nlit, lane, role_probe ? g_zprobe : nullptr);
+            role_end(17);
+        } else {
+            const int kk = wave - 1;  // 0 LL, 1 OF, 2 ML
+            const uint32_t sh = kk == 0 ? 0u : kk == 1 ? 16u : 8u;
+            uint32_t* const hk = E.shist + (kk == 0 ? 0 : kk == 1 ? 36 + 53 : 36);
+            if (nseq > 0) {
+                if (kk == 0) seq_table_wave(fse[0], hk, 36, nseq, kLLNorm, kLLLog, kLLMaxLog, lane);
+                if (kk == 1) seq_table_wave(fse[1], hk, 29, nseq, kOFNorm, kOFLog, kOFMaxLog, lane);
+                if (kk == 2) seq_table_wave(fse[2], hk, 53, nseq, kMLNorm, kMLLog, kMLMaxLog, lane);
+            }
+            if (wave == 1) role_end(19);
+            if (nseq >= 2 && fse[kk].mode != 1) {
+                const FseView tv = fse[kk].mode == 2 ? view(fse[kk]) : view(pre[kk]);
+                seq_chain_wave(tv, coded, nseq, sh, chains + (uint64_t)kk * kZBlockSeq,
+                               reinterpret_cast<uint16_t*>(chains + 3ull * kZBlockSeq) + (uint64_t)kk * kZBlockSeq,
+                               reinterpret_cast<uint8_t*>(chains + 3ull * kZBlockSeq + 3ull * kZBlockSeq / 2) +
+                                   (uint64_t)kk * (kZBlockSeq + 16),
+                               &ctl.seq_last[kk], lane, role_probe && kk == 0 ? g_zprobe : nullptr);
+                __threadfence_block();
+            }
+            if (wave == 1) role_end(20);
+        }
+        __syncthreads();
+        ZMARK(5);
+        // ---- Huffman sizes: thread t's literals [i0, i1) of the compacted list, a block scan
+        const uint32_t lit_mode = ctl.lit_mode;
+        const uint32_t per = ((nlit + kEThreads - 1) / kEThreads + 15) & ~15u;
+        const uint32_t i0 = min(nlit, (uint32_t)tid * per), i1 = min(nlit, i0 + per);
+        uint32_t bits_t = 0;
+        if (lit_mode == 2) for_literals(lits, i0, i1, [&](uint32_t, uint32_t sym) { bits_t += E.len[sym]; });
+        const uint32_t bincl = wave_incl(bits_t, lane);
+        if (lane == 63) ctl.wsum2[wave] = bincl;
+        const bool four = nlit >= 256;
+        const uint32_t seg = four ? (nlit + 3) / 4 : nlit;
+        __syncthreads();
+        ZMARK(4);
+        uint32_t bbase = bincl - bits_t;
+        for (int w2 = 0; w2 < wave; ++w2) bbase += ctl.wsum2[w2];
+        if (lit_mode == 2) {
+            if (tid == 0) {
+                ctl.segP[0] = 0;
+                uint32_t tot = 0;
+                for (int w2 = 0; w2 < kEWaves; ++w2) tot += ctl.wsum2[w2];
+                ctl.segP[4] = tot;
+                if (!four) ctl.segP[1] = tot;
+            }
+            // the thread holding literal index seg * s records the bits before it
+            if (four && i0 < i1 && (i0 / seg != (i1 - 1) / seg || i0 % seg == 0)) {
+                uint32_t pb = bbase;
+                for_literals(lits, i0, i1, [&](uint32_t idx, uint32_t sym) {
+                    if (idx == seg || idx == 2 * seg || idx == 3 * seg) ctl.segP[idx / seg] = pb;
+                    pb += E.len[sym];
+                });
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {  // literal section: size decision
+            uint32_t lm = lit_mode, sz = 0;
+            const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+            if (lm == 2) {
+                uint32_t sb = 0;
+                const int ns4 = four ? 4 : 1;
+                for (int s2 = 0; s2 < ns4; ++s2) sb += (ctl.segP[four ? s2 + 1 : 4] - ctl.segP[s2] + 8) / 8;
+                const uint32_t c = ctl.desc_len + (four ? 6u : 0u) + sb;
+                const uint32_t mx = max(nlit, c);
+                const uint32_t hs = mx < 1024 ? 3u : mx < 16384 ? 4u : 5u;
+                if (sb > kHufStreams || hs + c >= rawh + nlit) {
+                    lm = 0;
+                } else {
+                    sz = hs + c;
+                    ctl.huf_c = c;
+                    ctl.huf_hs = hs;
+                }
+            }
+            if (lm == 0) sz = rawh + nlit;
+            if (lm == 1) sz = rawh + 1;
+            ctl.lit_mode = lm;
+            ctl.lit_size = sz;
+        }
+        __syncthreads();
+        ZMARK(6);
+        const uint32_t lm = ctl.lit_mode, lsz = ctl.lit_size;
+        uint8_t* const lit_out = out + 3;
+        if (probe) g_zprobe[47] += 1;
+        // ---- the sequence section header (thread 0)
+        if (tid == 0) {
+            uint8_t* o = lit_out + lsz;
+            uint8_t* const o0 = o;
+            const uint32_t ns = nseq;
+            if (ns < 128) {
+                *o++ = (uint8_t)ns;
+            } else if (ns < 0x7F00) {
+                *o++ = (uint8_t)((ns >> 8) + 0x80);
+                *o++ = (uint8_t)ns;
+            } else {
+                *o++ = 0xFF;
+                *o++ = (uint8_t)(ns - 0x7F00);
+                *o++ = (uint8_t)((ns - 0x7F00) >> 8);
+            }
+            if (ns) {
+                *o++ = (uint8_t)(fse[0].mode << 6 | fse[1].mode << 4 | fse[2].mode << 2);
+                for (int kk = 0; kk < 3; ++kk)
+                    for (uint32_t i = 0; i < fse[kk].desc_len; ++i) *o++ = fse[kk].desc[i];
+            }
+            ctl.seq_hdr = (uint32_t)(o - o0);
+            if (ns == 1)  // a single sequence's states come from its own codes
+                for (int kk = 0; kk < 3; ++kk)
+                    if (fse[kk].mode != 1) {
+                        const uint32_t sh = kk == 0 ? 0u : kk == 1 ? 16u : 8u;
+                        const FseView tv = fse[kk].mode == 2 ? view(fse[kk]) : view(pre[kk]);
+                        ctl.seq_last[kk] = fse_init(tv, (coded[0].codes >> sh) & 0xFF);
+                    }
+        }
+        // ---- the literal section
+        if (lm == 2) {
+            const uint32_t words = kHufStreams / 4 + 4;
+            for (uint32_t i = tid; i < words; i += kEThreads) E.streams[i] = 0;
+            __syncthreads();
+            const uint32_t S0 = 0;
+            const uint32_t S1 = four ? (ctl.segP[1] - ctl.segP[0] + 8) / 8 : (ctl.segP[4] - ctl.segP[0] + 8) / 8;
+            const uint32_t S2 = four ? S1 + (ctl.segP[2] - ctl.segP[1] + 8) / 8 : S1;
+            const uint32_t S3 = four ? S2 + (ctl.segP[3] - ctl.segP[2] + 8) / 8 : S1;
+            const uint32_t S4 = four ? S3 + (ctl.segP[4] - ctl.segP[3] + 8) / 8 : S1;
+            auto Sat = [&](uint32_t g) { return g == 0 ? S0 : g == 1 ? S1 : g == 2 ? S2 : g == 3 ? S3 : S4; };
+            uint32_t pb = bbase;
+            for_literals(lits, i0, i1, [&](uint32_t idx, uint32_t sym) {
+                const uint32_t L = E.len[sym], cv = E.code[sym];
+                const uint32_t sg = four ? min(idx / seg, 3u) : 0u;
+                const uint32_t endP = four ? ctl.segP[sg + 1] : ctl.segP[4];
+                const uint32_t o = 8 * Sat(sg) + (endP - pb - L);
+                const uint64_t v = (uint64_t)cv << (o & 31);
+                atomicOr(&E.streams[o >> 5], (uint32_t)v);
+                if ((o & 31) + L > 32) atomicOr(&E.streams[(o >> 5) + 1], (uint32_t)(v >> 32));
+                pb += L;
+            });
+            if (tid < (four ? 4 : 1)) {  // end marks
+                const uint32_t bits = ctl.segP[four ? tid + 1 : 4] - ctl.segP[tid];
+                const uint32_t o = 8 * Sat((uint32_t)tid) + bits;
+                atomicOr(&E.streams[o >> 5], 1u << (o & 31));
+            }
+            __syncthreads();
+            const uint32_t hs = ctl.huf_hs, c = ctl.huf_c;
+            const uint32_t dl = ctl.desc_len;
+            uint8_t* const body = lit_out + hs;
+            if (tid == 0) {
+                if (hs == 3) {
+                    const uint32_t v = 2u | (four ? 1u : 0u) << 2 | nlit << 4 | c << 14;
+                    lit_out[0] = (uint8_t)v;
+                    lit_out[1] = (uint8_t)(v >> 8);
+                    lit_out[2] = (uint8_t)(v >> 16);
+                } else if (hs == 4) {
+                    const uint32_t v = 2u | 2u << 2 | nlit << 4 | c << 18;
+                    for (int i = 0; i < 4; ++i) lit_out[i] = (uint8_t)(v >> (8 * i));
+                } else {
+                    const uint64_t v = 2u | 3u << 2 | (uint64_t)nlit << 4 | (uint64_t)c << 22;
+                    for (int i = 0; i < 5; ++i) lit_out[i] = (uint8_t)(v >> (8 * i));
+                }
+                if (four)
+                    for (int s2 = 0; s2 < 3; ++s2) {
+                        const uint32_t sz = Sat((uint32_t)s2 + 1) - Sat((uint32_t)s2);
+                        body[dl + 2 * s2] = (uint8_t)sz;
+                        body[dl + 2 * s2 + 1] = (uint8_t)(sz >> 8);
+                    }
+            }
+            for (uint32_t i = tid; i < dl; i += kEThreads) body[i] = ctl.desc[i];
+            lds_to_global(body + dl + (four ? 6 : 0), E.streams, four ? S4 : S1, (uint32_t)tid, kEThreads);
+        } else {
+            const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+            if (tid == 0) {
+                const uint32_t t = lm;  // 0 raw, 1 RLE
+                if (rawh == 1) {
+                    lit_out[0] = (uint8_t)(t | nlit << 3);
+                } else if (rawh == 2) {
+                    lit_out[0] = (uint8_t)(t | 1u << 2 | nlit << 4);
+                    lit_out[1] = (uint8_t)(nlit >> 4);
+                } else {
+                    lit_out[0] = (uint8_t)(t | 3u << 2 | nlit << 4);
+                    lit_out[1] = (uint8_t)(nlit >> 4);
+                    lit_out[2] = (uint8_t)(nlit >> 12);
+                }
+                if (lm == 1) {  // the one distinct byte
+                    uint32_t s2 = 0;
+                    while (!E.hist[s2]) ++s2;
+                    lit_out[rawh] = (uint8_t)s2;
+                }
+            }
+            if (lm == 0) copy_global(lit_out + rawh, lits, nlit, (uint32_t)tid, kEThreads);
+        }
+        if (wave == 0) role_end(21);
+        __syncthreads();
+        ZMARK(7);
+        // ---- the sequence bit stream (the fused kernel's, over 256 threads)
+        {
+            const uint32_t ns = nseq, hdr = ctl.seq_hdr;
+            const uint32_t mode[3] = {fse[0].mode, fse[1].mode, fse[2].mode};
+            const uint32_t pq = (ns + kEThreads - 1) / kEThreads;
+            const uint32_t q0 = min(ns, (uint32_t)tid * pq), q1 = min(ns, q0 + pq);
+            uint32_t st = 0;
+            for (uint32_t q = q0; q < q1; ++q) st += seq_bits(coded[q], q, ns, chains, kZBlockSeq, mode);
+            const uint32_t si = wave_incl(st, lane);
+            if (lane == 63) ctl.wsum[wave] = si;
+            __syncthreads();
+            uint32_t pt = si - st, T = 0;
+            for (int w2 = 0; w2 < kEWaves; ++w2) {
+                pt += w2 < wave ? ctl.wsum[w2] : 0u;
+                T += ctl.wsum[w2];
+            }
+            uint32_t flushb = 0;
+            for (int kk = 0; kk < 3; ++kk)
+                if (ns && mode[kk] != 1) flushb += (uint32_t)(mode[kk] == 2 ? fse[kk].log : pre[kk].log);
+            const uint32_t sbytes = ns ? (T + flushb + 1 + 7) / 8 : 0u;
+            const uint32_t body = lsz + hdr + sbytes;
+            const bool ok = body < n;
+            const uint32_t lastw_l = ns ? (8u * (uint32_t)((uintptr_t)(lit_out + lsz + hdr) & 3u) + T + flushb) >> 5 : 0u;
+            if (ok && ns && lastw_l + 1 <= (uint32_t)(sizeof(E.streams) / 4)) {
+                uint8_t* const S0 = lit_out + lsz + hdr;
+                uint32_t* const Aw = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(S0) & ~(uintptr_t)3);
+                const uint32_t off0 = 8u * (uint32_t)(S0 - reinterpret_cast<uint8_t*>(Aw));
+                const uint32_t lastw = lastw_l;
+                uint32_t* const L = E.streams;
+                for (uint32_t wdx = tid; wdx <= lastw; wdx += kEThreads) L[wdx] = 0;
+                __syncthreads();
+                OrBitsL ob;
+                ob.init(L, off0 + (T - pt - st));
+                for (uint32_t q = q1; q-- > q0;) {
+                    const Coded x = coded[q];
+                    const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
+                    if (q + 1 < ns) {
+                        const uint32_t jj = ns - 2 - q;  // (step order)
+                        if (mode[1] != 1) {
+                            const uint32_t c = chains[kZBlockSeq + jj];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                        if (mode[2] != 1) {
+                            const uint32_t c = chains[2 * kZBlockSeq + jj];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                        if (mode[0] != 1) {
+                            const uint32_t c = chains[jj];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                    }
+                    ob.put(x.ll - kLLBase[llc], kLLBits[llc]);
+                    ob.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
+                    ob.put(x.ofv - (1u << ofc), ofc);
+                }
+                ob.done();
+                if (tid == kEThreads - 1) {  // the final states (ML, OF, LL) and the end mark
+                    OrBitsL fb;
+                    fb.init(L, off0 + T);
+                    if (mode[2] != 1) fb.put(ctl.seq_last[2], (uint32_t)(mode[2] == 2 ? fse[2].log : pre[2].log));
+                    if (mode[1] != 1) fb.put(ctl.seq_last[1], (uint32_t)(mode[1] == 2 ? fse[1].log : pre[1].log));
+                    if (mode[0] != 1) fb.put(ctl.seq_last[0], (uint32_t)(mode[0] == 2 ? fse[0].log : pre[0].log));
+                    fb.put(1, 1);
+                    fb.done();
+                }
+                __syncthreads();
+                for (uint32_t wdx = tid; wdx <= lastw; wdx += kEThreads)
+                    Aw[wdx] = wdx ? L[wdx] : (off0 ? Aw[0] & ((1u << off0) - 1u) : 0u) | L[0];
+            } else if (ok && ns) {
+                uint8_t* const S0 = lit_out + lsz + hdr;
+                uint32_t* const Aw = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(S0) & ~(uintptr_t)3);
+                const uint32_t off0 = 8u * (uint32_t)(S0 - reinterpret_cast<uint8_t*>(Aw));
+                const uint32_t lastw = (off0 + T + flushb + 1 - 1) >> 5;
+                if (tid == 0)
+                    for (uint8_t* b = S0; b < reinterpret_cast<uint8_t*>(Aw + 1); ++b) *b = 0;
+                for (uint32_t wdx = 1 + tid; wdx <= lastw; wdx += kEThreads) Aw[wdx] = 0;
+                __threadfence_block();  // the zeros (and the section header) stored before any atomicOr
+                __syncthreads();
+                OrBits ob;
+                ob.init(Aw, off0 + (T - pt - st));
+                for (uint32_t q = q1; q-- > q0;) {
+                    const Coded x = coded[q];
+                    const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
+                    if (q + 1 < ns) {
+                        const uint32_t jj = ns - 2 - q;
+                        if (mode[1] != 1) {
+                            const uint32_t c = chains[kZBlockSeq + jj];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                        if (mode[2] != 1) {
+                            const uint32_t c = chains[2 * kZBlockSeq + jj];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                        if (mode[0] != 1) {
+                            const uint32_t c = chains[jj];
+                            ob.put(c & 0xFFFF, c >> 16);
+                        }
+                    }
+                    ob.put(x.ll - kLLBase[llc], kLLBits[llc]);
+                    ob.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
+                    ob.put(x.ofv - (1u << ofc), ofc);
+                }
+                ob.done();
+                if (tid == kEThreads - 1) {
+                    OrBits fb;
+                    fb.init(Aw, off0 + T);
+                    if (mode[2] != 1) fb.put(ctl.seq_last[2], (uint32_t)(mode[2] == 2 ? fse[2].log : pre[2].log));
+                    if (mode[1] != 1) fb.put(ctl.seq_last[1], (uint32_t)(mode[1] == 2 ? fse[1].log : pre[1].log));
+                    if (mode[0] != 1) fb.put(ctl.seq_last[0], (uint32_t)(mode[0] == 2 ? fse[0].log : pre[0].log));
+                    fb.put(1, 1);
+                    fb.done();
+                }
+            }
+            if (tid == 0) {
+                ctl.seq_ok = ok;
+                ctl.seq_size = body;
+            }
+        }
+        __syncthreads();
+        ZMARK(8);
+        if (!ctl.seq_ok) {  // raw block
+            copy_global(out + 3, data + (c0 - base) + off, n, (uint32_t)tid, kEThreads);
+            if (tid == 0) {
+                write_block_header(out, last, 0, n);
+                sizes[k] = 3 + (uint64_t)n;
+            }
+        } else if (tid == 0) {
+            write_block_header(out, last, 2, ctl.seq_size);
+            sizes[k] = 3 + (uint64_t)ctl.seq_size;
+        }
+    }
+}
+
 // Per chunk: frame size, compressed-or-not, blob size.  fsz[n] = 0 (scan padding).
 __global__ void zstd_frame_sizes_kernel(const uint64_t* __restrict__ bounds, const uint64_t* __restrict__ first,
                                         const uint64_t* __restrict__ sizes, uint64_t n, int compress,
@@ -2584,7 +3305,7 @@ ArenaPool& zpool() {
     return *p;
 }
 enum ZSlot : unsigned { kZsBounds, kZsItems, kZsFirst, kZsSizes, kZsIpre, kZsBsz, kZsBoff, kZsComp, kZsCrc, kZsTmp,
-                        kZsSlots, kZsSeqs, kZsCoded, kZsChains };
+                        kZsSlots, kZsSeqs, kZsCoded, kZsChains, kZsZItems, kZsLits };
 
 }  // namespace
 }  // namespace pbs
@@ -2687,11 +3408,35 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
     Seq* z_seqs = nullptr;
     Coded* z_coded = nullptr;
     uint32_t* z_chains = nullptr;
+    // the split kernels (default; PBS_ZSTD_SPLIT=0: the fused kernel, A/B): the parse kernel on
+    // one workgroup per CU, the entropy kernel on two per CU, items in batches of zbatch whose
+    // coded sequences, literals and ZItem records wait in global memory between the two
+    static const bool split = [] {
+        const char* e = std::getenv("PBS_ZSTD_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    static const uint64_t zbatch = [] {
+        const char* e = std::getenv("PBS_ZSTD_BATCH");
+        const uint64_t v = e ? std::strtoull(e, nullptr, 0) : 0;
+        return v ? v : (uint64_t)8192;
+    }();
+    const uint64_t bmax = std::min<uint64_t>(ni, zbatch);
+    const unsigned grid_e = (unsigned)std::min<uint64_t>(bmax, 2ull * (uint64_t)use_cu);
+    ZItem* z_items = nullptr;
+    uint8_t* z_lits = nullptr;
     if (compress) {
         z_slots = ar->get<uint8_t>(kZsSlots, ni * kSlot);
         z_seqs = ar->get<Seq>(kZsSeqs, (size_t)grid * kZBlockSeq * sizeof(Seq));
-        z_coded = ar->get<Coded>(kZsCoded, (size_t)grid * kZBlockSeq * sizeof(Coded));
-        z_chains = ar->get<uint32_t>(kZsChains, (size_t)grid * 6 * kZBlockSeq * sizeof(uint32_t));
+        if (split) {
+            z_coded = ar->get<Coded>(kZsCoded, (size_t)bmax * kZBlockSeq * sizeof(Coded));
+            z_chains = ar->get<uint32_t>(kZsChains, (size_t)grid_e * 6 * kZBlockSeq * sizeof(uint32_t));
+            z_items = ar->get<ZItem>(kZsZItems, (size_t)bmax * sizeof(ZItem));
+            z_lits = ar->get<uint8_t>(kZsLits, (size_t)bmax * kEncBlock);
+            if (!z_items || !z_lits) fail(PBS_ERR_NOMEM);
+        } else {
+            z_coded = ar->get<Coded>(kZsCoded, (size_t)grid * kZBlockSeq * sizeof(Coded));
+            z_chains = ar->get<uint32_t>(kZsChains, (size_t)grid * 6 * kZBlockSeq * sizeof(uint32_t));
+        }
         if (!z_slots || !z_seqs || !z_coded || !z_chains) fail(PBS_ERR_NOMEM);
     }
     if (!d_bounds || !d_items || !d_first || !d_sizes || !d_ipre || !d_bsz || !d_boff || !d_comp || !d_crc || !d_tmp)
@@ -2719,9 +3464,22 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
             const unsigned long long z[48] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
         }
-        if (compress)
+        if (compress && split) {
+            for (uint64_t b0 = 0; b0 < ni; b0 += bmax) {
+                const uint64_t nb = std::min<uint64_t>(bmax, ni - b0);
+                hipLaunchKernelGGL(zstd_parse_kernel, dim3((unsigned)std::min<uint64_t>(nb, (uint64_t)grid)),
+                                   dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items + b0, nb, b0,
+                                   z_slots + b0 * kSlot, d_sizes + b0, z_seqs, z_coded, z_lits, z_items,
+                                   zprobe ? 1 : 0, dbg_item);
+                hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)std::min<uint64_t>(nb, (uint64_t)grid_e)),
+                                   dim3(kEThreads), 0, st, dev_data, base, d_bounds, d_items + b0, nb,
+                                   z_slots + b0 * kSlot, d_sizes + b0, z_coded, z_lits, z_items, z_chains,
+                                   zprobe ? 1 : 0);
+            }
+        } else if (compress) {
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
                                ni, z_slots, d_sizes, z_seqs, z_coded, z_chains, zprobe ? 1 : 0, dbg_item);
+        }
         if (compress && dbg_item >= 0) {
             static uint32_t h[kZWaves * (1 + 3 * kZSubSeq)];
             (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zdbg), sizeof h, 0, hipMemcpyDeviceToHost, st);

@@ -45,9 +45,11 @@
 // over gu = min(n_wg, passes / kSrvMinPasses) workgroups: the leader publishes it in the
 // ServerDispatch record (VRAM, beside the request record), every workgroup hashes a
 // contiguous range of passes (rows 0 and 1 from the 64 slot bytes before its first pass,
-// the slot's history for pass 0), reserves each hit pass's candidate slots with one device
-// atomic, and counts itself done after a system-scope release; the last one acknowledges.
-// The host sorts the returned candidates (runs in reservation order).  Requests of one or
+// the slot's history for pass 0), writes its candidates into its own region of the array and
+// acknowledges that region on its own line after a system-scope release (round 6; round 5
+// reserved slots with device atomics and counted the workgroups done, the last one
+// acknowledging); the host waits for the gu acknowledgements and reads the regions in order,
+// which is stream order.  Requests of one or
 // three passes stay with the leader alone (8 KiB round trip unchanged); the leader's exit
 // (quit or idle) is published in the same record, tagged with the launch's epoch.
 // 256 KiB reads 3.85 -> 6.97 GB/s, 1 MiB 3.18 -> 5.50, 64 KiB 3.39 -> 4.42, 8 KiB
@@ -65,7 +67,6 @@ constexpr int kSrvLaneBytes = 32;
 constexpr int kSrvPass = kSrvLaneBytes * kSrvThreads;  // bytes per pass (8 KiB)
 constexpr int kSrvRows = kSrvThreads + 2;              // chain rows: the two before the pass, then one per lane
 constexpr int kSrvAhead = 4;                           // passes whose bytes are in flight
-constexpr uint32_t kSrvMinPasses = 2;                  // split requests: passes per workgroup at least
 constexpr uint32_t kSrvEpochMask = 0x3FFFFFFFu;         // ServerDispatch tag bits 32..61: the launch's epoch
 constexpr uint64_t kSrvTagBusy = 1ull << 62;           // ServerDispatch tag: fields being rewritten
 
@@ -95,7 +96,6 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
     __shared__ uint32_t wsum[kSrvThreads / 64];
     __shared__ uint32_t s_go;    // 0 polling, 1 serve, 2 exit
     __shared__ uint32_t s_gu;    // workgroups serving the request
-    __shared__ uint32_t s_base;  // split request: this pass's first candidate index
     __shared__ uint64_t ctl[2];  // [0] seq | len << 32 [1] base
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t g = blockIdx.x;
@@ -206,8 +206,6 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                 __hip_atomic_store(&disp->len, (uint32_t)(ctl[0] >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&disp->base, ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&disp->gu, gu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&disp->cnt_cand, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&disp->cnt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&disp->tag, (uint64_t)seq | (uint64_t)epoch << 32, __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -232,6 +230,9 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
         };
         uint32_t total = 0;
         bool stored = false;  // some pass stored candidates (block-uniform)
+        // a split request's workgroup writes its own region of the candidate array
+        const uint32_t rcap = split ? kServerCand / gu : kServerCand;
+        const uint32_t rbase = split ? (g < gu ? g : 0u) * rcap : 0u;
         if (p_lo < p_hi) {
             srv_u32x4 ring[kSrvAhead][2];
 #pragma unroll
@@ -323,24 +324,16 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                         before += w2 < wave ? wsum[w2] : 0u;
                         all += wsum[w2];
                     }
-                    uint32_t first = total;
-                    if (split) {
-                        if (tid == 0)
-                            s_base = __hip_atomic_fetch_add(&disp->cnt_cand, all, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-                        __syncthreads();
-                        first = s_base;
-                    }
-                    uint32_t o = first + before + x - c;
+                    uint32_t o = total + before + x - c;
                     uint32_t m = bits;
                     while (m) {
                         const int bit = __builtin_ctz(m);
                         m &= m - 1;
-                        if (o < kServerCand) mb->cand[o] = pos0 + (uint64_t)(tid * kSrvLaneBytes + bit);
+                        if (o < rcap) mb->cand[rbase + o] = pos0 + (uint64_t)(tid * kSrvLaneBytes + bit);
                         ++o;
                     }
                     total += all;
-                    __syncthreads();  // wsum and s_base reused
+                    __syncthreads();  // wsum reused
                 }
                 // the next pass's rows 0 and 1 = this pass's last two rows (every reader of them
                 // is past the barrier above)
@@ -371,20 +364,17 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                 mb->probe[2] = t_hashed;
             }
             s_go = 0;
-            bool ack_here = !split;
             if (split && g < gu) {
-                // this workgroup's candidates (and probe stamps) out to memory, then counted
-                // done; the last of the gu stores the acknowledgement
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                const uint32_t before =
-                    __hip_atomic_fetch_add(&disp->cnt_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-                if (before == gu - 1) {
-                    ack_here = true;
-                    total = __hip_atomic_load(&disp->cnt_cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    stored = total != 0;
-                }
+                // this workgroup's acknowledgement of its region, on its own line (release: its
+                // candidates -- and the leader's probe stamps -- before it); the host waits for
+                // all gu of them.  (Round 5 counted the workgroups done with a device atomic and
+                // the last one acknowledged: a serial atomic and a second release per request.)
+                if (probe && leader) mb->probe[3] = wall_clock64();
+                const uint64_t ack = (uint64_t)seq | (uint64_t)(total < rcap ? total : rcap) << 32 |
+                                     (total > rcap ? 1ull << 63 : 0ull);
+                __hip_atomic_store(&mb->wg_ack[8 * g], ack, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            if (ack_here) {
+            if (!split) {
                 if (probe) mb->probe[3] = wall_clock64();
                 // ONE 8-byte store: seq, candidate count, overflow flag (the host reads them
                 // together); a release (an L2 write-back first) only when candidates -- or the

@@ -349,7 +349,7 @@ def test_scan_server_request_placement(gpu, oracle, monkeypatch, mode, feed, avg
     long requests in the pinned slot, one workgroup, and everything in pinned host memory
     (PBS_SERVER_VRAM=0): the oracle's cuts every way, over many requests that reuse the
     same slots (stale lines would show here); avg 1 KiB puts hundreds of candidates of
-    one request in every workgroup's range (the atomic reservation + host sort)."""
+    one request in every workgroup's range (each workgroup's own region of the array)."""
     for var, val in zip(("PBS_SERVER_VRAM", "PBS_SERVER_VRAM_MAX", "PBS_SERVER_WGS"), SERVER_MODES[mode]):
         if val is None:
             monkeypatch.delenv(var, raising=False)
@@ -372,16 +372,18 @@ def test_scan_server_request_placement(gpu, oracle, monkeypatch, mode, feed, avg
     assert np.array_equal(np.array(got, dtype=np.uint64), ref)
 
 
-@pytest.mark.parametrize("wgs", [None, "3"])
+@pytest.mark.parametrize("wgs,minpass", [(None, None), ("3", None), ("32", "1")])
 @pytest.mark.parametrize("avg", [4 * KiB, 64 * KiB])
-def test_scan_server_ragged_reads(gpu, oracle, monkeypatch, wgs, avg):
+def test_scan_server_ragged_reads(gpu, oracle, monkeypatch, wgs, minpass, avg):
     """scan() over reads of seeded ragged sizes (1 byte to 1.5 MiB, many just around the
     server's pass and split sizes), so requests split over the workgroups end at every
-    kind of boundary; the oracle's cuts (chunker.rs:127-181 driven like a reader loop)."""
-    if wgs is None:
-        monkeypatch.delenv("PBS_SERVER_WGS", raising=False)
-    else:
-        monkeypatch.setenv("PBS_SERVER_WGS", wgs)
+    kind of boundary -- also split one pass per workgroup over up to 32 of them; the
+    oracle's cuts (chunker.rs:127-181 driven like a reader loop)."""
+    for var, val in (("PBS_SERVER_WGS", wgs), ("PBS_SERVER_MINPASS", minpass)):
+        if val is None:
+            monkeypatch.delenv(var, raising=False)
+        else:
+            monkeypatch.setenv(var, val)
     rng = np.random.default_rng(0x5EED0012 + avg)
     n = 12 * MiB + 77
     data = gen_np.gen_random(n, 0x5EED0013)
