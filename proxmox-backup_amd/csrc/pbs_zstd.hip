@@ -720,7 +720,8 @@ __device__ __forceinline__ void wr_q(uint32_t (&r)[4], uint32_t i, uint32_t v) {
 // weights, the table (log <= 6: one cell per lane) and the output bytes live in registers,
 // so the serial encode is readlanes and scalar arithmetic (round 4's one-lane version
 // waited on LDS at every weight: ~40-60 us a block); counts and the direct form by lanes.
-__device__ __noinline__ bool huf_describe(EntropyArea& E, Ctl& ctl, FseT& t_scratch, uint32_t mb, uint32_t lastsym,
+template <class EA>
+__device__ __noinline__ bool huf_describe(EA& E, Ctl& ctl, FseT& t_scratch, uint32_t mb, uint32_t lastsym,
                                           int lane) {
     const uint32_t nwt = uni(lastsym);
     uint32_t wreg[4], wmax = 0;  // weight of symbol lane + 64 j
@@ -905,7 +906,21 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
     // the stream's codes in step order, a byte per step, so a lane's batch is one 8-byte load
     // (its recorded states one 16-byte load) instead of 2 x 8 loads of 64 cache lines each
     PBS_GLOBAL uint8_t* const cs = (PBS_GLOBAL uint8_t*)codes_g;
-    for (uint32_t j = (uint32_t)lane; j < m; j += 64) cs[j] = (uint8_t)((coded[ns - 2 - j].codes >> shift) & 0xFF);
+    // (8 records in flight per lane: the entropy kernel reads them from HBM, written by the
+    // parse kernel, not from this workgroup's L2)
+    for (uint32_t j0 = (uint32_t)lane; j0 < m; j0 += 8 * 64) {
+        uint32_t cv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t j = j0 + 64u * (uint32_t)u;
+            cv[u] = j < m ? coded[ns - 2 - j].codes : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t j = j0 + 64u * (uint32_t)u;
+            if (j < m) cs[j] = (uint8_t)((cv[u] >> shift) & 0xFF);
+        }
+    }
     __threadfence_block();  // (the other lanes' bytes before the batch loads)
     auto run = [&](uint32_t x, bool stop_on_meet) -> uint32_t {  // returns the end state, ~0u: met
         if (a >= b) return x;
@@ -1486,7 +1501,8 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
 // creation order, ties taking the leaf; parents in E.par, the root in ctl.root.  A step reads
 // the two heads of both queues at once (one LDS wait, not one per pop): the second pop
 // takes from these four; a head past its queue is read but not used.
-__device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) {
+template <class EA>
+__device__ __noinline__ void huf_merge(EA& E, Ctl& ctl, uint32_t dist) {
         const int m = (int)dist;
         int li = 0, ii = m, nn = m;
         while (nn < 2 * m - 1) {
@@ -1514,7 +1530,8 @@ __device__ __noinline__ void huf_merge(EntropyArea& E, Ctl& ctl, uint32_t dist) 
 // Literal section mode of a block (ONE WAVE): RLE (one distinct byte), raw, or Huffman
 // when the entropy estimate says it may pay -- then the code lengths (two-queue merge,
 // limited to 11 bits), canonical codes and the tree description.  ctl.lit_mode = lane 0's.
-__device__ __noinline__ void literal_mode_wave(EntropyArea& E, Ctl& ctl, FseT& fsc, uint32_t nlit, int lane,
+template <class EA>
+__device__ __noinline__ void literal_mode_wave(EA& E, Ctl& ctl, FseT& fsc, uint32_t nlit, int lane,
                                                unsigned long long* probe) {
     uint64_t tq = probe ? wall_clock64() : 0;
     auto mark = [&](int idx) {
@@ -1914,7 +1931,7 @@ __device__ __noinline__ void rep_code_wave(const uint32_t* nseq, const uint32_t*
 // 1, 23 rounds (ticks), 24 rounds, 25 chains; Huffman (wave 0): 26 rank, 27 merge, 28
 // lengths, 29 canonical codes, 30 description; 32/33 wave 0's walk ticks / rounds, 34 + w
 // wave w's parse.
-__device__ unsigned long long g_zprobe[48];
+__device__ unsigned long long g_zprobe[64];  // (48..56: the split entropy kernel's phases)
 // PBS_ZSTD_DEBUG_ITEM=k (diagnostics): the parse's sequences of item k -- per sub-block its
 // count, then its kZSubSeq {pos, ml, off} records -- copied out for a diff with the twin's
 // (zstd_twin_parse)
@@ -2517,12 +2534,12 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 // The same blocks in two kernels, byte for byte: zstd_parse_kernel (one 512-thread workgroup
 // per CU: stage, RLE test, parse, then per sub-block the repeat coding and code histograms,
 // the literal bitmap, the literal histogram and the literals compacted to global memory) and
-// zstd_entropy_kernel (256-thread workgroups, two per CU: literal mode on wave 0 beside the
+// zstd_entropy_kernel (256-thread workgroups, three per CU: literal mode on wave 0 beside the
 // LL / OF / ML tables and state chains on waves 1-3, then the literal section and the
 // sequence bit stream from the compacted literals and the coded sequences).  In the fused
 // kernel the entropy half ran on 4 of the block's 8 waves while the others waited at a
-// barrier and no other block could use the CU's LDS; here a CU runs two blocks' entropy
-// halves at once (~75 KiB of LDS each) and the parse kernel's waves never wait for one.
+// barrier and no other block could use the CU's LDS; here a CU runs three blocks' entropy
+// halves at once (52 KiB of LDS, 168 VGPRs each) and the parse kernel's waves never wait for one.
 // The batch of items between the two kernels lives in global memory (ZItem, the coded
 // sequences, the literals).
 constexpr int kEThreads = 256;
@@ -2546,6 +2563,28 @@ struct PArea {
 static_assert(sizeof(PArea) <= 64 * 1024, "the parse kernel's buffers fit the work area");
 struct PCtl {
     uint32_t nseq[kZWaves], lastend[kZWaves], wsum[kZWaves], wsum2[kZWaves], need_full;
+};
+// the entropy kernel's area: the fused kernel's EntropyArea without the literal bitmap (the
+// parse kernel's) and with a 36.5 KiB stream buffer -- Huffman streams up to kHufStreams
+// (48 KiB) longer than it are ORed into the output in global memory instead (same bytes),
+// and so is a sequence bit stream longer than it; with it three workgroups fit a CU's LDS
+constexpr uint32_t kEStreams = 36 * 1024 + 512;  // (3 x the LDS of a workgroup must stay under 160 KiB after the allocation granule)
+struct EArea {
+    // the Huffman merge's scratch (keys, tw, par: literal_mode_wave only) shares the stream
+    // buffer, which is free until the literal section
+    union {
+        uint32_t streams[kEStreams / 4 + 4];
+        struct {
+            uint32_t keys[256];
+            uint32_t tw[512];
+            uint16_t par[512];
+        };
+    };
+    uint32_t hist[256];
+    uint8_t lens[256];
+    uint8_t len[256];
+    uint16_t code[256];
+    uint32_t shist[36 + 53 + 32];
 };
 
 __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zstd_parse_kernel(
@@ -2800,8 +2839,11 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             zi->need_full = need_full;
         }
         ZMARK(2);
-        // ---- the literals compacted in order to global memory (through LDS, dword stores)
-        uint8_t* const lo = lit_items + k * (uint64_t)kEncBlock;
+        // ---- the literals compacted in order to global memory (through LDS, dword stores):
+        // for the entropy kernel, or -- raw literals for sure (no full histogram) -- straight
+        // to their place in the block (behind the raw literal header the entropy kernel writes)
+        const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+        uint8_t* const lo = need_full ? lit_items + k * (uint64_t)kEncBlock : out + 3 + rawh;
         for (uint32_t pb = 0; pb < nlit; pb += (uint32_t)sizeof(A.lit)) {
             const uint32_t pe = min(nlit, pb + (uint32_t)sizeof(A.lit));
             uint32_t idx = litbase;
@@ -2825,34 +2867,36 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 }
 
 // thread t of nt: the compacted literals [i0, i1) of `lits` (16-byte aligned) in order,
-// fn(index, byte); the next 16 bytes are loaded before the current ones are used
+// fn(index, byte); 64 bytes (four 16-byte loads) in flight at a time -- the parse kernel
+// wrote them, so they come from HBM
 template <typename F>
 __device__ __forceinline__ void for_literals(const uint8_t* __restrict__ lits, uint32_t i0, uint32_t i1, F&& fn) {
     if (i0 >= i1) return;
     const v4u* const q = reinterpret_cast<const v4u*>(lits);
-    uint32_t w0 = i0 >> 4;
     const uint32_t wl = (i1 - 1) >> 4;
-    v4u cur = q[w0];
-    for (;;) {
-        const v4u nxt = w0 < wl ? q[w0 + 1] : cur;
-        const uint32_t d[4] = {cur.x, cur.y, cur.z, cur.w};
+    for (uint32_t w0 = i0 >> 4; w0 <= wl; w0 += 4) {
+        v4u c[4];
 #pragma unroll
-        for (int b = 0; b < 16; ++b) {
-            const uint32_t i = 16 * w0 + (uint32_t)b;
-            if (i >= i0 && i < i1) fn(i, (d[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+        for (int k = 0; k < 4; ++k) c[k] = q[w0 + (uint32_t)k <= wl ? w0 + (uint32_t)k : wl];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (w0 + (uint32_t)k > wl) break;
+            const uint32_t d[4] = {c[k].x, c[k].y, c[k].z, c[k].w};
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+                const uint32_t i = 16 * (w0 + (uint32_t)k) + (uint32_t)b;
+                if (i >= i0 && i < i1) fn(i, (d[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+            }
         }
-        if (w0 == wl) break;
-        ++w0;
-        cur = nxt;
     }
 }
 
-__global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zstd_entropy_kernel(
+__global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void zstd_entropy_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, uint8_t* __restrict__ slots, uint64_t* __restrict__ sizes,
     const Coded* __restrict__ coded_items, const uint8_t* __restrict__ lit_items, const ZItem* __restrict__ zitems,
     uint32_t* __restrict__ chain_scratch, int probe_on) {
-    __shared__ __attribute__((aligned(16))) EntropyArea E;
+    __shared__ __attribute__((aligned(16))) EArea E;
     __shared__ FseT fse[3];   // LL, OF, ML
     __shared__ FseT fse_huf;  // the Huffman description's scratch
     __shared__ PreT pre[3];
@@ -2876,7 +2920,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
     }
     for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
         __syncthreads();  // LDS of the previous item
-        ZMARK(9);
+        ZMARK(54);
         const ZItem* const zi = zitems + k;
         if (uni(zi->kind)) continue;
         const uint64_t it = items[k];
@@ -2897,7 +2941,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         if (need_full) E.hist[tid] = zi->hist[tid];  // (kEThreads == 256)
         if (tid == 0) ctl.lit_mode = 0;
         __syncthreads();
-        ZMARK(3);
+        ZMARK(48);
         // ---- the literal mode (wave 0) beside the sequence tables and chains (waves 1-3)
         const bool role_probe = probe_on && blockIdx.x == 0;
         uint64_t zt = role_probe ? wall_clock64() : 0;
@@ -2933,7 +2977,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             if (wave == 1) role_end(20);
         }
         __syncthreads();
-        ZMARK(5);
+        ZMARK(49);
         // ---- Huffman sizes: thread t's literals [i0, i1) of the compacted list, a block scan
         const uint32_t lit_mode = ctl.lit_mode;
         const uint32_t per = ((nlit + kEThreads - 1) / kEThreads + 15) & ~15u;
@@ -2945,7 +2989,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         const bool four = nlit >= 256;
         const uint32_t seg = four ? (nlit + 3) / 4 : nlit;
         __syncthreads();
-        ZMARK(4);
+        ZMARK(50);
         uint32_t bbase = bincl - bits_t;
         for (int w2 = 0; w2 < wave; ++w2) bbase += ctl.wsum2[w2];
         if (lit_mode == 2) {
@@ -2990,10 +3034,10 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             ctl.lit_size = sz;
         }
         __syncthreads();
-        ZMARK(6);
+        ZMARK(51);
         const uint32_t lm = ctl.lit_mode, lsz = ctl.lit_size;
         uint8_t* const lit_out = out + 3;
-        if (probe) g_zprobe[47] += 1;
+        if (probe) g_zprobe[55] += 1;
         // ---- the sequence section header (thread 0)
         if (tid == 0) {
             uint8_t* o = lit_out + lsz;
@@ -3025,35 +3069,55 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
         // ---- the literal section
         if (lm == 2) {
-            const uint32_t words = kHufStreams / 4 + 4;
-            for (uint32_t i = tid; i < words; i += kEThreads) E.streams[i] = 0;
-            __syncthreads();
             const uint32_t S0 = 0;
             const uint32_t S1 = four ? (ctl.segP[1] - ctl.segP[0] + 8) / 8 : (ctl.segP[4] - ctl.segP[0] + 8) / 8;
             const uint32_t S2 = four ? S1 + (ctl.segP[2] - ctl.segP[1] + 8) / 8 : S1;
             const uint32_t S3 = four ? S2 + (ctl.segP[3] - ctl.segP[2] + 8) / 8 : S1;
             const uint32_t S4 = four ? S3 + (ctl.segP[4] - ctl.segP[3] + 8) / 8 : S1;
             auto Sat = [&](uint32_t g) { return g == 0 ? S0 : g == 1 ? S1 : g == 2 ? S2 : g == 3 ? S3 : S4; };
+            const uint32_t hs = ctl.huf_hs, c = ctl.huf_c;
+            const uint32_t dl = ctl.desc_len;
+            uint8_t* const body = lit_out + hs;
+            const uint32_t tot = four ? S4 : S1;
+            // the streams in LDS, or (longer than its buffer) straight into the output: its
+            // bytes zeroed, then ORed into the aligned words around them (the bytes before
+            // are the section header, ORed with zeros; the ones after are written later)
+            uint8_t* const sdst = body + dl + (four ? 6 : 0);
+            const bool in_lds = tot + 16 <= (uint32_t)sizeof(E.streams);
+            uint32_t* const gw = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(sdst) & ~(uintptr_t)3);
+            const uint32_t gsh = 8u * (uint32_t)(sdst - reinterpret_cast<uint8_t*>(gw));
+            if (in_lds) {
+                for (uint32_t i = tid; i < (tot + 3) / 4 + 2; i += kEThreads) E.streams[i] = 0;
+            } else {
+                for (uint32_t i = tid; i < tot; i += kEThreads) sdst[i] = 0;
+                __threadfence_block();
+            }
+            __syncthreads();
+            auto orbits = [&](uint32_t o, uint64_t v, uint32_t L) {
+                if (in_lds) {
+                    atomicOr(&E.streams[o >> 5], (uint32_t)(v << (o & 31)));
+                    if ((o & 31) + L > 32) atomicOr(&E.streams[(o >> 5) + 1], (uint32_t)((v << (o & 31)) >> 32));
+                } else {
+                    const uint32_t og = o + gsh;
+                    const uint64_t w = v << (og & 31);
+                    atomicOr(&gw[og >> 5], (uint32_t)w);
+                    if ((og & 31) + L > 32) atomicOr(&gw[(og >> 5) + 1], (uint32_t)(w >> 32));
+                }
+            };
             uint32_t pb = bbase;
             for_literals(lits, i0, i1, [&](uint32_t idx, uint32_t sym) {
                 const uint32_t L = E.len[sym], cv = E.code[sym];
                 const uint32_t sg = four ? min(idx / seg, 3u) : 0u;
                 const uint32_t endP = four ? ctl.segP[sg + 1] : ctl.segP[4];
-                const uint32_t o = 8 * Sat(sg) + (endP - pb - L);
-                const uint64_t v = (uint64_t)cv << (o & 31);
-                atomicOr(&E.streams[o >> 5], (uint32_t)v);
-                if ((o & 31) + L > 32) atomicOr(&E.streams[(o >> 5) + 1], (uint32_t)(v >> 32));
+                orbits(8 * Sat(sg) + (endP - pb - L), (uint64_t)cv, L);
                 pb += L;
             });
             if (tid < (four ? 4 : 1)) {  // end marks
                 const uint32_t bits = ctl.segP[four ? tid + 1 : 4] - ctl.segP[tid];
-                const uint32_t o = 8 * Sat((uint32_t)tid) + bits;
-                atomicOr(&E.streams[o >> 5], 1u << (o & 31));
+                orbits(8 * Sat((uint32_t)tid) + bits, 1ull, 1);
             }
+            if (!in_lds) __threadfence_block();
             __syncthreads();
-            const uint32_t hs = ctl.huf_hs, c = ctl.huf_c;
-            const uint32_t dl = ctl.desc_len;
-            uint8_t* const body = lit_out + hs;
             if (tid == 0) {
                 if (hs == 3) {
                     const uint32_t v = 2u | (four ? 1u : 0u) << 2 | nlit << 4 | c << 14;
@@ -3075,7 +3139,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                     }
             }
             for (uint32_t i = tid; i < dl; i += kEThreads) body[i] = ctl.desc[i];
-            lds_to_global(body + dl + (four ? 6 : 0), E.streams, four ? S4 : S1, (uint32_t)tid, kEThreads);
+            if (in_lds) lds_to_global(sdst, E.streams, tot, (uint32_t)tid, kEThreads);
         } else {
             const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
             if (tid == 0) {
@@ -3096,19 +3160,51 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                     lit_out[rawh] = (uint8_t)s2;
                 }
             }
-            if (lm == 0) copy_global(lit_out + rawh, lits, nlit, (uint32_t)tid, kEThreads);
+            // (without the full histogram the parse kernel put them in place already)
+            if (lm == 0 && need_full) copy_global(lit_out + rawh, lits, nlit, (uint32_t)tid, kEThreads);
         }
         if (wave == 0) role_end(21);
         __syncthreads();
-        ZMARK(7);
+        ZMARK(52);
         // ---- the sequence bit stream (the fused kernel's, over 256 threads)
         {
             const uint32_t ns = nseq, hdr = ctl.seq_hdr;
             const uint32_t mode[3] = {fse[0].mode, fse[1].mode, fse[2].mode};
             const uint32_t pq = (ns + kEThreads - 1) / kEThreads;
             const uint32_t q0 = min(ns, (uint32_t)tid * pq), q1 = min(ns, q0 + pq);
+            // (the coded records come from HBM -- the parse kernel wrote them -- so 8 are
+            // loaded, with their chain fields, before any is used)
+            auto load8 = [&](uint32_t qb, Coded (&x)[8], uint32_t (&cl)[8], uint32_t (&co)[8], uint32_t (&cm)[8]) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t q = qb + (uint32_t)u < q1 ? qb + (uint32_t)u : q1 - 1;
+                    const v4u r = *reinterpret_cast<const v4u*>(coded + q);
+                    x[u] = Coded{r.x, r.y, r.z, r.w};
+                    const uint32_t jj = q + 1 < ns ? ns - 2 - q : 0u;
+                    cl[u] = chains[jj];
+                    co[u] = chains[kZBlockSeq + jj];
+                    cm[u] = chains[2 * kZBlockSeq + jj];
+                }
+            };
             uint32_t st = 0;
-            for (uint32_t q = q0; q < q1; ++q) st += seq_bits(coded[q], q, ns, chains, kZBlockSeq, mode);
+            for (uint32_t qb = q0; qb < q1; qb += 8) {
+                Coded x[8];
+                uint32_t cl[8], co[8], cm[8];
+                load8(qb, x, cl, co, cm);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t q = qb + (uint32_t)u;
+                    if (q >= q1) break;
+                    const uint32_t llc = x[u].codes & 0xFF, mlc = (x[u].codes >> 8) & 0xFF, ofc = x[u].codes >> 16;
+                    uint32_t b = kLLBits[llc] + kMLBits[mlc] + ofc;
+                    if (q + 1 < ns) {
+                        if (mode[0] != 1) b += cl[u] >> 16;
+                        if (mode[1] != 1) b += co[u] >> 16;
+                        if (mode[2] != 1) b += cm[u] >> 16;
+                    }
+                    st += b;
+                }
+            }
             const uint32_t si = wave_incl(st, lane);
             if (lane == 63) ctl.wsum[wave] = si;
             __syncthreads();
@@ -3120,6 +3216,31 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             uint32_t flushb = 0;
             for (int kk = 0; kk < 3; ++kk)
                 if (ns && mode[kk] != 1) flushb += (uint32_t)(mode[kk] == 2 ? fse[kk].log : pre[kk].log);
+            // this thread's sequences into a bit writer, last first (the stream is backwards),
+            // 8 records loaded before any is written
+            auto put_range = [&](auto& ob) {
+                for (uint32_t qe = q1; qe > q0;) {
+                    const uint32_t qb = qe >= q0 + 8 ? qe - 8 : q0;
+                    Coded x[8];
+                    uint32_t cl[8], co[8], cm[8];
+                    load8(qb, x, cl, co, cm);
+#pragma unroll
+                    for (int u = 7; u >= 0; --u) {
+                        const uint32_t q = qb + (uint32_t)u;
+                        if (q >= qe) continue;
+                        const uint32_t llc = x[u].codes & 0xFF, mlc = (x[u].codes >> 8) & 0xFF, ofc = x[u].codes >> 16;
+                        if (q + 1 < ns) {
+                            if (mode[1] != 1) ob.put(co[u] & 0xFFFF, co[u] >> 16);
+                            if (mode[2] != 1) ob.put(cm[u] & 0xFFFF, cm[u] >> 16);
+                            if (mode[0] != 1) ob.put(cl[u] & 0xFFFF, cl[u] >> 16);
+                        }
+                        ob.put(x[u].ll - kLLBase[llc], kLLBits[llc]);
+                        ob.put(x[u].ml - kMLBase[mlc], kMLBits[mlc]);
+                        ob.put(x[u].ofv - (1u << ofc), ofc);
+                    }
+                    qe = qb;
+                }
+            };
             const uint32_t sbytes = ns ? (T + flushb + 1 + 7) / 8 : 0u;
             const uint32_t body = lsz + hdr + sbytes;
             const bool ok = body < n;
@@ -3134,28 +3255,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                 __syncthreads();
                 OrBitsL ob;
                 ob.init(L, off0 + (T - pt - st));
-                for (uint32_t q = q1; q-- > q0;) {
-                    const Coded x = coded[q];
-                    const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
-                    if (q + 1 < ns) {
-                        const uint32_t jj = ns - 2 - q;  // (step order)
-                        if (mode[1] != 1) {
-                            const uint32_t c = chains[kZBlockSeq + jj];
-                            ob.put(c & 0xFFFF, c >> 16);
-                        }
-                        if (mode[2] != 1) {
-                            const uint32_t c = chains[2 * kZBlockSeq + jj];
-                            ob.put(c & 0xFFFF, c >> 16);
-                        }
-                        if (mode[0] != 1) {
-                            const uint32_t c = chains[jj];
-                            ob.put(c & 0xFFFF, c >> 16);
-                        }
-                    }
-                    ob.put(x.ll - kLLBase[llc], kLLBits[llc]);
-                    ob.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
-                    ob.put(x.ofv - (1u << ofc), ofc);
-                }
+                put_range(ob);
                 ob.done();
                 if (tid == kEThreads - 1) {  // the final states (ML, OF, LL) and the end mark
                     OrBitsL fb;
@@ -3181,28 +3281,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                 __syncthreads();
                 OrBits ob;
                 ob.init(Aw, off0 + (T - pt - st));
-                for (uint32_t q = q1; q-- > q0;) {
-                    const Coded x = coded[q];
-                    const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
-                    if (q + 1 < ns) {
-                        const uint32_t jj = ns - 2 - q;
-                        if (mode[1] != 1) {
-                            const uint32_t c = chains[kZBlockSeq + jj];
-                            ob.put(c & 0xFFFF, c >> 16);
-                        }
-                        if (mode[2] != 1) {
-                            const uint32_t c = chains[2 * kZBlockSeq + jj];
-                            ob.put(c & 0xFFFF, c >> 16);
-                        }
-                        if (mode[0] != 1) {
-                            const uint32_t c = chains[jj];
-                            ob.put(c & 0xFFFF, c >> 16);
-                        }
-                    }
-                    ob.put(x.ll - kLLBase[llc], kLLBits[llc]);
-                    ob.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
-                    ob.put(x.ofv - (1u << ofc), ofc);
-                }
+                put_range(ob);
                 ob.done();
                 if (tid == kEThreads - 1) {
                     OrBits fb;
@@ -3220,7 +3299,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             }
         }
         __syncthreads();
-        ZMARK(8);
+        ZMARK(53);
         if (!ctl.seq_ok) {  // raw block
             copy_global(out + 3, data + (c0 - base) + off, n, (uint32_t)tid, kEThreads);
             if (tid == 0) {
@@ -3409,7 +3488,7 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
     Coded* z_coded = nullptr;
     uint32_t* z_chains = nullptr;
     // the split kernels (default; PBS_ZSTD_SPLIT=0: the fused kernel, A/B): the parse kernel on
-    // one workgroup per CU, the entropy kernel on two per CU, items in batches of zbatch whose
+    // one workgroup per CU, the entropy kernel on three per CU, items in batches of zbatch whose
     // coded sequences, literals and ZItem records wait in global memory between the two
     static const bool split = [] {
         const char* e = std::getenv("PBS_ZSTD_SPLIT");
@@ -3421,7 +3500,7 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
         return v ? v : (uint64_t)8192;
     }();
     const uint64_t bmax = std::min<uint64_t>(ni, zbatch);
-    const unsigned grid_e = (unsigned)std::min<uint64_t>(bmax, 2ull * (uint64_t)use_cu);
+    const unsigned grid_e = (unsigned)std::min<uint64_t>(bmax, 3ull * (uint64_t)use_cu);  // 3 per CU (52 KiB LDS, 168 VGPRs)
     ZItem* z_items = nullptr;
     uint8_t* z_lits = nullptr;
     if (compress) {
@@ -3461,7 +3540,7 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
             return e ? (int64_t)std::strtoll(e, nullptr, 0) : (int64_t)-1;
         }();
         if (compress && zprobe) {
-            const unsigned long long z[48] = {};
+            const unsigned long long z[64] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zprobe), z, sizeof z, 0, hipMemcpyHostToDevice, st);
         }
         if (compress && split) {
@@ -3491,7 +3570,7 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
                 }
         }
         if (compress && zprobe) {
-            unsigned long long h[48] = {};
+            unsigned long long h[64] = {};
             (void)hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_zprobe), sizeof h, 0, hipMemcpyDeviceToHost, st);
             (void)hipStreamSynchronize(st);
             const double nb = h[10] ? (double)h[10] : 1.0;
@@ -3513,6 +3592,16 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
                          h[32] / nb / 100, h[33] / nb, h[34] / nb / 100, h[35] / nb / 100, h[36] / nb / 100,
                          h[37] / nb / 100, h[38] / nb / 100, h[39] / nb / 100, h[40] / nb / 100, h[41] / nb / 100,
                          h[43] / nb / 100, h[44] / nb / 100, h[45] / nb / 100, h[46] / nb / 100, h[42] / nb / 100);
+            if (split) {
+                const double ne = h[55] ? (double)h[55] : 1.0;
+                std::fprintf(stderr,
+                             "zstd probe, entropy kernel (workgroup 0, us per block over %llu blocks): load %.1f roles %.1f "
+                             "sizes %.1f decision %.1f literals %.1f seqstream %.1f end %.1f | roles: litmode %.1f LLtable "
+                             "%.1f LLchain %.1f litsection %.1f\n",
+                             h[55], h[48] / ne / 100, h[49] / ne / 100, h[50] / ne / 100, h[51] / ne / 100,
+                             h[52] / ne / 100, h[53] / ne / 100, h[54] / ne / 100, h[17] / ne / 100, h[19] / ne / 100,
+                             h[20] / ne / 100, h[21] / ne / 100);
+            }
         }
         hipLaunchKernelGGL(zstd_frame_sizes_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
                            d_bounds, d_first, d_sizes, (uint64_t)n, compress, d_bsz, d_comp);

@@ -1,0 +1,11 @@
+#!/bin/bash
+# zstd split kernels: per-kernel time (rocprofv3 kernel trace) and rates vs fused
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp; O=${OUT:-gpurun_out/r06c}; mkdir -p $O
+step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
+PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+step tests_zstd 400 $PYT -m gpu tests/test_gpu_zstd.py tests/test_blob_fixture.py || exit 1
+step trace 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 scripts/zstd_bench.py --corpus text,pxar --gib 1 --reps 2 || exit 1
+step rate_split 200 env PBS_ZSTD_SPLIT=1 python3 scripts/zstd_bench.py --corpus text,pxar,vm --gib 1 --reps 3 || exit 1
+step rate_fused 200 env PBS_ZSTD_SPLIT=0 python3 scripts/zstd_bench.py --corpus text,pxar,vm --gib 1 --reps 3 || exit 1
+echo done
