@@ -56,8 +56,8 @@
 namespace {
 
 constexpr uint32_t kBlock = 64 * 1024;
-// one GPU wave's sub-block: the first four 8 KiB + 384 bytes, the last four 8 KiB - 384
-constexpr uint32_t kSubA = 8192 + 384, kSubB = 8192 - 384;
+// one GPU wave's sub-block: the first four 8 KiB + 768 bytes, the last four 8 KiB - 768
+constexpr uint32_t kSubA = 8192 + 768, kSubB = 8192 - 768;
 constexpr uint32_t sub_start(uint32_t w) { return w <= 4 ? w * kSubA : 4 * kSubA + (w - 4) * kSubB; }
 uint32_t sub_of(uint32_t pos) {  // the sub-block holding block position pos
     uint32_t w = 0;

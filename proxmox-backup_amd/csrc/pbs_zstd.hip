@@ -65,11 +65,13 @@ using namespace zstd;
 
 constexpr int kZThreads = 512;
 constexpr int kZWaves = kZThreads / 64;
-// One wave's sub-block: waves 0-3 take 8 KiB + 384, waves 4-7 8 KiB - 384.  Waves w and
+// One wave's sub-block: waves 0-3 take 8 KiB + 768, waves 4-7 8 KiB - 768.  Waves w and
 // w + 4 share a SIMD and the issue arbiter favours the older one: with equal sub-blocks
 // waves 4-7 parsed ~9 % longer (text: 692 vs 756 us per block) whichever sub-blocks they
-// got (profiles/r04/zstd_swap/), and then ran alone on their SIMDs.
-constexpr uint32_t kZSubA = 8192 + 384, kZSubB = 8192 - 384;
+// got (profiles/r04/zstd_swap/), and then ran alone on their SIMDs.  Round 4 moved 384
+// bytes; in the round-6 parse kernel waves 4-7 still took ~10 % longer per block (221 vs
+// 242-246 us, 25.8 vs 31 ns per byte: profiles/r06/zsplit/probe.log), so 768 now.
+constexpr uint32_t kZSubA = 8192 + 768, kZSubB = 8192 - 768;
 __device__ __host__ constexpr uint32_t zsub_start(int w) {  // block position of sub-block w (0..8)
     return w <= 4 ? (uint32_t)w * kZSubA : 4 * kZSubA + (uint32_t)(w - 4) * kZSubB;
 }
