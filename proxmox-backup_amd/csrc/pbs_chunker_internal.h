@@ -220,21 +220,15 @@ constexpr uint32_t kServerHostSlot = 1u << 30;  // req_len flag: the data are in
 // (profiles/r03/vram); with several workgroups per request (kSrvMaxWgs) it is not.
 constexpr uint32_t kServerVramMax = kServerMaxBytes;
 // Requests of at least 2 kSrvMinPasses passes are split over up to `n_wg` workgroups of the
-// server (PBS_SERVER_WGS): workgroup 0 polls the host's record and publishes such a
-// request here, in the same fine-grained VRAM allocation (+128 bytes); the others poll
-// this record (one L2/HBM load, no PCIe), each hashes a contiguous range of passes,
-// reserves candidate slots with a device atomic and counts itself done; the last one
-// stores the acknowledgement.  tag = seq | epoch << 32 | busy << 62 | quit << 63 (epoch: the
-// launch number mod 2^30, so a record left by an earlier launch is never taken for a
-// request; busy: the leader is rewriting the fields -- a seqlock, scan_server.h).
+// server (PBS_SERVER_WGS, scan_server.h): each polls the host's request record and hashes a
+// contiguous range of passes.  This record, in the same fine-grained VRAM allocation (+128
+// bytes), carries only the leader's exit: tag = last seq | epoch << 32 | 1 << 63 (epoch:
+// the launch number mod 2^30, so a record left by an earlier launch is never taken).
 struct alignas(64) ServerDispatch {
     uint64_t tag;
-    uint32_t len;   // the record's req_len (kServerHostSlot kept)
-    uint32_t gu;    // workgroups serving this request
-    uint64_t base;
 };
 constexpr uint32_t kSrvMaxWgs = 32;
-constexpr uint32_t kSrvMinPasses = 2;  // split requests: passes per workgroup at least (PBS_SERVER_MINPASS)
+constexpr uint32_t kSrvMinPasses = 1;  // split requests: passes per workgroup at least (PBS_SERVER_MINPASS; 2 until round 6)
 constexpr uint32_t kSrvDefaultWgs = 16;
 constexpr uint32_t kServerHeader = 256;  // VRAM allocation: record (0), dispatch (128), then the slot
 static_assert(sizeof(ServerDispatch) <= kServerHeader - 128, "dispatch record past the header");

@@ -41,19 +41,19 @@
 //
 // Split requests (round 5): one workgroup hashes ~6 GB/s (1.3 us per 8 KiB pass), so a
 // 256 KiB read cost 42 us of kernel time and the unchanged caller reached 3.8 GB/s against
-// 5.4 GB/s gathering 4 MiB per scan().  A request of >= 2 kSrvMinPasses passes is now split
-// over gu = min(n_wg, passes / kSrvMinPasses) workgroups: the leader publishes it in the
-// ServerDispatch record (VRAM, beside the request record), every workgroup hashes a
-// contiguous range of passes (rows 0 and 1 from the 64 slot bytes before its first pass,
-// the slot's history for pass 0), writes its candidates into its own region of the array and
-// acknowledges that region on its own line after a system-scope release (round 6; round 5
+// 5.4 GB/s gathering 4 MiB per scan().  A request of >= 2 kSrvMinPasses passes is split
+// over gu = min(n_wg, passes / kSrvMinPasses) workgroups (one pass each since round 6):
+// every workgroup polls the host's request record and computes the split from its length
+// (round 5: the leader re-published each request for the others, one more detection hop),
+// hashes a contiguous range of passes (rows 0 and 1 from the 64 slot bytes before its first
+// pass, the slot's history for pass 0), writes its candidates into its own region of the
+// array and acknowledges that region on its own line after a system-scope release (round 5
 // reserved slots with device atomics and counted the workgroups done, the last one
 // acknowledging); the host waits for the gu acknowledgements and reads the regions in order,
-// which is stream order.  Requests of one or
-// three passes stay with the leader alone (8 KiB round trip unchanged); the leader's exit
-// (quit or idle) is published in the same record, tagged with the launch's epoch.
+// which is stream order.  One-pass requests stay with the leader alone; the leader's exit
+// (quit or idle) is published in the ServerDispatch record, tagged with the launch's epoch.
 // 256 KiB reads 3.85 -> 6.97 GB/s, 1 MiB 3.18 -> 5.50, 64 KiB 3.39 -> 4.42, 8 KiB
-// 1.48 -> 1.49 (profiles/r05/scan_server).
+// 1.48 -> 1.49 (profiles/r05/scan_server); round 6: profiles/r06/server/.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -68,7 +68,6 @@ constexpr int kSrvPass = kSrvLaneBytes * kSrvThreads;  // bytes per pass (8 KiB)
 constexpr int kSrvRows = kSrvThreads + 2;              // chain rows: the two before the pass, then one per lane
 constexpr int kSrvAhead = 4;                           // passes whose bytes are in flight
 constexpr uint32_t kSrvEpochMask = 0x3FFFFFFFu;         // ServerDispatch tag bits 32..61: the launch's epoch
-constexpr uint64_t kSrvTagBusy = 1ull << 62;           // ServerDispatch tag: fields being rewritten
 
 typedef uint32_t srv_u32x4 __attribute__((ext_vector_type(4)));
 
@@ -95,7 +94,6 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
     __shared__ __attribute__((aligned(16))) uint8_t rows[kSrvRows * 128];
     __shared__ uint32_t wsum[kSrvThreads / 64];
     __shared__ uint32_t s_go;    // 0 polling, 1 serve, 2 exit
-    __shared__ uint32_t s_gu;    // workgroups serving the request
     __shared__ uint64_t ctl[2];  // [0] seq | len << 32 [1] base
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t g = blockIdx.x;
@@ -140,33 +138,27 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                 }
             }
         } else if (tid == 0) {
-            // the leader's dispatch record (split requests and the exit only)
-            // a seqlock: the leader marks the tag busy before it rewrites the fields and
-            // publishes the new tag after them, so fields read between two equal, not-busy
-            // loads of the tag are that request's.  (A follower with no share of request N
-            // may still be reading when N + 1 is published: without the re-check it could
-            // pair N's seq with N + 1's len, base and gu and serve N + 1 twice.)
+            // a follower polls the host's request record itself (one 16-byte load, consistent
+            // by construction: the host stores len and base before seq) and, for the exit, the
+            // leader's dispatch record.  (Until round 6 the leader re-published each request
+            // there for the followers: one more detection hop, ~1 us per split request, and
+            // the reason the record needed a seqlock.)
             for (;;) {
+                const srv_u32x4 r = *reinterpret_cast<const volatile srv_u32x4*>(&req->req_seq);
+                if (r.y & kServerQuit) {
+                    s_go = 2;
+                    break;
+                }
+                if (r.x != last) {
+                    ctl[0] = (uint64_t)r.x | ((uint64_t)r.y << 32);
+                    ctl[1] = (uint64_t)r.z | ((uint64_t)r.w << 32);
+                    s_go = 1;
+                    break;
+                }
                 const uint64_t t = __hip_atomic_load(&disp->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (((uint32_t)(t >> 32) & kSrvEpochMask) == epoch && !(t & kSrvTagBusy) &&
-                    ((t >> 63) || (uint32_t)t != last)) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the record's fields after its tag
-                    if (t >> 63) {
-                        s_go = 2;
-                        break;
-                    }
-                    const uint32_t len = __hip_atomic_load(&disp->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t b = __hip_atomic_load(&disp->base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t gu = __hip_atomic_load(&disp->gu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the fields before the re-check
-                    if (__hip_atomic_load(&disp->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == t) {
-                        ctl[0] = (uint64_t)(uint32_t)t | (uint64_t)len << 32;
-                        ctl[1] = b;
-                        s_gu = gu;
-                        s_go = 1;
-                        break;
-                    }
-                    continue;  // rewritten while read: load it again
+                if (((uint32_t)(t >> 32) & kSrvEpochMask) == epoch && (t >> 63)) {
+                    s_go = 2;
+                    break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
@@ -191,27 +183,11 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
         uint64_t t_loaded = 0, t_hashed = 0;
         const uint32_t seq = (uint32_t)ctl[0], len = (uint32_t)(ctl[0] >> 32) & ~kServerHostSlot;
         const uint32_t npass = (len + kSrvPass - 1) / kSrvPass;
-        // split the request over gu workgroups (the leader decides and publishes it)
-        uint32_t gu = 1;
-        if (leader) {
-            const uint32_t minp = (flags >> kSrvMinPassShift) & 0xFFu;  // 0: kSrvMinPasses
-            const uint32_t want = npass / (minp ? minp : kSrvMinPasses);
-            gu = want < 1 ? 1 : (want < n_wg ? want : n_wg);
-            if (gu > 1 && tid == 0) {
-                // busy first (the release orders it before the field stores), then the fields,
-                // then the tag (release: the fields before it)
-                __hip_atomic_store(&disp->tag, (uint64_t)last | (uint64_t)epoch << 32 | kSrvTagBusy,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                __hip_atomic_store(&disp->len, (uint32_t)(ctl[0] >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&disp->base, ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&disp->gu, gu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&disp->tag, (uint64_t)seq | (uint64_t)epoch << 32, __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-        } else {
-            gu = s_gu;
-        }
+        // the request's split over gu workgroups: every workgroup computes it from the length
+        // (the host does too, to know whose acknowledgements to wait for)
+        const uint32_t minp = (flags >> kSrvMinPassShift) & 0xFFu;  // 0: kSrvMinPasses
+        const uint32_t want = npass / (minp ? minp : kSrvMinPasses);
+        const uint32_t gu = want < 1 ? 1 : (want < n_wg ? want : n_wg);
         const bool split = gu > 1;
         // this workgroup's passes [p_lo, p_hi) (a follower beyond gu has none)
         const uint32_t p_lo = g < gu ? (uint32_t)((uint64_t)g * npass / gu) : npass;
@@ -374,7 +350,7 @@ __global__ __launch_bounds__(kSrvThreads) void scan_server_kernel(ServerMailbox*
                                      (total > rcap ? 1ull << 63 : 0ull);
                 __hip_atomic_store(&mb->wg_ack[8 * g], ack, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            if (!split) {
+            if (!split && leader) {  // (the followers see every request now, the unsplit ones too)
                 if (probe) mb->probe[3] = wall_clock64();
                 // ONE 8-byte store: seq, candidate count, overflow flag (the host reads them
                 // together); a release (an L2 write-back first) only when candidates -- or the
