@@ -71,7 +71,10 @@ constexpr int kZWaves = kZThreads / 64;
 // got (profiles/r04/zstd_swap/), and then ran alone on their SIMDs.  Round 4 moved 384
 // bytes; in the round-6 parse kernel waves 4-7 still took ~10 % longer per block (221 vs
 // 242-246 us, 25.8 vs 31 ns per byte: profiles/r06/zsplit/probe.log), so 768 now.
-constexpr uint32_t kZSubA = 8192 + 768, kZSubB = 8192 - 768;
+#ifndef PBS_ZSUB_DELTA
+#define PBS_ZSUB_DELTA 768  // (A/B builds only: the twin's kSubA / kSubB must follow)
+#endif
+constexpr uint32_t kZSubA = 8192 + PBS_ZSUB_DELTA, kZSubB = 8192 - PBS_ZSUB_DELTA;
 __device__ __host__ constexpr uint32_t zsub_start(int w) {  // block position of sub-block w (0..8)
     return w <= 4 ? (uint32_t)w * kZSubA : 4 * kZSubA + (uint32_t)(w - 4) * kZSubB;
 }
@@ -110,11 +113,15 @@ struct Coded {
 
 // The staged window in LDS: window byte P (P = 0 at the chunk byte `hist` before the
 // block) is LDS byte P + r.
+// (the LDS address space spelled out in the type: with a generic pointer every access
+// leans on the compiler inferring LDS through the noinline stages)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 struct Win {
-    const uint32_t* w;
+    const lds_u32* w;
     uint32_t r;
     __device__ __forceinline__ uint32_t byte(uint32_t P) const {
-        return reinterpret_cast<const uint8_t*>(w)[P + r];
+        return reinterpret_cast<const lds_u8*>(w)[P + r];
     }
     __device__ __forceinline__ uint32_t word(uint32_t P) const {  // 4 bytes little-endian
         const uint32_t o = P + r;
@@ -139,8 +146,8 @@ __device__ __forceinline__ uint32_t hash5(uint32_t w, uint32_t b4) {
 // (the LDS address space spelled out: a volatile generic access is not narrowed to LDS by
 // the compiler and would go out as flat loads and stores, waiting on the memory counter)
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
-__device__ __forceinline__ void tab_max(uint16_t* e, uint32_t v) {
-    volatile lds_u16* ve = (volatile lds_u16*)e;
+__device__ __forceinline__ void tab_max(lds_u16* e, uint32_t v) {
+    volatile lds_u16* ve = e;
     for (;;) {
         *ve = (uint16_t)v;
         if (*ve >= v) break;
@@ -150,14 +157,14 @@ __device__ __forceinline__ void tab_max(uint16_t* e, uint32_t v) {
 // tab_max over a lane's K positions: all writes, then all read-backs (in order: LDS ops of
 // a wave complete in issue order), then the rare retries
 template <int K>
-__device__ __forceinline__ void tab_max_batch(uint16_t* tw, const uint32_t* h, const uint32_t* v, const bool* ok) {
+__device__ __forceinline__ void tab_max_batch(lds_u16* tw, const uint32_t* h, const uint32_t* v, const bool* ok) {
 #if PBS_ZV_SERIALTAB
 #pragma unroll
     for (int i = 0; i < K; ++i)
         if (ok[i]) tab_max(&tw[h[i]], v[i]);
     return;
 #endif
-    volatile lds_u16* const base = (volatile lds_u16*)tw;
+    volatile lds_u16* const base = tw;
 #pragma unroll
     for (int i = 0; i < K; ++i)
         if (ok[i]) base[h[i]] = (uint16_t)v[i];
@@ -1121,7 +1128,7 @@ struct OrBitsL {
 //            per sequence, ~0.75 us.)
 // The sequences go to wseq (block positions, 64 at a time from lane registers); returns
 // their count | the end of the last match (block position) << 32.
-__device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restrict__ tabs, Seq* __restrict__ wseq_g,
+__device__ __noinline__ uint64_t parse_subblock(const Win W, lds_u16* __restrict__ tabs, Seq* __restrict__ wseq_g,
                                                 uint32_t hist, uint32_t N, int wave, int lane,
                                                 unsigned long long* probe) {
     PBS_GLOBAL uint32_t* const wseq_w = (PBS_GLOBAL uint32_t*)(wseq_g + (uint64_t)wave * kZSubSeq);
@@ -1132,9 +1139,9 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, uint16_t* __restric
     if (s0 < N) {
         const uint32_t se = uni(min(hist + zsub_start(wave + 1), N));
         const uint32_t wlo = uni(s0 - min(s0, kZHist));
-        uint16_t* const tw = tabs + wave * kZTab;
+        lds_u16* const tw = tabs + wave * kZTab;
 #pragma unroll
-        for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<uint32_t*>(tw)[lane + 64 * i] = 0;
+        for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<lds_u32*>(tw)[lane + 64 * i] = 0;
         // history: [wlo, s0) in rounds of kZHistRound positions every hs bytes (inserts only);
         // slot 0 (the round's first 64 positions) also looks up its candidates first: a
         // kZMin-byte match (not a run of one byte) sets the next round's step to 1, else it
@@ -2048,12 +2055,12 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             continue;
         }
         ZMARK(0);
-        const Win W{reinterpret_cast<const uint32_t*>(stage), r};
+        const Win W{(const lds_u32*)stage, r};
 
         // ---- parse: wave w owns the sub-block [s0, se) (window positions)
         {
             const uint64_t tw0 = probe_on && blockIdx.x == 0 ? wall_clock64() : 0;
-            const uint64_t pr = parse_subblock(W, tabs, wseq_all, hist, N, wave, lane,
+            const uint64_t pr = parse_subblock(W, (lds_u16*)tabs, wseq_all, hist, N, wave, lane,
                                                probe_on && blockIdx.x == 0 && wave == 0 ? g_zprobe : nullptr);
             const uint32_t ns = (uint32_t)pr, lastend = (uint32_t)(pr >> 32);
             if (probe_on && blockIdx.x == 0 && lane == 0) atomicAdd(&g_zprobe[34 + wave], wall_clock64() - tw0);
@@ -2565,6 +2572,7 @@ struct PArea {
 static_assert(sizeof(PArea) <= 64 * 1024, "the parse kernel's buffers fit the work area");
 struct PCtl {
     uint32_t nseq[kZWaves], lastend[kZWaves], wsum[kZWaves], wsum2[kZWaves], need_full;
+    uint32_t run_start[kZRuns], run_len[kZRuns], run_out[kZRuns];  // literal runs of a block with few sequences
 };
 // the entropy kernel's area: the fused kernel's EntropyArea without the literal bitmap (the
 // parse kernel's) and with a 36.5 KiB stream buffer -- Huffman streams up to kHufStreams
@@ -2589,21 +2597,36 @@ struct EArea {
     uint32_t shist[36 + 53 + 32];
 };
 
+// The split kernels' item dealing.  deal == nullptr: static, item k, k + grid, ... (the
+// stride passed in); otherwise the next unclaimed item of the launch's counter (zeroed
+// before the launch), so a workgroup that drew cheap items (RLE zero pages, raw blocks the
+// entropy kernel skips) takes more: the VM image's blocks are that uneven.  Every thread
+// of the workgroup calls it (it has two barriers).
+__device__ __forceinline__ uint64_t deal_item(uint32_t* deal, uint32_t& s_next, uint64_t stride_next) {
+    if (!deal) return stride_next;
+    __syncthreads();
+    if (threadIdx.x == 0) s_next = atomicAdd(deal, 1u);
+    __syncthreads();
+    return s_next;
+}
+
 __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zstd_parse_kernel(
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, uint64_t item_base, uint8_t* __restrict__ slots,
     uint64_t* __restrict__ sizes, Seq* __restrict__ seq_scratch, Coded* __restrict__ coded_items,
-    uint8_t* __restrict__ lit_items, ZItem* __restrict__ zitems, int probe_on, int64_t dbg_item) {
+    uint8_t* __restrict__ lit_items, ZItem* __restrict__ zitems, uint32_t* __restrict__ deal,
+    uint32_t* __restrict__ elist, int probe_on, int64_t dbg_item) {
     __shared__ uint4 stage[kZStageWords];
     __shared__ __attribute__((aligned(16))) uint8_t work[64 * 1024];
     __shared__ PCtl pc;
+    __shared__ uint32_t s_next;
     const int tid = threadIdx.x, lane = tid & 63, wave = (int)uni((uint32_t)tid >> 6);
     const bool probe = probe_on && blockIdx.x == 0 && tid == 0;
     uint64_t tp = probe ? wall_clock64() : 0;
     uint16_t* const tabs = reinterpret_cast<uint16_t*>(work);
     PArea& A = *reinterpret_cast<PArea*>(work);
     Seq* const wseq_all = seq_scratch + (uint64_t)blockIdx.x * kZBlockSeq;
-    for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
+    for (uint64_t k = deal_item(deal, s_next, blockIdx.x); k < nitems; k = deal_item(deal, s_next, k + gridDim.x)) {
         __syncthreads();  // LDS of the previous item
         ZMARK(9);
         ZItem* const zi = zitems + k;
@@ -2667,10 +2690,10 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             continue;
         }
         ZMARK(0);
-        const Win W{reinterpret_cast<const uint32_t*>(stage), r};
+        const Win W{(const lds_u32*)stage, r};
         {
             const uint64_t tw0 = probe_on && blockIdx.x == 0 ? wall_clock64() : 0;
-            const uint64_t pr = parse_subblock(W, tabs, wseq_all, hist, N, wave, lane,
+            const uint64_t pr = parse_subblock(W, (lds_u16*)tabs, wseq_all, hist, N, wave, lane,
                                                probe_on && blockIdx.x == 0 && wave == 0 ? g_zprobe : nullptr);
             if (probe_on && blockIdx.x == 0 && lane == 0) atomicAdd(&g_zprobe[34 + wave], wall_clock64() - tw0);
             if (lane == 0) {
@@ -2815,6 +2838,20 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
         __syncthreads();
         const uint32_t need_full = pc.need_full;
+        const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+        if (!need_full && rawh + nlit + 1 >= n) {
+            // raw literals and at least a one-byte sequence section: the compressed block
+            // cannot be shorter than the block (the entropy kernel's body < n test), so the raw
+            // block goes out here, from the staged window (the entropy kernel skips the item;
+            // from global memory it would read the 64 KiB again: a VM image's random pages)
+            stage_to_global(out + 3, W, hist, n, (uint32_t)tid, kZThreads);
+            if (tid == 0) {
+                write_block_header(out, last, 0, n);
+                sizes[k] = 3 + (uint64_t)n;
+                zi->kind = 1;
+            }
+            continue;
+        }
         if (need_full) {
             for (uint32_t i = tid; i < kZWaves * 256; i += kZThreads) A.wh[i] = 0;
             __syncthreads();
@@ -2839,14 +2876,36 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             zi->kind = 0;
             zi->nlit = nlit;
             zi->need_full = need_full;
+            if (deal) elist[atomicAdd(deal + 2, 1u)] = (uint32_t)k;  // the entropy kernel's items
         }
         ZMARK(2);
         // ---- the literals compacted in order to global memory (through LDS, dword stores):
         // for the entropy kernel, or -- raw literals for sure (no full histogram) -- straight
         // to their place in the block (behind the raw literal header the entropy kernel writes)
-        const uint32_t rawh = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
         uint8_t* const lo = need_full ? lit_items + k * (uint64_t)kEncBlock : out + 3 + rawh;
-        for (uint32_t pb = 0; pb < nlit; pb += (uint32_t)sizeof(A.lit)) {
+        uint32_t nseq_b = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kZWaves; ++w2) nseq_b += min(pc.nseq[w2], kZSubSeq);
+        if (nseq_b < kZRuns) {
+            // few sequences (a VM image's random pages: ~40 KB of literals in a handful of
+            // runs): the runs straight from the staged window with dword stores, as the fused
+            // kernel does -- the bitmap compaction below is an LDS byte round trip per literal
+            if (wave == 0) {
+                const Coded x = (uint32_t)lane < nseq_b ? coded[lane] : Coded{0, 0, 0, 0};
+                const uint32_t span = x.ll + x.ml, lit = x.ll;
+                const uint32_t si = wave_incl(span, lane), li = wave_incl(lit, lane);
+                if ((uint32_t)lane <= nseq_b) {
+                    pc.run_start[lane] = si - span;
+                    pc.run_out[lane] = li - lit;
+                    pc.run_len[lane] = (uint32_t)lane < nseq_b ? lit : n - (si - span);
+                }
+            }
+            __syncthreads();
+            for (uint32_t r2 = 0; r2 <= nseq_b; ++r2)
+                stage_to_global(lo + pc.run_out[r2], W, hist + pc.run_start[r2], pc.run_len[r2], (uint32_t)tid,
+                                kZThreads);
+        }
+        for (uint32_t pb = 0; pb < (nseq_b < kZRuns ? 0u : nlit); pb += (uint32_t)sizeof(A.lit)) {
             const uint32_t pe = min(nlit, pb + (uint32_t)sizeof(A.lit));
             uint32_t idx = litbase;
 #pragma unroll
@@ -2897,8 +2956,10 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
     const uint8_t* __restrict__ data, uint64_t base, const uint64_t* __restrict__ bounds,
     const uint64_t* __restrict__ items, uint64_t nitems, uint8_t* __restrict__ slots, uint64_t* __restrict__ sizes,
     const Coded* __restrict__ coded_items, const uint8_t* __restrict__ lit_items, const ZItem* __restrict__ zitems,
-    uint32_t* __restrict__ chain_scratch, int probe_on) {
+    uint32_t* __restrict__ chain_scratch, uint32_t* __restrict__ deal, const uint32_t* __restrict__ elist,
+    int probe_on) {
     __shared__ __attribute__((aligned(16))) EArea E;
+    __shared__ uint32_t s_next;
     __shared__ FseT fse[3];   // LL, OF, ML
     __shared__ FseT fse_huf;  // the Huffman description's scratch
     __shared__ PreT pre[3];
@@ -2920,9 +2981,13 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
         }
         q.log = t.log;
     }
-    for (uint64_t k = blockIdx.x; k < nitems; k += gridDim.x) {
+    // dealt: the items the parse kernel listed (the rest are done: RLE, raw, empty);
+    // static: every item, skipping those
+    const uint64_t ne = deal ? (uint64_t)*reinterpret_cast<volatile const uint32_t*>(deal + 1) : nitems;  // (deal[1]: the parse kernel's deal[2])
+    for (uint64_t e = deal_item(deal, s_next, blockIdx.x); e < ne; e = deal_item(deal, s_next, e + gridDim.x)) {
         __syncthreads();  // LDS of the previous item
         ZMARK(54);
+        const uint64_t k = deal ? (uint64_t)elist[e] : e;
         const ZItem* const zi = zitems + k;
         if (uni(zi->kind)) continue;
         const uint64_t it = items[k];
@@ -3386,7 +3451,7 @@ ArenaPool& zpool() {
     return *p;
 }
 enum ZSlot : unsigned { kZsBounds, kZsItems, kZsFirst, kZsSizes, kZsIpre, kZsBsz, kZsBoff, kZsComp, kZsCrc, kZsTmp,
-                        kZsSlots, kZsSeqs, kZsCoded, kZsChains, kZsZItems, kZsLits };
+                        kZsSlots, kZsSeqs, kZsCoded, kZsChains, kZsZItems, kZsLits, kZsDeal, kZsEList };
 
 }  // namespace
 }  // namespace pbs
@@ -3496,6 +3561,10 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
         const char* e = std::getenv("PBS_ZSTD_SPLIT");
         return !(e && e[0] == '0');
     }();
+    static const bool zdeal = [] {  // PBS_ZSTD_DEAL=0: items dealt statically (A/B)
+        const char* e = std::getenv("PBS_ZSTD_DEAL");
+        return !(e && e[0] == '0');
+    }();
     static const uint64_t zbatch = [] {
         const char* e = std::getenv("PBS_ZSTD_BATCH");
         const uint64_t v = e ? std::strtoull(e, nullptr, 0) : 0;
@@ -3505,6 +3574,9 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
     const unsigned grid_e = (unsigned)std::min<uint64_t>(bmax, 3ull * (uint64_t)use_cu);  // 3 per CU (52 KiB LDS, 168 VGPRs)
     ZItem* z_items = nullptr;
     uint8_t* z_lits = nullptr;
+    uint32_t* z_deal = nullptr;   // per batch: the parse and entropy counters, the entropy list's length
+    uint32_t* z_elist = nullptr;  // the batch's items left to the entropy kernel
+    const uint64_t nbatch = (ni + bmax - 1) / bmax;
     if (compress) {
         z_slots = ar->get<uint8_t>(kZsSlots, ni * kSlot);
         z_seqs = ar->get<Seq>(kZsSeqs, (size_t)grid * kZBlockSeq * sizeof(Seq));
@@ -3513,6 +3585,9 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
             z_chains = ar->get<uint32_t>(kZsChains, (size_t)grid_e * 6 * kZBlockSeq * sizeof(uint32_t));
             z_items = ar->get<ZItem>(kZsZItems, (size_t)bmax * sizeof(ZItem));
             z_lits = ar->get<uint8_t>(kZsLits, (size_t)bmax * kEncBlock);
+            if (zdeal && (!(z_deal = ar->get<uint32_t>(kZsDeal, (size_t)nbatch * 4 * sizeof(uint32_t))) ||
+                          !(z_elist = ar->get<uint32_t>(kZsEList, (size_t)bmax * sizeof(uint32_t)))))
+                fail(PBS_ERR_NOMEM);
             if (!z_items || !z_lits) fail(PBS_ERR_NOMEM);
         } else {
             z_coded = ar->get<Coded>(kZsCoded, (size_t)grid * kZBlockSeq * sizeof(Coded));
@@ -3529,7 +3604,8 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
         ok(hipMemcpyAsync(d_bounds, bounds, 2 * n * 8, hipMemcpyHostToDevice, st)) &&
             ok(hipMemcpyAsync(d_items, items.data(), ni * 8, hipMemcpyHostToDevice, st)) &&
             ok(hipMemcpyAsync(d_first, first.data(), (n + 1) * 8, hipMemcpyHostToDevice, st)) &&
-            ok(hipMemsetAsync(d_sizes, 0, (ni + 1) * 8, st));
+            ok(hipMemsetAsync(d_sizes, 0, (ni + 1) * 8, st)) &&
+            (!z_deal || ok(hipMemsetAsync(z_deal, 0, (size_t)nbatch * 4 * sizeof(uint32_t), st)));
     if (rc == PBS_OK) {
         (void)hipGetLastError();
         ok(hipEventRecord(ev[0], st));
@@ -3548,14 +3624,15 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
         if (compress && split) {
             for (uint64_t b0 = 0; b0 < ni; b0 += bmax) {
                 const uint64_t nb = std::min<uint64_t>(bmax, ni - b0);
+                uint32_t* const dl = z_deal ? z_deal + 4 * (b0 / bmax) : nullptr;
                 hipLaunchKernelGGL(zstd_parse_kernel, dim3((unsigned)std::min<uint64_t>(nb, (uint64_t)grid)),
                                    dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items + b0, nb, b0,
-                                   z_slots + b0 * kSlot, d_sizes + b0, z_seqs, z_coded, z_lits, z_items,
-                                   zprobe ? 1 : 0, dbg_item);
+                                   z_slots + b0 * kSlot, d_sizes + b0, z_seqs, z_coded, z_lits, z_items, dl,
+                                   z_elist, zprobe ? 1 : 0, dbg_item);
                 hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)std::min<uint64_t>(nb, (uint64_t)grid_e)),
                                    dim3(kEThreads), 0, st, dev_data, base, d_bounds, d_items + b0, nb,
                                    z_slots + b0 * kSlot, d_sizes + b0, z_coded, z_lits, z_items, z_chains,
-                                   zprobe ? 1 : 0);
+                                   dl ? dl + 1 : nullptr, z_elist, zprobe ? 1 : 0);
             }
         } else if (compress) {
             hipLaunchKernelGGL(zstd_block_kernel, dim3(grid), dim3(kZThreads), 0, st, dev_data, base, d_bounds, d_items,
