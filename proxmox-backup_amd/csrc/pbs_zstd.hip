@@ -1060,13 +1060,13 @@ struct OrBits {
     uint32_t wi;
     uint64_t acc;
     uint32_t n;
-    __device__ void init(uint32_t* words, uint32_t bit) {
+    __device__ __forceinline__ void init(uint32_t* words, uint32_t bit) {
         w = (PBS_GLOBAL uint32_t*)words;
         wi = bit >> 5;
         n = bit & 31;
         acc = 0;
     }
-    __device__ void put(uint64_t v, uint32_t nb) {
+    __device__ __forceinline__ void put(uint64_t v, uint32_t nb) {
         acc |= (v & ((1ull << nb) - 1ull)) << n;  // nb <= 31
         n += nb;
         if (n >= 32) {
@@ -1076,7 +1076,7 @@ struct OrBits {
             n -= 32;
         }
     }
-    __device__ void done() {
+    __device__ __forceinline__ void done() {
         if (n && (uint32_t)acc) __hip_atomic_fetch_or(&w[wi], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 };
@@ -1084,28 +1084,28 @@ struct OrBits {
 // The same into words staged in LDS (ds_or: no global atomics, whose completion later loads
 // of the thread would wait for on the in-order memory counter)
 struct OrBitsL {
-    uint32_t* w;  // LDS
+    lds_u32* w;  // (typed: a generic pointer made these flat atomics)
     uint32_t wi;
     uint64_t acc;
     uint32_t n;
-    __device__ void init(uint32_t* words, uint32_t bit) {
-        w = words;
+    __device__ __forceinline__ void init(uint32_t* words, uint32_t bit) {
+        w = (lds_u32*)words;
         wi = bit >> 5;
         n = bit & 31;
         acc = 0;
     }
-    __device__ void put(uint64_t v, uint32_t nb) {
+    __device__ __forceinline__ void put(uint64_t v, uint32_t nb) {
         acc |= (v & ((1ull << nb) - 1ull)) << n;  // nb <= 31
         n += nb;
         if (n >= 32) {
-            if ((uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
+            if ((uint32_t)acc) __hip_atomic_fetch_or(&w[wi], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             ++wi;
             acc >>= 32;
             n -= 32;
         }
     }
-    __device__ void done() {
-        if (n && (uint32_t)acc) atomicOr(&w[wi], (uint32_t)acc);
+    __device__ __forceinline__ void done() {
+        if (n && (uint32_t)acc) __hip_atomic_fetch_or(&w[wi], (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 };
 
@@ -3160,25 +3160,46 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
                 __threadfence_block();
             }
             __syncthreads();
+            // (two loops, each with its address space in the pointer's type: one lambda
+            // choosing between the buffers made every OR a flat atomic, LDS ones included)
+            lds_u32* const ls = (lds_u32*)E.streams;
+            PBS_GLOBAL uint32_t* const gg = (PBS_GLOBAL uint32_t*)gw;
             auto orbits = [&](uint32_t o, uint64_t v, uint32_t L) {
                 if (in_lds) {
-                    atomicOr(&E.streams[o >> 5], (uint32_t)(v << (o & 31)));
-                    if ((o & 31) + L > 32) atomicOr(&E.streams[(o >> 5) + 1], (uint32_t)((v << (o & 31)) >> 32));
+                    __hip_atomic_fetch_or(&ls[o >> 5], (uint32_t)(v << (o & 31)), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if ((o & 31) + L > 32)
+                        __hip_atomic_fetch_or(&ls[(o >> 5) + 1], (uint32_t)((v << (o & 31)) >> 32), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else {
                     const uint32_t og = o + gsh;
                     const uint64_t w = v << (og & 31);
-                    atomicOr(&gw[og >> 5], (uint32_t)w);
-                    if ((og & 31) + L > 32) atomicOr(&gw[(og >> 5) + 1], (uint32_t)(w >> 32));
+                    __hip_atomic_fetch_or(&gg[og >> 5], (uint32_t)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((og & 31) + L > 32)
+                        __hip_atomic_fetch_or(&gg[(og >> 5) + 1], (uint32_t)(w >> 32), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
                 }
             };
             uint32_t pb = bbase;
-            for_literals(lits, i0, i1, [&](uint32_t idx, uint32_t sym) {
+            auto lit_bits = [&](uint32_t idx, uint32_t sym, auto&& put) {
                 const uint32_t L = E.len[sym], cv = E.code[sym];
                 const uint32_t sg = four ? min(idx / seg, 3u) : 0u;
                 const uint32_t endP = four ? ctl.segP[sg + 1] : ctl.segP[4];
-                orbits(8 * Sat(sg) + (endP - pb - L), (uint64_t)cv, L);
+                put(8 * Sat(sg) + (endP - pb - L), (uint64_t)cv, L);
                 pb += L;
-            });
+            };
+            if (in_lds)
+                for_literals(lits, i0, i1, [&](uint32_t idx, uint32_t sym) {
+                    lit_bits(idx, sym, [&](uint32_t o, uint64_t v, uint32_t L) {
+                        __hip_atomic_fetch_or(&ls[o >> 5], (uint32_t)(v << (o & 31)), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if ((o & 31) + L > 32)
+                            __hip_atomic_fetch_or(&ls[(o >> 5) + 1], (uint32_t)((v << (o & 31)) >> 32),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    });
+                });
+            else
+                for_literals(lits, i0, i1, [&](uint32_t idx, uint32_t sym) { lit_bits(idx, sym, orbits); });
             if (tid < (four ? 4 : 1)) {  // end marks
                 const uint32_t bits = ctl.segP[four ? tid + 1 : 4] - ctl.segP[tid];
                 orbits(8 * Sat((uint32_t)tid) + bits, 1ull, 1);
