@@ -1043,7 +1043,7 @@ __device__ __noinline__ void seq_chain_wave(FseView t, const Coded* __restrict__
 __device__ __forceinline__ uint32_t seq_bits(const Coded& x, uint32_t q, uint32_t ns, const uint32_t* chains,
                                              uint32_t stride, const uint32_t* mode) {
     const uint32_t llc = x.codes & 0xFF, mlc = (x.codes >> 8) & 0xFF, ofc = x.codes >> 16;
-    uint32_t b = kLLBits[llc] + kMLBits[mlc] + ofc;
+    uint32_t b = ll_bits(llc) + ml_bits(mlc) + ofc;
     if (q + 1 < ns) {
         const uint32_t j = ns - 2 - q;  // the chains are in step order
         if (mode[0] != 1) b += chains[j] >> 16;
@@ -2457,8 +2457,8 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                             ob.put(c & 0xFFFF, c >> 16);
                         }
                     }
-                    ob.put(x.ll - kLLBase[llc], kLLBits[llc]);
-                    ob.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
+                    ob.put(x.ll - ll_base(llc), ll_bits(llc));
+                    ob.put(x.ml - ml_base(mlc), ml_bits(mlc));
                     ob.put(x.ofv - (1u << ofc), ofc);
                 }
                 ob.done();
@@ -2504,8 +2504,8 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                             ob.put(c & 0xFFFF, c >> 16);
                         }
                     }
-                    ob.put(x.ll - kLLBase[llc], kLLBits[llc]);
-                    ob.put(x.ml - kMLBase[mlc], kMLBits[mlc]);
+                    ob.put(x.ll - ll_base(llc), ll_bits(llc));
+                    ob.put(x.ml - ml_base(mlc), ml_bits(mlc));
                     ob.put(x.ofv - (1u << ofc), ofc);
                 }
                 ob.done();
@@ -3284,7 +3284,7 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
                     const uint32_t q = qb + (uint32_t)u;
                     if (q >= q1) break;
                     const uint32_t llc = x[u].codes & 0xFF, mlc = (x[u].codes >> 8) & 0xFF, ofc = x[u].codes >> 16;
-                    uint32_t b = kLLBits[llc] + kMLBits[mlc] + ofc;
+                    uint32_t b = ll_bits(llc) + ml_bits(mlc) + ofc;
                     if (q + 1 < ns) {
                         if (mode[0] != 1) b += cl[u] >> 16;
                         if (mode[1] != 1) b += co[u] >> 16;
@@ -3322,8 +3322,8 @@ __global__ __launch_bounds__(kEThreads) __attribute__((amdgpu_waves_per_eu(3, 3)
                             if (mode[2] != 1) ob.put(cm[u] & 0xFFFF, cm[u] >> 16);
                             if (mode[0] != 1) ob.put(cl[u] & 0xFFFF, cl[u] >> 16);
                         }
-                        ob.put(x[u].ll - kLLBase[llc], kLLBits[llc]);
-                        ob.put(x[u].ml - kMLBase[mlc], kMLBits[mlc]);
+                        ob.put(x[u].ll - ll_base(llc), ll_bits(llc));
+                        ob.put(x[u].ml - ml_base(mlc), ml_bits(mlc));
                         ob.put(x[u].ofv - (1u << ofc), ofc);
                     }
                     qe = qb;

@@ -53,21 +53,46 @@ constexpr int kLLMaxLog = 9, kMLMaxLog = 9, kOFMaxLog = 8;  // FSE_Compressed_Mo
 
 PBS_HD inline uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
+// The code tables as arithmetic (no table loads: on the GPU an indexed constant table is a
+// vector memory load per lookup, and the code search a dependent chain of them).  Equal to
+// kLLBase / kLLBits / kMLBase / kMLBits and to the table searches for every value
+// (tests/test_zstd_cpu.py::test_code_functions_match_tables).
 PBS_HD inline uint32_t ll_code(uint32_t ll) {
     if (ll < 16) return ll;
     if (ll >= 64) return highbit(ll) + 19;
-    uint32_t c = 16;
-    while (c < 24 && kLLBase[c + 1] <= ll) ++c;
-    return c;
+    if (ll < 24) return 16 + ((ll - 16) >> 1);
+    if (ll < 32) return 20 + ((ll - 24) >> 2);
+    if (ll < 48) return 22 + ((ll - 32) >> 3);
+    return 24;
 }
 
 PBS_HD inline uint32_t ml_code(uint32_t ml) {  // ml >= 3
     const uint32_t b = ml - 3;
     if (b < 32) return b;
     if (b >= 128) return highbit(b) + 36;
-    uint32_t c = 32;
-    while (c < 42 && kMLBase[c + 1] <= ml) ++c;
-    return c;
+    if (b < 40) return 32 + ((b - 32) >> 1);
+    if (b < 48) return 36 + ((b - 40) >> 2);
+    if (b < 64) return 38 + ((b - 48) >> 3);
+    if (b < 96) return 40 + ((b - 64) >> 4);
+    return 42;
+}
+
+PBS_HD inline uint32_t ll_bits(uint32_t c) {
+    return c < 16 ? 0u : c < 20 ? 1u : c < 22 ? 2u : c < 24 ? 3u : c == 24 ? 4u : c - 19;
+}
+PBS_HD inline uint32_t ll_base(uint32_t c) {
+    return c < 16 ? c : c < 20 ? 16 + 2 * (c - 16) : c < 22 ? 24 + 4 * (c - 20) : c < 24 ? 32 + 8 * (c - 22)
+                                                                                         : c == 24 ? 48u : 1u << (c - 19);
+}
+PBS_HD inline uint32_t ml_bits(uint32_t c) {
+    return c < 32 ? 0u : c < 36 ? 1u : c < 38 ? 2u : c < 40 ? 3u : c < 42 ? 4u : c == 42 ? 5u : c - 36;
+}
+PBS_HD inline uint32_t ml_base(uint32_t c) {
+    return c < 32 ? c + 3
+                  : c < 36 ? 35 + 2 * (c - 32)
+                           : c < 38 ? 43 + 4 * (c - 36)
+                                    : c < 40 ? 51 + 8 * (c - 38)
+                                             : c < 42 ? 67 + 16 * (c - 40) : c == 42 ? 99u : (1u << (c - 36)) + 3;
 }
 
 // floor(256 * log2(x)) for 1 <= x < 2^17, integer only: the cost unit of every entropy

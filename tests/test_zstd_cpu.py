@@ -88,3 +88,22 @@ def test_ratio_near_libzstd_level1(oracle, corpus):
         assert oracle.zstd_decompress(f, c.size) == c.tobytes()
         ours += len(f)
     assert ours <= ref * 1.10, (corpus, ours, ref, ours / ref)
+
+
+def test_code_functions_match_tables(tmp_path):
+    """The encoder's arithmetic code functions (zstd_enc.h: ll_code / ml_code and the
+    baseline / extra-bit functions the GPU kernels use instead of table loads) equal the RFC
+    8878 tables and their searches for every length a block can produce."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no g++")
+    root = Path(__file__).resolve().parent.parent
+    exe = tmp_path / "zstd_codes_check"
+    subprocess.run([cxx, "-std=c++17", "-O1", "-I", str(root / "proxmox-backup_amd" / "csrc"),
+                    str(root / "tests" / "cpp" / "zstd_codes_check.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and "bad 0" in r.stdout, r.stdout
