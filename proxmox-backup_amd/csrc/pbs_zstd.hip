@@ -3589,7 +3589,12 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
     static const uint64_t zbatch = [] {
         const char* e = std::getenv("PBS_ZSTD_BATCH");
         const uint64_t v = e ? std::strtoull(e, nullptr, 0) : 0;
-        return v ? v : (uint64_t)8192;
+        // 32768 items (2 GiB of input, ~11.5 GB of scratch: the coded sequences take the
+        // worst case per block): one batch per call up to that, and the tails of the two
+        // launches (an entropy workgroup holds ~11 items of a 8192-item batch, the last one
+        // alone) amortised -- text 36.9 -> 38.0, pxar 37.3 -> 39.1 GiB/s against 8192
+        // (profiles/r06/zbatch/)
+        return v ? v : (uint64_t)32768;
     }();
     const uint64_t bmax = std::min<uint64_t>(ni, zbatch);
     const unsigned grid_e = (unsigned)std::min<uint64_t>(bmax, 3ull * (uint64_t)use_cu);  // 3 per CU (52 KiB LDS, 168 VGPRs)
