@@ -13,7 +13,7 @@ for wl in vmimage random; do
     tag=$(echo $ctr | cut -d' ' -f1)
     timeout -k 10 200 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/${wl}_$tag" -o run -- \
         python3 bench.py --workload $wl --steps 3 --warmup 1 --cpu-baseline 0 --cpu-config1 0 \
-        --host-inclusive-gib 0 --secondary-random 0 > "$OUT/${wl}_$tag.log" 2>&1
+        --host-inclusive-gib 0 --secondary-random 0 --stages 0 > "$OUT/${wl}_$tag.log" 2>&1
     rc=$?; echo "$wl [$ctr] rc=$rc"
     [ $rc -eq 0 ] || exit $rc
   done
