@@ -28,8 +28,9 @@
 //
 // Parse (per 64 KiB block; eight ~8 KiB sub-blocks -- kSubA bytes for the first four,
 // kSubB for the last four -- one GPU wave each, own hash table; round 5):
-//   history  every position of the kHist bytes before the sub-block enters the table (the
-//            table keeps 1 + the LAST position per hash of kHashBytes bytes);
+//   history  the kWin bytes before the sub-block enter the table in rounds of kHistRound
+//            positions every `hs` bytes (hs >= kHistMinStep; the table keeps 1 + the LAST
+//            position per hash of kHashBytes bytes);
 //   rounds   of kRound positions sampled every `step` bytes (step 1 after a round in which
 //            the walk took a match, doubling to kMaxStep without; a round starts at the end
 //            of a match that ran past the previous one, the positions inside it are not
@@ -64,8 +65,11 @@ uint32_t sub_of(uint32_t pos) {  // the sub-block holding block position pos
     while (w < 7 && pos >= sub_start(w + 1)) ++w;
     return w;
 }
-constexpr uint32_t kHist = 16384;   // window before a sub-block (reaches into the previous block)
-constexpr uint32_t kRound = 256, kMaxStep = 8, kHistRound = 512, kHistMaxStep = 8, kHistStep0 = 1;
+// the window before a sub-block (reaches into the previous block) and the history rounds'
+// smallest step: 12 KiB and 2 since round 6 (16 KiB and 1 before; the GPU's kZWin /
+// kZHistMinStep, csrc/pbs_zstd.hip)
+constexpr uint32_t kWin = 12288, kHistMinStep = 2;
+constexpr uint32_t kRound = 256, kMaxStep = 8, kHistRound = 512, kHistMaxStep = 8, kHistStep0 = kHistMinStep;
 constexpr uint32_t kHashLog = 12, kCap = 32, kMinMatch = 5, kBack = 8;
 constexpr uint32_t kHufStreams = 48 * 1024;  // largest Huffman stream bytes of a block
 
@@ -101,12 +105,12 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
     for (uint32_t w = 0; w < 8 && avail + sub_start(w) < N; ++w) {
         const uint32_t s0 = avail + sub_start(w), se = std::min(avail + sub_start(w + 1), N);
         std::fill(table.begin(), table.end(), 0u);
-        const uint32_t wlo = s0 - std::min(s0, kHist);  // the sub-block's window start
+        const uint32_t wlo = s0 - std::min(s0, kWin);  // the sub-block's window start
         // history: the window before the sub-block in rounds of kHistRound positions every
         // `hs` bytes (inserts only; the table keeps the last position per hash); a round's
         // first 64 positions look up their candidates before its inserts, and when one of
-        // them matches kMinMatch bytes (not a run of one byte) the next round steps 1, else
-        // the step doubles up to kHistMaxStep
+        // them matches kMinMatch bytes (not a run of one byte) the next round steps
+        // kHistMinStep, else the step doubles up to kHistMaxStep
         uint32_t hs = kHistStep0;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kHistRound * hs;
@@ -130,7 +134,7 @@ void parse(const uint8_t* src, uint32_t n, uint32_t avail, std::vector<Seq>& seq
                 const bool run = rd32(b + p) == b[p] * 0x01010101u && b[p + 4] == b[p];
                 hit |= !run && std::memcmp(b + cand[j] - 1, b + p, hb) == 0;
             }
-            hs = hit ? 1 : std::min(2 * hs, kHistMaxStep);
+            hs = hit ? kHistMinStep : std::min(2 * hs, kHistMaxStep);
         }
         uint32_t cur = s0, step = std::min(hs, kMaxStep), rep = 0;  // rep 0: no offset in this sub-block yet
         for (uint32_t r0 = s0, rn; r0 < se; r0 = rn) {

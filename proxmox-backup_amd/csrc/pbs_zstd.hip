@@ -12,8 +12,9 @@
 //   RLE     every byte equal: a 4-byte RLE block (the zero pages of a VM image);
 //   parse   each of the 8 waves parses one ~8 KiB sub-block (8 KiB + 384 bytes for waves
 //           0-3, - 384 for waves 4-7: see kZSubA) with its own 4096-entry table
-//           of 16-bit window positions: the 16 KiB before the sub-block first enter the
-//           table in accelerated rounds, then rounds of 256 sampled positions (step 1
+//           of 16-bit window positions: the 12 KiB before the sub-block first enter the
+//           table in accelerated rounds (every 2nd position or sparser), then rounds of
+//           256 sampled positions (step 1
 //           after a round with a match, doubling to 8 without): candidates = the table
 //           (hash of 5 bytes; the last position of an EARLIER round) and the run
 //           candidate p - 1, the longer (capped at 32) winning; the wave's greedy walk
@@ -80,7 +81,19 @@ __device__ __host__ constexpr uint32_t zsub_start(int w) {  // block position of
 }
 constexpr uint32_t kZHist = 16384;   // window before a sub-block
 constexpr uint32_t kZRound = 256, kZHashLog = 12, kZCap = 32, kZMin = 5, kZMaxStep = 8, kZBack = 8;
-constexpr uint32_t kZHistRound = 512, kZHistStep0 = 1, kZHistMaxStep = 8;  // history rounds (see parse_subblock)
+// Since round 6 the history rounds step at least 2 bytes (1 before) and a sub-block's match
+// window reaches 12 KiB back (16 KiB before): text 38.0 -> 40.4, pxar 39.1 -> 41.5 GiB/s for
+// payloads 1.075 -> 1.092 x (text) and 1.034 -> 1.045 x (pxar) libzstd level 1
+// (profiles/r06/zwindow/; the twin's kHistMinStep / kWin follow).  The macros are for A/B
+// builds only.
+#ifndef PBS_ZHIST_MIN
+#define PBS_ZHIST_MIN 2
+#endif
+#ifndef PBS_ZWIN
+#define PBS_ZWIN 12288
+#endif
+constexpr uint32_t kZHistRound = 512, kZHistStep0 = PBS_ZHIST_MIN, kZHistMaxStep = 8;  // history rounds (see parse_subblock)
+constexpr uint32_t kZHistMinStep = PBS_ZHIST_MIN, kZWin = PBS_ZWIN;
 constexpr int kZPer = kZRound / 64;        // positions per lane and round
 constexpr int kZPerH = kZHistRound / 64;   // history positions per lane and round
 constexpr uint32_t kZTab = 1u << kZHashLog;
@@ -1138,14 +1151,15 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, lds_u16* __restrict
     uint32_t ns = 0, lastend = 0;
     if (s0 < N) {
         const uint32_t se = uni(min(hist + zsub_start(wave + 1), N));
-        const uint32_t wlo = uni(s0 - min(s0, kZHist));
+        const uint32_t wlo = uni(s0 - min(s0, kZWin));
         lds_u16* const tw = tabs + wave * kZTab;
 #pragma unroll
         for (int i = 0; i < (int)(kZTab / 2 / 64); ++i) reinterpret_cast<lds_u32*>(tw)[lane + 64 * i] = 0;
         // history: [wlo, s0) in rounds of kZHistRound positions every hs bytes (inserts only);
         // slot 0 (the round's first 64 positions) also looks up its candidates first: a
-        // kZMin-byte match (not a run of one byte) sets the next round's step to 1, else it
-        // doubles up to kZHistMaxStep (random bytes need no dense history)
+        // kZMin-byte match (not a run of one byte) sets the next round's step to
+        // kZHistMinStep, else it doubles up to kZHistMaxStep (random bytes need no dense
+        // history)
         uint32_t hs = kZHistStep0;
         for (uint32_t r0 = wlo, rn; r0 < s0; r0 = rn) {
             rn = r0 + kZHistRound * hs;
@@ -1173,7 +1187,7 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, lds_u16* __restrict
             const uint32_t b = w0 & 0xFF;
             const bool run = w0 == b * 0x01010101u && b40 == b;
             const bool hit = t0 && !run && cw == w0 && c4 == b40;
-            hs = uni(__ballot(hit) ? 1u : min(2 * hs, kZHistMaxStep));
+            hs = uni(__ballot(hit) ? kZHistMinStep : min(2 * hs, kZHistMaxStep));
         }
         if (probe) t_hist = wall_clock64();
         uint64_t t_walk = 0;
