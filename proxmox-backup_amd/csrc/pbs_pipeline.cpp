@@ -288,7 +288,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     uint64_t* q_ctl = nullptr;
     pbs::DigestJob* q_jobs = nullptr;
     pbs::DigestQueueDev* d_q = nullptr;
-    bool q_running = false;
+    std::atomic<bool> q_running{false};
     const size_t hq_need = 64 + std::max<size_t>(cap, 1) * sizeof(pbs::DigestJob);
     if (ok && A->hq_bytes < hq_need) {
         if (A->hq) (void)hipHostFree(A->hq);
@@ -327,15 +327,28 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     // tests/test_gpu_digest.py::test_pipeline_beside_null_stream_work)
     const int q_wgs = (int)env_u64("PBS_PIPE_QUEUE_WGS", (uint64_t)dig * 2);
     const uint64_t q_idle = env_u64("PBS_PIPE_IDLE_MS", 50) * 100000ull;  // wall_clock64: 100 MHz
-    uint64_t q_launches = 0;
-    auto q_launch = [&]() {
+    std::atomic<uint64_t> q_launches{0};
+    // a launch skipped because the grid was still resident: it may have been on its idle
+    // exit and leave the jobs just published, so the next tries (the next piece, the upload
+    // worker's wait, the final drain) launch it again once it has gone
+    std::atomic<bool> relaunch_due{false};
+    std::mutex qmu;  // launches come from this thread and the upload worker
+    auto q_launch_locked = [&]() {
         if (!q_running) return;
-        if (q_launches && hipStreamQuery(s_dig[0]) == hipErrorNotReady) return;  // still resident
+        if (q_launches && hipStreamQuery(s_dig[0]) == hipErrorNotReady) {  // still resident
+            relaunch_due = true;
+            return;
+        }
+        relaunch_due = false;
         if (pbs::launch_sha256_queue(d_data, key, key_len, q_jobs_dev, q_ctl_dev, d_q, d_dig, q_wgs, q_idle,
                                      s_dig[0]) == hipSuccess)
             ++q_launches;
         else
             q_running = false;  // the host hashes what the queue did not take
+    };
+    auto q_launch = [&]() {
+        std::lock_guard<std::mutex> g(qmu);
+        q_launch_locked();
     };
     uint64_t nj = 0;  // jobs published
 
@@ -510,9 +523,10 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
                     // the batch's digests: host-routed ones by their flags, GPU jobs by theirs
                     const Clock::time_point tw = Clock::now();
                     bool fin = false;
-                    for (;;) {
+                    for (unsigned spin = 0;; ++spin) {
                         fin = dig_final.load(std::memory_order_acquire);
                         if (fin) break;
+                        if (spin % 64 == 63 && relaunch_due.load(std::memory_order_relaxed)) q_launch();
                         bool all = true;
                         for (size_t i = i0; i < i1 && all; ++i)
                             all = hmask[i] ? hs.flag(i)
@@ -727,6 +741,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         last_chunk_at = ms_since(t0);
     }
     if (q_running) publish(true);  // every path: the queue grid drains
+    if (relaunch_due) q_launch();
     if (q_launches && rc != PBS_OK) (void)hipStreamSynchronize(s_dig[0]);  // before its memory goes
     hs.finish();
     // the routing is done: this thread hashes what is left of the host share, beside the
@@ -737,6 +752,16 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     double gpu_done_at = 0;
     if (rc == PBS_OK && ok) {
         for (int i = 0; i < kDigestStreams; ++i) hip_ok(hipStreamSynchronize(s_dig[i]));
+        {
+            // no launch after this point; one still due (the grid exited before the final
+            // count and left jobs) runs now, drained, before the digests are read
+            std::lock_guard<std::mutex> g(qmu);
+            if (relaunch_due) {
+                q_launch_locked();
+                hip_ok(hipStreamSynchronize(s_dig[0]));
+            }
+            q_running = false;
+        }
         gpu_done_at = ms_since(t0);
         if (rc == PBS_OK && n) {
             if (hpool.empty()) {
@@ -756,7 +781,12 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
     }
     for (auto& th : hpool) th.join();  // error paths
     // error paths too: nothing of this call may still run when the work area returns to
-    // the pool (no hipFree any more to wait for it)
+    // the pool (no hipFree any more to wait for it), and the upload worker launches nothing
+    // from here on
+    {
+        std::lock_guard<std::mutex> g(qmu);
+        q_running = false;
+    }
     for (hipStream_t s : {s_copy, s_scan, s_dig[0], s_dig[1], s_dig[2], s_dig[3]})
         if (s) (void)hipStreamSynchronize(s);
     if (!host_done_at && hs.chunks()) host_done_at = ms_since(t0);
@@ -800,7 +830,7 @@ int pipeline_run(size_t avg, const uint8_t* host, size_t len, size_t piece, cons
         timing->host_work_ms = hs.last_done_us() / 1000.0;
         if (std::getenv("PBS_PIPE_DEBUG")) {
             std::fprintf(stderr, "digest queue: jobs %llu claimed %llu launches %llu mirror %llx polls %llu last_h %llx; seen:",
-                         (unsigned long long)nj, qd.next, (unsigned long long)q_launches, qd.mirror, qd.polls,
+                         (unsigned long long)nj, qd.next, (unsigned long long)q_launches.load(), qd.mirror, qd.polls,
                          qd.last_h);
             for (unsigned long long i = 0; i < qd.nseen && i < 16; ++i)
                 std::fprintf(stderr, " %llx@%.3fms", qd.seen[i], (qd.seen_t[i] - qd.seen_t[0]) / 1e5);
