@@ -3596,14 +3596,15 @@ extern "C" int pbs_blob_encode_spans_device(const uint8_t* dev_data, size_t data
         const char* e = std::getenv("PBS_ZSTD_SPLIT");
         return !(e && e[0] == '0');
     }();
-    static const bool zdeal = [] {  // PBS_ZSTD_DEAL=0: items dealt statically (A/B)
+    // (read per call, so a test can run many small batches and both dealings in one process)
+    const bool zdeal = [] {  // PBS_ZSTD_DEAL=0: items dealt statically (A/B)
         const char* e = std::getenv("PBS_ZSTD_DEAL");
         return !(e && e[0] == '0');
     }();
-    static const uint64_t zbatch = [] {
+    const uint64_t zbatch = [] {
         const char* e = std::getenv("PBS_ZSTD_BATCH");
         const uint64_t v = e ? std::strtoull(e, nullptr, 0) : 0;
-        // 32768 items (2 GiB of input, ~11.5 GB of scratch: the coded sequences take the
+        // 32768 items (2 GiB of input, ~10 GB of scratch: the coded sequences take the
         // worst case per block): one batch per call up to that, and the tails of the two
         // launches (an entropy workgroup holds ~11 items of a 8192-item batch, the last one
         // alone) amortised -- text 36.9 -> 38.0, pxar 37.3 -> 39.1 GiB/s against 8192

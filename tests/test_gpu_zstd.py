@@ -80,6 +80,18 @@ def test_blob_encode_mixed_chunks(gpu, oracle, torch_dev, pad):
     assert comp.sum() >= 6 and tm["compressed_chunks"] == comp.sum()
 
 
+@pytest.mark.parametrize("batch,deal", [("7", "1"), ("7", "0"), ("64", "1")])
+def test_blob_encode_batches(gpu, oracle, torch_dev, monkeypatch, batch, deal):
+    """Many parse / entropy launch pairs in one call (PBS_ZSTD_BATCH items each: the
+    default 32 768 makes every other test here one batch), the items dealt by each batch's
+    counters or statically, the entropy kernel over each batch's list: the twin's blobs."""
+    monkeypatch.setenv("PBS_ZSTD_BATCH", batch)
+    monkeypatch.setenv("PBS_ZSTD_DEAL", deal)
+    data, bounds = _mixed()
+    blob, offs, crcs, comp, tm = _encode(gpu, torch_dev, data, bounds, pad=1)
+    _check(oracle, data, bounds, blob, offs, crcs, comp)
+
+
 def test_blob_encode_uncompressed(gpu, oracle, torch_dev):
     """compress = false (DataBlob::encode(.., false), :162-173): every blob raw."""
     data, bounds = _mixed()
