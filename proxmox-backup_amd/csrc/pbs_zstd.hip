@@ -1273,8 +1273,9 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, lds_u16* __restrict
             }
             qmark(44);
             // lengths: the common prefix from byte 4 on (bytes 0-4 are equal), 8 bytes a step
-            // (a lane done, or not matching, reads its own position on both sides), a slot only
-            // while one of its lanes goes on
+            // (a lane done, or not matching, reads the sub-block start on both sides: one
+            // address for all of them, a broadcast, where its own position cost the LDS a
+            // bank access per lane), a slot only while one of its lanes goes on
             const bool alt = __ballot(anyA) != 0;
             for (uint32_t k = 4; k < kZCap; k += 8) {
                 bool more = false;
@@ -1284,7 +1285,7 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, lds_u16* __restrict
 #pragma unroll
                 for (int i = 0; i < kZPer; ++i) {
                     const bool g = go[i] && k < lim[i];
-                    const uint32_t sa = g ? S[i] + k : P[i], pa = g ? P[i] + k : P[i];
+                    const uint32_t sa = g ? S[i] + k : s0, pa = g ? P[i] + k : s0;
                     xd0[i] = W.word(sa) ^ W.word(pa);
                     xd1[i] = W.word(sa + 4) ^ W.word(pa + 4);
                 }
@@ -1292,7 +1293,7 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, lds_u16* __restrict
 #pragma unroll
                     for (int i = 0; i < kZPer; ++i) {
                         const bool ga = goA[i] && k < lim[i];
-                        const uint32_t sb2 = ga ? P[i] - 1 + k : P[i], pb2 = ga ? P[i] + k : P[i];
+                        const uint32_t sb2 = ga ? P[i] - 1 + k : s0, pb2 = ga ? P[i] + k : s0;
                         xa0[i] = W.word(sb2) ^ W.word(pb2);
                         xa1[i] = W.word(sb2 + 4) ^ W.word(pb2 + 4);
                     }
@@ -1329,7 +1330,8 @@ __device__ __noinline__ uint64_t parse_subblock(const Win W, lds_u16* __restrict
             uint32_t D[kZPer];
             unsigned long long m[kZPer];
             // the backward extension's words, every slot's read together (a slot without a
-            // table or run candidate, or too near the window start, reads its own position)
+            // table or run candidate, or too near the window start, reads position 8: one
+            // address for all such lanes, a broadcast)
             uint32_t bx1[kZPer], bx2[kZPer];
 #pragma unroll
             for (int i = 0; i < kZPer; ++i) {
