@@ -2308,7 +2308,7 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             if ((uint32_t)lane <= nseq) {
                 ctl.run_start[lane] = si - span;
                 ctl.run_out[lane] = li - lit;
-                ctl.run_len[lane] = (uint32_t)lane < nseq ? lit : n - (si - span);
+                ctl.run_len[lane] = (uint32_t)lane < nseq ? lit : (n > si - span ? n - (si - span) : 0u);  // (never a wrapped length)
             }
         }
         // ---- Huffman sizes: per-thread code-length sums, block scan, segment totals
@@ -2913,7 +2913,7 @@ __global__ __launch_bounds__(kZThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
                 if ((uint32_t)lane <= nseq_b) {
                     pc.run_start[lane] = si - span;
                     pc.run_out[lane] = li - lit;
-                    pc.run_len[lane] = (uint32_t)lane < nseq_b ? lit : n - (si - span);
+                    pc.run_len[lane] = (uint32_t)lane < nseq_b ? lit : (n > si - span ? n - (si - span) : 0u);  // (never a wrapped length)
                 }
             }
             __syncthreads();
